@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""hhuff benchmark -- BASELINE.json metric "GiB/s device-resident Huffman decode+encode, 16M header strings
+mean 48B" on configuration 4 (16M strings, lengths U[24,72], header alphabet), one MI355X per rank.
+
+One step = one pass of the hot path over one batch, inputs resident in HBM:
+    encode  all N plain strings         (hhuff_encode_batch, h2o_hpack_encode_huffman per element)
+    decode  the N_ok Huffman strings    (hhuff_decode_batch, h2o_hpack_decode_huffman per element)
+            packed contiguously, i.e. the compressible strings as they would arrive on the wire
+value = sum over ranks of plain bytes P / max over ranks of (t_encode + t_decode)   [GiB/s, 2^30]
+Multi-GPU (torchrun, one process per GPU, RCCL): each rank owns an independent shard of N strings
+(weak scaling); no collective on the data path, only barriers / a max-reduce of the timing.
+
+Extra JSON fields: per-direction rates, `roofline` for the dominant kernel (decode; algorithmic bytes
+B_dec = H + P_ok + 9 N_ok + 4 + ceil(N_ok / 8) per launch over its HIP-event duration), and
+`cpu_baseline` (oracle restatement of h2o's CPU path on this host's cores, rank 0 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy peak ~6300
+GIB = float(1 << 30)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c4")
+    ap.add_argument("--n", type=int, default=None, help="strings per rank (default: the config's N)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1 << 21, help="strings in the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=None)
+    ap.add_argument("--only", choices=["encode", "decode"], default=None, help="profile one direction")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from h2o_amd import codec, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    codec.lib()
+
+    # ---- synthetic batch, device resident -------------------------------------------------------
+    b = synth.make_batch_torch(args.config, n=args.n, seed=1000 + rank)
+    n = b["n"]
+    P = int(b["total"])
+    off32 = b["off"].to(torch.int32)
+    lens = (b["off"][1:] - b["off"][:-1])
+    enc_out = torch.empty(P + 16, dtype=torch.uint8, device="cuda")
+    enc_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    enc_st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(b["data"], off32, n, out=enc_out, out_len=enc_len, status=enc_st)
+    # the wire: compressible strings, packed contiguously (second encode with explicit destinations)
+    ok = enc_len != -1
+    idx = torch.nonzero(ok).squeeze(1)
+    n_ok = int(idx.numel())
+    hl = enc_len[idx].to(torch.int64)
+    h_off = torch.zeros(n_ok + 1, dtype=torch.int64, device="cuda")
+    h_off[1:] = torch.cumsum(hl, 0)
+    H = int(h_off[-1].item())
+    huff = torch.empty(H + 16, dtype=torch.uint8, device="cuda")
+    tmp_len = torch.empty(n_ok, dtype=torch.int32, device="cuda")
+    codec.encode_batch(b["data"], off32[idx].contiguous(), n_ok, in_len=lens[idx].to(torch.int32).contiguous(),
+                       out=huff, out_off=h_off[:-1].to(torch.int32).contiguous(), out_len=tmp_len, in_size=P)
+    # is_name bits of the kept strings
+    bits = ((b["is_name_bits"].to(torch.int64) & 0xFFFFFFFF).unsqueeze(1) >> torch.arange(32, device="cuda")) & 1
+    names_ok = bits.reshape(-1)[:n][idx]
+    nw = (n_ok + 31) // 32
+    padn = torch.zeros(nw * 32, dtype=torch.int64, device="cuda")
+    padn[:n_ok] = names_ok
+    w = (padn.view(nw, 32) << torch.arange(32, device="cuda")).sum(1)
+    names_bits = torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32).contiguous()
+    h_off32 = h_off.to(torch.int32).contiguous()
+    P_ok = int(hl.numel() and lens[idx].sum().item())
+    dec_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
+    dec_len = torch.empty(n_ok, dtype=torch.int32, device="cuda")
+    dec_st = torch.empty(n_ok, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    del tmp_len
+
+    def run_encode():
+        codec.encode_batch(b["data"], off32, n, out=enc_out, out_len=enc_len, status=enc_st, in_size=P)
+
+    def run_decode():
+        codec.decode_batch(huff, h_off32, n_ok, is_name_bits=names_bits, out=dec_out, out_len=dec_len, status=dec_st,
+                           in_size=H)
+
+    # correctness spot check before timing: decoded lengths equal the plain lengths of the kept strings
+    run_decode()
+    torch.cuda.synchronize()
+    assert bool((dec_len == lens[idx].to(torch.int32)).all()), "decode does not invert encode"
+
+    # ---- timed region ----------------------------------------------------------------------------
+    do_enc = args.only in (None, "encode")
+    do_dec = args.only in (None, "decode")
+    for _ in range(args.warmup):
+        if do_enc:
+            run_encode()
+        if do_dec:
+            run_decode()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1, e2 in ev:
+        e0.record()
+        if do_enc:
+            run_encode()
+        e1.record()
+        if do_dec:
+            run_decode()
+        e2.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t_wall = time.perf_counter() - t0
+    t_enc = sorted(a.elapsed_time(b_) for a, b_, _ in ev)
+    t_dec = sorted(b_.elapsed_time(c) for _, b_, c in ev)
+    t_enc_avg = sum(t_enc) / len(t_enc)
+    t_dec_avg = sum(t_dec) / len(t_dec)
+    ms_step = t_wall * 1e3 / args.steps
+    if world > 1:
+        t = torch.tensor([ms_step], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms_step = float(t.item())
+        tot = torch.tensor([P, P_ok, n, n_ok], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tot)
+        P_all, P_ok_all, n_all, n_ok_all = (float(x) for x in tot.tolist())
+    else:
+        P_all, P_ok_all, n_all, n_ok_all = float(P), float(P_ok), float(n), float(n_ok)
+
+    if rank == 0:
+        B_dec = H + P_ok + 9 * n_ok + 4 + (n_ok + 7) // 8
+        B_enc = P + int(hl.sum().item()) + 9 * n + 4
+        dec_gbps = B_dec / (t_dec_avg * 1e-3) / 1e9
+        enc_gbps = B_enc / (t_enc_avg * 1e-3) / 1e9
+        dominant = "decode" if t_dec_avg >= t_enc_avg or args.only == "decode" else "encode"
+        if args.only == "encode":
+            dominant = "encode"
+        ach = dec_gbps if dominant == "decode" else enc_gbps
+        value = P_all / GIB / (ms_step * 1e-3)
+        line = {
+            "metric": "GiB/s device-resident Huffman decode+encode, 16M header strings mean 48B",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded, header alphabet P~2^-nbits, 1% adversarial)",
+            "config": {"workload": "%s: %d header strings/GPU, lengths %s, encode all + decode the compressible"
+                                   % (args.config, n, synth.CONFIGS[args.config]["lengths"]),
+                       "strings_per_gpu": n, "global_strings": int(n_all), "plain_bytes_per_gpu": P,
+                       "huffman_bytes_per_gpu": H, "parallelism": "shard%d" % world},
+            "encode_ms": round(t_enc_avg, 4),
+            "decode_ms": round(t_dec_avg, 4),
+            "encode_gibps": round(P / GIB / (t_enc_avg * 1e-3), 3) if do_enc else None,
+            "decode_gibps": round(P_ok / GIB / (t_dec_avg * 1e-3), 3) if do_dec else None,
+            "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "algorithmic_bytes": B_dec if dominant == "decode" else B_enc},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(b, args, np)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(b, args, np):
+    """h2o's CPU path (oracle restatement, same algorithm as lib/http2/hpack.c) on this host's cores, on a
+    bounded sample (the first `cpu_sample` strings of rank 0's batch), encode + decode like one step."""
+    from oracle import oracle as O
+
+    o = O.oracle()
+    m = min(args.cpu_sample, b["n"])
+    off = b["off"][:m + 1].cpu().numpy().astype(np.uint32)
+    data = b["data"][:int(off[-1])].cpu().numpy()
+    names = b["is_name_bits"][:(m + 31) // 32].cpu().numpy().view(np.uint32)
+    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+    enc, el, _ = o.encode_batch(data, off, m, nthreads=threads)  # also produces the decode input
+    ok = el != O.FAIL
+    hl = np.where(ok, el, 0).astype(np.uint32)
+    starts = off[:-1].copy()
+    best = None
+    for _ in range(3):
+        t0 = time.perf_counter()
+        o.encode_batch(data, off, m, nthreads=threads)
+        t1 = time.perf_counter()
+        o.decode_batch(enc, starts, m, in_len=hl, is_name_bits=names, nthreads=threads)
+        t2 = time.perf_counter()
+        best = (t2 - t0) if best is None else min(best, t2 - t0)
+    P = float(off[-1])
+    return {"value": round(P / GIB / best, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": "%d strings (%.1f MB) of rank 0's batch, encode + decode, best of 3, %d threads"
+                      % (m, P / 1e6, threads)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,189 @@
+"""ctypes bindings of the hhuff C-ABI (include/hhuff.h) -- the host-side mirror of h2o's interface.
+
+Per-string functions keep h2o's names and meaning (lib/http2/hpack.c:117 / :774):
+    decode_huffman(src, is_name, soft_errors=0) -> (bytes | None, soft_errors)   None <=> SIZE_MAX
+    encode_huffman(src)                         -> bytes | None                 None <=> SIZE_MAX
+Batch functions run the HIP kernels on device tensors (torch is used only for memory and streams):
+    decode_batch(...), encode_batch(...)       device-resident arrays, async on the current stream
+    decode_batch_host(...), encode_batch_host(...)   numpy arrays, H2D/D2H included
+There is no CPU codec behind any of these: if libhhuff.so is missing or no GPU is present they raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libhhuff.so")
+
+FAIL_LEN = 0xFFFFFFFF
+SOFT_NAME = 0x1
+SOFT_VALUE = 0x2
+STATUS_FAIL = 0x80
+STATUS_TOO_LONG = 0xC0
+SIZE_MAX = ctypes.c_size_t(-1).value
+
+_vp = ctypes.c_void_p
+_lib = None
+
+
+class HhuffError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libhhuff.so (fails loudly when the HIP extension is not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HhuffError("libhhuff.so not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = ctypes.CDLL(LIB_PATH)
+        L.h2o_hpack_decode_huffman.restype = ctypes.c_size_t
+        L.h2o_hpack_decode_huffman.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint), ctypes.c_char_p,
+                                               ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p)]
+        L.h2o_hpack_encode_huffman.restype = ctypes.c_size_t
+        L.h2o_hpack_encode_huffman.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+        L.hhuff_decode_batch.restype = ctypes.c_int
+        L.hhuff_decode_batch.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]
+        L.hhuff_encode_batch.restype = ctypes.c_int
+        L.hhuff_encode_batch.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp]
+        L.hhuff_decode_batch_host.restype = ctypes.c_int
+        L.hhuff_decode_batch_host.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64,
+                                              _vp, _vp, _vp, ctypes.c_int]
+        L.hhuff_encode_batch_host.restype = ctypes.c_int
+        L.hhuff_encode_batch_host.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint64,
+                                              _vp, _vp, _vp, ctypes.c_int]
+        L.hhuff_version.restype = ctypes.c_char_p
+        L.hhuff_last_error_string.restype = ctypes.c_char_p
+        L.hhuff_grid_size.restype = ctypes.c_int
+        L.hhuff_grid_size.argtypes = [ctypes.c_int, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+# symbols include/hhuff.h declares (checked by tests/test_capi_symbols.py)
+EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decode_batch", "hhuff_encode_batch",
+            "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_version", "hhuff_last_error_string",
+            "hhuff_grid_size")
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise HhuffError("%s failed (%d): %s" % (what, rc, lib().hhuff_last_error_string().decode()))
+
+
+# ---------------------------------------------------------------------------------------------------
+# per-string (h2o signatures)
+# ---------------------------------------------------------------------------------------------------
+def decode_huffman(src: bytes, is_name: bool = False, soft_errors: int = 0):
+    """h2o_hpack_decode_huffman: -> (decoded bytes or None for SIZE_MAX, soft_errors word)."""
+    buf = ctypes.create_string_buffer(max(1, 2 * len(src)))
+    soft = ctypes.c_uint(soft_errors)
+    err = ctypes.c_char_p()
+    r = lib().h2o_hpack_decode_huffman(buf, ctypes.byref(soft), src, len(src), int(bool(is_name)), ctypes.byref(err))
+    if r == SIZE_MAX:
+        return None, soft.value
+    return buf.raw[:r], soft.value
+
+
+def encode_huffman(src: bytes):
+    """h2o_hpack_encode_huffman: -> Huffman bytes, or None when not shorter than the input (SIZE_MAX)."""
+    buf = ctypes.create_string_buffer(max(1, len(src)))
+    r = lib().h2o_hpack_encode_huffman(buf, src, len(src))
+    if r == SIZE_MAX:
+        return None
+    return buf.raw[:r]
+
+
+# ---------------------------------------------------------------------------------------------------
+# device batch API (torch tensors; uint32 arrays are carried in int32 tensors, same bits)
+# ---------------------------------------------------------------------------------------------------
+def _dp(t):
+    if t is None:
+        return None
+    assert t.is_cuda and t.is_contiguous(), "device batch arrays must be contiguous device tensors"
+    return t.data_ptr()
+
+
+def _stream(stream):
+    import torch
+
+    s = torch.cuda.current_stream() if stream is None else stream
+    return s.cuda_stream
+
+
+def decode_slot_size(in_size: int) -> int:
+    """bytes the implicit decode layout (out_off = floor(8 * in_off / 5)) needs"""
+    return (in_size * 8) // 5 + 16
+
+
+def decode_batch(data, in_off, n, in_len=None, is_name_bits=None, out=None, out_off=None, out_len=None, status=None,
+                 in_size=None, stream=None):
+    """Batched h2o_hpack_decode_huffman on device tensors; returns (out, out_len, status)."""
+    import torch
+
+    dev = data.device
+    in_size = data.numel() if in_size is None else in_size
+    if out is None:
+        out = torch.empty(decode_slot_size(in_size) if out_off is None else in_size * 2 + 16, dtype=torch.uint8,
+                          device=dev)
+    if out_len is None:
+        out_len = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    _check(lib().hhuff_decode_batch(_dp(data), in_size, _dp(in_off), _dp(in_len), n, _dp(is_name_bits), _dp(out),
+                                    _dp(out_off), _dp(out_len), _dp(status), _stream(stream)), "hhuff_decode_batch")
+    return out, out_len, status
+
+
+def encode_batch(data, in_off, n, in_len=None, out=None, out_off=None, out_len=None, status=None, in_size=None,
+                 stream=None):
+    """Batched h2o_hpack_encode_huffman on device tensors; returns (out, out_len, status)."""
+    import torch
+
+    dev = data.device
+    in_size = data.numel() if in_size is None else in_size
+    if out is None:
+        out = torch.empty(in_size + 16, dtype=torch.uint8, device=dev)
+    if out_len is None:
+        out_len = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    _check(lib().hhuff_encode_batch(_dp(data), in_size, _dp(in_off), _dp(in_len), n, _dp(out), _dp(out_off),
+                                    _dp(out_len), _dp(status), _stream(stream)), "hhuff_encode_batch")
+    return out, out_len, status
+
+
+# ---------------------------------------------------------------------------------------------------
+# host batch API (numpy arrays; H2D/D2H inside the library)
+# ---------------------------------------------------------------------------------------------------
+def _hp(a):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
+
+
+def decode_batch_host(data, in_off, n, in_len=None, is_name_bits=None, out_off=None, out_size=None, device=0):
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if out_size is None:
+        out_size = decode_slot_size(data.size)
+    out = np.zeros(max(1, out_size), np.uint8)
+    out_len = np.zeros(max(1, n), np.uint32)
+    status = np.zeros(max(1, n), np.uint8)
+    _check(lib().hhuff_decode_batch_host(_hp(data), data.size, _hp(in_off), _hp(in_len), n, _hp(is_name_bits), _hp(out),
+                                         out.size, _hp(out_off), _hp(out_len), _hp(status), device),
+           "hhuff_decode_batch_host")
+    return out, out_len[:n], status[:n]
+
+
+def encode_batch_host(data, in_off, n, in_len=None, out_off=None, out_size=None, device=0):
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if out_size is None:
+        out_size = data.size + 16
+    out = np.zeros(max(1, out_size), np.uint8)
+    out_len = np.zeros(max(1, n), np.uint32)
+    status = np.zeros(max(1, n), np.uint8)
+    _check(lib().hhuff_encode_batch_host(_hp(data), data.size, _hp(in_off), _hp(in_len), n, _hp(out), out.size,
+                                         _hp(out_off), _hp(out_len), _hp(status), device), "hhuff_encode_batch_host")
+    return out, out_len[:n], status[:n]

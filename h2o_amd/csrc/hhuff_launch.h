@@ -1,0 +1,13 @@
+// Internal launch interface between the C-ABI shim (hhuff_capi.hip) and the kernels (hhuff_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace hhuff {
+hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
+                         const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
+                         uint8_t* status, hipStream_t stream);
+hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
+                         uint8_t* out, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, hipStream_t stream);
+int grid_size(int device, int which);
+}  // namespace hhuff

@@ -1,0 +1,109 @@
+/*
+ * hhuff -- MI355X-native HPACK/QPACK Huffman codec: the drop-in C-ABI boundary.
+ *
+ * Library: h2o_amd/libhhuff.so (HIP kernels for gfx950 + host shim).  Plain C types only: no HIP,
+ * torch or C++ types appear in these signatures; streams are passed as `void *` (a hipStream_t, or
+ * NULL for the legacy default stream).
+ *
+ * 1. Per-string symbols with h2o's exact signatures and semantics.  A maintainer links libhhuff in
+ *    place of the definitions in lib/http2/hpack.c.  Each call runs the HIP
+ *    kernels on a batch of one string, synchronously, on a per-thread stream of the current device.
+ *    Launch latency (~10-20 us) makes this the compatibility path; throughput comes from the batch API.
+ * 2. Batch entry points on device-resident arrays (the hot path) and on host arrays (pinned staging,
+ *    H2D/D2H included).  Element i of a batch has exactly the per-string semantics of (1).
+ *
+ * Batch array contract (all offsets/lengths u32; a batch addresses < 4 GiB of input):
+ *   string i      in[in_off[i] .. in_off[i] + len_i)
+ *                 len_i = in_len ? in_len[i] : in_off[i+1] - in_off[i]   (in_off has n+1 entries then)
+ *   in_size       bytes readable at `in` (the kernels never read past it)
+ *   is_name_bits  u32[(n+31)/32]; bit (i & 31) of word (i >> 5) set => string i is a header name
+ *                 (NULL => every string is a header value)
+ *   device `in` must be 16-byte aligned and `out` 4-byte aligned (hipMalloc / torch allocations are);
+ *   strings may start at any byte.
+ *   Per-string length limit: 2^29 - 1 bytes (status HHUFF_STATUS_TOO_LONG above it).
+ */
+#ifndef HHUFF_H
+#define HHUFF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HHUFF_FAIL_LEN 0xFFFFFFFFu   /* out_len of a string whose per-string call returns SIZE_MAX */
+#define HHUFF_SOFT_NAME 0x01u        /* H2O_HPACK_SOFT_ERROR_BIT_INVALID_NAME  (include/h2o/hpack.h:50) */
+#define HHUFF_SOFT_VALUE 0x02u       /* H2O_HPACK_SOFT_ERROR_BIT_INVALID_VALUE (include/h2o/hpack.h:51) */
+#define HHUFF_STATUS_FAIL 0x80u      /* hard failure: the per-string call returns SIZE_MAX */
+#define HHUFF_STATUS_TOO_LONG 0xC0u  /* string longer than the per-string limit (never produced by h2o) */
+
+#define HHUFF_OK 0
+#define HHUFF_EINVAL (-1) /* bad argument (NULL array, misaligned base, n too large) */
+#define HHUFF_EHIP (-2)   /* a HIP runtime call failed; see hhuff_last_error_string() */
+#define HHUFF_ENODEV (-3) /* no gfx950 device / code object not loadable */
+
+/* ---------------------------------------------------------------------------------------------
+ * (1) h2o per-string symbols
+ * ------------------------------------------------------------------------------------------- */
+
+/* Replaces lib/http2/hpack.c:117 (declared include/h2o/hpack.h:69-70).
+ * Returns the decoded length, or SIZE_MAX on a hard error (EOS symbol, padding longer than 7 bits or not
+ * all ones).  On success ORs HHUFF_SOFT_NAME / HHUFF_SOFT_VALUE into *soft_errors (never clears it).
+ * `dst` must hold at least 2 * len bytes (h2o's contract; floor(8 * len / 5) suffices).  *err_desc is
+ * never written (the reference's upper-case hard error at hpack.c:142-144 is unreachable). */
+size_t h2o_hpack_decode_huffman(char *dst, unsigned *soft_errors, const uint8_t *src, size_t len, int is_name,
+                                const char **err_desc);
+
+/* Replaces lib/http2/hpack.c:774 (declared include/h2o/hpack.h:60).
+ * Returns the Huffman length when it is strictly shorter than `len`, else SIZE_MAX (also for len == 0).
+ * `dst` must hold `len` bytes; its contents are unspecified on SIZE_MAX. */
+size_t h2o_hpack_encode_huffman(uint8_t *dst, const uint8_t *src, size_t len);
+
+/* ---------------------------------------------------------------------------------------------
+ * (2) batch API, device-resident arrays (hot path).  Asynchronous on `stream`.
+ * ------------------------------------------------------------------------------------------- */
+
+/* Batched h2o_hpack_decode_huffman (hpack.c:117-156; callers hpack.c:241, qpack.c:228/370/579).
+ *   out       decoded string i at out + (out_off ? out_off[i] : floor(8 * in_off[i] / 5)); the region
+ *             must hold floor(8 * len_i / 5) bytes (the implicit layout is valid whenever the input
+ *             strings do not overlap).  Bytes of the region past out_len[i] are unspecified.
+ *   out_len   u32[n]: decoded length, or HHUFF_FAIL_LEN
+ *   status    u8[n]:  soft-error bits on success, HHUFF_STATUS_FAIL on a hard error */
+int hhuff_decode_batch(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, const uint32_t *in_len, uint32_t n,
+                       const uint32_t *is_name_bits, uint8_t *out, const uint32_t *out_off, uint32_t *out_len,
+                       uint8_t *status, void *stream);
+
+/* Batched h2o_hpack_encode_huffman (hpack.c:774-804; callers hpack.c:820, qpack.c:1046).
+ *   out       Huffman string i at out + (out_off ? out_off[i] : in_off[i]); the region must hold len_i
+ *             bytes.  Contents unspecified where out_len[i] == HHUFF_FAIL_LEN.
+ *   out_len   u32[n]: Huffman length (< len_i), or HHUFF_FAIL_LEN when not shorter (SIZE_MAX)
+ *   status    u8[n] or NULL: 0, or HHUFF_STATUS_FAIL */
+int hhuff_encode_batch(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, const uint32_t *in_len, uint32_t n,
+                       uint8_t *out, const uint32_t *out_off, uint32_t *out_len, uint8_t *status, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * (3) batch API, host arrays: pinned staging + H2D, kernels, D2H on an internal stream of `device`.
+ *     Synchronous.  Same array contract; `out` is a host buffer sized for the implicit layout
+ *     (decode: floor(8 * in_size / 5) bytes, encode: in_size bytes) when out_off is NULL.
+ * ------------------------------------------------------------------------------------------- */
+int hhuff_decode_batch_host(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, const uint32_t *in_len,
+                            uint32_t n, const uint32_t *is_name_bits, uint8_t *out, uint64_t out_size,
+                            const uint32_t *out_off, uint32_t *out_len, uint8_t *status, int device);
+int hhuff_encode_batch_host(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, const uint32_t *in_len,
+                            uint32_t n, uint8_t *out, uint64_t out_size, const uint32_t *out_off, uint32_t *out_len,
+                            uint8_t *status, int device);
+
+/* ---------------------------------------------------------------------------------------------
+ * (4) library info
+ * ------------------------------------------------------------------------------------------- */
+const char *hhuff_version(void);
+/* Text of the last HIP error seen by this thread ("" if none). */
+const char *hhuff_last_error_string(void);
+/* Number of workgroups the decode / encode launches use on `device` (grid sizing, for profiling). */
+int hhuff_grid_size(int device, int which /* 0 decode, 1 encode */);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

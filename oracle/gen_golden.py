@@ -1,0 +1,340 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/* with the REAL reference codec -- test infrastructure only.
+
+Runs here, in the build container, where oracle/_ref/libh2oref.so is compiled from
+/root/reference/lib/http2/hpack.c and lib/http3/qpack.c (oracle/Makefile).  The fixtures it writes are
+data (inputs + the reference's outputs) and travel to the GPU box; the reference does not.
+
+Fixture sets (numpy .npz, arrays only, no pickles):
+  kat.npz          known answers from the reference's own tests (t/00unit/lib/http2/hpack.c:175-186,
+                   :293-306, :474-513, :666-682; t/00unit/lib/http3/qpack.c:236) and SURVEY Appendix A
+  corpus.npz       every Huffman-flagged literal string in fuzz/http2-corpus (HEADERS + CONTINUATION
+                   blocks, our own HPACK walker), decoded by the reference; raw literals encoded by it
+  random_<cfg>.npz seeded synthetic batches per benchmark configuration (h2o_amd/synth.py), encoded and
+                   re-decoded by the reference, plus the plain bytes decoded as (mostly invalid) Huffman
+  adversarial.npz  hand-built decode edge cases (padding, EOS, truncation, long codes, names/values)
+  framing.npz      HPACK h2o_hpack_encode_string and QPACK flatten_string (prefix 3/5/7) outputs
+
+Usage:  python3 oracle/gen_golden.py            (rewrites tests/golden/)
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path[0] = ROOT  # import `oracle` as the package, not this directory
+
+from h2o_amd import synth  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+REF_ROOT = "/root/reference"
+PREFACE = b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n"
+
+
+def pack(strings):
+    return synth.pack(list(strings))
+
+
+# ------------------------------------------------------------------------------------------------
+# reference runs
+# ------------------------------------------------------------------------------------------------
+def ref_decode_set(strings, is_name):
+    """-> dict of arrays: inputs + reference verdicts (soft bits from a zero word and from 0x2/0x1 preset)."""
+    r = O.ref()
+    out_len, status, decoded = [], [], []
+    soft_preset = []
+    for s, nm in zip(strings, is_name):
+        d, soft = r.decode(s, bool(nm))
+        _, soft_p = r.decode(s, bool(nm), soft_in=0x2 if nm else 0x1)
+        soft_preset.append(soft_p)
+        if d is None:
+            out_len.append(O.FAIL)
+            status.append(O.STATUS_FAIL)
+        else:
+            out_len.append(len(d))
+            status.append(soft)
+            decoded.append(d)
+    data, off = pack(strings)
+    dec_data, dec_off = pack(decoded)
+    return dict(dec_in=data, dec_in_off=off, is_name_bits=synth.bits_from_bools(is_name),
+                dec_len=np.asarray(out_len, np.uint32), dec_status=np.asarray(status, np.uint8),
+                dec_soft_preset=np.asarray(soft_preset, np.uint8), dec_out=dec_data, dec_out_off=dec_off)
+
+
+def ref_encode_set(strings):
+    r = O.ref()
+    out_len, encoded = [], []
+    for s in strings:
+        e = r.encode(s)
+        if e is None:
+            out_len.append(O.FAIL)
+        else:
+            out_len.append(len(e))
+            encoded.append(e)
+    data, off = pack(strings)
+    ed, eo = pack(encoded)
+    return dict(enc_in=data, enc_in_off=off, enc_len=np.asarray(out_len, np.uint32), enc_out=ed, enc_out_off=eo)
+
+
+# ------------------------------------------------------------------------------------------------
+# fuzz corpus walker (HTTP/2 frames -> HPACK header blocks -> string literals)
+# ------------------------------------------------------------------------------------------------
+def _int(buf, p, prefix):
+    """RFC 7541 5.1 prefix integer -> (value, new position) or (None, None)."""
+    if p >= len(buf):
+        return None, None
+    mx = (1 << prefix) - 1
+    v = buf[p] & mx
+    p += 1
+    if v < mx:
+        return v, p
+    shift = 0
+    while p < len(buf) and shift <= 56:
+        b = buf[p]
+        p += 1
+        v += (b & 127) << shift
+        if not b & 128:
+            return v, p
+        shift += 7
+    return None, None
+
+
+def header_blocks(raw):
+    b = raw[len(PREFACE):] if raw.startswith(PREFACE) else raw
+    pos, blocks, cur = 0, [], None
+    while pos + 9 <= len(b):
+        L = int.from_bytes(b[pos:pos + 3], "big")
+        typ, flags = b[pos + 3], b[pos + 4]
+        pos += 9
+        payload = b[pos:pos + L]
+        pos += L
+        if len(payload) < L:
+            break
+        if typ == 1:
+            p = payload
+            if flags & 0x8:
+                if not p or p[0] >= len(p):
+                    continue
+                p = p[1:len(p) - p[0]]
+            if flags & 0x20:
+                p = p[5:]
+            cur = bytearray(p)
+            if flags & 0x4:
+                blocks.append(bytes(cur))
+                cur = None
+        elif typ == 9 and cur is not None:
+            cur += payload
+            if flags & 0x4:
+                blocks.append(bytes(cur))
+                cur = None
+    if cur:
+        blocks.append(bytes(cur))
+    return blocks
+
+
+def block_strings(block):
+    """-> list of (is_name, huffman_flag, bytes) for every string literal of an HPACK block"""
+    out, p = [], 0
+
+    def string(p):
+        if p >= len(block):
+            return None, None, None
+        h = bool(block[p] & 0x80)
+        n, p = _int(block, p, 7)
+        if n is None or p + n > len(block):
+            return None, None, None
+        return h, block[p:p + n], p + n
+
+    while p < len(block):
+        c = block[p]
+        if c & 0x80:
+            _, p = _int(block, p, 7)
+            if p is None:
+                break
+            continue
+        if c & 0x40:
+            idx, p = _int(block, p, 6)
+        elif c & 0x20:
+            _, p = _int(block, p, 5)
+            if p is None:
+                break
+            continue
+        else:
+            idx, p = _int(block, p, 4)
+        if p is None:
+            break
+        if idx == 0:
+            h, s, p = string(p)
+            if p is None:
+                break
+            out.append((True, h, s))
+        h, s, p = string(p)
+        if p is None:
+            break
+        out.append((False, h, s))
+    return out
+
+
+def corpus_strings():
+    d = os.path.join(REF_ROOT, "fuzz", "http2-corpus")
+    huff, raw = [], []
+    for f in sorted(os.listdir(d)):
+        with open(os.path.join(d, f), "rb") as fh:
+            data = fh.read()
+        for blk in header_blocks(data):
+            for is_name, h, s in block_strings(blk):
+                (huff if h else raw).append((is_name, bytes(s)))
+    return huff, raw
+
+
+# ------------------------------------------------------------------------------------------------
+# fixture sets
+# ------------------------------------------------------------------------------------------------
+def huff_bits(s):
+    """Huffman bytes of `s` by direct bit packing (valid even when not shorter than `s`)."""
+    bits = "".join(format(synth.tables.ENC_CODE[c], "0%db" % synth.tables.ENC_NBITS[c]) for c in s)
+    bits += "1" * (-len(bits) % 8)
+    return int(bits, 2).to_bytes(len(bits) // 8, "big") if bits else b""
+
+
+def kat_set():
+    enc = huff_bits
+    dec_cases = [
+        (bytes.fromhex("f1e3c2e5f23a6ba0ab90f4ff"), 0),  # hpack test :175-186 -> www.example.com
+        (bytes.fromhex("a8eb10649cbf"), 0),  # RFC 7541 C.4.2 "no-cache"
+        (bytes.fromhex("25a849e95ba97d7f"), 1),  # C.4.3 "custom-key"
+        (bytes.fromhex("25a849e95bb8e8b4bf"), 0),  # C.4.3 "custom-value"
+        (bytes.fromhex("f2b543a4bf"), 1),  # hpack test :474-488 "x-name"
+        (bytes.fromhex("49509f"), 0),  # hpack test :505-513 "test"
+        (bytes.fromhex("5071ff"), 0),  # :666-682 " ab" (soft: leading SP)
+        (bytes.fromhex("ffffea1c7f"), 0),  # "\tab" (soft: leading HT)
+        (bytes.fromhex("1c6a7f"), 0),  # "ab " (soft: trailing SP)
+        (b"", 0), (b"", 1),  # empty value ok / empty name soft
+        (b"\xff", 0), (b"\x1f", 0), (b"\x1e", 0), (b"\x07\xff", 0), (b"\xff\xff\xff\xff", 0),
+        (enc(b"Aeeeeeee"), 1), (enc(b":Aeeeeeee"), 1), (enc(b":Path"), 1), (enc(b"Content-Type"), 1),
+        (enc(b"ae eeeee"), 1), (enc(b"ae eeeee"), 0), (enc(b"aeeeeeee\n"), 0), (enc(b"aeeeeeee\x7f"), 0),
+        (enc(b"\taeeeeeee"), 0), (enc(b"aeeeeeee\t"), 0), (enc(b"aeeeeeee\x80"), 0), (enc(b"aeeeeeee\x80"), 1),
+    ]
+    d = ref_encode_set([b"www.example.com", b"", b"a", b"aa", b"A", b"\x00", b"aaa", b"ABCDEFGH", b"00000000",
+                        b"no-cache", b"custom-key", b"custom-value", b"x-name", b"test", b" ab",
+                        b"private", b"Mon, 21 Oct 2013 20:13:21 GMT", b"https://www.example.com"]
+                       + [b"X" * k for k in range(1, 9)])
+    d.update(ref_decode_set([s for s, _ in dec_cases], [n for _, n in dec_cases]))
+    return d
+
+
+def random_set(cfg, n, seed):
+    b = synth.make_batch(cfg, n=n, seed=seed, adversarial_frac=0.05)
+    plain = synth.unpack(b["data"], b["off"])
+    d = ref_encode_set(plain)
+    # decode inputs: every successful encoding (wire-like), then the plain bytes read as Huffman
+    names = np.unpackbits(b["is_name_bits"].view(np.uint8), bitorder="little")[:n].astype(bool)
+    encs = [r for r in synth.unpack(d["enc_out"], d["enc_out_off"])]
+    enc_names = [nm for nm, L in zip(names, d["enc_len"]) if L != O.FAIL]
+    dec_in = encs + plain
+    dec_names = list(enc_names) + list(names)
+    d.update(ref_decode_set(dec_in, dec_names))
+    d["seed"] = np.asarray([seed], np.int64)
+    return d
+
+
+def adversarial_set(seed=7):
+    rng = np.random.default_rng(seed)
+    r = O.ref()
+    cases = []
+    # random byte strings
+    for _ in range(3000):
+        L = int(rng.integers(0, 48))
+        cases.append(bytes(rng.integers(0, 256, L, dtype=np.uint8)))
+    # valid encodings of varied plain strings, then mutated
+    syms, p = synth.header_alphabet()
+    for _ in range(1500):
+        L = int(rng.integers(1, 40))
+        s = bytes(rng.choice(syms, L, p=p)) if rng.random() < 0.7 else bytes(rng.integers(0, 256, L, dtype=np.uint8))
+        e = r.encode(s)
+        if e is None:
+            continue
+        cases.append(e)
+        cases.append(e + b"\xff")  # padding > 7 bits
+        cases.append(e[:-1])  # truncated
+        b = bytearray(e)
+        b[-1] ^= 1  # padding bit flipped
+        cases.append(bytes(b))
+        b = bytearray(e)
+        b[int(rng.integers(0, len(b)))] ^= 1 << int(rng.integers(0, 8))  # random bit flip
+        cases.append(bytes(b))
+        k = int(rng.integers(0, len(e)))
+        cases.append(e[:k] + b"\xff\xff\xff\xff" + e[k:])  # EOS-containing run of ones
+    # strings of long codes only (control bytes, high bytes)
+    for _ in range(300):
+        L = int(rng.integers(1, 20))
+        s = bytes(rng.choice(np.r_[0:32, 127:256], L).astype(np.uint8))
+        cases.append(huff_bits(s))
+    # EOS exactly at the end / after a symbol, with 0-7 bits of padding around it
+    for pre in range(0, 8):
+        bits = "0" * 5 * pre + "1" * 30
+        bits += "1" * (-len(bits) % 8)
+        cases.append(int(bits, 2).to_bytes(len(bits) // 8, "big"))
+    is_name = rng.random(len(cases)) < 0.5
+    return ref_decode_set(cases, is_name)
+
+
+def framing_set(seed=11):
+    rng = np.random.default_rng(seed)
+    r = O.ref()
+    strings = [b"", b"a", b"www.example.com", b"X" * 200, bytes(range(256))]
+    syms, p = synth.header_alphabet()
+    for _ in range(300):
+        L = int(rng.choice([rng.integers(0, 30), rng.integers(100, 200), rng.integers(256, 768), rng.integers(1000, 3000)]))
+        if rng.random() < 0.5:
+            s = bytes(rng.choice(synth.COOKIE_CHARSET, L))
+        else:
+            s = bytes(rng.choice(syms, L, p=p))
+        strings.append(s)
+    prefix = rng.choice([3, 5, 7], len(strings)).astype(np.uint8)
+    first = rng.integers(0, 256, len(strings), dtype=np.uint8)
+    raw = rng.random(len(strings)) < 0.1
+    hpack_out = [r.encode_string(s) for s in strings]
+    qpack_out = [r.flatten_string(s, int(pb), int(fb), bool(rw)) for s, pb, fb, rw in zip(strings, prefix, first, raw)]
+    data, off = pack(strings)
+    hd, ho = pack(hpack_out)
+    qd, qo = pack(qpack_out)
+    # prefix-integer known answers (hpack.c:52-83 / :757-772)
+    ints = [0, 1, 2, 30, 31, 32, 62, 63, 64, 126, 127, 128, 254, 255, 256, 1337, 4096, 16383, 16384, 2 ** 21,
+            2 ** 28 - 1, 2 ** 31, 2 ** 40 + 5, 2 ** 62, 2 ** 63 - 1]
+    int_out = []
+    for pb in (3, 4, 5, 6, 7):
+        for v in ints:
+            int_out.append(r.encode_int(v, pb))
+    iod, ioo = pack(int_out)
+    return dict(fr_in=data, fr_in_off=off, fr_prefix=prefix, fr_first=first, fr_raw=raw.astype(np.uint8),
+                hpack_out=hd, hpack_out_off=ho, qpack_out=qd, qpack_out_off=qo,
+                int_values=np.asarray(ints, np.uint64), int_out=iod, int_out_off=ioo)
+
+
+def main():
+    if not O.ref_available():
+        sys.exit("oracle/_ref/libh2oref.so missing: run `make -C oracle` where /root/reference exists")
+    os.makedirs(GOLDEN, exist_ok=True)
+    sets = {"kat": kat_set()}
+    huff, raw = corpus_strings()
+    c = ref_decode_set([s for _, s in huff], [nm for nm, _ in huff])
+    c.update(ref_encode_set([s for _, s in raw]))
+    sets["corpus"] = c
+    for cfg, n, seed in (("c2", 3000, 101), ("c3", 1200, 102), ("c4", 3000, 103), ("c5", 300, 104)):
+        sets["random_" + cfg] = random_set(cfg, n, seed)
+    sets["adversarial"] = adversarial_set()
+    sets["framing"] = framing_set()
+    for name, arrays in sets.items():
+        path = os.path.join(GOLDEN, name + ".npz")
+        np.savez_compressed(path, **arrays)
+        nd = len(arrays.get("dec_len", []))
+        ne = len(arrays.get("enc_len", []))
+        print("%-16s decode %6d  encode %6d  %8d bytes" % (name, nd, ne, os.path.getsize(path)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+"""ORACLE ctypes bindings -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+It binds oracle/liboracle.so (the clean-room CPU restatement, huff_oracle.c) and, when it was built in
+the container that has /root/reference, oracle/_ref/libh2oref.so (the real reference codec).
+
+Batch helpers take numpy arrays in the include/hhuff.h layout and return numpy arrays.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FAIL = 0xFFFFFFFF
+STATUS_FAIL = 0x80
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+def build():
+    """Compile liboracle.so (and _ref when /root/reference is present)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def _ptr(a, t):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(t)
+
+
+class _Codec:
+    def __init__(self, path, prefix):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path + " not built (run make -C oracle)")
+        self.lib = ctypes.CDLL(path)
+        self.prefix = prefix
+        L = self.lib
+        P = prefix
+        self._dec = getattr(L, P + "_decode_huffman")
+        self._dec.restype = ctypes.c_size_t
+        self._dec.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint), ctypes.c_char_p, ctypes.c_size_t,
+                              ctypes.c_int]
+        self._enc = getattr(L, P + "_encode_huffman")
+        self._enc.restype = ctypes.c_size_t
+        self._enc.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+        self._encstr = getattr(L, P + "_encode_string")
+        self._encstr.restype = ctypes.c_size_t
+        self._encstr.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+        self._flat = getattr(L, P + "_flatten_string")
+        self._flat.restype = ctypes.c_size_t
+        self._flat.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_int]
+        self._encint = getattr(L, P + "_encode_int")
+        self._encint.restype = ctypes.c_void_p
+        self._encint.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint]
+        self._decint = getattr(L, P + "_decode_int")
+        self._decint.restype = ctypes.c_int64
+        self._decint.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+        for name, extra in (("decode_batch", [_u32p, _u8p, _u32p, _u32p, _u8p, ctypes.c_int]),
+                            ("encode_batch", [_u8p, _u32p, _u32p, _u8p, ctypes.c_int]),
+                            ("flatten_batch", [_u8p, ctypes.c_uint, _u32p, _u8p, _u32p, _u32p, ctypes.c_int])):
+            f = getattr(L, P + "_" + name)
+            f.restype = ctypes.c_int
+            f.argtypes = [_u8p, _u32p, _u32p, ctypes.c_uint32] + extra
+
+    # ---- per-string (h2o signatures) ----
+    def decode(self, src: bytes, is_name: bool = False, soft_in: int = 0):
+        """-> (bytes or None on SIZE_MAX, soft_errors word)"""
+        buf = ctypes.create_string_buffer(max(1, 2 * len(src)))
+        soft = ctypes.c_uint(soft_in)
+        r = self._dec(buf, ctypes.byref(soft), src, len(src), int(is_name))
+        if r == ctypes.c_size_t(-1).value:
+            return None, soft.value
+        return buf.raw[:r], soft.value
+
+    def encode(self, src: bytes):
+        """-> bytes or None on SIZE_MAX"""
+        buf = ctypes.create_string_buffer(max(1, len(src)))
+        r = self._enc(buf, src, len(src))
+        if r == ctypes.c_size_t(-1).value:
+            return None
+        return buf.raw[:r]
+
+    def encode_string(self, src: bytes) -> bytes:
+        buf = ctypes.create_string_buffer(len(src) + 11)
+        r = self._encstr(buf, src, len(src))
+        return buf.raw[:r]
+
+    def flatten_string(self, src: bytes, prefix_bits: int, first: int = 0, raw: bool = False) -> bytes:
+        buf = ctypes.create_string_buffer(len(src) + 11)
+        buf[0] = first
+        r = self._flat(buf, src, len(src), prefix_bits, int(raw))
+        return buf.raw[:r]
+
+    def encode_int(self, value: int, prefix_bits: int, first: int = 0) -> bytes:
+        buf = ctypes.create_string_buffer(16)
+        buf[0] = first
+        end = self._encint(ctypes.addressof(buf), value, prefix_bits)
+        return buf.raw[:end - ctypes.addressof(buf)]
+
+    def decode_int(self, data: bytes, prefix_bits: int):
+        """-> (value or negative error, bytes consumed)"""
+        buf = ctypes.create_string_buffer(data, max(1, len(data)))
+        p = ctypes.c_void_p(ctypes.addressof(buf))
+        v = self._decint(ctypes.byref(p), ctypes.addressof(buf) + len(data), prefix_bits)
+        return v, p.value - ctypes.addressof(buf)
+
+    # ---- batch (include/hhuff.h layout) ----
+    def decode_batch(self, data, in_off, n, in_len=None, is_name_bits=None, out_off=None, out_size=None, nthreads=1):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        if out_size is None:
+            end = int(in_off[n]) if in_len is None else int((in_off[:n].astype(np.uint64) + in_len).max(initial=0))
+            out_size = (end * 8) // 5 + 16
+        out = np.zeros(max(1, out_size), np.uint8)
+        out_len = np.zeros(n, np.uint32)
+        status = np.zeros(n, np.uint8)
+        rc = getattr(self.lib, self.prefix + "_decode_batch")(
+            _ptr(data, _u8p), _ptr(in_off, _u32p), _ptr(in_len, _u32p), n, _ptr(is_name_bits, _u32p),
+            _ptr(out, _u8p), _ptr(out_off, _u32p), _ptr(out_len, _u32p), _ptr(status, _u8p), nthreads)
+        assert rc == 0
+        return out, out_len, status
+
+    def encode_batch(self, data, in_off, n, in_len=None, out_off=None, out_size=None, nthreads=1):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        if out_size is None:
+            out_size = data.size + 16
+        out = np.zeros(max(1, out_size), np.uint8)
+        out_len = np.zeros(n, np.uint32)
+        status = np.zeros(n, np.uint8)
+        rc = getattr(self.lib, self.prefix + "_encode_batch")(
+            _ptr(data, _u8p), _ptr(in_off, _u32p), _ptr(in_len, _u32p), n, _ptr(out, _u8p), _ptr(out_off, _u32p),
+            _ptr(out_len, _u32p), _ptr(status, _u8p), nthreads)
+        assert rc == 0
+        return out, out_len, status
+
+    def flatten_batch(self, data, in_off, n, prefix_bits, in_len=None, first_bytes=None, raw_bits=None,
+                      out_off=None, out_size=None, nthreads=1):
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        if out_size is None:
+            out_size = data.size + 11 * n + 16
+        out = np.zeros(max(1, out_size), np.uint8)
+        out_len = np.zeros(n, np.uint32)
+        rc = getattr(self.lib, self.prefix + "_flatten_batch")(
+            _ptr(data, _u8p), _ptr(in_off, _u32p), _ptr(in_len, _u32p), n, _ptr(first_bytes, _u8p), prefix_bits,
+            _ptr(raw_bits, _u32p), _ptr(out, _u8p), _ptr(out_off, _u32p), _ptr(out_len, _u32p), nthreads)
+        assert rc == 0
+        return out, out_len
+
+
+_oracle = None
+_ref = None
+
+
+def oracle() -> _Codec:
+    """The clean-room restatement (liboracle.so)."""
+    global _oracle
+    if _oracle is None:
+        _oracle = _Codec(os.path.join(HERE, "liboracle.so"), "orc")
+    return _oracle
+
+
+def ref_available() -> bool:
+    return os.path.exists(os.path.join(HERE, "_ref", "libh2oref.so"))
+
+
+def ref() -> _Codec:
+    """The real reference codec (only in the build container)."""
+    global _ref
+    if _ref is None:
+        _ref = _Codec(os.path.join(HERE, "_ref", "libh2oref.so"), "ref")
+    return _ref

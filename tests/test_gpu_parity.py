@@ -1,0 +1,246 @@
+"""HIP path parity: the kernels (through the C-ABI) against the reference's golden vectors and the
+CPU restatement on seeded inputs; size-independent properties at full benchmark sizes."""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_SETS, compact, load_golden
+from h2o_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+FAIL = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    from h2o_amd import build
+
+    build.build(verbose=False)
+    return torch
+
+
+def _dev(torch, a):
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    if a.size == 0:
+        a = np.zeros(1, a.dtype)
+    return torch.from_numpy(a.copy()).cuda()
+
+
+def _host(t, dtype):
+    return t.cpu().numpy().view(dtype)
+
+
+def gpu_decode(torch, data, off, n, in_len=None, is_name_bits=None, out_off=None, out_size=None):
+    from h2o_amd import codec
+
+    d = _dev(torch, data)
+    in_size = int(np.asarray(data).size)
+    out = None
+    if out_size is not None:
+        out = torch.zeros(out_size, dtype=torch.uint8, device="cuda")
+    o, ol, st = codec.decode_batch(d, _dev(torch, off), n, in_len=None if in_len is None else _dev(torch, in_len),
+                                   is_name_bits=None if is_name_bits is None else _dev(torch, is_name_bits),
+                                   out=out, out_off=None if out_off is None else _dev(torch, out_off), in_size=in_size)
+    torch.cuda.synchronize()
+    return _host(o, np.uint8), _host(ol, np.uint32)[:n], _host(st, np.uint8)[:n]
+
+
+def gpu_encode(torch, data, off, n, in_len=None, out_off=None, out_size=None):
+    from h2o_amd import codec
+
+    d = _dev(torch, data)
+    in_size = int(np.asarray(data).size)
+    out = None
+    if out_size is not None:
+        out = torch.zeros(out_size, dtype=torch.uint8, device="cuda")
+    o, ol, st = codec.encode_batch(d, _dev(torch, off), n, in_len=None if in_len is None else _dev(torch, in_len),
+                                   out=out, out_off=None if out_off is None else _dev(torch, out_off), in_size=in_size)
+    torch.cuda.synchronize()
+    return _host(o, np.uint8), _host(ol, np.uint32)[:n], _host(st, np.uint8)[:n]
+
+
+# ------------------------------------------------------------------------------------------------
+# golden vectors from the reference
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+def test_decode_golden(torch_cuda, name):
+    g = load_golden(name)
+    if "dec_len" not in g:
+        pytest.skip("no decode vectors")
+    n = len(g["dec_len"])
+    out, out_len, status = gpu_decode(torch_cuda, g["dec_in"], g["dec_in_off"], n, is_name_bits=g["is_name_bits"])
+    np.testing.assert_array_equal(out_len, g["dec_len"])
+    np.testing.assert_array_equal(status, g["dec_status"])
+    slots = (g["dec_in_off"][:n].astype(np.uint64) * 8) // 5
+    assert compact(out, slots, out_len) == g["dec_out"].tobytes()
+
+
+@pytest.mark.parametrize("name", GOLDEN_SETS)
+def test_encode_golden(torch_cuda, name):
+    g = load_golden(name)
+    if "enc_len" not in g:
+        pytest.skip("no encode vectors")
+    n = len(g["enc_len"])
+    out, out_len, status = gpu_encode(torch_cuda, g["enc_in"], g["enc_in_off"], n)
+    np.testing.assert_array_equal(out_len, g["enc_len"])
+    np.testing.assert_array_equal(status, np.where(g["enc_len"] == FAIL, 0x80, 0).astype(np.uint8))
+    assert compact(out, g["enc_in_off"][:n], out_len) == g["enc_out"].tobytes()
+
+
+# ------------------------------------------------------------------------------------------------
+# seeded batches against the CPU restatement
+# ------------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("cfg,n,seed", [("c2", 100000, 1), ("c3", 40000, 2), ("c4", 100000, 3), ("c5", 6000, 4)])
+def test_random_batches_vs_oracle(torch_cuda, oracle_codec, cfg, n, seed):
+    b = synth.make_batch(cfg, n=n, seed=seed, adversarial_frac=0.02)
+    o_out, o_len, o_st = oracle_codec.encode_batch(b["data"], b["off"], n, nthreads=8)
+    g_out, g_len, g_st = gpu_encode(torch_cuda, b["data"], b["off"], n)
+    np.testing.assert_array_equal(g_len, o_len)
+    np.testing.assert_array_equal(g_st, o_st)
+    assert compact(g_out, b["off"][:n], g_len) == compact(o_out, b["off"][:n], o_len)
+    # decode the Huffman strings where they lie (pairs layout), and the plain bytes as garbage Huffman
+    lens = np.where(o_len != FAIL, o_len, 0).astype(np.uint32)
+    starts = b["off"][:n].copy()
+    out_off = ((starts.astype(np.uint64) * 8) // 5).astype(np.uint32)
+    od = oracle_codec.decode_batch(o_out, starts, n, in_len=lens, is_name_bits=b["is_name_bits"], nthreads=8)
+    gd = gpu_decode(torch_cuda, o_out, starts, n, in_len=lens, is_name_bits=b["is_name_bits"])
+    np.testing.assert_array_equal(gd[1], od[1])
+    np.testing.assert_array_equal(gd[2], od[2])
+    assert compact(gd[0], out_off, gd[1]) == compact(od[0], out_off, od[1])
+    od = oracle_codec.decode_batch(b["data"], b["off"], n, is_name_bits=b["is_name_bits"], nthreads=8)
+    gd = gpu_decode(torch_cuda, b["data"], b["off"], n, is_name_bits=b["is_name_bits"])
+    np.testing.assert_array_equal(gd[1], od[1])
+    np.testing.assert_array_equal(gd[2], od[2])
+    slots = (b["off"][:n].astype(np.uint64) * 8) // 5
+    assert compact(gd[0], slots, gd[1]) == compact(od[0], slots, od[1])
+
+
+def test_explicit_out_off_unaligned_and_long_strings(torch_cuda, oracle_codec):
+    """explicit destinations at odd byte offsets, strings longer than the LDS stage (global path),
+    empty strings, strings starting at every alignment"""
+    rng = np.random.default_rng(5)
+    syms, p = synth.header_alphabet()
+    strings = []
+    for i in range(3000):
+        L = int(rng.choice([0, 1, 2, 3, 5, 17, 100, 700, 5000, 30000], p=[.05, .05, .05, .05, .2, .3, .15, .1, .04, .01]))
+        strings.append(bytes(rng.choice(syms, L, p=p)))
+    data, off = synth.pack(strings)
+    n = len(strings)
+    # explicit encode destinations: reversed order with 1..7 bytes of gap (never 4-aligned on purpose)
+    gaps = rng.integers(1, 8, n)
+    lens = np.diff(off).astype(np.uint64)
+    dst = np.zeros(n, np.uint64)
+    pos = 3
+    for i in reversed(range(n)):
+        dst[i] = pos
+        pos += int(lens[i]) + int(gaps[i])
+    e_out, e_len, _ = gpu_encode(torch_cuda, data, off, n, out_off=dst.astype(np.uint32), out_size=pos + 16)
+    o_out, o_len, _ = oracle_codec.encode_batch(data, off, n)
+    np.testing.assert_array_equal(e_len, o_len)
+    assert compact(e_out, dst, e_len) == compact(o_out, off[:n], o_len)
+    # bytes in the gaps must be untouched (zero)
+    mask = np.ones(pos + 16, bool)
+    for i in range(n):
+        if e_len[i] != FAIL:
+            mask[int(dst[i]):int(dst[i]) + int(e_len[i])] = False
+        else:
+            mask[int(dst[i]):int(dst[i]) + int(lens[i])] = False
+    assert not e_out[mask].any()
+    # decode those Huffman strings from their scattered places into explicit odd destinations
+    hl = np.where(e_len != FAIL, e_len, 0).astype(np.uint32)
+    names = synth.bits_from_bools(rng.random(n) < 0.5)
+    d_dst = np.zeros(n, np.uint64)
+    pos = 1
+    for i in range(n):
+        d_dst[i] = pos
+        pos += (int(hl[i]) * 8) // 5 + int(gaps[i])
+    g = gpu_decode(torch_cuda, e_out, dst.astype(np.uint32), n, in_len=hl, is_name_bits=names,
+                   out_off=d_dst.astype(np.uint32), out_size=pos + 16)
+    o = oracle_codec.decode_batch(e_out, dst.astype(np.uint32), n, in_len=hl, is_name_bits=names,
+                                  out_off=d_dst.astype(np.uint32), out_size=pos + 16)
+    np.testing.assert_array_equal(g[1], o[1])
+    np.testing.assert_array_equal(g[2], o[2])
+    assert compact(g[0], d_dst, g[1]) == compact(o[0], d_dst, o[1])
+    # round trip: compressible strings decode back to themselves
+    for i in np.nonzero(e_len != FAIL)[0][:500]:
+        assert g[0][int(d_dst[i]):int(d_dst[i]) + int(g[1][i])].tobytes() == strings[i]
+
+
+# ------------------------------------------------------------------------------------------------
+# per-string h2o symbols and the host batch API
+# ------------------------------------------------------------------------------------------------
+def test_per_string_symbols(torch_cuda, oracle_codec):
+    from h2o_amd import codec
+
+    assert codec.decode_huffman(bytes.fromhex("f1e3c2e5f23a6ba0ab90f4ff")) == (b"www.example.com", 0)
+    assert codec.encode_huffman(b"www.example.com") == bytes.fromhex("f1e3c2e5f23a6ba0ab90f4ff")
+    assert codec.encode_huffman(b"") is None
+    assert codec.decode_huffman(b"", True) == (b"", 1)
+    assert codec.decode_huffman(b"\xff", False, 2) == (None, 2)
+    g = load_golden("kat")
+    strings = synth.unpack(g["dec_in"], g["dec_in_off"])
+    names = np.unpackbits(g["is_name_bits"].view(np.uint8), bitorder="little")[:len(strings)]
+    for s, nm in zip(strings, names):
+        assert codec.decode_huffman(s, bool(nm)) == oracle_codec.decode(s, bool(nm))
+        assert codec.decode_huffman(s, bool(nm), 3) == oracle_codec.decode(s, bool(nm), 3)
+    for s in synth.unpack(g["enc_in"], g["enc_in_off"]):
+        assert codec.encode_huffman(s) == oracle_codec.encode(s)
+
+
+def test_host_batch_api(torch_cuda, oracle_codec):
+    from h2o_amd import codec
+
+    b = synth.make_batch("c2", n=20000, seed=77, adversarial_frac=0.05)
+    n = b["n"]
+    out, ol, st = codec.encode_batch_host(b["data"], b["off"], n)
+    o_out, o_len, o_st = oracle_codec.encode_batch(b["data"], b["off"], n)
+    np.testing.assert_array_equal(ol, o_len)
+    assert compact(out, b["off"][:n], ol) == compact(o_out, b["off"][:n], o_len)
+    out, ol, st = codec.decode_batch_host(b["data"], b["off"], n, is_name_bits=b["is_name_bits"])
+    o = oracle_codec.decode_batch(b["data"], b["off"], n, is_name_bits=b["is_name_bits"])
+    np.testing.assert_array_equal(ol, o[1])
+    np.testing.assert_array_equal(st, o[2])
+
+
+# ------------------------------------------------------------------------------------------------
+# full benchmark size (config 4: 16M strings, mean 48 B): size-independent properties
+# ------------------------------------------------------------------------------------------------
+def test_c4_full_size_round_trip(torch_cuda):
+    import torch
+
+    from h2o_amd import codec
+
+    b = synth.make_batch_torch("c4", seed=2024)
+    n = b["n"]
+    off32 = b["off"].to(torch.int32)
+    e_out, e_len, e_st = codec.encode_batch(b["data"], off32, n)
+    ok = e_len != -1
+    # every success is strictly shorter; failures are exactly the SIZE_MAX verdicts
+    lens = (b["off"][1:] - b["off"][:-1])
+    assert bool((e_len[ok].to(torch.int64) < lens[ok]).all())
+    assert bool(((e_st == 0x80) == ~ok).all())
+    # decode the Huffman strings in place (pairs layout) and compare with the plain input
+    hl = torch.where(ok, e_len, torch.zeros_like(e_len))
+    d_out, d_len, d_st = codec.decode_batch(e_out, off32[:-1].contiguous(), n, in_len=hl.contiguous(),
+                                            is_name_bits=b["is_name_bits"], in_size=b["total"])
+    torch.cuda.synchronize()
+    assert bool((d_len[ok] == lens[ok].to(torch.int32)).all())
+    # checksum of checksums: per-string byte sums of decoded vs plain, for the successful ones
+    plain_sum = torch.zeros(n, dtype=torch.int64, device="cuda")
+    seg = torch.repeat_interleave(torch.arange(n, device="cuda"), lens)
+    plain_sum.index_add_(0, seg, b["data"].to(torch.int64))
+    slot = (b["off"][:-1] * 8) // 5
+    dec_idx = torch.repeat_interleave(slot, lens) + (torch.arange(int(b["total"]), device="cuda") -
+                                                     torch.repeat_interleave(b["off"][:-1], lens))
+    dec_bytes = d_out[dec_idx].to(torch.int64)
+    dec_sum = torch.zeros(n, dtype=torch.int64, device="cuda")
+    dec_sum.index_add_(0, seg, dec_bytes)
+    assert bool((dec_sum[ok] == plain_sum[ok]).all())
+    # exact byte equality for the successful strings
+    okb = torch.repeat_interleave(ok, lens)
+    assert bool((d_out[dec_idx][okb] == b["data"][okb]).all())
