@@ -89,7 +89,7 @@ int check_batch(const uint8_t* in, const uint32_t* in_off, uint32_t n, const uin
     if (n == 0) return HHUFF_OK;
     if (!in || !in_off || !out || !out_len) return arg_fail("NULL array");
     if (((uintptr_t)in & 15) != 0) return arg_fail("`in` must be 16-byte aligned");
-    if (((uintptr_t)out & 3) != 0) return arg_fail("`out` must be 4-byte aligned");
+    if (((uintptr_t)out & 15) != 0) return arg_fail("`out` must be 16-byte aligned");
     if (n > 0xFFFFFFFEu) return arg_fail("n too large");
     return HHUFF_OK;
 }

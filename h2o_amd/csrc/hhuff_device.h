@@ -3,13 +3,15 @@
 // Semantics restated from the reference (file:line under /root/reference):
 //   decode  lib/http2/hpack.c:85-156   (nibble FSM; accept rule misc/mkhufftbl.py:374-381)
 //   encode  lib/http2/hpack.c:774-804  (40-bit accumulator; SIZE_MAX unless strictly shorter)
-// The MI355X formulation is different from the reference's (same results, bit for bit):
-//   * decode consumes a 12-bit window per step through a 4096-entry LUT staged in LDS that yields up to
-//     two symbols; codes longer than 12 bits (and EOS) take a canonical-code path.  The bit stream is
-//     padded with ones past the end of the string, so "at most 7 padding bits, all ones" becomes
-//     "remaining bits <= 7 and the next 8 bits of the window are 0xFF".
-//   * encode packs codes MSB-first into a 64-bit accumulator and emits whole 32-bit words; a string
-//     fails as soon as its Huffman length can no longer be shorter than its input.
+// The MI355X formulation differs from the reference's (same results, bit for bit):
+//   * decode peeks a 12-bit window per step through a 4096-entry LUT in LDS that yields up to two
+//     symbols.  Codes longer than 12 bits (and EOS) go through the leading-ones table: every RFC 7541
+//     code is k leading ones, a zero, and at most 5 more bits, so k = clz(~window) plus <= 5 bits index
+//     a 348-entry table.  A symbol is taken only when its whole code lies inside the string, so bits
+//     past the end never matter; the string is accepted iff no EOS was decoded and the R <= 7 unused
+//     bits are all ones (the reference's ACCEPTED state, mkhufftbl.py:374-381).
+//   * encode packs codes MSB-first into a 64-bit accumulator and emits 32 bits at a time; a string
+//     fails as soon as its Huffman length can no longer be shorter than its input (hpack.c:789-800).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,22 +27,21 @@ constexpr uint8_t kStatusFail = 0x80;
 constexpr uint8_t kStatusTooLong = 0xC0;
 constexpr uint32_t kMaxStrLen = (1u << 29) - 1;
 
-constexpr uint32_t c_len[HHUFF_NUM_LENGTHS] = HHUFF_LEN_INIT;
-constexpr uint32_t c_lim1[HHUFF_NUM_LENGTHS] = HHUFF_LIM1_INIT;
-constexpr uint32_t c_first[HHUFF_NUM_LENGTHS] = HHUFF_FIRST_INIT;
-constexpr uint32_t c_base[HHUFF_NUM_LENGTHS] = HHUFF_BASE_INIT;
-
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+// decode slot of an input offset: floor(8 * x / 5), the tight output bound (shortest code = 5 bits)
+__device__ __forceinline__ uint64_t dec_slot(uint32_t x) { return ((uint64_t)x * 8u) / 5u; }
+
 // ---------------------------------------------------------------------------------------------------
-// Byte sources.  word(a) returns the little-endian dword at 4-aligned byte position a.
+// Byte sources.  word(a) returns the little-endian dword at 4-aligned position a.
 // ---------------------------------------------------------------------------------------------------
-struct LdsSource {  // a wave's staged input span; positions are relative to the 16-aligned span start
+struct LdsSource {  // a wave's staged input span; positions relative to the 16-aligned span start
     const uint32_t* base;
-    __device__ __forceinline__ uint32_t word(uint32_t a) const { return base[a >> 2]; }
+    uint32_t last;  // last readable dword position (reads are clamped: bits past a string are don't-care)
+    __device__ __forceinline__ uint32_t word(uint32_t a) const { return base[min(a, last) >> 2]; }
 };
 
-struct GlobalSource {  // positions are absolute offsets into `in`; never reads at or past in_size
+struct GlobalSource {  // absolute offsets into `in`; never reads at or past in_size
     const uint8_t* in;
     uint64_t in_size;
     __device__ __forceinline__ uint32_t word(uint32_t a) const {
@@ -53,20 +54,45 @@ struct GlobalSource {  // positions are absolute offsets into `in`; never reads 
 };
 
 // ---------------------------------------------------------------------------------------------------
-// Output writer: lane-private byte stream into global memory with dword stores.  Bytes before the first
-// 4-aligned address are stored singly (the destination region may start at any byte, and its
-// neighbours belong to other lanes).  Invariant after flush(): pending <= 3.
+// Byte sinks.
+// LdsSink: bytes go to the wave's LDS output stage (copied out coalesced afterwards).
+// RegSink: lane-private byte stream straight to global memory, dword stores once 4-aligned.
 // ---------------------------------------------------------------------------------------------------
-struct Writer {
+struct LdsSink {
+    uint8_t* base;  // LDS
+    uint32_t op;    // next byte position
+    uint32_t start;
+    uint32_t trash;  // lane-private scratch byte for predicated-off second writes
+    __device__ __forceinline__ void put1(uint32_t b) { base[op] = (uint8_t)b; op += 1; }
+    __device__ __forceinline__ void put12(uint32_t syms, bool two) {
+        base[op] = (uint8_t)syms;
+        base[two ? op + 1 : trash] = (uint8_t)(syms >> 8);
+        op += two ? 2u : 1u;
+    }
+    __device__ __forceinline__ void put4(uint32_t w) {  // w: 4 bytes in output order, first in bits 0..7
+        base[op] = (uint8_t)w;
+        base[op + 1] = (uint8_t)(w >> 8);
+        base[op + 2] = (uint8_t)(w >> 16);
+        base[op + 3] = (uint8_t)(w >> 24);
+        op += 4;
+    }
+    __device__ __forceinline__ void putn(uint32_t w, uint32_t n) {
+        for (uint32_t k = 0; k < n; ++k) base[op + k] = (uint8_t)(w >> (8 * k));
+        op += n;
+    }
+    __device__ __forceinline__ uint32_t count() const { return op - start; }
+    __device__ __forceinline__ void finish() {}
+};
+
+struct RegSink {
     uint8_t* p;
     uint64_t acc;  // pending bytes, first byte in bits 0..7
-    uint32_t pending;
-
-    __device__ __forceinline__ void init(uint8_t* dst) { p = dst; acc = 0; pending = 0; }
-    // append k (<= 4) bytes packed little-endian in `bytes`
+    uint32_t pending, cnt;
+    __device__ __forceinline__ void init(uint8_t* dst) { p = dst; acc = 0; pending = 0; cnt = 0; }
     __device__ __forceinline__ void push(uint32_t bytes, uint32_t k) {
         acc |= (uint64_t)bytes << (8 * pending);
         pending += k;
+        cnt += k;
         if (__builtin_expect(((uintptr_t)p & 3) != 0, 0)) {
             while (pending > 0 && ((uintptr_t)p & 3) != 0) {
                 *p++ = (uint8_t)acc;
@@ -81,13 +107,12 @@ struct Writer {
             pending -= 4;
         }
     }
+    __device__ __forceinline__ void put1(uint32_t b) { push(b & 0xFFu, 1); }
+    __device__ __forceinline__ void put12(uint32_t syms, bool two) { push(two ? (syms & 0xFFFFu) : (syms & 0xFFu), two ? 2u : 1u); }
+    __device__ __forceinline__ void put4(uint32_t w) { push(w, 4); }
+    __device__ __forceinline__ void putn(uint32_t w, uint32_t n) { push(w, n); }
+    __device__ __forceinline__ uint32_t count() const { return cnt; }
     __device__ __forceinline__ void finish() {
-        if (pending >= 2 && ((uintptr_t)p & 1) == 0) {
-            *reinterpret_cast<uint16_t*>(p) = (uint16_t)acc;
-            p += 2;
-            acc >>= 16;
-            pending -= 2;
-        }
         while (pending > 0) {
             *p++ = (uint8_t)acc;
             acc >>= 8;
@@ -97,151 +122,139 @@ struct Writer {
 };
 
 // ---------------------------------------------------------------------------------------------------
-// Huffman bit reader: 64-bit MSB-aligned window over the string's bytes, ones past the end.
+// Huffman bit reader: 64-bit MSB-aligned window; invariant at the top of a step: nb >= 33.
 // ---------------------------------------------------------------------------------------------------
 template <class Src>
 struct BitReader {
-    uint64_t buf;  // next bits of the stream, MSB first; bits below the valid count are zero
+    uint64_t buf;  // next bits, MSB first; bits below the valid count are zero
     uint32_t nb;   // valid bits in buf
     uint32_t a;    // position of the next dword to load (4-aligned)
-    uint32_t end;  // string end position
 
-    __device__ __forceinline__ uint32_t fetch(const Src& src, uint32_t pos) const {
-        // big-endian word of the 4 bytes at pos; bytes at or past `end` read as 0xFF
-        int32_t rem = (int32_t)(end - pos);
-        uint32_t raw = 0xFFFFFFFFu;
-        if (rem > 0) raw = src.word(pos);
-        uint32_t w = bswap32(raw);
-        uint32_t ones = rem >= 4 ? 0u : (rem <= 0 ? 0xFFFFFFFFu : (0xFFFFFFFFu >> (8 * rem)));
-        return w | ones;
-    }
-    __device__ __forceinline__ void init(const Src& src, uint32_t start, uint32_t len) {
-        end = start + len;
+    __device__ __forceinline__ void init(const Src& src, uint32_t start) {
         a = start & ~3u;
         uint32_t skip = start & 3u;
-        uint32_t w = fetch(src, a) << (8 * skip);
-        buf = (uint64_t)w << 32;
+        buf = (uint64_t)(bswap32(src.word(a)) << (8 * skip)) << 32;
         nb = 32 - 8 * skip;
         a += 4;
+        refill(src);
     }
     __device__ __forceinline__ void refill(const Src& src) {
-        uint32_t w = fetch(src, a);
-        buf |= (uint64_t)w << (32 - nb);
+        buf |= (uint64_t)bswap32(src.word(a)) << (32 - nb);
         nb += 32;
         a += 4;
     }
+    __device__ __forceinline__ void consume(uint32_t n, const Src& src) {
+        buf <<= n;
+        nb -= n;
+        if (nb <= 32) refill(src);
+    }
+    __device__ __forceinline__ uint32_t hi() const { return (uint32_t)(buf >> 32); }
+};
+
+struct DecTables {  // LDS copies
+    const uint32_t* lut;    // 4096 window entries
+    const uint32_t* kinfo;  // 31 leading-ones entries
+    const uint32_t* ones;   // HHUFF_ONES_NENT symbol entries
+};
+
+struct DecResult {
+    uint32_t len;
+    uint8_t status;
+    uint32_t flags;
+    bool ok;
 };
 
 // ---------------------------------------------------------------------------------------------------
-// decode one string (h2o_hpack_decode_huffman semantics).  lut = the 4096-entry window table in LDS.
+// decode one string (h2o_hpack_decode_huffman semantics) from `src` [start, start+len) into `sink`.
+// Returns ok / decoded count / accumulated invalid-char flags (bit0 name, bit1 value); the caller
+// derives the status from the first and last decoded bytes.
 // ---------------------------------------------------------------------------------------------------
-template <class Src>
-__device__ __forceinline__ void decode_string(const Src& src, uint32_t start, uint32_t len, bool is_name, uint8_t* dst,
-                                              const uint32_t* __restrict__ lut, const uint16_t* __restrict__ sorted_syms,
-                                              const uint32_t* __restrict__ inv_maps, uint32_t& out_len,
-                                              uint8_t& status) {
-    if (len > kMaxStrLen) {
-        out_len = kFailLen;
-        status = kStatusTooLong;
-        return;
-    }
+template <class Src, class Sink>
+__device__ __forceinline__ DecResult decode_core(const Src& src, uint32_t start, uint32_t len, Sink& sink,
+                                                 const DecTables& T) {
     BitReader<Src> br;
-    br.init(src, start, len);
-    Writer wr;
-    wr.init(dst);
+    br.init(src, start);
     uint32_t R = 8 * len;  // string bits not yet consumed
-    uint32_t cnt = 0, first = 0, last = 0, flags = 0;
+    uint32_t flags = 0;
     bool fail = false;
     for (;;) {
-        if (br.nb <= 32) br.refill(src);
-        uint32_t e = lut[(uint32_t)(br.buf >> (64 - HHUFF_LUT_BITS))];
-        uint32_t consumed, syms, nsym, fl;
+        const uint32_t w = br.hi();
+        const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
         if (__builtin_expect((e & kLong) != 0, 0)) {
-            // canonical decode of a code longer than the window (hpack.c:85-99 walks the same tree)
-            uint32_t t = (uint32_t)(br.buf >> 32);
-            uint32_t j = HHUFF_FIRST_LONG_IDX;
-#pragma unroll
-            for (int k = HHUFF_FIRST_LONG_IDX; k < HHUFF_NUM_LENGTHS - 1; ++k) j += (t > c_lim1[k]) ? 1u : 0u;
-            uint32_t L = 0, f = 0, b = 0;
-#pragma unroll
-            for (int k = HHUFF_FIRST_LONG_IDX; k < HHUFF_NUM_LENGTHS; ++k)
-                if (j == (uint32_t)k) { L = c_len[k]; f = c_first[k]; b = c_base[k]; }
+            // code longer than the window (or EOS): leading-ones table
+            const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);  // ~w | 1: 32 ones -> 31, capped
+            const uint32_t ki = T.kinfo[k];
+            const uint32_t idx = (ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)));
+            const uint32_t le = T.ones[idx];
+            const uint32_t L = (le >> 9) & 31u;
             if (L > R) break;  // incomplete code: padding
-            uint32_t sym = sorted_syms[b + (t >> (32 - L)) - f];
-            if (sym == kEos) { fail = true; break; }  // EOS inside the string (hpack.c:88-89)
-            consumed = L;
-            syms = sym;
-            nsym = 1;
-            fl = ((inv_maps[sym >> 5] >> (sym & 31)) & 1u) | (((inv_maps[8 + (sym >> 5)] >> (sym & 31)) & 1u) << 1);
+            const uint32_t sym = le & 0x1FFu;
+            if (sym == kEos) {  // EOS inside the string (hpack.c:88-89)
+                fail = true;
+                break;
+            }
+            sink.put1(sym);
+            flags |= (le >> 14) & 3u;
+            R -= L;
+            br.consume(L, src);
         } else {
-            uint32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+            const uint32_t L1 = (e >> 16) & 15u;
             if (L1 > R) break;  // fewer bits left than the next code: padding
-            bool take2 = ((e >> 24) & 1u) && L12 <= R;
-            consumed = take2 ? L12 : L1;
-            nsym = take2 ? 2u : 1u;
-            syms = take2 ? (e & 0xFFFFu) : (e & 0xFFu);
-            uint32_t f4 = (e >> 25) & (take2 ? 15u : 3u);
-            fl = (f4 | (f4 >> 2)) & 3u;
+            const uint32_t L12 = (e >> 20) & 15u;
+            const bool two = (e & (1u << 24)) && L12 <= R;
+            const uint32_t cons = two ? L12 : L1;
+            sink.put12(e, two);
+            flags |= (e >> 25) & (two ? 15u : 3u);
+            R -= cons;
+            br.consume(cons, src);
         }
-        flags |= fl;
-        first = cnt == 0 ? (syms & 0xFFu) : first;
-        last = (syms >> (8 * (nsym - 1))) & 0xFFu;
-        wr.push(syms, nsym);
-        cnt += nsym;
-        br.buf <<= consumed;
-        br.nb -= consumed;
-        R -= consumed;
     }
+    DecResult r;
     // accept iff no EOS and the padding is <= 7 bits of ones (mkhufftbl.py:374-381, hpack.c:132-133)
-    if (fail || R > 7 || (uint32_t)(br.buf >> 56) != 0xFFu) {
-        out_len = kFailLen;
-        status = kStatusFail;
-        return;
-    }
-    wr.finish();
-    out_len = cnt;
-    uint8_t st;
-    if (is_name) {  // hpack.c:136-147 (':'-prefixed names are not validated; upper case is only soft)
-        st = (cnt == 0 || ((flags & 1u) && first != ':')) ? 0x1 : 0x0;
-    } else {  // hpack.c:150-152 + header_value_valid_as_whole :110-115
-        bool ws = cnt != 0 && (first == ' ' || first == '\t' || last == ' ' || last == '\t');
-        st = ((flags & 2u) || ws) ? 0x2 : 0x0;
-    }
-    status = st;
+    r.ok = !fail && R <= 7 && ((br.hi() >> 24) | (0xFFu >> R)) == 0xFFu;
+    r.len = sink.count();
+    r.flags = (flags | (flags >> 2)) & 3u;
+    r.status = 0;
+    return r;
+}
+
+// hpack.c:136-152: soft-error bits from the accumulated flags and the first / last decoded bytes
+__device__ __forceinline__ uint8_t soft_bits(bool is_name, uint32_t cnt, uint32_t flags, uint32_t first, uint32_t last) {
+    if (is_name)  // ':'-prefixed names are not validated; upper case is only soft (hpack.c:136-147)
+        return (cnt == 0 || ((flags & 1u) && first != ':')) ? 0x1 : 0x0;
+    const bool ws = cnt != 0 && (first == ' ' || first == '\t' || last == ' ' || last == '\t');  // :110-115
+    return ((flags & 2u) || ws) ? 0x2 : 0x0;
 }
 
 // ---------------------------------------------------------------------------------------------------
 // encode one string (h2o_hpack_encode_huffman semantics).  enc = 256 x {code, nbits} in LDS.
-// Writes at most len - 1 bytes at dst.
+// Emits at most len - 1 bytes into `sink`; returns the Huffman length or kFailLen.
 // ---------------------------------------------------------------------------------------------------
-template <class Src>
-__device__ __forceinline__ void encode_string(const Src& src, uint32_t start, uint32_t len, uint8_t* dst,
-                                              const uint2* __restrict__ enc, uint32_t& out_len) {
-    if (len > kMaxStrLen) {
-        out_len = kFailLen;
-        return;
-    }
-    Writer wr;
-    wr.init(dst);
-    uint64_t acc = 0;   // code bits, MSB-aligned
-    uint32_t an = 0;    // bits in acc (< 32 between symbols)
+template <class Src, class Sink>
+__device__ __forceinline__ uint32_t encode_core(const Src& src, uint32_t start, uint32_t len, Sink& sink,
+                                                const uint2* __restrict__ enc) {
+    uint64_t acc = 0;  // code bits, MSB-aligned
+    uint32_t an = 0;   // bits in acc (< 32 between symbols)
     uint32_t emitted = 0;
     bool fail = false;
     const uint32_t end = start + len;
     for (uint32_t a = start & ~3u; a < end; a += 4) {
-        uint32_t w = src.word(a);
+        const uint32_t w = src.word(a);
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
-            uint32_t pos = a + k;
-            bool valid = pos >= start && pos < end;
-            uint2 ent = enc[(w >> (8 * k)) & 0xFFu];
-            uint32_t nb = valid ? ent.y : 0u;
-            uint64_t code = valid ? (uint64_t)ent.x : 0ull;
+            const uint32_t pos = a + k;
+            const bool valid = pos >= start && pos < end;
+            const uint2 ent = enc[(w >> (8 * k)) & 0xFFu];
+            const uint32_t nb = valid ? ent.y : 0u;
+            const uint64_t code = valid ? (uint64_t)ent.x : 0ull;
             acc |= code << (64 - an - nb);
             an += nb;
             if (an >= 32) {
-                if (emitted + 4 >= len) { fail = true; break; }  // cannot end up shorter than the input
-                wr.push(bswap32((uint32_t)(acc >> 32)), 4);
+                if (emitted + 4 >= len) {  // can no longer end up shorter than the input
+                    fail = true;
+                    break;
+                }
+                sink.put4(bswap32((uint32_t)(acc >> 32)));
                 emitted += 4;
                 acc <<= 32;
                 an -= 32;
@@ -249,15 +262,12 @@ __device__ __forceinline__ void encode_string(const Src& src, uint32_t start, ui
         }
         if (fail) break;
     }
-    uint32_t tail = (an + 7) >> 3;
-    if (fail || emitted + tail >= len) {  // hpack.c:789-791, :799-800
-        out_len = kFailLen;
-        return;
-    }
-    if (an != 0) acc |= ~0ull >> an;  // pad with the EOS prefix (hpack.c:795-798)
-    if (tail) wr.push(bswap32((uint32_t)(acc >> 32)) & (0xFFFFFFFFu >> (8 * (4 - tail))), tail);
-    wr.finish();
-    out_len = emitted + tail;
+    const uint32_t tail = (an + 7) >> 3;
+    if (fail || emitted + tail >= len) return kFailLen;  // hpack.c:789-791, :799-800
+    if (an != 0) acc |= ~0ull >> an;                        // pad with the EOS prefix (hpack.c:795-798)
+    if (tail) sink.putn(bswap32((uint32_t)(acc >> 32)), tail);
+    sink.finish();
+    return emitted + tail;
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -272,6 +282,22 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
     return v;
+}
+// exclusive prefix sum over the wave
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x - v;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 }  // namespace hhuff

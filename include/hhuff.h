@@ -18,7 +18,7 @@
  *   in_size       bytes readable at `in` (the kernels never read past it)
  *   is_name_bits  u32[(n+31)/32]; bit (i & 31) of word (i >> 5) set => string i is a header name
  *                 (NULL => every string is a header value)
- *   device `in` must be 16-byte aligned and `out` 4-byte aligned (hipMalloc / torch allocations are);
+ *   device `in` and `out` must be 16-byte aligned (hipMalloc / torch allocations are);
  *   strings may start at any byte.
  *   Per-string length limit: 2^29 - 1 bytes (status HHUFF_STATUS_TOO_LONG above it).
  */

@@ -218,6 +218,40 @@ def long_tables(lens, codes, order):
     return L_out, lim1, first, base
 
 
+def ones_tables(lens, codes):
+    """Leading-ones decode: every code is k leading ones, then (k < 30) a zero, then at most m_k <= 5
+    more bits that select the symbol (canonical structure of the RFC 7541 code).
+    kinfo[k] = base_k | m_k << 16 for k = 0..30 (k >= 30 is EOS); entry[base_k + next m_k bits] =
+    sym | len << 9 | name-invalid << 14 | value-invalid << 15.  Indices past a shorter code repeat it."""
+    by_k = {}
+    for s in range(NSYM):
+        b = format(codes[s], "0%db" % lens[s])
+        k = len(b) - len(b.lstrip("1"))
+        by_k.setdefault(k, []).append(s)
+    kinfo, entries = [], []
+    for k in range(31):
+        syms = by_k.get(k, [])
+        m = max(lens[s] for s in syms) - (k + 1) if k < 30 else 0
+        m = max(m, 0)
+        base = len(entries)
+        for v in range(1 << m):
+            hit = None
+            for s in syms:
+                rest = lens[s] - (k + 1) if k < 30 else 0
+                tail = codes[s] & ((1 << rest) - 1) if rest > 0 else 0
+                if rest <= m and (v >> (m - rest)) == tail:
+                    hit = s
+            assert hit is not None, (k, v)
+            e = hit | lens[hit] << 9
+            if hit < 256 and hit not in NAME_VALID:
+                e |= 1 << 14
+            if hit < 256 and hit not in VALUE_VALID:
+                e |= 1 << 15
+            entries.append(e)
+        kinfo.append(base | m << 16)
+    return kinfo, entries
+
+
 def bitmap(pred):
     words = [0] * 8
     for c in range(256):
@@ -241,6 +275,7 @@ HEADER_NOTE = """/* GENERATED by tools/gen_tables.py from the RFC 7541 Appendix 
 
 def product_header(lens, codes, order, lut, longt):
     L_out, lim1, first, base = longt
+    kinfo, kent = ones_tables(lens, codes)
     name_inv = bitmap(lambda c: c not in NAME_VALID)
     value_inv = bitmap(lambda c: c not in VALUE_VALID)
     out = [HEADER_NOTE, "#pragma once", "#include <stdint.h>", ""]
@@ -262,6 +297,14 @@ def product_header(lens, codes, order, lut, longt):
     out.append("/* symbols in canonical (length, symbol) order; 256 = EOS */")
     out.append("#define HHUFF_SORTED_SYMS_INIT { \\")
     out.append(fmt_array(order, 16, "{}").replace("\n", " \\\n") + " \\\n}")
+    out.append("")
+    out.append("/* leading-ones decode (any code length): k = leading ones of the 32-bit window (capped at 30),")
+    out.append(" * kinfo[k] = base | m << 16; entry = HHUFF_ONES_ENT[base + the m bits after the first zero] =")
+    out.append(" * sym | len << 9 | name-invalid << 14 | value-invalid << 15 (see tools/gen_tables.py:ones_tables) */")
+    out.append("#define HHUFF_ONES_NENT %d" % len(kent))
+    out.append("#define HHUFF_ONES_KINFO_INIT { %s }" % ", ".join("0x%05xu" % v for v in kinfo))
+    out.append("#define HHUFF_ONES_ENT_INIT { \\")
+    out.append(fmt_array(kent, 12, "0x{:04x}u").replace("\n", " \\\n") + " \\\n}")
     out.append("")
     out.append("/* encode table: code (right-aligned) and bit length per byte value; EOS is never encoded */")
     out.append("#define HHUFF_ENC_CODE_INIT { \\")
