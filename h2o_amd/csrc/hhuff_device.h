@@ -4,8 +4,8 @@
 //   decode  lib/http2/hpack.c:85-156   (nibble FSM; accept rule misc/mkhufftbl.py:374-381)
 //   encode  lib/http2/hpack.c:774-804  (40-bit accumulator; SIZE_MAX unless strictly shorter)
 // The MI355X formulation differs from the reference's (same results, bit for bit):
-//   * decode peeks a 12-bit window per step through a 4096-entry LUT in LDS that yields up to two
-//     symbols.  Codes longer than 12 bits (and EOS) go through the leading-ones table: every RFC 7541
+//   * decode peeks a 13-bit window per step through an 8192-entry LUT in LDS that yields up to two
+//     symbols.  Codes longer than 13 bits (and EOS) go through the leading-ones table: every RFC 7541
 //     code is k leading ones, a zero, and at most 5 more bits, so k = clz(~window) plus <= 5 bits index
 //     a 348-entry table.  A symbol is taken only when its whole code lies inside the string, so bits
 //     past the end never matter; the string is accepted iff no EOS was decoded and the R <= 7 unused
@@ -152,7 +152,7 @@ struct BitReader {
 };
 
 struct DecTables {  // LDS copies
-    const uint32_t* lut;    // 4096 window entries
+    const uint32_t* lut;    // 2^HHUFF_LUT_BITS window entries
     const uint32_t* kinfo;  // 31 leading-ones entries
     const uint32_t* ones;   // HHUFF_ONES_NENT symbol entries
 };
@@ -218,6 +218,77 @@ __device__ __forceinline__ DecResult decode_core(const Src& src, uint32_t start,
     return r;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Staged decode of one string per lane, all 64 lanes in lock step (same results as decode_core).
+// Every step is predicated instead of branching: the window-LUT read and the next input word are
+// fetched together from LDS, up to two symbols are written to the LDS output stage (writes that are
+// switched off go to a lane-private trash byte), and the 64-bit window is refilled without a branch.
+// Codes longer than the window take a wave-uniform detour through the leading-ones table.
+// `active` = this lane has a string to decode (len <= kMaxStrLen).
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ DecResult decode_staged_lane(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
+                                                        bool active, uint8_t* obuf, uint32_t op0, uint32_t trash,
+                                                        const DecTables& T) {
+    uint32_t a = start & ~3u;
+    const uint32_t skip = start & 3u;
+    uint64_t buf = (uint64_t)(bswap32(stage[min(a, last) >> 2]) << (8 * skip)) << 32;
+    uint32_t nb = 32 - 8 * skip;
+    a += 4;
+    buf |= (uint64_t)bswap32(stage[min(a, last) >> 2]) << (32 - nb);
+    nb += 32;
+    a += 4;
+    uint32_t R = active ? 8 * len : 0u;  // string bits not yet consumed
+    uint32_t op = op0, flags = 0;
+    bool fail = false;
+    for (;;) {
+        const uint32_t w = (uint32_t)(buf >> 32);
+        const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+        const uint32_t word = stage[min(a, last) >> 2];  // next refill word, fetched beside the LUT entry
+        const bool isl = (e & kLong) != 0;
+        const uint32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+        const bool ok1 = active && !isl && L1 <= R;
+        const bool two = ok1 && (e & (1u << 24)) != 0 && L12 <= R;
+        uint32_t cons = two ? L12 : (ok1 ? L1 : 0u);
+        obuf[ok1 ? op : trash] = (uint8_t)e;
+        obuf[two ? op + 1 : trash] = (uint8_t)(e >> 8);
+        op += (ok1 ? 1u : 0u) + (two ? 1u : 0u);
+        flags |= (e >> 25) & (two ? 15u : (ok1 ? 3u : 0u));
+        bool stay = ok1;
+        if (__any(active && isl)) {  // wave-uniform: codes longer than the window, EOS
+            if (active && isl) {
+                const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                const uint32_t ki = T.kinfo[k];
+                const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                const uint32_t L = (le >> 9) & 31u;
+                const bool okL = L <= R;
+                const bool eos = (le & 0x1FFu) == kEos;
+                const bool ok = okL && !eos;
+                fail = fail || (okL && eos);  // EOS inside the string (hpack.c:88-89)
+                obuf[ok ? op : trash] = (uint8_t)le;
+                op += ok ? 1u : 0u;
+                flags |= ok ? ((le >> 14) & 3u) : 0u;
+                cons = ok ? L : 0u;
+                stay = ok;
+            }
+        }
+        active = active && stay;
+        R -= cons;
+        buf <<= cons;
+        nb -= cons;
+        const bool need = nb <= 32;
+        buf |= (uint64_t)(need ? bswap32(word) : 0u) << ((32 - nb) & 63u);
+        nb += need ? 32u : 0u;
+        a += need ? 4u : 0u;
+        if (!__any(active)) break;
+    }
+    DecResult r;
+    r.ok = !fail && R <= 7 && ((uint32_t)(buf >> 56) | (0xFFu >> R)) == 0xFFu;
+    r.len = op - op0;
+    r.flags = (flags | (flags >> 2)) & 3u;
+    r.status = 0;
+    return r;
+}
+
 // hpack.c:136-152: soft-error bits from the accumulated flags and the first / last decoded bytes
 __device__ __forceinline__ uint8_t soft_bits(bool is_name, uint32_t cnt, uint32_t flags, uint32_t first, uint32_t last) {
     if (is_name)  // ':'-prefixed names are not validated; upper case is only soft (hpack.c:136-147)
@@ -268,6 +339,87 @@ __device__ __forceinline__ uint32_t encode_core(const Src& src, uint32_t start, 
     if (tail) sink.putn(bswap32((uint32_t)(acc >> 32)), tail);
     sink.finish();
     return emitted + tail;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Staged encode of one string per lane, all lanes in lock step, one input dword per step (same results
+// as encode_core).  `enc` = 512 x {code, nbits} in LDS; entries 256..511 are {0, 0} and stand for bytes
+// outside the string, selected with one v_perm per byte.  Fast path: the dword's four codes are all
+// <= 8 bits, so they combine into one 32-bit chunk, enter the 64-bit accumulator at once and leave at
+// most one 32-bit word.  Output words are OR-ed (ds_or_b32) into a zeroed LDS stage at dword
+// granularity: the stream is pre-shifted by the slot's byte offset within its dword, so lanes whose
+// slots share a dword never overwrite each other.  Other dwords (a code longer than 8 bits) take a
+// wave-uniform per-byte detour.  Returns the Huffman length or kFailLen; `active` = len in 1..limit.
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void enc_put(uint32_t* obuf32, uint64_t& acc, uint32_t& an, uint32_t& opw, bool on) {
+    const bool emit = on && an >= 32;
+    atomicOr(&obuf32[opw], emit ? bswap32((uint32_t)(acc >> 32)) : 0u);
+    acc = emit ? acc << 32 : acc;
+    an -= emit ? 32u : 0u;
+    opw += emit ? 1u : 0u;
+}
+
+__device__ __forceinline__ uint32_t encode_staged_lane(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
+                                                       bool active, uint32_t* obuf32, uint32_t opb,
+                                                       const uint2* __restrict__ enc) {
+    const uint32_t end = start + len;
+    const uint32_t limit = 8 * len - 7;  // fail as soon as the code bits reach it: ceil(bits/8) >= len
+    uint64_t acc = 0;                     // code bits, MSB-aligned, after (opb & 3) zero bytes
+    uint32_t an = 8 * (opb & 3u);         // bits in acc
+    uint32_t opw = opb >> 2;              // next LDS output dword
+    uint32_t tb = 0;                      // code bits of the string so far
+    bool fail = false;
+    for (uint32_t a = start & ~3u;; a += 4) {
+        const uint32_t w = stage[min(a, last) >> 2];
+        const int32_t dlo = (int32_t)(start - a), dhi = (int32_t)(end - a);
+        const uint32_t nlo = (uint32_t)min(max(dlo, 0), 4), nhi = active ? (uint32_t)min(max(dhi, 0), 4) : 0u;
+        const uint32_t vm = (uint32_t)(0xFFFFFFFFull >> (8 * (4 - nhi))) & (uint32_t)(0xFFFFFFFFull << (8 * nlo));
+        const uint32_t iw = ~vm & 0x01010101u;  // 1 in every byte outside the string
+        const uint2 e0 = enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0400u)];
+        const uint2 e1 = enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)];
+        const uint2 e2 = enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)];
+        const uint2 e3 = enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)];
+        const bool lng = max(max(e0.y, e1.y), max(e2.y, e3.y)) > 8;
+        const bool fast = active && !lng;
+        const uint32_t n = e0.y + e1.y + e2.y + e3.y;
+        uint32_t c = (((e0.x << e1.y | e1.x) << e2.y | e2.x) << e3.y) | e3.x;
+        const bool over = fast && tb + n >= limit;
+        fail = fail || over;
+        const bool put = fast && !over;
+        c = put ? c : 0u;
+        const uint32_t nn = put ? n : 0u;
+        acc |= (uint64_t)c << ((64 - an - nn) & 63u);
+        an += nn;
+        tb += nn;
+        enc_put(obuf32, acc, an, opw, put);
+        bool stay = put;
+        if (__any(active && lng)) {  // a code longer than 8 bits in this dword: byte by byte
+            if (active && lng) {
+                bool ok = true;
+                const uint2 ek[4] = {e0, e1, e2, e3};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const bool ov = ok && tb + ek[k].y >= limit;
+                    fail = fail || ov;
+                    ok = ok && !ov;
+                    const uint32_t nk = ok ? ek[k].y : 0u;
+                    acc |= (uint64_t)(ok ? ek[k].x : 0u) << ((64 - an - nk) & 63u);
+                    an += nk;
+                    tb += nk;
+                    enc_put(obuf32, acc, an, opw, ok);
+                }
+                stay = ok;
+            }
+        }
+        active = active && stay && dhi > 4;  // more bytes after this dword
+        if (!__any(active)) break;
+    }
+    if (fail || len == 0 || len > kMaxStrLen) return kFailLen;
+    // pad the partial byte with ones (EOS prefix, hpack.c:795-798) and flush the last <= 4 bytes
+    const uint32_t an8 = (an + 7) & ~7u;
+    acc |= (~0ull >> an) & ~(~0ull >> an8);
+    if (an) atomicOr(&obuf32[opw], bswap32((uint32_t)(acc >> 32)));
+    return (tb + 7) >> 3;
 }
 
 // ---------------------------------------------------------------------------------------------------

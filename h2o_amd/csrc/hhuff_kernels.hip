@@ -10,7 +10,7 @@
 //     LDS position congruent to the destination mod 4).
 // Tiles whose span exceeds the stage, and batches of long strings, use the direct variant: lanes read
 // their input from global memory and write through a register accumulator with dword stores.
-// The decode LUT (16 KiB) + leading-ones tables / encode table (2 KiB) live in LDS per workgroup.
+// The decode LUT (32 KiB) + leading-ones tables / encode table (4 KiB) live in LDS per workgroup.
 //
 // Reference semantics: lib/http2/hpack.c:117-156 (decode), :774-804 (encode); see hhuff_device.h.
 #include <hip/hip_runtime.h>
@@ -204,23 +204,22 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         if (span <= IN_STAGE && ospan <= OUT_STAGE) {
             stage_span(stage, A.in, A.in_size, a0, span, lane);
             wave_lds_sync();
-            if (t.valid) {
-                if (t.len > kMaxStrLen) {
+            {
+                const bool act = t.valid && t.len <= kMaxStrLen;
+                const uint32_t rel = t.len ? t.s - a0 : 0u;
+                const uint32_t last = span ? span - 4u : 0u;
+                const DecResult r =
+                    decode_staged_lane(stage, last, rel, t.len, act, obuf, op0, OUT_STAGE + (uint32_t)lane, T);
+                if (t.valid && t.len > kMaxStrLen) {
                     ol = kFailLen;
                     st = kStatusTooLong;
+                } else if (r.ok) {
+                    ol = r.len;
+                    const uint32_t first = r.len ? obuf[op0] : 0u, lastc = r.len ? obuf[op0 + r.len - 1] : 0u;
+                    st = soft_bits(is_name, r.len, r.flags, first, lastc);
                 } else {
-                    LdsSink sink{obuf, op0, op0, OUT_STAGE + (uint32_t)lane};
-                    const uint32_t rel = t.len ? t.s - a0 : 0u;
-                    const uint32_t last = span ? span - 4u : 0u;
-                    DecResult r = decode_core(LdsSource{stage, last}, rel, t.len, sink, T);
-                    if (r.ok) {
-                        ol = r.len;
-                        const uint32_t first = r.len ? obuf[op0] : 0u, lastc = r.len ? obuf[op0 + r.len - 1] : 0u;
-                        st = soft_bits(is_name, r.len, r.flags, first, lastc);
-                    } else {
-                        ol = kFailLen;
-                        st = kStatusFail;
-                    }
+                    ol = kFailLen;
+                    st = kStatusFail;
                 }
             }
             wave_lds_sync();
@@ -289,14 +288,16 @@ __device__ __forceinline__ void finish_encode(const EncArgs& A, uint32_t i, uint
 
 template <int WAVES, int STAGE>
 __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
-    __shared__ __attribute__((aligned(16))) uint2 s_enc[256];
+    __shared__ __attribute__((aligned(16))) uint2 s_enc[512];  // 256..511: bytes outside a string
     __shared__ __attribute__((aligned(16))) uint32_t s_in[WAVES][STAGE / 4];
-    __shared__ __attribute__((aligned(16))) uint8_t s_out[WAVES][STAGE];
-    load_enc_table(s_enc, WAVES * 64);
+    __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][STAGE / 4 + 4];
+    for (uint32_t k = threadIdx.x; k < 512; k += WAVES * 64)
+        s_enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
     __syncthreads();
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t* stage = s_in[wave];
-    uint8_t* obuf = s_out[wave];
+    uint32_t* obuf32 = s_out[wave];
+    const uint8_t* obuf = reinterpret_cast<const uint8_t*>(obuf32);
     const bool region = A.in_len == nullptr && A.out_off == nullptr;
     const uint64_t stride = (uint64_t)gridDim.x * WAVES * 64;
     for (uint64_t base = ((uint64_t)blockIdx.x * WAVES + wave) * 64; base < A.n; base += stride) {
@@ -318,11 +319,13 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
         uint32_t ol = kFailLen;
         if (span <= STAGE && ospan <= STAGE) {
             stage_span(stage, A.in, A.in_size, a0, span, lane);
+            for (uint32_t k = (uint32_t)lane * 16u; k < ospan + 16u; k += 64u * 16u)
+                *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(obuf32) + k) = make_uint4(0u, 0u, 0u, 0u);
             wave_lds_sync();
-            if (t.valid && t.len <= kMaxStrLen) {
-                LdsSink sink{obuf, op0, op0, 0};
-                ol = encode_core(LdsSource{stage, span ? span - 4u : 0u}, t.len ? t.s - a0 : 0u, t.len, sink, s_enc);
-            }
+            const bool act = t.valid && t.len != 0 && t.len <= kMaxStrLen;
+            const uint32_t r = encode_staged_lane(stage, span ? span - 4u : 0u, t.len ? t.s - a0 : 0u, t.len, act, obuf32,
+                                                  op0, s_enc);
+            if (act) ol = r;
             wave_lds_sync();
             if (region) {
                 region_copy(A.out, a0, obuf, ospan, t.lo, t.hi, lane);
@@ -360,7 +363,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_direct_kernel(EncArgs A) {
 
 // ------------------------------------------------------------------------------------------------
 // launch configuration (LDS per workgroup in brackets)
-//   decode staged:        16 waves/WG, 3 KiB in + 4.5 KiB out per wave   [~142 KiB, 1 WG/CU]
+//   decode staged:        16 waves/WG, 3 KiB in + 4.5 KiB out per wave   [~158 KiB, 1 WG/CU]
 //   decode staged (long):  6 waves/WG, 8 KiB in + 12.9 KiB out per wave [~144 KiB, 1 WG/CU]
 //   decode direct:         4 waves/WG, tables only                        [~17.5 KiB]
 //   encode staged:        16 waves/WG, 3.5 KiB in + out per wave          [~114 KiB, 1 WG/CU]

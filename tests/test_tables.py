@@ -48,7 +48,7 @@ def test_window_lut_matches_tree():
     lut = G.window_lut(root)
     for w in range(1 << G.LUT_BITS):
         e = lut[w]
-        syms = _tree_decode(format(w, "012b"), root)
+        syms = _tree_decode(format(w, "0%db" % G.LUT_BITS), root)
         if not syms:
             assert e & (1 << 29)
             continue

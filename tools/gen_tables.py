@@ -50,7 +50,7 @@ F_INV_NAME = 8
 F_INV_VALUE = 16
 F_UPPER = 32
 
-LUT_BITS = 12  # GPU decode window
+LUT_BITS = 13  # GPU decode window
 
 
 def code_lengths():
@@ -167,11 +167,11 @@ def decode_prefix(root, bits, nbits):
 
 
 def window_lut(root):
-    """GPU decode LUT indexed by the next 12 bits of the stream.
+    """GPU decode LUT indexed by the next LUT_BITS (13) bits of the stream.
 
     u32 entry: [7:0] sym1 | [15:8] sym2 | [19:16] len1 | [23:20] len1+len2 | [24] has2 |
                [25] sym1 name-invalid | [26] sym1 value-invalid | [27] sym2 name-invalid |
-               [28] sym2 value-invalid | [29] LONG (first code longer than 12 bits)
+               [28] sym2 value-invalid | [29] LONG (first code longer than the window)
     EOS (30 bits) never fits a window, so LONG covers it."""
     lut = []
     W = LUT_BITS
@@ -284,7 +284,7 @@ def product_header(lens, codes, order, lut, longt):
     out.append("#define HHUFF_FIRST_LONG_IDX %d  /* index of the first code length > HHUFF_LUT_BITS */"
                % next(i for i, L in enumerate(L_out) if L > LUT_BITS))
     out.append("")
-    out.append("/* decode window LUT, 2^12 x u32: see tools/gen_tables.py:window_lut for the bit layout */")
+    out.append("/* decode window LUT, 2^%d x u32: see tools/gen_tables.py:window_lut for the bit layout */" % LUT_BITS)
     out.append("#define HHUFF_DEC_LUT_INIT { \\")
     out.append(fmt_array(lut, 8, "0x{:08x}u").replace("\n", " \\\n") + " \\\n}")
     out.append("")
