@@ -38,18 +38,69 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=1 << 21, help="strings in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--only", choices=["encode", "decode"], default=None, help="profile one direction")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-host", action="store_true", help="skip the H2D/D2H-inclusive measurement")
     return ap.parse_args()
+
+
+def pmc_traffic(args):
+    """HBM bytes per launch of each hhuff kernel from rocprofv3 PMC counters, one counter per pass
+    (MI355X_MICROARCH.md HBM section): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE
+    reports half the bytes of a wide (16 B/lane) coalesced streaming read, the form of the kernels'
+    input staging, so it is doubled.  Runs this script as a child of rocprofv3 BEFORE this process
+    touches the GPU.  Returns {kernel: bytes} or {} when rocprofv3 is unavailable."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(exe):
+        return {}
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "2", "--warmup", "1",
+             "--no-cpu-baseline", "--no-traffic", "--no-host", "--config", args.config]
+    if args.n:
+        child += ["--n", str(args.n)]
+    vals = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="hhuff_pmc_")
+        try:
+            subprocess.run([exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--"] + child,
+                           check=True, timeout=600, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           env=dict(os.environ, TMPDIR="/tmp"))
+            for root, _, files in os.walk(d):
+                for f in files:
+                    if f.endswith("counter_collection.csv"):
+                        for r in csv.DictReader(open(os.path.join(root, f))):
+                            if "hhuff::" not in r["Kernel_Name"]:
+                                continue
+                            k = "decode" if "decode" in r["Kernel_Name"] else "encode"
+                            vals.setdefault((k, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
+        except Exception:
+            return {}
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    out = {}
+    for k in ("decode", "encode"):
+        f, w = vals.get((k, "FETCH_SIZE")), vals.get((k, "WRITE_SIZE"))
+        if f and w:
+            out[k] = (2.0 * sum(f) / len(f) + sum(w) / len(w)) * 1024.0
+    return out
 
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    traffic = {}
+    if not args.pmc_child and not args.no_traffic and world == 1:
+        traffic = pmc_traffic(args)  # child processes; this process has not touched the GPU yet
     import numpy as np
     import torch
     import torch.distributed as dist
 
     from h2o_amd import codec, synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -182,14 +233,64 @@ def main():
             "encode_gibps": round(P / GIB / (t_enc_avg * 1e-3), 3) if do_enc else None,
             "decode_gibps": round(P_ok / GIB / (t_dec_avg * 1e-3), 3) if do_dec else None,
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
+                         "traffic": round(traffic[dominant]) if dominant in traffic else None,
                          "algorithmic_bytes": B_dec if dominant == "decode" else B_enc},
+            "traffic_bytes_per_launch": {k: round(v) for k, v in traffic.items()} or None,
         }
+        if not args.no_host and not args.pmc_child:
+            line["host_inclusive"] = host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, P_ok, torch)
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(b, args, np)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, P_ok, torch, reps=3):
+    """The same step with the strings starting and ending in pinned host memory: H2D of the inputs,
+    encode + decode, D2H of the outputs, all on one stream (PCIe-bound; recorded in DESIGN.md, never
+    `value`)."""
+    from h2o_amd import codec
+
+    def pin(t):
+        return t.cpu().pin_memory()
+
+    h_plain, h_off, h_huff, h_hoff, h_names = pin(b["data"]), pin(off32), pin(huff[:H]), pin(h_off32), pin(names_bits)
+    d_plain, d_off = torch.empty(P + 16, dtype=torch.uint8, device="cuda"), torch.empty_like(off32)
+    d_huff, d_hoff, d_names = torch.empty(H + 16, dtype=torch.uint8, device="cuda"), torch.empty_like(h_off32), \
+        torch.empty_like(names_bits)
+    e_out = torch.empty(P + 16, dtype=torch.uint8, device="cuda")
+    e_len, e_st = torch.empty(n, dtype=torch.int32, device="cuda"), torch.empty(n, dtype=torch.uint8, device="cuda")
+    d_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
+    d_len, d_st = torch.empty(n_ok, dtype=torch.int32, device="cuda"), torch.empty(n_ok, dtype=torch.uint8, device="cuda")
+    o_enc, o_elen, o_est = torch.empty(P, dtype=torch.uint8).pin_memory(), torch.empty(n, dtype=torch.int32).pin_memory(), \
+        torch.empty(n, dtype=torch.uint8).pin_memory()
+    o_dec, o_dlen, o_dst = torch.empty(d_out.numel(), dtype=torch.uint8).pin_memory(), \
+        torch.empty(n_ok, dtype=torch.int32).pin_memory(), torch.empty(n_ok, dtype=torch.uint8).pin_memory()
+    times = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d_plain[:P].copy_(h_plain, non_blocking=True)
+        d_off.copy_(h_off, non_blocking=True)
+        d_huff[:H].copy_(h_huff, non_blocking=True)
+        d_hoff.copy_(h_hoff, non_blocking=True)
+        d_names.copy_(h_names, non_blocking=True)
+        codec.encode_batch(d_plain, d_off, n, out=e_out, out_len=e_len, status=e_st, in_size=P)
+        codec.decode_batch(d_huff, d_hoff, n_ok, is_name_bits=d_names, out=d_out, out_len=d_len, status=d_st,
+                           in_size=H)
+        o_enc.copy_(e_out[:P], non_blocking=True)
+        o_elen.copy_(e_len, non_blocking=True)
+        o_est.copy_(e_st, non_blocking=True)
+        o_dec.copy_(d_out, non_blocking=True)
+        o_dlen.copy_(d_len, non_blocking=True)
+        o_dst.copy_(d_st, non_blocking=True)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    t = min(times[1:])
+    return {"value": round(P / GIB / t, 3), "unit": "GiB/s", "ms_per_step": round(t * 1e3, 3),
+            "note": "pinned host in/out, H2D + encode + decode + D2H on one stream, best of %d" % reps}
 
 
 def cpu_baseline(b, args, np):

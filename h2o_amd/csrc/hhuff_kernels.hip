@@ -169,7 +169,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     __shared__ uint32_t s_kinfo[32];
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
     __shared__ __attribute__((aligned(16))) uint32_t s_in[WAVES][IN_STAGE / 4];
-    __shared__ __attribute__((aligned(16))) uint8_t s_out[WAVES][OUT_STAGE + 64];  // + one trash byte per lane
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[WAVES][OUT_STAGE + 256];  // + a trash dword per lane
     load_dec_tables(s_lut, s_kinfo, s_ones, WAVES * 64);
     __syncthreads();
     const DecTables T{s_lut, s_kinfo, s_ones};
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
                 const uint32_t rel = t.len ? t.s - a0 : 0u;
                 const uint32_t last = span ? span - 4u : 0u;
                 const DecResult r =
-                    decode_staged_lane(stage, last, rel, t.len, act, obuf, op0, OUT_STAGE + (uint32_t)lane, T);
+                    decode_staged_lane(stage, last, rel, t.len, act, obuf, op0, OUT_STAGE + 4u * (uint32_t)lane, T);
                 if (t.valid && t.len > kMaxStrLen) {
                     ol = kFailLen;
                     st = kStatusTooLong;
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_direct_kernel(EncArgs A) {
 // The variant is picked from the mean bytes per string (in_size / n).
 // ------------------------------------------------------------------------------------------------
 #define DEC_S decode_staged_kernel<16, 3072, 4608>
-#define DEC_L decode_staged_kernel<6, 8192, 13184>
+#define DEC_L decode_staged_kernel<6, 8192, 12928>
 #define DEC_D decode_direct_kernel<4>
 #define ENC_S encode_staged_kernel<16, 3584>
 #define ENC_L encode_staged_kernel<8, 8192>
