@@ -47,6 +47,9 @@ def lib():
         L.hhuff_decode_batch.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]
         L.hhuff_encode_batch.restype = ctypes.c_int
         L.hhuff_encode_batch.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp]
+        L.hhuff_flatten_batch.restype = ctypes.c_int
+        L.hhuff_flatten_batch.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint, _vp, _vp,
+                                          _vp, _vp, _vp]
         L.hhuff_decode_batch_host.restype = ctypes.c_int
         L.hhuff_decode_batch_host.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64,
                                               _vp, _vp, _vp, ctypes.c_int]
@@ -63,6 +66,7 @@ def lib():
 
 # symbols include/hhuff.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decode_batch", "hhuff_encode_batch",
+            "hhuff_flatten_batch",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_version", "hhuff_last_error_string",
             "hhuff_grid_size")
 
@@ -152,6 +156,23 @@ def encode_batch(data, in_off, n, in_len=None, out=None, out_off=None, out_len=N
     _check(lib().hhuff_encode_batch(_dp(data), in_size, _dp(in_off), _dp(in_len), n, _dp(out), _dp(out_off),
                                     _dp(out_len), _dp(status), _stream(stream)), "hhuff_encode_batch")
     return out, out_len, status
+
+
+def flatten_batch(data, in_off, n, prefix_bits=7, in_len=None, first_bytes=None, raw_bits=None, out=None, out_off=None,
+                  out_len=None, in_size=None, stream=None):
+    """Batched QPACK flatten_string / HPACK h2o_hpack_encode_string framing; returns (out, out_len)."""
+    import torch
+
+    dev = data.device
+    in_size = data.numel() if in_size is None else in_size
+    if out is None:
+        out = torch.empty(in_size + 11 * max(n, 1) + 16, dtype=torch.uint8, device=dev)
+    if out_len is None:
+        out_len = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    _check(lib().hhuff_flatten_batch(_dp(data), in_size, _dp(in_off), _dp(in_len), n, _dp(first_bytes), prefix_bits,
+                                     _dp(raw_bits), _dp(out), _dp(out_off), _dp(out_len), _stream(stream)),
+           "hhuff_flatten_batch")
+    return out, out_len
 
 
 # ---------------------------------------------------------------------------------------------------

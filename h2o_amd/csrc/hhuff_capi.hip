@@ -119,6 +119,17 @@ HHUFF_API int hhuff_encode_batch(const uint8_t* in, uint64_t in_size, const uint
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "encode launch");
 }
 
+HHUFF_API int hhuff_flatten_batch(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len,
+                                  uint32_t n, const uint8_t* first_bytes, unsigned prefix_bits, const uint32_t* raw_bits,
+                                  uint8_t* out, const uint32_t* out_off, uint32_t* out_len, void* stream) {
+    int rc = check_batch(in, in_off, n, out, out_len);
+    if (rc) return rc;
+    if (prefix_bits < 1 || prefix_bits > 7) return arg_fail("prefix_bits must be in 1..7");
+    hipError_t e = hhuff::launch_flatten(in, in_size, in_off, in_len, n, first_bytes, prefix_bits, raw_bits, out, out_off,
+                                         out_len, (hipStream_t)stream);
+    return e == hipSuccess ? HHUFF_OK : hip_fail(e, "flatten launch");
+}
+
 // ---------------------------------------------------------------------------------------------------
 // (1) h2o per-string symbols: a batch of one on the thread's stream, synchronously
 // device/pinned layout: [meta 32 B: u32 in_off[2], out_len, is_name word, u8 status][input][output]

@@ -89,8 +89,8 @@ struct RegSink {
     uint64_t acc;  // pending bytes, first byte in bits 0..7
     uint32_t pending, cnt;
     __device__ __forceinline__ void init(uint8_t* dst) { p = dst; acc = 0; pending = 0; cnt = 0; }
-    __device__ __forceinline__ void push(uint32_t bytes, uint32_t k) {
-        acc |= (uint64_t)bytes << (8 * pending);
+    __device__ __forceinline__ void push(uint32_t bytes, uint32_t k) {  // k in 1..4
+        acc |= (uint64_t)(bytes & (0xFFFFFFFFu >> (32 - 8 * k))) << (8 * pending);
         pending += k;
         cnt += k;
         if (__builtin_expect(((uintptr_t)p & 3) != 0, 0)) {

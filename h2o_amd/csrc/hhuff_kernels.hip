@@ -362,6 +362,106 @@ __global__ __launch_bounds__(WAVES * 64) void encode_direct_kernel(EncArgs A) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// string-literal framing: HPACK h2o_hpack_encode_string (hpack.c:816-837) and QPACK flatten_string
+// (qpack.c:1042-1066), batched.  Per string: Huffman iff not flagged raw and strictly shorter
+// (hpack.c:818-821, qpack.c:1046), then [first byte with the H bit | prefix integer][payload].
+// One lane per string, direct global path: a bit-count pass fixes the header length, then the payload
+// is written behind it through the register sink (any destination alignment).
+// ------------------------------------------------------------------------------------------------
+struct FlatArgs {
+    const uint8_t* in;
+    uint64_t in_size;
+    const uint32_t* in_off;
+    const uint32_t* in_len;
+    uint32_t n;
+    const uint8_t* first_bytes;
+    uint32_t prefix_bits;
+    const uint32_t* raw_bits;
+    uint8_t* out;
+    const uint32_t* out_off;
+    uint32_t* out_len;
+};
+
+// RFC 7541 5.1 prefix integer (hpack.c:757-772) OR-ed into first byte h0: up to 6 bytes for v < 2^32
+__device__ __forceinline__ void push_prefix_int(RegSink& sink, uint32_t h0, uint32_t v, uint32_t p) {
+    const uint32_t pmax = (1u << p) - 1u;
+    uint64_t hb;
+    uint32_t hn = 1;
+    if (v < pmax) {
+        hb = h0 | v;
+    } else {
+        hb = h0 | pmax;
+        v -= pmax;
+        while (v >= 128) {
+            hb |= (uint64_t)(0x80u | (v & 127u)) << (8 * hn);
+            ++hn;
+            v >>= 7;
+        }
+        hb |= (uint64_t)v << (8 * hn);
+        ++hn;
+    }
+    sink.push((uint32_t)hb, min(hn, 4u));
+    if (hn > 4) sink.push((uint32_t)(hb >> 32), hn - 4);
+}
+
+__device__ __forceinline__ uint32_t count_code_bits(const GlobalSource& src, uint32_t start, uint32_t len,
+                                                    const uint2* __restrict__ enc) {
+    uint32_t bits = 0;
+    const uint32_t end = start + len;
+    for (uint32_t a = start & ~3u; a < end; a += 4) {
+        const uint32_t w = src.word(a);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t pos = a + k;
+            bits += (pos >= start && pos < end) ? enc[(w >> (8 * k)) & 0xFFu].y : 0u;
+        }
+    }
+    return bits;
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void flatten_direct_kernel(FlatArgs A) {
+    __shared__ __attribute__((aligned(16))) uint2 s_enc[256];
+    load_enc_table(s_enc, WAVES * 64);
+    __syncthreads();
+    const uint32_t p = A.prefix_bits;
+    const GlobalSource src{A.in, A.in_size};
+    const uint64_t stride = (uint64_t)gridDim.x * WAVES * 64;
+    for (uint64_t i = (uint64_t)blockIdx.x * WAVES * 64 + threadIdx.x; i < A.n; i += stride) {
+        const uint32_t s = A.in_off[i];
+        const uint32_t len = A.in_len ? A.in_len[i] : A.in_off[i + 1] - s;
+        const uint32_t first = A.first_bytes ? A.first_bytes[i] : 0u;
+        const bool raw = A.raw_bits ? ((A.raw_bits[i >> 5] >> (i & 31)) & 1u) : false;
+        RegSink sink;
+        sink.init(A.out + (A.out_off ? (uint64_t)A.out_off[i] : (uint64_t)s + 11u * i));
+        if (len > kMaxStrLen) {
+            A.out_len[i] = kFailLen;
+            continue;
+        }
+        const uint32_t bits = (raw || len == 0) ? 0u : count_code_bits(src, s, len, s_enc);
+        const bool huff = !raw && len != 0 && bits <= 8 * len - 8;  // ceil(bits / 8) < len (hpack.c:799-800)
+        if (huff) {
+            push_prefix_int(sink, (first & ~((1u << p) - 1u)) | (1u << p), (bits + 7) >> 3, p);  // qpack.c:1054-1056
+            encode_core(src, s, len, sink, s_enc);
+        } else {
+            push_prefix_int(sink, first & ~((2u << p) - 1u), len, p);  // qpack.c:1048-1049 (hpack.c:806-814)
+            uint32_t a = s & ~3u, rem = len;
+            uint32_t skip = s & 3u;
+            while (rem) {
+                const uint32_t w = src.word(a) >> (8 * skip);
+                const uint32_t k = min(4u - skip, rem);
+                sink.push(w, k);
+                rem -= k;
+                a += 4;
+                skip = 0;
+            }
+            sink.finish();
+        }
+        A.out_len[i] = sink.count();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // launch configuration (LDS per workgroup in brackets)
 //   decode staged:        16 waves/WG, 3 KiB in + 4.5 KiB out per wave   [~158 KiB, 1 WG/CU]
 //   decode staged (long):  6 waves/WG, 8 KiB in + 12.9 KiB out per wave [~144 KiB, 1 WG/CU]
@@ -377,8 +477,9 @@ __global__ __launch_bounds__(WAVES * 64) void encode_direct_kernel(EncArgs A) {
 #define ENC_S encode_staged_kernel<16, 3584>
 #define ENC_L encode_staged_kernel<8, 8192>
 #define ENC_D encode_direct_kernel<4>
+#define FLAT_D flatten_direct_kernel<4>
 
-enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kNumVariants };
+enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kNumVariants };
 
 static const void* variant_fn(int v) {
     switch (v) {
@@ -387,6 +488,7 @@ static const void* variant_fn(int v) {
         case kDecD: return (const void*)DEC_D;
         case kEncS: return (const void*)ENC_S;
         case kEncL: return (const void*)ENC_L;
+        case kFlatD: return (const void*)FLAT_D;
         default: return (const void*)ENC_D;
     }
 }
@@ -462,6 +564,16 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         case kEncL: hipLaunchKernelGGL(ENC_L, dim3(grid), dim3(512), 0, stream, A); break;
         default: hipLaunchKernelGGL(ENC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
+                          const uint8_t* first_bytes, uint32_t prefix_bits, const uint32_t* raw_bits, uint8_t* out,
+                          const uint32_t* out_off, uint32_t* out_len, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    FlatArgs A{in, in_size, in_off, in_len, n, first_bytes, prefix_bits, raw_bits, out, out_off, out_len};
+    const int grid = grid_for(kFlatD, current_device(), n);
+    hipLaunchKernelGGL(FLAT_D, dim3(grid), dim3(256), 0, stream, A);
     return hipGetLastError();
 }
 

@@ -9,5 +9,8 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
                          uint8_t* status, hipStream_t stream);
 hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
                          uint8_t* out, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, hipStream_t stream);
+hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
+                          const uint8_t* first_bytes, uint32_t prefix_bits, const uint32_t* raw_bits, uint8_t* out,
+                          const uint32_t* out_off, uint32_t* out_len, hipStream_t stream);
 int grid_size(int device, int which);
 }  // namespace hhuff

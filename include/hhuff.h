@@ -82,6 +82,21 @@ int hhuff_decode_batch(const uint8_t *in, uint64_t in_size, const uint32_t *in_o
 int hhuff_encode_batch(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, const uint32_t *in_len, uint32_t n,
                        uint8_t *out, const uint32_t *out_off, uint32_t *out_len, uint8_t *status, void *stream);
 
+/* Batched string-literal framing: QPACK flatten_string (lib/http3/qpack.c:1042-1066) and, with
+ * first_bytes == NULL and prefix_bits == 7, HPACK h2o_hpack_encode_string (lib/http2/hpack.c:816-837).
+ * Per string: Huffman when not flagged in raw_bits (QPACK's dont_compress) and strictly shorter, i.e.
+ *   [first & ~(2^p - 1) | 2^p, prefix-int(hufflen)] [Huffman bytes]
+ * else raw:
+ *   [first & ~(2^(p+1) - 1), prefix-int(len)] [the bytes]
+ *   first_bytes  u8[n]: the caller's first byte (bits above the H bit are kept), NULL => 0
+ *   prefix_bits  length-prefix width p in 1..7 (QPACK: 7 values, 5 encoder-stream names, 3 literal names)
+ *   raw_bits     bitmask, NULL => all eligible for Huffman
+ *   out          string i at out + (out_off ? out_off[i] : in_off[i] + 11 * i); region of len_i + 11 bytes
+ *   out_len      u32[n]: framed length */
+int hhuff_flatten_batch(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, const uint32_t *in_len, uint32_t n,
+                        const uint8_t *first_bytes, unsigned prefix_bits, const uint32_t *raw_bits, uint8_t *out,
+                        const uint32_t *out_off, uint32_t *out_len, void *stream);
+
 /* ---------------------------------------------------------------------------------------------
  * (3) batch API, host arrays: pinned staging + H2D, kernels, D2H on an internal stream of `device`.
  *     Synchronous.  Same array contract; `out` is a host buffer sized for the implicit layout

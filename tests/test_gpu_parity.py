@@ -244,3 +244,61 @@ def test_c4_full_size_round_trip(torch_cuda):
     # exact byte equality for the successful strings
     okb = torch.repeat_interleave(ok, lens)
     assert bool((d_out[dec_idx][okb] == b["data"][okb]).all())
+
+
+# ------------------------------------------------------------------------------------------------
+# string-literal framing (HPACK h2o_hpack_encode_string, QPACK flatten_string)
+# ------------------------------------------------------------------------------------------------
+def gpu_flatten(torch, data, off, n, prefix_bits, in_len=None, first=None, raw_bits=None, out_off=None, out_size=None):
+    from h2o_amd import codec
+
+    out = torch.zeros(out_size, dtype=torch.uint8, device="cuda") if out_size else None
+    o, ol = codec.flatten_batch(_dev(torch, data), _dev(torch, off), n, prefix_bits,
+                                in_len=None if in_len is None else _dev(torch, in_len),
+                                first_bytes=None if first is None else _dev(torch, first),
+                                raw_bits=None if raw_bits is None else _dev(torch, raw_bits),
+                                out=out, out_off=None if out_off is None else _dev(torch, out_off),
+                                in_size=int(np.asarray(data).size))
+    torch.cuda.synchronize()
+    return _host(o, np.uint8), _host(ol, np.uint32)[:n]
+
+
+def test_framing_golden(torch_cuda):
+    g = load_golden("framing")
+    strings = synth.unpack(g["fr_in"], g["fr_in_off"])
+    n = len(strings)
+    hp = synth.unpack(g["hpack_out"], g["hpack_out_off"])
+    qp = synth.unpack(g["qpack_out"], g["qpack_out_off"])
+    # HPACK encode_string == flatten(prefix 7, first byte 0, nothing raw)
+    out, ol = gpu_flatten(torch_cuda, g["fr_in"], g["fr_in_off"], n, 7)
+    slots = g["fr_in_off"][:n].astype(np.uint64) + 11 * np.arange(n, dtype=np.uint64)
+    assert [out[int(s):int(s) + int(L)].tobytes() for s, L in zip(slots, ol)] == hp
+    # QPACK flatten_string: per-string prefix width -> one launch per width over (offset, length) pairs
+    lens = np.diff(g["fr_in_off"]).astype(np.uint32)
+    raw_all = g["fr_raw"].astype(bool)
+    for pb in (3, 5, 7):
+        idx = np.nonzero(g["fr_prefix"] == pb)[0]
+        m = len(idx)
+        dst = np.zeros(m, np.uint64)
+        pos = 0
+        for j, i in enumerate(idx):
+            dst[j] = pos
+            pos += int(lens[i]) + 11 + (j % 5)  # odd gaps: destinations at every alignment
+        out, ol = gpu_flatten(torch_cuda, g["fr_in"], g["fr_in_off"][idx].copy(), m, pb, in_len=lens[idx].copy(),
+                              first=g["fr_first"][idx].copy(), raw_bits=synth.bits_from_bools(raw_all[idx]),
+                              out_off=dst.astype(np.uint32), out_size=pos + 16)
+        got = [out[int(d):int(d) + int(L)].tobytes() for d, L in zip(dst, ol)]
+        assert got == [qp[i] for i in idx]
+
+
+@pytest.mark.parametrize("cfg,n,pb", [("c5", 20000, 7), ("c2", 50000, 5), ("c3", 20000, 3)])
+def test_framing_vs_oracle(torch_cuda, oracle_codec, cfg, n, pb):
+    b = synth.make_batch(cfg, n=n, seed=17 + pb, adversarial_frac=0.05)
+    rng = np.random.default_rng(pb)
+    first = rng.integers(0, 256, n, dtype=np.uint8)
+    raw = synth.bits_from_bools(rng.random(n) < 0.1)
+    o_out, o_len = oracle_codec.flatten_batch(b["data"], b["off"], n, pb, first_bytes=first, raw_bits=raw)
+    g_out, g_len = gpu_flatten(torch_cuda, b["data"], b["off"], n, pb, first=first, raw_bits=raw)
+    np.testing.assert_array_equal(g_len, o_len)
+    slots = b["off"][:n].astype(np.uint64) + 11 * np.arange(n, dtype=np.uint64)
+    assert compact(g_out, slots, g_len) == compact(o_out, slots, o_len)
