@@ -20,6 +20,16 @@
 
 namespace hhuff {
 
+#ifndef HHUFF_DEC_LUT64
+#define HHUFF_DEC_LUT64 0
+#endif
+#ifndef HHUFF_DEC_OUTACC
+#define HHUFF_DEC_OUTACC 0
+#endif
+#ifndef HHUFF_DEC_UNROLL2
+#define HHUFF_DEC_UNROLL2 0
+#endif
+
 constexpr uint32_t kLong = 1u << 29;
 constexpr uint32_t kEos = 256;
 constexpr uint32_t kFailLen = 0xFFFFFFFFu;
@@ -238,20 +248,42 @@ __device__ __forceinline__ DecResult decode_staged_lane(const uint32_t* stage, u
     nb += 32;
     a += 4;
     uint32_t R = active ? 8 * len : 0u;  // string bits not yet consumed
-    uint32_t op = op0, flags = 0;
+    uint32_t flags = 0;
     bool fail = false;
-    for (;;) {
+#if HHUFF_DEC_OUTACC
+    // output bytes gather in a 64-bit register and leave as whole dwords OR-ed into the zeroed stage
+    uint32_t* obuf32 = reinterpret_cast<uint32_t*>(obuf);
+    uint64_t oacc = 0;
+    uint32_t opend = op0 & 3u, opw = op0 >> 2, cnt = 0;
+    (void)trash;
+#else
+    uint32_t op = op0;
+#endif
+    auto step = [&]() {
         const uint32_t w = (uint32_t)(buf >> 32);
+#if HHUFF_DEC_LUT64
+        const uint32_t li = w >> (32 - HHUFF_LUT_BITS);
+        const uint2 ep = reinterpret_cast<const uint2*>(T.lut)[li >> 1];  // 64 banks for 8-byte reads
+        const uint32_t e = (li & 1u) ? ep.y : ep.x;
+#else
         const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+#endif
         const uint32_t word = stage[min(a, last) >> 2];  // next refill word, fetched beside the LUT entry
         const bool isl = (e & kLong) != 0;
         const uint32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
         const bool ok1 = active && !isl && L1 <= R;
         const bool two = ok1 && (e & (1u << 24)) != 0 && L12 <= R;
         uint32_t cons = two ? L12 : (ok1 ? L1 : 0u);
+#if HHUFF_DEC_OUTACC
+        oacc |= (uint64_t)(e & (two ? 0xFFFFu : (ok1 ? 0xFFu : 0u))) << (8 * opend);
+        const uint32_t ns = (ok1 ? 1u : 0u) + (two ? 1u : 0u);
+        opend += ns;
+        cnt += ns;
+#else
         obuf[ok1 ? op : trash] = (uint8_t)e;
         obuf[two ? op + 1 : trash] = (uint8_t)(e >> 8);
         op += (ok1 ? 1u : 0u) + (two ? 1u : 0u);
+#endif
         flags |= (e >> 25) & (two ? 15u : (ok1 ? 3u : 0u));
         bool stay = ok1;
         if (__any(active && isl)) {  // wave-uniform: codes longer than the window, EOS
@@ -264,13 +296,26 @@ __device__ __forceinline__ DecResult decode_staged_lane(const uint32_t* stage, u
                 const bool eos = (le & 0x1FFu) == kEos;
                 const bool ok = okL && !eos;
                 fail = fail || (okL && eos);  // EOS inside the string (hpack.c:88-89)
+#if HHUFF_DEC_OUTACC
+                oacc |= (uint64_t)(ok ? (le & 0xFFu) : 0u) << (8 * opend);
+                opend += ok ? 1u : 0u;
+                cnt += ok ? 1u : 0u;
+#else
                 obuf[ok ? op : trash] = (uint8_t)le;
                 op += ok ? 1u : 0u;
+#endif
                 flags |= ok ? ((le >> 14) & 3u) : 0u;
                 cons = ok ? L : 0u;
                 stay = ok;
             }
         }
+#if HHUFF_DEC_OUTACC
+        const uint32_t f = opend >= 4 ? 1u : 0u;
+        atomicOr(&obuf32[opw], f ? (uint32_t)oacc : 0u);
+        oacc >>= 32u * f;
+        opend -= 4u * f;
+        opw += f;
+#endif
         active = active && stay;
         R -= cons;
         buf <<= cons;
@@ -279,8 +324,93 @@ __device__ __forceinline__ DecResult decode_staged_lane(const uint32_t* stage, u
         buf |= (uint64_t)(need ? bswap32(word) : 0u) << ((32 - nb) & 63u);
         nb += need ? 32u : 0u;
         a += need ? 4u : 0u;
+    };
+    for (;;) {
+        step();
+#if HHUFF_DEC_UNROLL2
+        step();
+#endif
         if (!__any(active)) break;
     }
+#if HHUFF_DEC_OUTACC
+    if (opend) atomicOr(&obuf32[opw], (uint32_t)oacc);
+#endif
+    DecResult r;
+    r.ok = !fail && R <= 7 && ((uint32_t)(buf >> 56) | (0xFFu >> R)) == 0xFFu;
+#if HHUFF_DEC_OUTACC
+    r.len = cnt;
+#else
+    r.len = op - op0;
+#endif
+    r.flags = (flags | (flags >> 2)) & 3u;
+    r.status = 0;
+    return r;
+}
+
+// Same as decode_staged_lane with every per-lane predicate held as a 0/1 integer in a VGPR (no lane
+// masks, no SALU mask algebra): selects become multiply-adds, R is kept complemented (nR = ~R) so that
+// "L <= R" is the sign bit of L + nR.  Two steps per vote.
+__device__ __forceinline__ DecResult decode_staged_lane_i(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
+                                                          bool active, uint8_t* obuf, uint32_t op0, uint32_t trash,
+                                                          const DecTables& T) {
+    uint32_t a = start & ~3u;
+    const uint32_t skip = start & 3u;
+    uint64_t buf = (uint64_t)(bswap32(stage[min(a, last) >> 2]) << (8 * skip)) << 32;
+    uint32_t nb = 32 - 8 * skip;
+    a += 4;
+    buf |= (uint64_t)bswap32(stage[min(a, last) >> 2]) << (32 - nb);
+    nb += 32;
+    a += 4;
+    uint32_t nR = ~(active ? 8 * len : 0u);  // ~(string bits not yet consumed)
+    uint32_t act = active ? 1u : 0u;
+    uint32_t op = op0, flags = 0, fail = 0;
+    auto step = [&]() {
+        const uint32_t w = (uint32_t)(buf >> 32);
+        const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+        const uint32_t word = stage[min(a, last) >> 2];
+        const uint32_t isl = (e >> 29) & 1u;
+        const uint32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+        const uint32_t ok1 = act & (isl ^ 1u) & ((L1 + nR) >> 31);                 // L1 <= R
+        const uint32_t two = ok1 & (e >> 24) & ((L12 + nR) >> 31);                 // bit 24 = second symbol
+        uint32_t cons = __umul24(ok1, L1) + __umul24(two, L12 - L1);
+        obuf[trash - __umul24(ok1, trash - op)] = (uint8_t)e;  // trash > op: both mul24 operands < 2^24
+        obuf[trash - __umul24(two, trash - op - 1u)] = (uint8_t)(e >> 8);
+        op += ok1 + two;
+        flags |= (e >> 25) & (3u * ok1 + 12u * two);
+        uint32_t nact = ok1;
+        const uint32_t lact = act & isl;
+        if (__any(lact != 0u)) {  // wave-uniform: codes longer than the window, EOS
+            if (lact) {
+                const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                const uint32_t ki = T.kinfo[k];
+                const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                const uint32_t L = (le >> 9) & 31u;
+                const uint32_t okL = (L + nR) >> 31;
+                const uint32_t eos = (le & 0x1FFu) == kEos ? 1u : 0u;
+                const uint32_t ok = okL & (eos ^ 1u);
+                fail |= okL & eos;  // EOS inside the string (hpack.c:88-89)
+                obuf[trash - __umul24(ok, trash - op)] = (uint8_t)le;
+                op += ok;
+                flags |= ((le >> 14) & 3u) * ok;
+                cons = __umul24(ok, L);
+                nact = ok;
+            }
+        }
+        act = nact;
+        nR += cons;
+        buf <<= cons;
+        nb -= cons;
+        const uint32_t need = (nb - 33u) >> 31;  // nb <= 32
+        buf |= (uint64_t)(bswap32(word) & (0u - need)) << ((32u - nb) & 63u);
+        nb += need << 5;
+        a += need << 2;
+    };
+    for (;;) {
+        step();
+        step();
+        if (!__any(act != 0u)) break;
+    }
+    const uint32_t R = ~nR;
     DecResult r;
     r.ok = !fail && R <= 7 && ((uint32_t)(buf >> 56) | (0xFFu >> R)) == 0xFFu;
     r.len = op - op0;
@@ -416,6 +546,74 @@ __device__ __forceinline__ uint32_t encode_staged_lane(const uint32_t* stage, ui
     }
     if (fail || len == 0 || len > kMaxStrLen) return kFailLen;
     // pad the partial byte with ones (EOS prefix, hpack.c:795-798) and flush the last <= 4 bytes
+    const uint32_t an8 = (an + 7) & ~7u;
+    acc |= (~0ull >> an) & ~(~0ull >> an8);
+    if (an) atomicOr(&obuf32[opw], bswap32((uint32_t)(acc >> 32)));
+    return (tb + 7) >> 3;
+}
+
+// Same contract as encode_staged_lane, with a wave-uniform trip count: `jmax` = the largest number of
+// input dwords over the wave's lanes, so the loop needs no vote; lanes that finished or failed run with
+// every byte masked out (their table entries are {0, 0}).  The first / last dword masks are precomputed.
+__device__ __forceinline__ uint32_t encode_staged_lane_u(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
+                                                         bool active, uint32_t* obuf32, uint32_t opb,
+                                                         const uint2* __restrict__ enc, uint32_t jmax) {
+    const uint32_t end = start + len;
+    const uint32_t a0 = start & ~3u;
+    const uint32_t ndw = active ? (end - a0 + 3u) >> 2 : 0u;
+    const uint32_t mfirst = 0xFFFFFFFFu << (8u * (start & 3u));
+    const uint32_t mlast = (uint32_t)(0xFFFFFFFFull >> ((32u - 8u * (end & 3u)) & 31u));
+    const uint32_t limit = active ? 8 * len - 7 : 0xFFFFFFFFu;
+    uint64_t acc = 0;
+    uint32_t an = 8 * (opb & 3u);
+    uint32_t opw = opb >> 2;
+    uint32_t tb = 0;
+    bool live = active, fail = false;
+    for (uint32_t j = 0; j < jmax; ++j) {
+        const uint32_t w = stage[min(a0 + 4u * j, last) >> 2];
+        uint32_t vm = j == 0 ? mfirst : 0xFFFFFFFFu;
+        vm &= (j + 1 == ndw) ? mlast : 0xFFFFFFFFu;
+        vm = (live && j < ndw) ? vm : 0u;
+        const uint32_t iw = ~vm & 0x01010101u;
+        const uint2 e0 = enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0400u)];
+        const uint2 e1 = enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)];
+        const uint2 e2 = enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)];
+        const uint2 e3 = enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)];
+        const bool lng = max(max(e0.y, e1.y), max(e2.y, e3.y)) > 8;
+        const uint32_t n = e0.y + e1.y + e2.y + e3.y;
+        const bool over = tb + n >= limit;
+        if (__any(lng && !over)) {  // a code longer than 8 bits: byte by byte (wave-uniform detour)
+            if (lng && !over) {
+                const uint2 ek[4] = {e0, e1, e2, e3};
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t nk = ek[k].y;
+                    acc |= (uint64_t)ek[k].x << ((64u - an - nk) & 63u);
+                    an += nk;
+                    tb += nk;
+                    const uint32_t e = an >= 32 ? 1u : 0u;
+                    atomicOr(&obuf32[opw], e ? bswap32((uint32_t)(acc >> 32)) : 0u);
+                    acc <<= 32u * e;
+                    an -= 32u * e;
+                    opw += e;
+                }
+            }
+        }
+        fail = fail || over;
+        live = live && !over;
+        const bool put = live && !lng;
+        const uint32_t c = put ? ((((e0.x << e1.y | e1.x) << e2.y | e2.x) << e3.y) | e3.x) : 0u;
+        const uint32_t nn = put ? n : 0u;
+        acc |= (uint64_t)c << ((64u - an - nn) & 63u);
+        an += nn;
+        tb += nn;
+        const uint32_t e = an >= 32 ? 1u : 0u;
+        atomicOr(&obuf32[opw], e ? bswap32((uint32_t)(acc >> 32)) : 0u);
+        acc <<= 32u * e;
+        an -= 32u * e;
+        opw += e;
+    }
+    if (fail || !active) return kFailLen;
     const uint32_t an8 = (an + 7) & ~7u;
     acc |= (~0ull >> an) & ~(~0ull >> an8);
     if (an) atomicOr(&obuf32[opw], bswap32((uint32_t)(acc >> 32)));

@@ -72,6 +72,78 @@ __device__ __forceinline__ void stage_span(uint32_t* stage, const uint8_t* __res
     }
 }
 
+// Software pipelining across tiles: the next tile's offsets (and is-name word / destination) and its
+// input span are loaded into registers while the current tile is decoded or encoded from LDS, so the
+// wave never sits on a global-memory round trip between tiles.  Nothing on the LDS path of a tile
+// issues a global load, so no vmcnt wait there can be held up by the prefetch.
+#ifdef HHUFF_NO_SPAN_PREFETCH
+constexpr bool kSpanPrefetch = false;  // A/B switch: load the next span only after the current tile
+#else
+constexpr bool kSpanPrefetch = true;
+#endif
+
+struct TileIn {  // per-lane prefetched fields of one tile
+    uint32_t s, len, name_word, dst;
+};
+
+__device__ __forceinline__ TileIn issue_tile(uint64_t base, int lane, uint32_t n, const uint32_t* __restrict__ in_off,
+                                             const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ name_bits,
+                                             const uint32_t* __restrict__ out_off) {
+    TileIn r{0u, 0u, 0u, 0u};
+    const uint64_t i = base + lane;
+    if (i < n) {
+        r.s = in_off[i];
+        r.len = in_len ? in_len[i] : in_off[i + 1];  // end offset for the contiguous layout (minus s later)
+        if (name_bits) r.name_word = name_bits[i >> 5];
+        if (out_off) r.dst = out_off[i];
+    }
+    return r;
+}
+
+__device__ __forceinline__ Tile finish_tile(uint64_t base, int lane, uint32_t n, const TileIn& in, bool pairs) {
+    Tile t;
+    t.i = (uint32_t)base + lane;
+    t.valid = (uint64_t)base + lane < n;
+    t.s = in.s;
+    t.len = t.valid ? (pairs ? in.len : in.len - in.s) : 0u;
+    const bool has = t.valid && t.len != 0;
+    t.lo = wave_min_u32(has ? t.s : 0xFFFFFFFFu);
+    t.hi = wave_max_u32(has ? t.s + t.len : 0u);
+    return t;
+}
+
+template <int NCH>
+struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lane per KiB
+    uint4 v[NCH];
+    __device__ __forceinline__ void issue(const uint8_t* __restrict__ in, uint64_t in_size, uint32_t a0, uint32_t span,
+                                          int lane) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const uint32_t k = (uint32_t)c * 1024u + (uint32_t)lane * 16u;
+            const uint64_t g = (uint64_t)a0 + k;
+            if (k < span && g + 16 <= in_size) v[c] = *reinterpret_cast<const uint4*>(in + g);
+        }
+    }
+    __device__ __forceinline__ void commit(uint32_t* stage, const uint8_t* __restrict__ in, uint64_t in_size, uint32_t a0,
+                                           uint32_t span, int lane) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const uint32_t k = (uint32_t)c * 1024u + (uint32_t)lane * 16u;
+            if (k < span) {
+                const uint64_t g = (uint64_t)a0 + k;
+                uint4 x = v[c];
+                if (g + 16 > in_size) {  // the chunk holding the end of the input buffer
+                    uint32_t w[4] = {0, 0, 0, 0};
+                    for (uint32_t b = 0; b < 16; ++b)
+                        if (g + b < in_size) w[b >> 2] |= (uint32_t)in[g + b] << (8 * (b & 3));
+                    x = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(stage) + k) = x;
+            }
+        }
+    }
+};
+
 // Write LDS bytes [0, ospan) to global [gbase, gbase + ospan) (gbase 16-aligned), keeping only the
 // global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
 __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds, uint32_t ospan,
@@ -177,66 +249,116 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     uint32_t* stage = s_in[wave];
     uint8_t* obuf = s_out[wave];
     const bool region = A.in_len == nullptr && A.out_off == nullptr;
+    const bool pairs = A.in_len != nullptr;
     const uint64_t stride = (uint64_t)gridDim.x * WAVES * 64;
-    for (uint64_t base = ((uint64_t)blockIdx.x * WAVES + wave) * 64; base < A.n; base += stride) {
-        const Tile t = load_tile(base, lane, A.n, A.in_off, A.in_len);
-        const bool is_name = t.valid && A.is_name_bits ? ((A.is_name_bits[t.i >> 5] >> (t.i & 31)) & 1u) : false;
-        const uint32_t a0 = t.lo & ~15u;
-        const uint32_t span = t.hi > t.lo ? ((t.hi + 15u) & ~15u) - a0 : 0u;
-        // output stage layout
-        uint64_t dst_g = 0, obase = 0, olo = 0, ohi = 0;
-        uint32_t op0, ospan;
+    uint64_t base = ((uint64_t)blockIdx.x * WAVES + wave) * 64;
+    if (base >= A.n) return;
+
+    // per-tile layout: input span and output stage extent
+    struct Plan {
+        Tile t;
+        uint32_t a0, span, op0, ospan;
+        uint64_t obase, olo, ohi, dst_g;
+        bool fits;
+    };
+    auto plan = [&](uint64_t b, const TileIn& ti) {
+        Plan P;
+        P.t = finish_tile(b, lane, A.n, ti, pairs);
+        const Tile& t = P.t;
+        P.a0 = t.lo & ~15u;
+        P.span = t.hi > t.lo ? ((t.hi + 15u) & ~15u) - P.a0 : 0u;
+        P.obase = P.olo = P.ohi = P.dst_g = 0;
         if (region) {
-            olo = dec_slot(t.lo);
-            ohi = dec_slot(t.hi);
-            obase = olo & ~15ull;
-            ospan = t.hi > t.lo ? (uint32_t)(ohi - obase) : 0u;
-            op0 = t.len ? (uint32_t)(dec_slot(t.s) - obase) : 0u;
+            P.olo = dec_slot(t.lo);
+            P.ohi = dec_slot(t.hi);
+            P.obase = P.olo & ~15ull;
+            P.ospan = t.hi > t.lo ? (uint32_t)(P.ohi - P.obase) : 0u;
+            P.op0 = t.len ? (uint32_t)(dec_slot(t.s) - P.obase) : 0u;
         } else {
-            dst_g = A.out_off ? (uint64_t)(t.valid ? A.out_off[t.i] : 0u) : dec_slot(t.s);
+            P.dst_g = A.out_off ? (uint64_t)ti.dst : dec_slot(t.s);
             const uint32_t cap = t.valid ? (uint32_t)(((uint64_t)min(t.len, kMaxStrLen) * 8u) / 5u) + 3u : 0u;
             const uint32_t pre = wave_excl_scan(cap, lane);
-            ospan = __shfl(pre + cap, 63, 64);
-            op0 = pre + ((uint32_t)(((uintptr_t)A.out + dst_g) - pre) & 3u);
+            P.ospan = __shfl(pre + cap, 63, 64);
+            P.op0 = pre + ((uint32_t)(((uintptr_t)A.out + P.dst_g) - pre) & 3u);
         }
+        P.fits = P.span <= IN_STAGE && P.ospan <= OUT_STAGE;
+        return P;
+    };
+
+    SpanPrefetch<(IN_STAGE + 1023) / 1024> pf;
+    TileIn ti = issue_tile(base, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
+    Plan cur = plan(base, ti);
+    uint32_t cur_name = ti.name_word;
+    if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
+    if (base + stride < A.n) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
+    if (cur.fits) pf.commit(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+    for (;;) {
+        const uint64_t nbase = base + stride;
+        const bool have_next = nbase < A.n;
+        Plan nxt;
+        uint32_t nxt_name = 0;
+        if (have_next) {
+            nxt = plan(nbase, ti);
+            nxt_name = ti.name_word;
+            if (kSpanPrefetch && nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+            if (nbase + stride < A.n)
+                ti = issue_tile(nbase + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
+        }
+        // ---- the current tile ----
+        const Tile& t = cur.t;
+        const bool is_name = t.valid && A.is_name_bits ? ((cur_name >> (t.i & 31)) & 1u) : false;
         uint32_t ol = 0;
         uint8_t st = 0;
-        if (span <= IN_STAGE && ospan <= OUT_STAGE) {
-            stage_span(stage, A.in, A.in_size, a0, span, lane);
+        if (cur.fits) {
+#if HHUFF_DEC_OUTACC
+            for (uint32_t k = (uint32_t)lane * 16u; k < cur.ospan + 16u; k += 64u * 16u)
+                *reinterpret_cast<uint4*>(obuf + k) = make_uint4(0u, 0u, 0u, 0u);
+#endif
             wave_lds_sync();
-            {
-                const bool act = t.valid && t.len <= kMaxStrLen;
-                const uint32_t rel = t.len ? t.s - a0 : 0u;
-                const uint32_t last = span ? span - 4u : 0u;
-                const DecResult r =
-                    decode_staged_lane(stage, last, rel, t.len, act, obuf, op0, OUT_STAGE + 4u * (uint32_t)lane, T);
-                if (t.valid && t.len > kMaxStrLen) {
-                    ol = kFailLen;
-                    st = kStatusTooLong;
-                } else if (r.ok) {
-                    ol = r.len;
-                    const uint32_t first = r.len ? obuf[op0] : 0u, lastc = r.len ? obuf[op0 + r.len - 1] : 0u;
-                    st = soft_bits(is_name, r.len, r.flags, first, lastc);
-                } else {
-                    ol = kFailLen;
-                    st = kStatusFail;
-                }
+            const bool act = t.valid && t.len <= kMaxStrLen;
+            const uint32_t rel = t.len ? t.s - cur.a0 : 0u;
+            const uint32_t last = cur.span ? cur.span - 4u : 0u;
+#if HHUFF_DEC_VOTE1
+            const DecResult r =
+                decode_staged_lane(stage, last, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
+#else
+            const DecResult r =
+                decode_staged_lane_i(stage, last, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
+#endif
+            if (t.valid && t.len > kMaxStrLen) {
+                ol = kFailLen;
+                st = kStatusTooLong;
+            } else if (r.ok) {
+                ol = r.len;
+                const uint32_t first = r.len ? obuf[cur.op0] : 0u, lastc = r.len ? obuf[cur.op0 + r.len - 1] : 0u;
+                st = soft_bits(is_name, r.len, r.flags, first, lastc);
+            } else {
+                ol = kFailLen;
+                st = kStatusFail;
             }
             wave_lds_sync();
             if (region) {
-                region_copy(A.out, obase, obuf, ospan, olo, ohi, lane);
+                region_copy(A.out, cur.obase, obuf, cur.ospan, cur.olo, cur.ohi, lane);
             } else if (t.valid && ol != kFailLen) {
-                lane_copy(A.out + dst_g, obuf + op0, ol);
+                lane_copy(A.out + cur.dst_g, obuf + cur.op0, ol);
             }
             wave_lds_sync();
         } else if (t.valid) {
-            const uint64_t d = A.out_off ? (uint64_t)A.out_off[t.i] : dec_slot(t.s);
+            const uint64_t d = A.out_off ? cur.dst_g : dec_slot(t.s);
             decode_direct(A, t.s, t.len, is_name, A.out + d, T, ol, st);
         }
         if (t.valid) {
             A.out_len[t.i] = ol;
             A.status[t.i] = st;
         }
+        if (!have_next) break;
+        if (nxt.fits) {
+            if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+            pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+        }
+        cur = nxt;
+        cur_name = nxt_name;
+        base = nbase;
     }
 }
 
@@ -299,46 +421,90 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
     uint32_t* obuf32 = s_out[wave];
     const uint8_t* obuf = reinterpret_cast<const uint8_t*>(obuf32);
     const bool region = A.in_len == nullptr && A.out_off == nullptr;
+    const bool pairs = A.in_len != nullptr;
     const uint64_t stride = (uint64_t)gridDim.x * WAVES * 64;
-    for (uint64_t base = ((uint64_t)blockIdx.x * WAVES + wave) * 64; base < A.n; base += stride) {
-        const Tile t = load_tile(base, lane, A.n, A.in_off, A.in_len);
-        const uint32_t a0 = t.lo & ~15u;
-        const uint32_t span = t.hi > t.lo ? ((t.hi + 15u) & ~15u) - a0 : 0u;
-        uint64_t dst_g = 0;
-        uint32_t op0, ospan;
+    uint64_t base = ((uint64_t)blockIdx.x * WAVES + wave) * 64;
+    if (base >= A.n) return;
+
+    struct Plan {
+        Tile t;
+        uint32_t a0, span, op0, ospan;
+        uint64_t dst_g;
+        bool fits;
+    };
+    auto plan = [&](uint64_t b, const TileIn& ti) {
+        Plan P;
+        P.t = finish_tile(b, lane, A.n, ti, pairs);
+        const Tile& t = P.t;
+        P.a0 = t.lo & ~15u;
+        P.span = t.hi > t.lo ? ((t.hi + 15u) & ~15u) - P.a0 : 0u;
+        P.dst_g = 0;
         if (region) {  // output slot = input offset: the output stage mirrors the input stage
-            ospan = span;
-            op0 = t.len ? t.s - a0 : 0u;
+            P.ospan = P.span;
+            P.op0 = t.len ? t.s - P.a0 : 0u;
         } else {
-            dst_g = A.out_off ? (uint64_t)(t.valid ? A.out_off[t.i] : 0u) : (uint64_t)t.s;
+            P.dst_g = A.out_off ? (uint64_t)ti.dst : (uint64_t)t.s;
             const uint32_t cap = t.valid ? min(t.len, kMaxStrLen) + 3u : 0u;
             const uint32_t pre = wave_excl_scan(cap, lane);
-            ospan = __shfl(pre + cap, 63, 64);
-            op0 = pre + ((uint32_t)(((uintptr_t)A.out + dst_g) - pre) & 3u);
+            P.ospan = __shfl(pre + cap, 63, 64);
+            P.op0 = pre + ((uint32_t)(((uintptr_t)A.out + P.dst_g) - pre) & 3u);
         }
+        P.fits = P.span <= STAGE && P.ospan <= STAGE;
+        return P;
+    };
+
+    SpanPrefetch<(STAGE + 1023) / 1024> pf;
+    TileIn ti = issue_tile(base, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
+    Plan cur = plan(base, ti);
+    if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
+    if (base + stride < A.n) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
+    if (cur.fits) pf.commit(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+    for (;;) {
+        const uint64_t nbase = base + stride;
+        const bool have_next = nbase < A.n;
+        Plan nxt;
+        if (have_next) {
+            nxt = plan(nbase, ti);
+            if (kSpanPrefetch && nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+            if (nbase + stride < A.n) ti = issue_tile(nbase + stride, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
+        }
+        // ---- the current tile ----
+        const Tile& t = cur.t;
         uint32_t ol = kFailLen;
-        if (span <= STAGE && ospan <= STAGE) {
-            stage_span(stage, A.in, A.in_size, a0, span, lane);
-            for (uint32_t k = (uint32_t)lane * 16u; k < ospan + 16u; k += 64u * 16u)
+        if (cur.fits) {
+            for (uint32_t k = (uint32_t)lane * 16u; k < cur.ospan + 16u; k += 64u * 16u)
                 *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(obuf32) + k) = make_uint4(0u, 0u, 0u, 0u);
             wave_lds_sync();
             const bool act = t.valid && t.len != 0 && t.len <= kMaxStrLen;
-            const uint32_t r = encode_staged_lane(stage, span ? span - 4u : 0u, t.len ? t.s - a0 : 0u, t.len, act, obuf32,
-                                                  op0, s_enc);
+            const uint32_t rel = t.len ? t.s - cur.a0 : 0u;
+            const uint32_t last = cur.span ? cur.span - 4u : 0u;
+#ifdef HHUFF_ENC_VOTE_LOOP
+            const uint32_t r = encode_staged_lane(stage, last, rel, t.len, act, obuf32, cur.op0, s_enc);
+#else
+            const uint32_t jmax = wave_max_u32(act ? ((rel + t.len - (rel & ~3u) + 3u) >> 2) : 0u);
+            const uint32_t r = encode_staged_lane_u(stage, last, rel, t.len, act, obuf32, cur.op0, s_enc, jmax);
+#endif
             if (act) ol = r;
             wave_lds_sync();
             if (region) {
-                region_copy(A.out, a0, obuf, ospan, t.lo, t.hi, lane);
+                region_copy(A.out, cur.a0, obuf, cur.ospan, t.lo, t.hi, lane);
             } else if (t.valid && ol != kFailLen) {
-                lane_copy(A.out + dst_g, obuf + op0, ol);
+                lane_copy(A.out + cur.dst_g, obuf + cur.op0, ol);
             }
             wave_lds_sync();
         } else if (t.valid && t.len <= kMaxStrLen) {
             RegSink sink;
-            sink.init(A.out + (A.out_off ? (uint64_t)A.out_off[t.i] : (uint64_t)t.s));
+            sink.init(A.out + (A.out_off ? cur.dst_g : (uint64_t)t.s));
             ol = encode_core(GlobalSource{A.in, A.in_size}, t.s, t.len, sink, s_enc);
         }
         if (t.valid) finish_encode(A, t.i, t.len, ol);
+        if (!have_next) break;
+        if (nxt.fits) {
+            if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+            pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+        }
+        cur = nxt;
+        base = nbase;
     }
 }
 
@@ -358,6 +524,205 @@ __global__ __launch_bounds__(WAVES * 64) void encode_direct_kernel(EncArgs A) {
             ol = encode_core(GlobalSource{A.in, A.in_size}, s, len, sink, s_enc);
         }
         finish_encode(A, (uint32_t)i, len, ol);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Byte-balanced encode for the implicit contiguous layout (out_off == NULL, in_len == NULL).
+// A tile is K consecutive strings; its input span is staged in LDS and split into 16-byte chunks,
+// one per lane (every lane does the same work whatever the string lengths).  Per chunk round:
+//   A. each lane looks up its 16 bytes' {code, nbits} and sums the bits; a wave exclusive scan gives
+//      every chunk its bit offset G inside the tile's concatenated code stream;
+//   B. the lane that holds a string's first byte records gbase[s] = G at that byte (LDS);
+//   C. each lane emits its codes at bit 8 * start[s] + (G - gbase[s]) of the string's slot in the
+//      zeroed LDS output stage (slot = input offset, h2o's contract), OR-ing whole dwords (ds_or_b32) so
+//      neighbouring lanes and strings never overwrite each other.  Codes that would end past the
+//      string's capacity (8 * len bits) are dropped: that string fails anyway.
+// Finally gbase[s+1] - gbase[s] is each string's code length: Huffman length = ceil(bits / 8) when it is
+// strictly shorter than the string (hpack.c:789-800), else SIZE_MAX; the last byte is padded with ones.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ void chunk_flush(uint32_t* obuf32, uint64_t& acc, uint32_t& fill, uint32_t& dw) {
+    if (fill >= 32) {
+        atomicOr(&obuf32[dw], bswap32((uint32_t)(acc >> 32)));
+        acc <<= 32;
+        fill -= 32;
+        dw += 1;
+    }
+}
+
+template <int WAVES, int STAGE, int KMAX>
+__global__ __launch_bounds__(WAVES * 64) void encode_chunked_kernel(EncArgs A, uint32_t K) {
+    __shared__ __attribute__((aligned(16))) uint2 s_enc[512];  // 256..511: bytes outside any string
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[WAVES][STAGE / 4];
+    __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][STAGE / 4 + 4];
+    __shared__ uint32_t s_start[WAVES][KMAX + 1];  // string starts relative to the span start, + end
+    __shared__ uint32_t s_gbase[WAVES][KMAX + 1];  // tile bit offset at each string start, + total
+    for (uint32_t k = threadIdx.x; k < 512; k += WAVES * 64)
+        s_enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t* stage = s_in[wave];
+    uint32_t* obuf32 = s_out[wave];
+    uint32_t* start = s_start[wave];
+    uint32_t* gbase = s_gbase[wave];
+    const uint64_t ntiles = ((uint64_t)A.n + K - 1) / K;
+    for (uint64_t tile = (uint64_t)blockIdx.x * WAVES + wave; tile < ntiles; tile += (uint64_t)gridDim.x * WAVES) {
+        const uint64_t t0 = tile * K;
+        const uint32_t ns = (uint32_t)min((uint64_t)K, (uint64_t)A.n - t0);
+        const uint32_t lo = A.in_off[t0], hi = A.in_off[t0 + ns];
+        const uint32_t a0 = lo & ~15u;
+        const uint32_t span = ((hi + 15u) & ~15u) - a0;
+        if (span > STAGE) {  // a tile of long strings: one lane per string, straight from global memory
+            for (uint32_t j = lane; j < ns; j += 64) {
+                const uint32_t i = (uint32_t)t0 + j, s = A.in_off[i], len = A.in_off[i + 1] - s;
+                uint32_t ol = kFailLen;
+                if (len <= kMaxStrLen) {
+                    RegSink sink;
+                    sink.init(A.out + s);
+                    ol = encode_core(GlobalSource{A.in, A.in_size}, s, len, sink, s_enc);
+                }
+                finish_encode(A, i, len, ol);
+            }
+            continue;
+        }
+        for (uint32_t j = lane; j <= ns; j += 64) start[j] = A.in_off[t0 + j] - a0;
+        stage_span(stage, A.in, A.in_size, a0, span, lane);
+        for (uint32_t k = (uint32_t)lane * 16u; k < span + 16u; k += 64u * 16u)
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(obuf32) + k) = make_uint4(0u, 0u, 0u, 0u);
+        wave_lds_sync();
+        const uint32_t sbeg = start[0], send = start[ns];  // bytes outside [sbeg, send) belong to no string
+        uint32_t carry = 0;
+        for (uint32_t c0 = 0; c0 < span; c0 += 1024u) {
+            const uint32_t p = c0 + 16u * (uint32_t)lane;  // this lane's chunk [p, p + 16)
+            const bool live = p < span;
+            // ---- A: lookups and bit totals per dword ----
+            uint32_t cd[4], nd[4], lng = 0;
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t pos = p + 4u * d;
+                const uint32_t w = live ? stage[pos >> 2] : 0u;
+                const int32_t dlo = (int32_t)(sbeg - pos), dhi = (int32_t)(send - pos);
+                const uint32_t nlo = (uint32_t)min(max(dlo, 0), 4), nhi = live ? (uint32_t)min(max(dhi, 0), 4) : 0u;
+                const uint32_t vm = (uint32_t)(0xFFFFFFFFull >> (8 * (4 - nhi))) & (uint32_t)(0xFFFFFFFFull << (8 * nlo));
+                const uint32_t iw = ~vm & 0x01010101u;
+                const uint2 e0 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0400u)];
+                const uint2 e1 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)];
+                const uint2 e2 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)];
+                const uint2 e3 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)];
+                nd[d] = e0.y + e1.y + e2.y + e3.y;
+                cd[d] = (((e0.x << e1.y | e1.x) << e2.y | e2.x) << e3.y) | e3.x;
+                lng |= (max(max(e0.y, e1.y), max(e2.y, e3.y)) > 8 ? 1u : 0u) << d;
+            }
+            const uint32_t tot = nd[0] + nd[1] + nd[2] + nd[3];
+            const uint32_t excl = wave_excl_scan(tot, lane);
+            const uint32_t G0 = carry + excl;
+            carry += __shfl(excl + tot, 63, 64);
+            // ---- B: record gbase for every string that starts in [p, p + 16) ----
+            // first string index with start >= p (binary search over start[0..ns))
+            uint32_t lo_i = 0, hi_i = ns;
+            while (lo_i < hi_i) {
+                const uint32_t mid = (lo_i + hi_i) >> 1;
+                if (start[mid] < p) lo_i = mid + 1;
+                else hi_i = mid;
+            }
+            const uint32_t sfirst = lo_i;
+            if (live) {
+                for (uint32_t j = sfirst; j < ns && start[j] < p + 16u; ++j) {
+                    const uint32_t q = start[j];  // bits of the chunk bytes before q
+                    uint32_t bits = 0;
+                    for (uint32_t b = p; b < q; ++b) {
+                        const uint32_t byte = (stage[b >> 2] >> (8 * (b & 3u))) & 0xFFu;
+                        bits += (b >= sbeg && b < send) ? s_enc[byte].y : 0u;
+                    }
+                    gbase[j] = G0 + bits;
+                }
+            }
+            wave_lds_sync();
+            // ---- C: emit ----
+            if (live) {
+                // the string holding byte p: last s with start[s] <= p and start[s+1] > p
+                int32_t s = (int32_t)sfirst;
+                if (s < (int32_t)ns && start[s] == p) {
+                    while (s + 1 < (int32_t)ns && start[s + 1] == p) ++s;  // skip empty strings at p
+                } else {
+                    s -= 1;
+                }
+                uint32_t G = G0;
+                uint64_t acc = 0;
+                uint32_t fill = 0, dw = 0, rel = 0, capb = 0, nxt = sbeg;
+                bool open = false;
+                auto open_seg = [&](int32_t si) {
+                    const uint32_t st = start[si];
+                    nxt = start[si + 1];
+                    rel = G - gbase[si];
+                    capb = 8u * (nxt - st);
+                    const uint32_t P = 8u * st + rel;
+                    acc = 0;
+                    fill = P & 31u;
+                    dw = P >> 5;
+                    open = true;
+                };
+                auto close_seg = [&]() {
+                    if (open && fill) atomicOr(&obuf32[dw], bswap32((uint32_t)(acc >> 32)));
+                    open = false;
+                };
+                if (s >= 0 && s < (int32_t)ns && p < start[s + 1]) open_seg(s);
+                else nxt = s < 0 ? sbeg : 0xFFFFFFFFu;  // before the first string / past the last
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const uint32_t pos = p + 4u * d;
+                    if (open && pos + 4u <= nxt && !((lng >> d) & 1u)) {  // whole dword in one string, short codes
+                        if (rel + nd[d] <= capb) {
+                            acc |= (uint64_t)cd[d] << ((64u - fill - nd[d]) & 63u);
+                            fill += nd[d];
+                            chunk_flush(obuf32, acc, fill, dw);
+                        }
+                        rel += nd[d];
+                        G += nd[d];
+                    } else {
+                        const uint32_t w = stage[pos >> 2];
+                        for (uint32_t k = 0; k < 4; ++k) {
+                            const uint32_t b = pos + k;
+                            if (b >= send) break;
+                            if (b >= nxt || (!open && b >= sbeg)) {  // a string starts here
+                                close_seg();
+                                int32_t si = s < 0 ? 0 : s + 1;
+                                while (si + 1 < (int32_t)ns && start[si + 1] <= b) ++si;  // skip empty strings
+                                s = si;
+                                open_seg(si);
+                            }
+                            if (!open) continue;
+                            const uint2 e = s_enc[(w >> (8 * k)) & 0xFFu];
+                            if (rel + e.y <= capb) {
+                                acc |= (uint64_t)e.x << ((64u - fill - e.y) & 63u);
+                                fill += e.y;
+                                chunk_flush(obuf32, acc, fill, dw);
+                            }
+                            rel += e.y;
+                            G += e.y;
+                        }
+                    }
+                }
+                close_seg();
+            }
+        }
+        if (lane == 0) gbase[ns] = carry;
+        wave_lds_sync();
+        // ---- per string: length, verdict, padding ----
+        for (uint32_t j = lane; j < ns; j += 64) {
+            const uint32_t T = gbase[j + 1] - gbase[j], len = start[j + 1] - start[j];
+            const bool ok = len != 0 && T + 8u <= 8u * len;  // ceil(T / 8) < len
+            if (ok && (T & 7u)) {  // ones after the last code up to the byte boundary (hpack.c:795-798)
+                const uint32_t P = 8u * start[j] + T;
+                const uint32_t nbit = 8u - (P & 7u);  // 1..7, inside one byte
+                const uint32_t mask = ((1u << nbit) - 1u) << (31u - (P & 31u) - (nbit - 1u));
+                atomicOr(&obuf32[P >> 5], bswap32(mask));
+            }
+            finish_encode(A, (uint32_t)t0 + j, len, ok ? (T + 7u) >> 3 : kFailLen);
+        }
+        wave_lds_sync();
+        region_copy(A.out, a0, reinterpret_cast<const uint8_t*>(obuf32), span, lo, hi, lane);
+        wave_lds_sync();
     }
 }
 
@@ -478,8 +843,10 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_direct_kernel(FlatArgs A) 
 #define ENC_L encode_staged_kernel<8, 8192>
 #define ENC_D encode_direct_kernel<4>
 #define FLAT_D flatten_direct_kernel<4>
+#define ENC_C encode_chunked_kernel<12, 4096, 128>
+#define ENC_CL encode_chunked_kernel<8, 8192, 64>
 
-enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kNumVariants };
+enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncC, kEncCL, kNumVariants };
 
 static const void* variant_fn(int v) {
     switch (v) {
@@ -489,6 +856,8 @@ static const void* variant_fn(int v) {
         case kEncS: return (const void*)ENC_S;
         case kEncL: return (const void*)ENC_L;
         case kFlatD: return (const void*)FLAT_D;
+        case kEncC: return (const void*)ENC_C;
+        case kEncCL: return (const void*)ENC_CL;
         default: return (const void*)ENC_D;
     }
 }
@@ -498,6 +867,8 @@ static int variant_threads(int v) {
         case kEncS: return 1024;
         case kDecL: return 384;
         case kEncL: return 512;
+        case kEncC: return 768;
+        case kEncCL: return 512;
         default: return 256;
     }
 }
@@ -557,6 +928,23 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
                          uint8_t* out, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     EncArgs A{in, in_size, in_off, in_len, n, out, out_off, out_len, status};
+#ifdef HHUFF_ENCODE_CHUNKED
+    if (in_len == nullptr && out_off == nullptr) {  // contiguous implicit layout: byte-balanced chunks
+        const uint64_t mean = in_size / n;
+        const bool big = mean > 96;
+        const uint32_t stage = big ? 8192u : 4096u, kmax = big ? 64u : 128u;
+        const uint64_t k = mean ? (stage * 3u / 5u) / mean : kmax;
+        const uint32_t K = (uint32_t)(k < 1 ? 1 : (k > kmax ? kmax : k));
+        const uint64_t tiles = ((uint64_t)n + K - 1) / K;
+        const int v = big ? kEncCL : kEncC;
+        const int waves = big ? 8 : 12;
+        const int g = grid_for(v, current_device(), 0xFFFFFFFFu);
+        const int grid = (int)((tiles + waves - 1) / waves < (uint64_t)g ? (tiles + waves - 1) / waves : g);
+        if (big) hipLaunchKernelGGL(ENC_CL, dim3(grid), dim3(512), 0, stream, A, K);
+        else hipLaunchKernelGGL(ENC_C, dim3(grid), dim3(768), 0, stream, A, K);
+        return hipGetLastError();
+    }
+#endif
     const int v = pick_encode(in_size, n);
     const int grid = grid_for(v, current_device(), n);
     switch (v) {

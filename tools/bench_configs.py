@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Secondary measurements for the other BASELINE.json configurations (the headline is bench.py, config 4):
+  c2  1M strings mean 32 B, decode only
+  c3  1M strings Zipf 8..512 B, encode + decode round trip, P / (t_enc + t_dec)
+  c5  512K QPACK values mean 512 B (cookie/URI charset), encode only with flatten_string(prefix 7) framing
+Prints one JSON line per config.  Device-resident, HIP-event timing on the launch stream."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GIB = float(1 << 30)
+
+
+def timed(torch, fn, steps=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    t = sorted(a.elapsed_time(b) for a, b in ev)
+    return t[len(t) // 2]
+
+
+def packed_huffman(torch, codec, b):
+    """encode once, keep the compressible strings packed contiguously (the wire)"""
+    n, P = b["n"], int(b["total"])
+    off32 = b["off"].to(torch.int32)
+    lens = b["off"][1:] - b["off"][:-1]
+    _, el, _ = codec.encode_batch(b["data"], off32, n, in_size=P)
+    idx = torch.nonzero(el != -1).squeeze(1)
+    hl = el[idx].to(torch.int64)
+    h_off = torch.zeros(idx.numel() + 1, dtype=torch.int64, device="cuda")
+    h_off[1:] = torch.cumsum(hl, 0)
+    H = int(h_off[-1].item())
+    huff = torch.empty(H + 16, dtype=torch.uint8, device="cuda")
+    codec.encode_batch(b["data"], off32[idx].contiguous(), idx.numel(), in_len=lens[idx].to(torch.int32).contiguous(),
+                       out=huff, out_off=h_off[:-1].to(torch.int32).contiguous(), in_size=P)
+    return huff, h_off.to(torch.int32), int(idx.numel()), H, int(lens[idx].sum().item())
+
+
+def main():
+    import torch
+
+    from h2o_amd import codec, synth
+
+    torch.cuda.set_device(0)
+    cfgs = sys.argv[1:] or ["c2", "c3", "c5"]
+    for cfg in cfgs:
+        b = synth.make_batch_torch(cfg, seed=7)
+        n, P = b["n"], int(b["total"])
+        off32 = b["off"].to(torch.int32)
+        line = {"config": cfg, "strings": n, "plain_bytes": P}
+        if cfg in ("c2", "c3"):
+            huff, h_off, n_ok, H, P_ok = packed_huffman(torch, codec, b)
+            d_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
+            d_len = torch.empty(n_ok, dtype=torch.int32, device="cuda")
+            d_st = torch.empty(n_ok, dtype=torch.uint8, device="cuda")
+            t_dec = timed(torch, lambda: codec.decode_batch(huff, h_off, n_ok, out=d_out, out_len=d_len, status=d_st,
+                                                            in_size=H))
+            line.update(decode_ms=round(t_dec, 4), decode_gibps=round(P_ok / GIB / (t_dec * 1e-3), 2),
+                        huffman_bytes=H)
+            if cfg == "c3":
+                e_out = torch.empty(P + 16, dtype=torch.uint8, device="cuda")
+                e_len = torch.empty(n, dtype=torch.int32, device="cuda")
+                e_st = torch.empty(n, dtype=torch.uint8, device="cuda")
+                t_enc = timed(torch, lambda: codec.encode_batch(b["data"], off32, n, out=e_out, out_len=e_len,
+                                                                status=e_st, in_size=P))
+                line.update(encode_ms=round(t_enc, 4), encode_gibps=round(P / GIB / (t_enc * 1e-3), 2),
+                            round_trip_gibps=round(P / GIB / ((t_enc + t_dec) * 1e-3), 2))
+        else:
+            f_out = torch.empty(P + 11 * n + 16, dtype=torch.uint8, device="cuda")
+            f_len = torch.empty(n, dtype=torch.int32, device="cuda")
+            t = timed(torch, lambda: codec.flatten_batch(b["data"], off32, n, 7, out=f_out, out_len=f_len, in_size=P))
+            line.update(flatten_ms=round(t, 4), flatten_gibps=round(P / GIB / (t * 1e-3), 2),
+                        framed_bytes=int(f_len.to(torch.int64).sum().item()))
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
