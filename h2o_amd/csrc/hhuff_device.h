@@ -20,17 +20,9 @@
 
 namespace hhuff {
 
-#ifndef HHUFF_DEC_LUT64
-#define HHUFF_DEC_LUT64 0
-#endif
-#ifndef HHUFF_DEC_OUTACC
-#define HHUFF_DEC_OUTACC 0
-#endif
-#ifndef HHUFF_DEC_UNROLL2
-#define HHUFF_DEC_UNROLL2 0
-#endif
 
-constexpr uint32_t kLong = 1u << 29;
+constexpr uint32_t kLong = 1u << 31;  // window LUT bits: tools/gen_tables.py:window_lut
+constexpr uint32_t kHas2 = 1u << 30;
 constexpr uint32_t kEos = 256;
 constexpr uint32_t kFailLen = 0xFFFFFFFFu;
 constexpr uint8_t kStatusFail = 0x80;
@@ -211,10 +203,10 @@ __device__ __forceinline__ DecResult decode_core(const Src& src, uint32_t start,
             const uint32_t L1 = (e >> 16) & 15u;
             if (L1 > R) break;  // fewer bits left than the next code: padding
             const uint32_t L12 = (e >> 20) & 15u;
-            const bool two = (e & (1u << 24)) && L12 <= R;
+            const bool two = (e & kHas2) && L12 <= R;
             const uint32_t cons = two ? L12 : L1;
             sink.put12(e, two);
-            flags |= (e >> 25) & (two ? 15u : 3u);
+            flags |= (e >> 24) & (two ? 15u : 3u);
             R -= cons;
             br.consume(cons, src);
         }
@@ -230,126 +222,12 @@ __device__ __forceinline__ DecResult decode_core(const Src& src, uint32_t start,
 
 // ---------------------------------------------------------------------------------------------------
 // Staged decode of one string per lane, all 64 lanes in lock step (same results as decode_core).
-// Every step is predicated instead of branching: the window-LUT read and the next input word are
-// fetched together from LDS, up to two symbols are written to the LDS output stage (writes that are
-// switched off go to a lane-private trash byte), and the 64-bit window is refilled without a branch.
-// Codes longer than the window take a wave-uniform detour through the leading-ones table.
-// `active` = this lane has a string to decode (len <= kMaxStrLen).
+// Every per-lane predicate is a 0/1 integer in a VGPR (no lane masks, no SALU mask algebra): selects
+// become multiply-adds, R is kept complemented (nR = ~R) so that "L <= R" is the sign bit of L + nR.
+// Up to two symbols per step are written to the LDS output stage (writes that are switched off go to a
+// lane-private trash byte); the 64-bit window is refilled without a branch; codes longer than the
+// window take a wave-uniform detour through the leading-ones table.  Two steps per vote.
 // ---------------------------------------------------------------------------------------------------
-__device__ __forceinline__ DecResult decode_staged_lane(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
-                                                        bool active, uint8_t* obuf, uint32_t op0, uint32_t trash,
-                                                        const DecTables& T) {
-    uint32_t a = start & ~3u;
-    const uint32_t skip = start & 3u;
-    uint64_t buf = (uint64_t)(bswap32(stage[min(a, last) >> 2]) << (8 * skip)) << 32;
-    uint32_t nb = 32 - 8 * skip;
-    a += 4;
-    buf |= (uint64_t)bswap32(stage[min(a, last) >> 2]) << (32 - nb);
-    nb += 32;
-    a += 4;
-    uint32_t R = active ? 8 * len : 0u;  // string bits not yet consumed
-    uint32_t flags = 0;
-    bool fail = false;
-#if HHUFF_DEC_OUTACC
-    // output bytes gather in a 64-bit register and leave as whole dwords OR-ed into the zeroed stage
-    uint32_t* obuf32 = reinterpret_cast<uint32_t*>(obuf);
-    uint64_t oacc = 0;
-    uint32_t opend = op0 & 3u, opw = op0 >> 2, cnt = 0;
-    (void)trash;
-#else
-    uint32_t op = op0;
-#endif
-    auto step = [&]() {
-        const uint32_t w = (uint32_t)(buf >> 32);
-#if HHUFF_DEC_LUT64
-        const uint32_t li = w >> (32 - HHUFF_LUT_BITS);
-        const uint2 ep = reinterpret_cast<const uint2*>(T.lut)[li >> 1];  // 64 banks for 8-byte reads
-        const uint32_t e = (li & 1u) ? ep.y : ep.x;
-#else
-        const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
-#endif
-        const uint32_t word = stage[min(a, last) >> 2];  // next refill word, fetched beside the LUT entry
-        const bool isl = (e & kLong) != 0;
-        const uint32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
-        const bool ok1 = active && !isl && L1 <= R;
-        const bool two = ok1 && (e & (1u << 24)) != 0 && L12 <= R;
-        uint32_t cons = two ? L12 : (ok1 ? L1 : 0u);
-#if HHUFF_DEC_OUTACC
-        oacc |= (uint64_t)(e & (two ? 0xFFFFu : (ok1 ? 0xFFu : 0u))) << (8 * opend);
-        const uint32_t ns = (ok1 ? 1u : 0u) + (two ? 1u : 0u);
-        opend += ns;
-        cnt += ns;
-#else
-        obuf[ok1 ? op : trash] = (uint8_t)e;
-        obuf[two ? op + 1 : trash] = (uint8_t)(e >> 8);
-        op += (ok1 ? 1u : 0u) + (two ? 1u : 0u);
-#endif
-        flags |= (e >> 25) & (two ? 15u : (ok1 ? 3u : 0u));
-        bool stay = ok1;
-        if (__any(active && isl)) {  // wave-uniform: codes longer than the window, EOS
-            if (active && isl) {
-                const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
-                const uint32_t ki = T.kinfo[k];
-                const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
-                const uint32_t L = (le >> 9) & 31u;
-                const bool okL = L <= R;
-                const bool eos = (le & 0x1FFu) == kEos;
-                const bool ok = okL && !eos;
-                fail = fail || (okL && eos);  // EOS inside the string (hpack.c:88-89)
-#if HHUFF_DEC_OUTACC
-                oacc |= (uint64_t)(ok ? (le & 0xFFu) : 0u) << (8 * opend);
-                opend += ok ? 1u : 0u;
-                cnt += ok ? 1u : 0u;
-#else
-                obuf[ok ? op : trash] = (uint8_t)le;
-                op += ok ? 1u : 0u;
-#endif
-                flags |= ok ? ((le >> 14) & 3u) : 0u;
-                cons = ok ? L : 0u;
-                stay = ok;
-            }
-        }
-#if HHUFF_DEC_OUTACC
-        const uint32_t f = opend >= 4 ? 1u : 0u;
-        atomicOr(&obuf32[opw], f ? (uint32_t)oacc : 0u);
-        oacc >>= 32u * f;
-        opend -= 4u * f;
-        opw += f;
-#endif
-        active = active && stay;
-        R -= cons;
-        buf <<= cons;
-        nb -= cons;
-        const bool need = nb <= 32;
-        buf |= (uint64_t)(need ? bswap32(word) : 0u) << ((32 - nb) & 63u);
-        nb += need ? 32u : 0u;
-        a += need ? 4u : 0u;
-    };
-    for (;;) {
-        step();
-#if HHUFF_DEC_UNROLL2
-        step();
-#endif
-        if (!__any(active)) break;
-    }
-#if HHUFF_DEC_OUTACC
-    if (opend) atomicOr(&obuf32[opw], (uint32_t)oacc);
-#endif
-    DecResult r;
-    r.ok = !fail && R <= 7 && ((uint32_t)(buf >> 56) | (0xFFu >> R)) == 0xFFu;
-#if HHUFF_DEC_OUTACC
-    r.len = cnt;
-#else
-    r.len = op - op0;
-#endif
-    r.flags = (flags | (flags >> 2)) & 3u;
-    r.status = 0;
-    return r;
-}
-
-// Same as decode_staged_lane with every per-lane predicate held as a 0/1 integer in a VGPR (no lane
-// masks, no SALU mask algebra): selects become multiply-adds, R is kept complemented (nR = ~R) so that
-// "L <= R" is the sign bit of L + nR.  Two steps per vote.
 __device__ __forceinline__ DecResult decode_staged_lane_i(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
                                                           bool active, uint8_t* obuf, uint32_t op0, uint32_t trash,
                                                           const DecTables& T) {
@@ -368,15 +246,17 @@ __device__ __forceinline__ DecResult decode_staged_lane_i(const uint32_t* stage,
         const uint32_t w = (uint32_t)(buf >> 32);
         const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
         const uint32_t word = stage[min(a, last) >> 2];
-        const uint32_t isl = (e >> 29) & 1u;
+        const uint32_t isl = e >> 31;
         const uint32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
         const uint32_t ok1 = act & (isl ^ 1u) & ((L1 + nR) >> 31);                 // L1 <= R
-        const uint32_t two = ok1 & (e >> 24) & ((L12 + nR) >> 31);                 // bit 24 = second symbol
+        const uint32_t two = ok1 & (e >> 30) & ((L12 + nR) >> 31);                 // bit 30 = second symbol
         uint32_t cons = __umul24(ok1, L1) + __umul24(two, L12 - L1);
+#ifndef HHUFF_ABL_NOWRITE
         obuf[trash - __umul24(ok1, trash - op)] = (uint8_t)e;  // trash > op: both mul24 operands < 2^24
         obuf[trash - __umul24(two, trash - op - 1u)] = (uint8_t)(e >> 8);
+#endif
         op += ok1 + two;
-        flags |= (e >> 25) & (3u * ok1 + 12u * two);
+        flags |= (e >> 24) & (3u * ok1 + 12u * two);
         uint32_t nact = ok1;
         const uint32_t lact = act & isl;
         if (__any(lact != 0u)) {  // wave-uniform: codes longer than the window, EOS
@@ -415,6 +295,95 @@ __device__ __forceinline__ DecResult decode_staged_lane_i(const uint32_t* stage,
     r.ok = !fail && R <= 7 && ((uint32_t)(buf >> 56) | (0xFFu >> R)) == 0xFFu;
     r.len = op - op0;
     r.flags = (flags | (flags >> 2)) & 3u;
+    r.status = 0;
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Staged decode, v5 step.  Same results as decode_core; the stage holds big-endian (byte-swapped)
+// dwords so that the 32-bit window at any bit is one v_alignbit of two of them:
+//   pm = p - 1 (p = next unread bit, MSB first), q = pm >> 5 (arithmetic), x0 = stage[q], x1 = stage[q+1]
+//   window = alignbit(x0, x1, ~pm)                      (bits p .. p+31; x0 unused when p % 32 == 0)
+// c = p - end - 1 is negative while bits remain, so "a code of L bits fits" is the sign of L + c; with
+// LONG / HAS2 in the LUT's top bits the take-masks m1 (first symbol) and m2 (second symbol) are sign
+// bits of one AND each.  Switched-off writes are steered to a lane-private trash byte with v_bfi, so no
+// byte outside [op0, op0 + count) is ever written.  A lane whose next code can never fit is parked by
+// pushing c positive.  x2 = stage[q+2] is fetched one step ahead, so only the LUT read is on the
+// step's dependency chain.  Two steps per vote.
+// ---------------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(size_t)(const lds_u8*)p; }
+__device__ __forceinline__ void lds_st8(uint32_t addr, uint32_t v) { *(lds_u8*)(size_t)addr = (uint8_t)v; }
+__device__ __forceinline__ uint32_t sel_bits(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+__device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage, uint32_t start, uint32_t len,
+                                                           bool active, uint8_t* obuf, uint32_t op0, uint32_t trash_off,
+                                                           const DecTables& T) {
+    const lds_u32* st = (const lds_u32*)stage;
+    int32_t pm = (int32_t)(8u * start) - 1;
+    const int32_t end = (int32_t)(8u * (start + len));
+    int32_t c = active ? pm - end : 0x40000000;
+    int32_t q = pm >> 5;
+    uint32_t x0 = st[q], x1 = st[q + 1], x2 = st[q + 2];
+    const uint32_t o0 = lds_addr(obuf) + op0, trash = lds_addr(obuf) + trash_off;
+    uint32_t o = o0, acc1 = 0, acc2 = 0, accl = 0, fail = 0;
+    int32_t prog = 0;
+    auto step = [&]() {
+        const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+        const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+        const int32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+        const int32_t s1 = L1 + c, s2 = L12 + c;
+        const uint32_t m1 = (uint32_t)((s1 & ~(int32_t)e) >> 31);         // first code fits, not LONG
+        const uint32_t m2 = (uint32_t)((s2 & (int32_t)(e << 1)) >> 31);  // HAS2 and both fit
+        int32_t cons = (int32_t)sel_bits(m2, (uint32_t)L12, m1 & (uint32_t)L1);
+        lds_st8(sel_bits(m1, o - m2, trash), e >> 8);  // second symbol, or onto the first one's byte
+        lds_st8(sel_bits(m1, o, trash), e);
+        o = o - m1 - m2;
+        acc1 |= e & m1;
+        acc2 |= e & m2;
+        const bool lact = (s1 & (int32_t)e) < 0;  // LONG entry and >= LUT_BITS + 1 bits left
+        uint32_t consl = 0;
+        if (__builtin_amdgcn_ballot_w64(lact) != 0) {  // wave-uniform: codes longer than the window, EOS
+            if (lact) {
+                const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                const uint32_t ki = T.kinfo[k];
+                const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                const int32_t L = (le >> 9) & 31u;
+                const uint32_t fits = (uint32_t)((L + c) >> 31);
+                const uint32_t eos = (le & 0x1FFu) == kEos ? 0xFFFFFFFFu : 0u;
+                const uint32_t okm = fits & ~eos;
+                fail |= fits & eos & 1u;  // EOS inside the string (hpack.c:88-89)
+                lds_st8(sel_bits(okm, o, trash), le);
+                o -= okm;
+                accl |= le & okm;
+                consl = okm & (uint32_t)L;
+                c = (int32_t)sel_bits(okm, (uint32_t)c, 0x40000000u);  // park: EOS, or a code that cannot fit
+            }
+        }
+        cons |= (int32_t)consl;  // LONG lanes took no window symbol, so cons was 0 there
+        c += cons;
+        pm += cons;
+        const int32_t qn = pm >> 5;
+        const bool adv = qn != q;
+        x0 = adv ? x1 : x0;
+        x1 = adv ? x2 : x1;
+        q = qn;
+        x2 = st[q + 2];
+        prog = cons;
+    };
+    for (;;) {
+        step();
+        step();
+        if (!__any(prog != 0)) break;
+    }
+    DecResult r;
+    const uint32_t R = ~(uint32_t)c;  // string bits left (meaningless for parked lanes, which fail)
+    const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+    r.ok = active && !fail && R <= 7 && (w | (0xFFFFFFFFu >> (R & 31u))) == 0xFFFFFFFFu;
+    r.len = o - o0;
+    r.flags = ((acc1 >> 24) | (acc2 >> 26) | (accl >> 14)) & 3u;
     r.status = 0;
     return r;
 }

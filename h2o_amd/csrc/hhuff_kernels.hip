@@ -82,6 +82,11 @@ constexpr bool kSpanPrefetch = false;  // A/B switch: load the next span only af
 constexpr bool kSpanPrefetch = true;
 #endif
 
+#ifndef HHUFF_DEC_I  // A/B knob: 1 = previous decode step (decode_staged_lane_i, little-endian stage)
+#define HHUFF_DEC_I 0
+#endif
+constexpr bool kDecSwap = !HHUFF_DEC_I;
+
 struct TileIn {  // per-lane prefetched fields of one tile
     uint32_t s, len, name_word, dst;
 };
@@ -124,6 +129,7 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
             if (k < span && g + 16 <= in_size) v[c] = *reinterpret_cast<const uint4*>(in + g);
         }
     }
+    template <bool kSwap = false>  // kSwap: store big-endian dwords (the v5 decode window reads them)
     __device__ __forceinline__ void commit(uint32_t* stage, const uint8_t* __restrict__ in, uint64_t in_size, uint32_t a0,
                                            uint32_t span, int lane) {
 #pragma unroll
@@ -138,6 +144,7 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
                         if (g + b < in_size) w[b >> 2] |= (uint32_t)in[g + b] << (8 * (b & 3));
                     x = make_uint4(w[0], w[1], w[2], w[3]);
                 }
+                if (kSwap) x = make_uint4(bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w));
                 *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(stage) + k) = x;
             }
         }
@@ -237,11 +244,20 @@ __device__ __forceinline__ void decode_direct(const DecArgs& A, uint32_t s, uint
 
 template <int WAVES, int IN_STAGE, int OUT_STAGE>
 __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
-    __shared__ uint32_t s_kinfo[32];
-    __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
-    __shared__ __attribute__((aligned(16))) uint32_t s_in[WAVES][IN_STAGE / 4];
-    __shared__ __attribute__((aligned(16))) uint8_t s_out[WAVES][OUT_STAGE + 256];  // + a trash dword per lane
+    // one LDS object, window LUT first: its byte offsets then fit the ds_read address with no base add
+    struct __attribute__((aligned(16))) Smem {
+        uint32_t lut[1u << HHUFF_LUT_BITS];
+        uint32_t kinfo[32];
+        uint32_t ones[(HHUFF_ONES_NENT + 3) & ~3];
+        uint32_t in[WAVES][IN_STAGE / 4];
+        uint8_t out[WAVES][OUT_STAGE + 256];  // + a trash dword per lane
+    };
+    __shared__ Smem sm;
+    uint32_t* s_lut = sm.lut;
+    uint32_t* s_kinfo = sm.kinfo;
+    uint32_t* s_ones = sm.ones;
+    auto& s_in = sm.in;
+    auto& s_out = sm.out;
     load_dec_tables(s_lut, s_kinfo, s_ones, WAVES * 64);
     __syncthreads();
     const DecTables T{s_lut, s_kinfo, s_ones};
@@ -291,7 +307,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     uint32_t cur_name = ti.name_word;
     if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
     if (base + stride < A.n) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
-    if (cur.fits) pf.commit(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+    if (cur.fits) pf.template commit<kDecSwap>(stage, A.in, A.in_size, cur.a0, cur.span, lane);
     for (;;) {
         const uint64_t nbase = base + stride;
         const bool have_next = nbase < A.n;
@@ -310,20 +326,16 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         uint32_t ol = 0;
         uint8_t st = 0;
         if (cur.fits) {
-#if HHUFF_DEC_OUTACC
-            for (uint32_t k = (uint32_t)lane * 16u; k < cur.ospan + 16u; k += 64u * 16u)
-                *reinterpret_cast<uint4*>(obuf + k) = make_uint4(0u, 0u, 0u, 0u);
-#endif
             wave_lds_sync();
             const bool act = t.valid && t.len <= kMaxStrLen;
             const uint32_t rel = t.len ? t.s - cur.a0 : 0u;
             const uint32_t last = cur.span ? cur.span - 4u : 0u;
-#if HHUFF_DEC_VOTE1
-            const DecResult r =
-                decode_staged_lane(stage, last, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
-#else
+#if HHUFF_DEC_I
             const DecResult r =
                 decode_staged_lane_i(stage, last, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
+#else
+            (void)last;
+            const DecResult r = decode_staged_lane_v5(stage, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
 #endif
             if (t.valid && t.len > kMaxStrLen) {
                 ol = kFailLen;
@@ -354,7 +366,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         if (!have_next) break;
         if (nxt.fits) {
             if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
-            pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+            pf.template commit<kDecSwap>(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
         }
         cur = nxt;
         cur_name = nxt_name;
@@ -836,7 +848,10 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_direct_kernel(FlatArgs A) 
 //   encode direct:         4 waves/WG                                      [2 KiB]
 // The variant is picked from the mean bytes per string (in_size / n).
 // ------------------------------------------------------------------------------------------------
-#define DEC_S decode_staged_kernel<16, 3072, 4608>
+#ifndef HHUFF_DSW  // waves per workgroup of the short-string decode (A/B knob)
+#define HHUFF_DSW 16
+#endif
+#define DEC_S decode_staged_kernel<HHUFF_DSW, 3072, 4608>
 #define DEC_L decode_staged_kernel<6, 8192, 12928>
 #define DEC_D decode_direct_kernel<4>
 #define ENC_S encode_staged_kernel<16, 3584>
@@ -863,7 +878,7 @@ static const void* variant_fn(int v) {
 }
 static int variant_threads(int v) {
     switch (v) {
-        case kDecS:
+        case kDecS: return HHUFF_DSW * 64;
         case kEncS: return 1024;
         case kDecL: return 384;
         case kEncL: return 512;
@@ -917,7 +932,7 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     const int v = pick_decode(in_size, n);
     const int grid = grid_for(v, current_device(), n);
     switch (v) {
-        case kDecS: hipLaunchKernelGGL(DEC_S, dim3(grid), dim3(1024), 0, stream, A); break;
+        case kDecS: hipLaunchKernelGGL(DEC_S, dim3(grid), dim3(HHUFF_DSW * 64), 0, stream, A); break;
         case kDecL: hipLaunchKernelGGL(DEC_L, dim3(grid), dim3(384), 0, stream, A); break;
         default: hipLaunchKernelGGL(DEC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }

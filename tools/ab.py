@@ -31,6 +31,8 @@ def run(names, cfg="c4", rounds=5, steps=10):
 
     from h2o_amd import synth
 
+    # ablation configs (not product configs): fixed-length strings isolate lane imbalance
+    synth.CONFIGS.setdefault("c4u", dict(n=1 << 24, lengths=("uniform", 48, 48), alphabet="header"))
     torch.cuda.set_device(0)
     libs = {}
     vp = ctypes.c_void_p
@@ -109,7 +111,7 @@ def run(names, cfg="c4", rounds=5, steps=10):
             chk = chk + (content_sum(e_out, e_pos), content_sum(d_out, d_pos))
             if ref is None:
                 ref = chk
-            assert chk == ref, (nm, chk, ref)
+            assert chk == ref or nm.startswith("x_"), (nm, chk, ref)  # x_*: ablation builds, output not checked
     for nm in names:
         e = sorted(res[nm]["enc"])
         d = sorted(res[nm]["dec"])

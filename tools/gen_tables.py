@@ -169,33 +169,36 @@ def decode_prefix(root, bits, nbits):
 def window_lut(root):
     """GPU decode LUT indexed by the next LUT_BITS (13) bits of the stream.
 
-    u32 entry: [7:0] sym1 | [15:8] sym2 | [19:16] len1 | [23:20] len1+len2 | [24] has2 |
-               [25] sym1 name-invalid | [26] sym1 value-invalid | [27] sym2 name-invalid |
-               [28] sym2 value-invalid | [29] LONG (first code longer than the window)
+    u32 entry: [7:0] sym1 | [15:8] sym2 | [19:16] L1 | [23:20] L12 = L1 + L2 (= L1 without a second
+               symbol) | [24] sym1 name-invalid | [25] sym1 value-invalid | [26] sym2 name-invalid |
+               [27] sym2 value-invalid | [30] HAS2 | [31] LONG (first code longer than the window).
+    LONG entries carry L1 = L12 = LUT_BITS + 1, the shortest code they can stand for, so "L1 fits in
+    the bits left" tells the kernel whether a long code can still fit.  HAS2 and LONG sit in the top
+    bits so that a sign-bit AND with (L + c) yields the take/skip masks directly.
     EOS (30 bits) never fits a window, so LONG covers it."""
     lut = []
     W = LUT_BITS
     for w in range(1 << W):
         r1 = decode_prefix(root, w, W)
         if r1 is None:
-            lut.append(1 << 29)
+            lut.append(1 << 31 | (W + 1) << 16 | (W + 1) << 20)
             continue
         s1, l1 = r1
         e = s1 | l1 << 16 | l1 << 20
         if s1 not in NAME_VALID:
-            e |= 1 << 25
+            e |= 1 << 24
         if s1 not in VALUE_VALID:
-            e |= 1 << 26
+            e |= 1 << 25
         rest = W - l1
         if rest >= 5:
             r2 = decode_prefix(root, w & ((1 << rest) - 1), rest)
             if r2 is not None:
                 s2, l2 = r2
-                e = (e & ~(0xF << 20)) | s2 << 8 | (l1 + l2) << 20 | 1 << 24
+                e = (e & ~(0xF << 20)) | s2 << 8 | (l1 + l2) << 20 | 1 << 30
                 if s2 not in NAME_VALID:
-                    e |= 1 << 27
+                    e |= 1 << 26
                 if s2 not in VALUE_VALID:
-                    e |= 1 << 28
+                    e |= 1 << 27
         lut.append(e)
     return lut
 
