@@ -524,18 +524,23 @@ __device__ __forceinline__ uint32_t encode_staged_lane(const uint32_t* stage, ui
 // Same contract as encode_staged_lane, with a wave-uniform trip count: `jmax` = the largest number of
 // input dwords over the wave's lanes, so the loop needs no vote; lanes that finished or failed run with
 // every byte masked out (their table entries are {0, 0}).  The first / last dword masks are precomputed.
-__device__ __forceinline__ uint32_t encode_staged_lane_u(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
-                                                         bool active, uint32_t* obuf32, uint32_t opb,
-                                                         const uint2* __restrict__ enc, uint32_t jmax) {
+// Encode the stage bytes [start, start + len) with the first code bit landing at bit `startbit` of the
+// LDS output stage (MSB-first dwords, OR-ed in, so neighbouring chunks may share a dword).  The trip
+// count jmax is wave-uniform (>= this lane's dword count).  `limit`: fail as soon as the code bits
+// reach it (8 * len - 7 for a whole string: ceil(bits / 8) >= len; ~0 for a chunk of a longer string
+// whose verdict is already known).  `pad`: this chunk ends the string, so fill its last byte with
+// ones (EOS prefix, hpack.c:795-798).  Returns the code bits, or kFailLen.
+__device__ __forceinline__ uint32_t encode_chunk(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
+                                                 bool active, uint32_t* obuf32, uint32_t startbit,
+                                                 const uint2* __restrict__ enc, uint32_t jmax, uint32_t limit, bool pad) {
     const uint32_t end = start + len;
     const uint32_t a0 = start & ~3u;
     const uint32_t ndw = active ? (end - a0 + 3u) >> 2 : 0u;
     const uint32_t mfirst = 0xFFFFFFFFu << (8u * (start & 3u));
     const uint32_t mlast = (uint32_t)(0xFFFFFFFFull >> ((32u - 8u * (end & 3u)) & 31u));
-    const uint32_t limit = active ? 8 * len - 7 : 0xFFFFFFFFu;
     uint64_t acc = 0;
-    uint32_t an = 8 * (opb & 3u);
-    uint32_t opw = opb >> 2;
+    uint32_t an = startbit & 31u;
+    uint32_t opw = startbit >> 5;
     uint32_t tb = 0;
     bool live = active, fail = false;
     for (uint32_t j = 0; j < jmax; ++j) {
@@ -583,10 +588,42 @@ __device__ __forceinline__ uint32_t encode_staged_lane_u(const uint32_t* stage, 
         opw += e;
     }
     if (fail || !active) return kFailLen;
-    const uint32_t an8 = (an + 7) & ~7u;
-    acc |= (~0ull >> an) & ~(~0ull >> an8);
+    if (pad) {
+        const uint32_t an8 = (an + 7) & ~7u;
+        acc |= (~0ull >> an) & ~(~0ull >> an8);
+    }
     if (an) atomicOr(&obuf32[opw], bswap32((uint32_t)(acc >> 32)));
-    return (tb + 7) >> 3;
+    return tb;
+}
+
+// Whole string at byte `opb` of the output stage: returns the Huffman length in bytes or kFailLen.
+__device__ __forceinline__ uint32_t encode_staged_lane_u(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
+                                                         bool active, uint32_t* obuf32, uint32_t opb,
+                                                         const uint2* __restrict__ enc, uint32_t jmax) {
+    const uint32_t tb = encode_chunk(stage, last, start, len, active, obuf32, 8u * opb, enc, jmax,
+                                     active ? 8 * len - 7 : 0xFFFFFFFFu, true);
+    return tb == kFailLen ? kFailLen : (tb + 7) >> 3;
+}
+
+// Code bits of the stage bytes [start, start + len) (pass 1 of the proportional-lane encode).
+__device__ __forceinline__ uint32_t chunk_code_bits(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
+                                                    bool active, const uint2* __restrict__ enc, uint32_t jmax) {
+    const uint32_t end = start + len;
+    const uint32_t a0 = start & ~3u;
+    const uint32_t ndw = active ? (end - a0 + 3u) >> 2 : 0u;
+    const uint32_t mfirst = 0xFFFFFFFFu << (8u * (start & 3u));
+    const uint32_t mlast = (uint32_t)(0xFFFFFFFFull >> ((32u - 8u * (end & 3u)) & 31u));
+    uint32_t tb = 0;
+    for (uint32_t j = 0; j < jmax; ++j) {
+        const uint32_t w = stage[min(a0 + 4u * j, last) >> 2];
+        uint32_t vm = j == 0 ? mfirst : 0xFFFFFFFFu;
+        vm &= (j + 1 == ndw) ? mlast : 0xFFFFFFFFu;
+        vm = j < ndw ? vm : 0u;
+        const uint32_t iw = ~vm & 0x01010101u;
+        tb += enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0400u)].y + enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)].y +
+              enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)].y + enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)].y;
+    }
+    return tb;
 }
 
 // ---------------------------------------------------------------------------------------------------

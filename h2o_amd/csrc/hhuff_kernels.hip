@@ -520,6 +520,158 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Proportional-lane staged encode (contiguous layout, output slot = in_off: the wire / bench layout).
+// A tile is K consecutive strings staged in LDS.  String j gets g_j = 1 + floor((64 - K) len_j / span)
+// lanes, each encoding an equal share of the string, so every lane has about span / 64 bytes whatever
+// the length mix (Zipf mixes, 512-B QPACK values).  Strings spread over several lanes take two passes:
+// pass 1 counts each share's code bits, a wave scan turns the counts into each share's starting bit
+// and the string's total (hence its verdict, hpack.c:799-800), pass 2 emits the shares into the
+// OR-combined output stage.  Single-lane strings skip pass 1 and fail early as in encode_staged_kernel.
+// Tiles whose span exceeds the stage (strings longer than ~STAGE / 1) fall back to the direct loop.
+// ------------------------------------------------------------------------------------------------
+template <int WAVES, int STAGE>
+__global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32_t K) {
+    struct __attribute__((aligned(16))) Smem {
+        uint2 enc[512];  // 256..511: bytes outside a share
+        uint32_t in[WAVES][STAGE / 4];
+        uint32_t out[WAVES][STAGE / 4 + 4];
+        uint32_t lmap[WAVES][64];
+    };
+    __shared__ Smem sm;
+    for (uint32_t k = threadIdx.x; k < 512; k += WAVES * 64)
+        sm.enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
+    __syncthreads();
+    const uint2* s_enc = sm.enc;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t* stage = sm.in[wave];
+    uint32_t* obuf32 = sm.out[wave];
+    const uint8_t* obuf = reinterpret_cast<const uint8_t*>(obuf32);
+    uint32_t* lmap = sm.lmap[wave];
+    const uint64_t ntiles = ((uint64_t)A.n + K - 1) / K;
+    const uint64_t tstride = (uint64_t)gridDim.x * WAVES;
+    uint64_t t = (uint64_t)blockIdx.x * WAVES + wave;
+    if (t >= ntiles) return;
+
+    struct Plan {
+        uint64_t i0;
+        uint32_t kt, s, e, lo, hi, a0, span;
+        bool fits;
+    };
+    auto issue = [&](uint64_t tt, uint32_t& s0, uint32_t& e0) {
+        const uint64_t i = tt * K + lane;
+        s0 = e0 = 0;
+        if ((uint32_t)lane < K && i < A.n) {
+            s0 = A.in_off[i];
+            e0 = A.in_off[i + 1];
+        }
+    };
+    auto plan = [&](uint64_t tt, uint32_t s0, uint32_t e0) {
+        Plan P;
+        P.i0 = tt * K;
+        P.kt = (uint32_t)min<uint64_t>(K, A.n - P.i0);
+        P.s = s0;
+        P.e = e0;
+        P.lo = (uint32_t)__shfl((int)s0, 0, 64);
+        P.hi = (uint32_t)__shfl((int)e0, (int)P.kt - 1, 64);
+        P.a0 = P.lo & ~15u;
+        P.span = P.hi > P.lo ? ((P.hi + 15u) & ~15u) - P.a0 : 0u;
+        P.fits = P.span <= STAGE;
+        return P;
+    };
+
+    SpanPrefetch<(STAGE + 1023) / 1024> pf;
+    uint32_t ns, ne;
+    issue(t, ns, ne);
+    Plan cur = plan(t, ns, ne);
+    if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
+    if (t + tstride < ntiles) issue(t + tstride, ns, ne);
+    if (cur.fits) pf.commit(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+    for (;;) {
+        const uint64_t tn = t + tstride;
+        const bool have_next = tn < ntiles;
+        Plan nxt;
+        if (have_next) {
+            nxt = plan(tn, ns, ne);
+            if (kSpanPrefetch && nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+            if (tn + tstride < ntiles) issue(tn + tstride, ns, ne);
+        }
+        // ---- the current tile ----
+        const bool own = (uint32_t)lane < cur.kt;
+        const uint32_t len = own ? cur.e - cur.s : 0u;
+        uint32_t ol = kFailLen;
+        if (cur.fits) {
+            for (uint32_t k = (uint32_t)lane * 16u; k < cur.span + 16u; k += 64u * 16u)
+                *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(obuf32) + k) = make_uint4(0u, 0u, 0u, 0u);
+            // lanes per string, first lane of each string, lane -> string map
+            const uint32_t total = cur.hi - cur.lo;
+            const uint32_t g = own ? 1u + (uint32_t)(((uint64_t)(64u - cur.kt) * len) / (total ? total : 1u)) : 0u;
+            const uint32_t L = wave_excl_scan(g, lane);
+            const uint32_t used = (uint32_t)__shfl((int)(L + g), (int)cur.kt - 1, 64);
+            lmap[lane] = 0;
+            wave_lds_sync();
+            if (own) lmap[L] = (uint32_t)lane;
+            wave_lds_sync();
+            uint32_t j = lmap[lane];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {  // inclusive max scan: the string whose first lane is at or below
+                const uint32_t y = (uint32_t)__shfl_up((int)j, o, 64);
+                if (lane >= o) j = max(j, y);
+            }
+            const bool act = (uint32_t)lane < used;
+            const uint32_t sj = (uint32_t)__shfl((int)cur.s, (int)j, 64);
+            const uint32_t lj = (uint32_t)__shfl((int)len, (int)j, 64);
+            const uint32_t Lj = (uint32_t)__shfl((int)L, (int)j, 64);
+            const uint32_t gj = (uint32_t)__shfl((int)g, (int)j, 64);
+            const uint32_t sub = (uint32_t)lane - Lj;
+            const uint32_t C = gj > 1 ? (((lj + gj - 1) / gj) + 3u) & ~3u : lj;
+            const uint32_t c0 = min(sub * C, lj), c1 = min(sub * C + C, lj);
+            const uint32_t cs = sj - cur.a0 + c0, clen = c1 - c0;
+            const bool multi = gj > 1;
+            const bool big = act && lj <= kMaxStrLen;
+            const uint32_t last = cur.span ? cur.span - 4u : 0u;
+            const uint32_t ndw = big && clen ? (cs + clen - (cs & ~3u) + 3u) >> 2 : 0u;
+            const uint32_t jmax = wave_max_u32(ndw);
+            uint32_t off = 0, tot = 0;
+            bool sfail = false;
+            wave_lds_sync();
+            if (__any(multi && big)) {  // pass 1: code bits of every share, then starting bits and totals
+                const uint32_t b = chunk_code_bits(stage, last, cs, clen, big && multi, s_enc, jmax);
+                const uint32_t x = wave_excl_scan(b, lane);
+                const uint32_t xs = (uint32_t)__shfl((int)x, (int)Lj, 64);
+                const uint32_t xe = (uint32_t)__shfl((int)(x + b), (int)(Lj + gj - 1), 64);
+                off = x - xs;
+                tot = xe - xs;
+                sfail = multi && ((tot + 7u) >> 3) >= lj;
+            }
+            const uint32_t r = encode_chunk(stage, last, cs, clen, big && !sfail && clen != 0, obuf32,
+                                            8u * (sj - cur.a0) + off, s_enc, jmax,
+                                            multi ? 0xFFFFFFFFu : 8u * lj - 7u, c1 == lj);  // the share holding the string's end pads it
+            uint32_t res = kFailLen;  // verdict of this lane's string, as seen by the string's first lane
+            if (act && lj != 0 && lj <= kMaxStrLen) {
+                if (multi) res = sfail ? kFailLen : (tot + 7u) >> 3;
+                else res = r == kFailLen ? kFailLen : (r + 7u) >> 3;
+            }
+            ol = (uint32_t)__shfl((int)res, (int)L, 64);
+            wave_lds_sync();
+            region_copy(A.out, cur.a0, obuf, cur.span, cur.lo, cur.hi, lane);
+            wave_lds_sync();
+        } else if (own && len <= kMaxStrLen) {
+            RegSink sink;
+            sink.init(A.out + cur.s);
+            ol = encode_core(GlobalSource{A.in, A.in_size}, cur.s, len, sink, s_enc);
+        }
+        if (own) finish_encode(A, (uint32_t)(cur.i0 + lane), len, ol);
+        if (!have_next) break;
+        if (nxt.fits) {
+            if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+            pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+        }
+        cur = nxt;
+        t = tn;
+    }
+}
+
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void encode_direct_kernel(EncArgs A) {
     __shared__ __attribute__((aligned(16))) uint2 s_enc[256];
@@ -858,10 +1010,11 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_direct_kernel(FlatArgs A) 
 #define ENC_L encode_staged_kernel<8, 8192>
 #define ENC_D encode_direct_kernel<4>
 #define FLAT_D flatten_direct_kernel<4>
+#define ENC_P encode_pl_kernel<16, 3584>
 #define ENC_C encode_chunked_kernel<12, 4096, 128>
 #define ENC_CL encode_chunked_kernel<8, 8192, 64>
 
-enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncC, kEncCL, kNumVariants };
+enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncC, kEncCL, kEncP, kNumVariants };
 
 static const void* variant_fn(int v) {
     switch (v) {
@@ -873,6 +1026,7 @@ static const void* variant_fn(int v) {
         case kFlatD: return (const void*)FLAT_D;
         case kEncC: return (const void*)ENC_C;
         case kEncCL: return (const void*)ENC_CL;
+        case kEncP: return (const void*)ENC_P;
         default: return (const void*)ENC_D;
     }
 }
@@ -884,6 +1038,7 @@ static int variant_threads(int v) {
         case kEncL: return 512;
         case kEncC: return 768;
         case kEncCL: return 512;
+        case kEncP: return 1024;
         default: return 256;
     }
 }
@@ -916,6 +1071,16 @@ static int pick_decode(uint64_t in_size, uint32_t n) {
     if (mean <= 40) return kDecS;
     if (mean <= 128) return kDecL;
     return kDecD;
+}
+#ifndef HHUFF_ENC_PL  // A/B knobs: proportional-lane encode from this mean string length up (0 = always)
+#define HHUFF_ENC_PL 53
+#endif
+#ifndef HHUFF_ENC_PL_K  // strings per tile (0 = from the mean length)
+#define HHUFF_ENC_PL_K 0
+#endif
+static bool use_pl_encode(uint64_t in_size, uint32_t n) {
+    const uint64_t mean = n ? in_size / n : 0;
+    return HHUFF_ENC_PL >= 0 && mean >= (uint64_t)HHUFF_ENC_PL;
 }
 static int pick_encode(uint64_t in_size, uint32_t n) {
     const uint64_t mean = n ? in_size / n : 0;
@@ -960,6 +1125,19 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         return hipGetLastError();
     }
 #endif
+    if (in_len == nullptr && out_off == nullptr && use_pl_encode(in_size, n)) {
+        // contiguous wire layout: proportional-lane tiles of K strings (about 5/8 of a stage of bytes)
+        const uint64_t mean = in_size / n;
+        uint32_t K = HHUFF_ENC_PL_K ? (uint32_t)HHUFF_ENC_PL_K
+                                    : (uint32_t)(mean ? (3584u * 5u / 8u) / mean : 64u);
+        K = K < 1 ? 1u : (K > 64 ? 64u : K);
+        const uint64_t tiles = ((uint64_t)n + K - 1) / K;
+        const int g = grid_for(kEncP, current_device(), 0xFFFFFFFFu);
+        const uint64_t want = (tiles + 15) / 16;
+        const int grid = (int)(want < (uint64_t)g ? (want ? want : 1) : g);
+        hipLaunchKernelGGL(ENC_P, dim3(grid), dim3(1024), 0, stream, A, K);
+        return hipGetLastError();
+    }
     const int v = pick_encode(in_size, n);
     const int grid = grid_for(v, current_device(), n);
     switch (v) {

@@ -171,6 +171,36 @@ def test_explicit_out_off_unaligned_and_long_strings(torch_cuda, oracle_codec):
         assert g[0][int(d_dst[i]):int(d_dst[i]) + int(g[1][i])].tobytes() == strings[i]
 
 
+def test_contiguous_mixed_lengths_proportional_lanes(torch_cuda, oracle_codec):
+    """contiguous wire layout with a long-tailed length mix: strings spread over many lanes
+    (proportional-lane encode), incompressible long strings (multi-lane failures), empty and 1-3 byte
+    strings, and strings longer than the LDS stage (the tile falls back to the direct loop)"""
+    rng = np.random.default_rng(11)
+    syms, p = synth.header_alphabet()
+    strings = []
+    for i in range(6000):
+        L = int(rng.choice([0, 1, 2, 3, 9, 40, 130, 400, 900, 2500, 6000],
+                           p=[.03, .03, .03, .03, .1, .25, .2, .15, .1, .05, .03]))
+        kind = rng.random()
+        if kind < 0.08:  # incompressible: long codes only
+            s = bytes(rng.choice(np.frombuffer(b"{}~^|<>\\", np.uint8), L))
+        elif kind < 0.12:  # arbitrary bytes
+            s = bytes(rng.integers(0, 256, L, dtype=np.uint8))
+        else:
+            s = bytes(rng.choice(syms, L, p=p))
+        strings.append(s)
+    data, off = synth.pack(strings)
+    n = len(strings)
+    assert data.size // n >= 53  # mean length selects the proportional-lane kernel
+    g_out, g_len, g_st = gpu_encode(torch_cuda, data, off, n)
+    o_out, o_len, o_st = oracle_codec.encode_batch(data, off, n, nthreads=8)
+    np.testing.assert_array_equal(g_len, o_len)
+    np.testing.assert_array_equal(g_st, o_st)
+    assert compact(g_out, off[:n], g_len) == compact(o_out, off[:n], o_len)
+    ok = np.nonzero(g_len != FAIL)[0]
+    assert len(ok) > 1000 and (np.diff(off)[ok] > 400).sum() > 100
+
+
 # ------------------------------------------------------------------------------------------------
 # per-string h2o symbols and the host batch API
 # ------------------------------------------------------------------------------------------------
