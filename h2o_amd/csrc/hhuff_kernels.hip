@@ -990,6 +990,164 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_direct_kernel(FlatArgs A) 
     }
 }
 
+// Prefix integer (hpack.c:757-772) as bytes, OR-ed into first byte h0; returns the byte count (<= 6).
+__device__ __forceinline__ uint32_t prefix_int_bytes(uint32_t h0, uint32_t v, uint32_t p, uint64_t& hb) {
+    const uint32_t pmax = (1u << p) - 1u;
+    uint32_t hn = 1;
+    if (v < pmax) {
+        hb = h0 | v;
+    } else {
+        hb = h0 | pmax;
+        v -= pmax;
+        while (v >= 128) {
+            hb |= (uint64_t)(0x80u | (v & 127u)) << (8 * hn);
+            ++hn;
+            v >>= 7;
+        }
+        hb |= (uint64_t)v << (8 * hn);
+        ++hn;
+    }
+    return hn;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Proportional-lane framing (QPACK flatten_string / HPACK h2o_hpack_encode_string) for the contiguous
+// layout with the implicit output slots in_off[i] + 11 i.  Same share split as encode_pl_kernel; the
+// bit-count pass runs for every string because the header's length depends on the Huffman length
+// (qpack.c:1052-1060); raw fallbacks copy their shares after the raw header (qpack.c:1046-1051).
+// ------------------------------------------------------------------------------------------------
+template <int WAVES, int STAGE>
+__global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint32_t K) {
+    constexpr uint32_t OSTAGE = STAGE + 11u * 64u + 32u;
+    struct __attribute__((aligned(16))) Smem {
+        uint2 enc[512];
+        uint32_t in[WAVES][STAGE / 4];
+        uint32_t out[WAVES][OSTAGE / 4 + 4];
+        uint32_t lmap[WAVES][64];
+    };
+    __shared__ Smem sm;
+    for (uint32_t k = threadIdx.x; k < 512; k += WAVES * 64)
+        sm.enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
+    __syncthreads();
+    const uint2* s_enc = sm.enc;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t* stage = sm.in[wave];
+    uint32_t* obuf32 = sm.out[wave];
+    uint8_t* obuf = reinterpret_cast<uint8_t*>(obuf32);
+    uint32_t* lmap = sm.lmap[wave];
+    const uint32_t p = A.prefix_bits;
+    const uint64_t ntiles = ((uint64_t)A.n + K - 1) / K;
+    for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles; t += (uint64_t)gridDim.x * WAVES) {
+        const uint64_t i0 = t * K;
+        const uint32_t kt = (uint32_t)min<uint64_t>(K, A.n - i0);
+        const bool own = (uint32_t)lane < kt;
+        const uint64_t i = i0 + lane;
+        uint32_t s = 0, e = 0, first = 0;
+        bool rawf = false;
+        if (own) {
+            s = A.in_off[i];
+            e = A.in_off[i + 1];
+            first = A.first_bytes ? A.first_bytes[i] : 0u;
+            rawf = A.raw_bits ? ((A.raw_bits[i >> 5] >> (i & 31)) & 1u) != 0 : false;
+        }
+        const uint32_t len = e - s;
+        const uint32_t lo = (uint32_t)__shfl((int)s, 0, 64), hi = (uint32_t)__shfl((int)e, (int)kt - 1, 64);
+        const uint32_t a0 = lo & ~15u;
+        const uint32_t span = hi > lo ? ((hi + 15u) & ~15u) - a0 : 0u;
+        const uint64_t O = (uint64_t)s + 11u * i;  // output slot (owner lanes)
+        const uint64_t olo = (uint64_t)lo + 11u * i0, ohi = (uint64_t)hi + 11u * (i0 + kt);
+        const uint64_t ob = olo & ~15ull;
+        const uint32_t ospan = (uint32_t)(((ohi + 15u) & ~15ull) - ob);
+        uint32_t ol = kFailLen;
+        if (span <= STAGE && ospan <= OSTAGE) {
+            stage_span(stage, A.in, A.in_size, a0, span, lane);
+            for (uint32_t k = (uint32_t)lane * 16u; k < ospan + 16u; k += 64u * 16u)
+                *reinterpret_cast<uint4*>(obuf + k) = make_uint4(0u, 0u, 0u, 0u);
+            const uint32_t total = hi - lo;
+            const uint32_t g = own ? 1u + (uint32_t)(((uint64_t)(64u - kt) * len) / (total ? total : 1u)) : 0u;
+            const uint32_t L = wave_excl_scan(g, lane);
+            const uint32_t used = (uint32_t)__shfl((int)(L + g), (int)kt - 1, 64);
+            lmap[lane] = 0;
+            wave_lds_sync();
+            if (own) lmap[L] = (uint32_t)lane;
+            wave_lds_sync();
+            uint32_t j = lmap[lane];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)j, o, 64);
+                if (lane >= o) j = max(j, y);
+            }
+            const bool act = (uint32_t)lane < used;
+            const uint32_t sj = (uint32_t)__shfl((int)s, (int)j, 64);
+            const uint32_t lj = (uint32_t)__shfl((int)len, (int)j, 64);
+            const uint32_t Lj = (uint32_t)__shfl((int)L, (int)j, 64);
+            const uint32_t gj = (uint32_t)__shfl((int)g, (int)j, 64);
+            const bool rj = __shfl((int)rawf, (int)j, 64) != 0;
+            const uint32_t sub = (uint32_t)lane - Lj;
+            const uint32_t C = gj > 1 ? (((lj + gj - 1) / gj) + 3u) & ~3u : lj;
+            const uint32_t c0 = min(sub * C, lj), c1 = min(sub * C + C, lj);
+            const uint32_t cs = sj - a0 + c0, clen = c1 - c0;
+            const bool ok = act && lj <= kMaxStrLen;
+            const uint32_t last = span ? span - 4u : 0u;
+            const uint32_t ndw = ok && clen ? (cs + clen - (cs & ~3u) + 3u) >> 2 : 0u;
+            const uint32_t jmax = wave_max_u32(ndw);
+            wave_lds_sync();
+            // pass 1: code bits per share -> starting bit of each share, string totals, verdicts
+            const uint32_t b = chunk_code_bits(stage, last, cs, clen, ok && !rj, s_enc, jmax);
+            const uint32_t x = wave_excl_scan(b, lane);
+            const uint32_t xs = (uint32_t)__shfl((int)x, (int)Lj, 64);
+            const uint32_t xe = (uint32_t)__shfl((int)(x + b), (int)(Lj + gj - 1), 64);
+            const uint32_t tot = xe - xs;
+            const bool huff = ok && !rj && lj != 0 && tot <= 8u * lj - 8u;  // ceil(bits / 8) < len (hpack.c:799-800)
+            // header (the string's first lane) and payload offset in the slot
+            const uint32_t fj = (uint32_t)__shfl((int)first, (int)j, 64);
+            const uint32_t hlen = (tot + 7u) >> 3;
+            uint64_t hb = 0;
+            const uint32_t hn = huff ? prefix_int_bytes((fj & ~((1u << p) - 1u)) | (1u << p), hlen, p, hb)
+                                     : prefix_int_bytes(fj & ~((2u << p) - 1u), lj, p, hb);
+            const uint32_t orel = (uint32_t)((uint64_t)sj + 11u * (i0 + j) - ob);  // slot start in the out stage
+            if (ok && sub == 0)
+                for (uint32_t k = 0; k < hn; ++k) obuf[orel + k] = (uint8_t)(hb >> (8 * k));
+            // pass 2: Huffman shares emit their bits; raw shares copy their bytes
+            encode_chunk(stage, last, cs, clen, huff && clen != 0, obuf32, 8u * (orel + hn) + (x - xs), s_enc, jmax,
+                         0xFFFFFFFFu, c1 == lj);
+            if (ok && !huff && clen) {
+                const uint8_t* in8 = reinterpret_cast<const uint8_t*>(stage);
+                for (uint32_t k = 0; k < clen; ++k) obuf[orel + hn + c0 + k] = in8[cs + k];
+            }
+            const uint32_t res = ok ? hn + (huff ? hlen : lj) : kFailLen;
+            ol = (uint32_t)__shfl((int)res, (int)L, 64);
+            wave_lds_sync();
+            region_copy(A.out, ob, obuf, ospan, olo, ohi, lane);
+            wave_lds_sync();
+        } else if (own && len <= kMaxStrLen) {  // tile larger than the stage: one string per lane from global
+            const GlobalSource src{A.in, A.in_size};
+            RegSink sink;
+            sink.init(A.out + O);
+            const uint32_t bits = (rawf || len == 0) ? 0u : count_code_bits(src, s, len, s_enc);
+            const bool huff = !rawf && len != 0 && bits <= 8 * len - 8;
+            if (huff) {
+                push_prefix_int(sink, (first & ~((1u << p) - 1u)) | (1u << p), (bits + 7) >> 3, p);
+                encode_core(src, s, len, sink, s_enc);
+            } else {
+                push_prefix_int(sink, first & ~((2u << p) - 1u), len, p);
+                uint32_t a = s & ~3u, rem = len, skip = s & 3u;
+                while (rem) {
+                    const uint32_t w = src.word(a) >> (8 * skip);
+                    const uint32_t k = min(4u - skip, rem);
+                    sink.push(w, k);
+                    rem -= k;
+                    a += 4;
+                    skip = 0;
+                }
+                sink.finish();
+            }
+            ol = sink.count();
+        }
+        if (own) A.out_len[i] = ol;
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // launch configuration (LDS per workgroup in brackets)
 //   decode staged:        16 waves/WG, 3 KiB in + 4.5 KiB out per wave   [~158 KiB, 1 WG/CU]
@@ -1011,10 +1169,11 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_direct_kernel(FlatArgs A) 
 #define ENC_D encode_direct_kernel<4>
 #define FLAT_D flatten_direct_kernel<4>
 #define ENC_P encode_pl_kernel<16, 3584>
+#define FLAT_P flatten_pl_kernel<16, 3584>
 #define ENC_C encode_chunked_kernel<12, 4096, 128>
 #define ENC_CL encode_chunked_kernel<8, 8192, 64>
 
-enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncC, kEncCL, kEncP, kNumVariants };
+enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncC, kEncCL, kEncP, kFlatP, kNumVariants };
 
 static const void* variant_fn(int v) {
     switch (v) {
@@ -1027,6 +1186,7 @@ static const void* variant_fn(int v) {
         case kEncC: return (const void*)ENC_C;
         case kEncCL: return (const void*)ENC_CL;
         case kEncP: return (const void*)ENC_P;
+        case kFlatP: return (const void*)FLAT_P;
         default: return (const void*)ENC_D;
     }
 }
@@ -1038,7 +1198,8 @@ static int variant_threads(int v) {
         case kEncL: return 512;
         case kEncC: return 768;
         case kEncCL: return 512;
-        case kEncP: return 1024;
+        case kEncP:
+        case kFlatP: return 1024;
         default: return 256;
     }
 }
@@ -1153,6 +1314,17 @@ hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* i
                           const uint32_t* out_off, uint32_t* out_len, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     FlatArgs A{in, in_size, in_off, in_len, n, first_bytes, prefix_bits, raw_bits, out, out_off, out_len};
+    if (in_len == nullptr && out_off == nullptr) {  // contiguous layout, implicit slots: proportional lanes
+        const uint64_t mean = in_size / n;
+        uint32_t K = (uint32_t)(mean ? (3584u * 5u / 8u) / mean : 64u);
+        K = K < 1 ? 1u : (K > 64 ? 64u : K);
+        const uint64_t tiles = ((uint64_t)n + K - 1) / K;
+        const int g = grid_for(kFlatP, current_device(), 0xFFFFFFFFu);
+        const uint64_t want = (tiles + 15) / 16;
+        const int grid = (int)(want < (uint64_t)g ? (want ? want : 1) : g);
+        hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K);
+        return hipGetLastError();
+    }
     const int grid = grid_for(kFlatD, current_device(), n);
     hipLaunchKernelGGL(FLAT_D, dim3(grid), dim3(256), 0, stream, A);
     return hipGetLastError();
