@@ -56,6 +56,12 @@ def lib():
         L.hhuff_encode_batch_host.restype = ctypes.c_int
         L.hhuff_encode_batch_host.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint64,
                                               _vp, _vp, _vp, ctypes.c_int]
+        L.hhuff_decode_batch_host_pipelined.restype = ctypes.c_int
+        L.hhuff_decode_batch_host_pipelined.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, _vp,
+                                                        ctypes.c_uint64, _vp, _vp, ctypes.c_int, ctypes.c_uint64]
+        L.hhuff_encode_batch_host_pipelined.restype = ctypes.c_int
+        L.hhuff_encode_batch_host_pipelined.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, ctypes.c_uint64,
+                                                        _vp, _vp, ctypes.c_int, ctypes.c_uint64]
         L.hhuff_version.restype = ctypes.c_char_p
         L.hhuff_last_error_string.restype = ctypes.c_char_p
         L.hhuff_grid_size.restype = ctypes.c_int
@@ -67,7 +73,8 @@ def lib():
 # symbols include/hhuff.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decode_batch", "hhuff_encode_batch",
             "hhuff_flatten_batch",
-            "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_version", "hhuff_last_error_string",
+            "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
+            "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string",
             "hhuff_grid_size")
 
 
@@ -207,4 +214,30 @@ def encode_batch_host(data, in_off, n, in_len=None, out_off=None, out_size=None,
     status = np.zeros(max(1, n), np.uint8)
     _check(lib().hhuff_encode_batch_host(_hp(data), data.size, _hp(in_off), _hp(in_len), n, _hp(out), out.size,
                                          _hp(out_off), _hp(out_len), _hp(status), device), "hhuff_encode_batch_host")
+    return out, out_len[:n], status[:n]
+
+
+def decode_batch_host_pipelined(data, in_off, n, is_name_bits=None, out=None, chunk_bytes=0, device=0):
+    """Pipelined host decode (contiguous layout).  `out` may be a caller buffer (e.g. pinned memory)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if out is None:
+        out = np.zeros(decode_slot_size(data.size), np.uint8)
+    out_len = np.zeros(max(1, n), np.uint32)
+    status = np.zeros(max(1, n), np.uint8)
+    _check(lib().hhuff_decode_batch_host_pipelined(_hp(data), data.size, _hp(in_off), n, _hp(is_name_bits), _hp(out),
+                                                   out.size, _hp(out_len), _hp(status), device, chunk_bytes),
+           "hhuff_decode_batch_host_pipelined")
+    return out, out_len[:n], status[:n]
+
+
+def encode_batch_host_pipelined(data, in_off, n, out=None, chunk_bytes=0, device=0):
+    """Pipelined host encode (contiguous layout, output slot = in_off)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    if out is None:
+        out = np.zeros(data.size + 16, np.uint8)
+    out_len = np.zeros(max(1, n), np.uint32)
+    status = np.zeros(max(1, n), np.uint8)
+    _check(lib().hhuff_encode_batch_host_pipelined(_hp(data), data.size, _hp(in_off), n, _hp(out), out.size,
+                                                   _hp(out_len), _hp(status), device, chunk_bytes),
+           "hhuff_encode_batch_host_pipelined")
     return out, out_len[:n], status[:n]

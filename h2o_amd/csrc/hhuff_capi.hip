@@ -7,6 +7,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <thread>
+#include <vector>
+
 #include "hhuff.h"
 #include "hhuff_launch.h"
 
@@ -224,11 +228,18 @@ struct Carve {
 
 size_t in_off_count(const uint32_t* in_len, uint32_t n) { return in_len ? n : (size_t)n + 1; }
 
+constexpr uint64_t kDefaultChunk = 64ull << 20;  // pipelined host path: input bytes per chunk
+int pipelined(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+              const uint32_t* is_name_bits, uint8_t* out, uint64_t out_size, uint32_t* out_len, uint8_t* status,
+              int device, uint64_t chunk_bytes);
+
 int host_batch(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len,
                uint32_t n, const uint32_t* is_name_bits, uint8_t* out, uint64_t out_size, const uint32_t* out_off,
                uint32_t* out_len, uint8_t* status, int device) {
     if (n == 0) return HHUFF_OK;
     if (!in || !in_off || !out || !out_len || (decode && !status)) return arg_fail("NULL array");
+    if (!in_len && !out_off && in_size >= 2 * kDefaultChunk && in_off[n] <= in_size)  // large contiguous batch
+        return pipelined(decode, in, in_size, in_off, n, is_name_bits, out, out_size, out_len, status, device, 0);
     Ctx& c = t_ctx;
     int rc = c.bind(device);
     if (rc) return rc;
@@ -265,7 +276,207 @@ int host_batch(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t*
     return HHUFF_OK;
 }
 
+// ---------------------------------------------------------------------------------------------------
+// (3b) pipelined host path: pageable -> pinned -> device -> pinned -> pageable, chunk by chunk
+//
+// The batch (contiguous layout, implicit output slots) is cut at multiples of 32 strings into chunks
+// of about `chunk_bytes` input bytes.  Chunk k runs on stream k % depth: H2D of its input bytes,
+// offsets and is-name words, the kernel, D2H of its output slots, lengths and statuses.  While the GPU
+// works on chunks k-1 and k-2 the calling thread (plus helper threads) copies chunk k's input into its
+// pinned slot and chunk k-depth's results out of theirs, so host copies, both DMA directions and the
+// kernels overlap.  Caller buffers that are already pinned are used by the DMA engines directly.
+// The kernel sees absolute offsets: `in` and `out` are passed shifted back by the chunk base (a
+// multiple of 80 bytes, so the decode slot floor(8 base / 5) stays 16-byte aligned).
+// ---------------------------------------------------------------------------------------------------
+constexpr int kDepth = 3;
+
+bool is_pinned(const void* p) {
+    if (!p) return true;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// memcpy split over a few threads for large copies (the host staging copies bound the host path)
+void par_copy(void* dst, const void* src, size_t n) {
+    const size_t kMin = 4u << 20;
+    unsigned t = std::thread::hardware_concurrency();
+    t = t == 0 ? 1 : (t > 8 ? 8 : t);
+    if (n < kMin || t == 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t per = ((n / t) + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (unsigned k = 1; k < t && k * per < n; ++k)
+        th.emplace_back([=] { memcpy((uint8_t*)dst + k * per, (const uint8_t*)src + k * per, std::min(per, n - k * per)); });
+    memcpy(dst, src, std::min(per, n));
+    for (auto& x : th) x.join();
+}
+
+struct Slot {
+    hipStream_t s = nullptr;
+    uint8_t *d = nullptr, *h = nullptr;
+    size_t dcap = 0, hcap = 0;
+    bool busy = false;
+    // chunk bookkeeping for the host-side unstaging
+    uint64_t i0 = 0, m = 0, out_lo = 0, out_n = 0;
+    size_t h_out = 0, h_len = 0, h_st = 0;
+};
+
+struct Pipe {
+    int dev = -1;
+    Slot slot[kDepth];
+    ~Pipe() {
+        for (auto& x : slot) {
+            if (x.d) (void)hipFree(x.d);
+            if (x.h) (void)hipHostFree(x.h);
+            if (x.s) (void)hipStreamDestroy(x.s);
+        }
+    }
+    int bind(int device) {
+        if (dev == device) return HHUFF_OK;
+        for (auto& x : slot) {
+            if (x.d) (void)hipFree(x.d), x.d = nullptr, x.dcap = 0;
+            if (x.s) (void)hipStreamDestroy(x.s), x.s = nullptr;
+            HIP_TRY(hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking), "hipStreamCreate");
+        }
+        dev = device;
+        return HHUFF_OK;
+    }
+};
+thread_local Pipe t_pipe;
+
+int grow(Slot& x, size_t dneed, size_t hneed) {
+    if (dneed > x.dcap) {
+        if (x.d) (void)hipFree(x.d), x.d = nullptr, x.dcap = 0;
+        HIP_TRY(hipMalloc(&x.d, dneed + dneed / 8), "hipMalloc");
+        x.dcap = dneed + dneed / 8;
+    }
+    if (hneed > x.hcap) {
+        if (x.h) (void)hipHostFree(x.h), x.h = nullptr, x.hcap = 0;
+        HIP_TRY(hipHostMalloc(&x.h, hneed + hneed / 8, hipHostMallocDefault), "hipHostMalloc");
+        x.hcap = hneed + hneed / 8;
+    }
+    return HHUFF_OK;
+}
+
+int pipelined(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+              const uint32_t* is_name_bits, uint8_t* out, uint64_t out_size, uint32_t* out_len, uint8_t* status,
+              int device, uint64_t chunk_bytes) {
+    if (chunk_bytes == 0) chunk_bytes = kDefaultChunk;
+    Ctx& c = t_ctx;
+    int rc = c.bind(device);
+    if (rc) return rc;
+    Pipe& P = t_pipe;
+    rc = P.bind(c.dev);
+    if (rc) return rc;
+    const bool pin_in = is_pinned(in), pin_out = is_pinned(out);
+    auto slot_of = [&](uint64_t pos) { return decode ? (pos * 8) / 5 : pos; };  // implicit output slot
+    // chunk boundaries: multiples of 32 strings, about chunk_bytes of input each
+    std::vector<uint64_t> cut{0};
+    while (cut.back() < n) {
+        const uint64_t a = cut.back();
+        const uint64_t target = (uint64_t)in_off[a] + chunk_bytes;
+        uint64_t b = (uint64_t)(std::upper_bound(in_off + a, in_off + n + 1, (uint32_t)std::min<uint64_t>(target, 0xFFFFFFFFull)) -
+                                in_off);  // first string starting past the target
+        b = b > a + 32 ? ((b - a) / 32) * 32 + a : a + 32;
+        cut.push_back(std::min<uint64_t>(b, n));
+    }
+    auto drain = [&](Slot& x) -> int {
+        if (!x.busy) return HHUFF_OK;
+        HIP_TRY(hipStreamSynchronize(x.s), "sync");
+        if (!pin_out && x.out_n) par_copy(out + x.out_lo, x.h + x.h_out, x.out_n);
+        memcpy(out_len + x.i0, x.h + x.h_len, x.m * 4);
+        if (status) memcpy(status + x.i0, x.h + x.h_st, x.m);
+        x.busy = false;
+        return HHUFF_OK;
+    };
+    for (size_t k = 0; k + 1 < cut.size(); ++k) {
+        Slot& x = P.slot[k % kDepth];
+        rc = drain(x);
+        if (rc) return rc;
+        const uint64_t i0 = cut[k], i1 = cut[k + 1], m = i1 - i0;
+        const uint64_t s0 = in_off[i0], e0 = in_off[i1];
+        const uint64_t base = (s0 / 80) * 80;
+        const uint64_t nbytes = e0 - base;
+        const uint64_t olo = slot_of(s0), ohi = std::min<uint64_t>(slot_of(e0), out_size);
+        const uint64_t obase = slot_of(base);
+        const uint64_t ocap = slot_of(e0) - obase + 16;
+        const size_t nw = decode && is_name_bits ? (size_t)(m + 31) / 32 : 0;
+        // device slot layout: [in bytes][in_off m+1][names][out][out_len m][status m]
+        const size_t o_in = 0, o_off = up16(nbytes + 16), o_nm = o_off + up16((m + 1) * 4), o_out = o_nm + up16(nw * 4),
+                     o_len = o_out + up16(ocap), o_st = o_len + up16(m * 4), dneed = o_st + up16(m);
+        // pinned slot layout: [in bytes][in_off][names] | [out][out_len][status]
+        const size_t hneed = dneed;
+        rc = grow(x, dneed, hneed);
+        if (rc) return rc;
+        if (pin_in) {
+            HIP_TRY(hipMemcpyAsync(x.d + o_in, in + base, nbytes, hipMemcpyHostToDevice, x.s), "H2D in");
+        } else {
+            par_copy(x.h + o_in, in + base, nbytes);
+            HIP_TRY(hipMemcpyAsync(x.d + o_in, x.h + o_in, nbytes, hipMemcpyHostToDevice, x.s), "H2D in");
+        }
+        memcpy(x.h + o_off, in_off + i0, (m + 1) * 4);
+        if (nw) memcpy(x.h + o_nm, is_name_bits + i0 / 32, nw * 4);
+        HIP_TRY(hipMemcpyAsync(x.d + o_off, x.h + o_off, (o_nm - o_off) + nw * 4, hipMemcpyHostToDevice, x.s),
+                "H2D offsets");
+        const uint8_t* d_in = x.d + o_in - base;  // absolute offsets address the chunk
+        uint8_t* d_out = x.d + o_out - obase;
+        const uint32_t* d_off = reinterpret_cast<const uint32_t*>(x.d + o_off);
+        uint32_t* d_len = reinterpret_cast<uint32_t*>(x.d + o_len);
+        uint8_t* d_st = x.d + o_st;
+        hipError_t e = decode ? hhuff::launch_decode(d_in, e0, d_off, nullptr, (uint32_t)m,
+                                                     nw ? reinterpret_cast<const uint32_t*>(x.d + o_nm) : nullptr, d_out,
+                                                     nullptr, d_len, d_st, x.s, nbytes)
+                              : hhuff::launch_encode(d_in, e0, d_off, nullptr, (uint32_t)m, d_out, nullptr, d_len,
+                                                     status ? d_st : nullptr, x.s, nbytes);
+        if (e != hipSuccess) return hip_fail(e, decode ? "decode launch" : "encode launch");
+        x.i0 = i0;
+        x.m = m;
+        x.out_lo = olo;
+        x.out_n = ohi > olo ? ohi - olo : 0;
+        x.h_out = o_out;
+        x.h_len = o_len;
+        x.h_st = o_st;
+        if (x.out_n) {
+            if (pin_out)
+                HIP_TRY(hipMemcpyAsync(out + olo, d_out + olo, x.out_n, hipMemcpyDeviceToHost, x.s), "D2H out");
+            else
+                HIP_TRY(hipMemcpyAsync(x.h + o_out, d_out + olo, x.out_n, hipMemcpyDeviceToHost, x.s), "D2H out");
+        }
+        HIP_TRY(hipMemcpyAsync(x.h + o_len, x.d + o_len, o_st + m - o_len, hipMemcpyDeviceToHost, x.s), "D2H len");
+        x.busy = true;
+    }
+    for (auto& x : P.slot) {
+        rc = drain(x);
+        if (rc) return rc;
+    }
+    return HHUFF_OK;
+}
+
 }  // namespace
+
+HHUFF_API int hhuff_decode_batch_host_pipelined(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+                                                const uint32_t* is_name_bits, uint8_t* out, uint64_t out_size,
+                                                uint32_t* out_len, uint8_t* status, int device, uint64_t chunk_bytes) {
+    if (n == 0) return HHUFF_OK;
+    if (!in || !in_off || !out || !out_len || !status) return arg_fail("NULL array");
+    if (in_off[n] > in_size) return arg_fail("in_off[n] > in_size");
+    return pipelined(true, in, in_size, in_off, n, is_name_bits, out, out_size, out_len, status, device, chunk_bytes);
+}
+
+HHUFF_API int hhuff_encode_batch_host_pipelined(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+                                                uint8_t* out, uint64_t out_size, uint32_t* out_len, uint8_t* status,
+                                                int device, uint64_t chunk_bytes) {
+    if (n == 0) return HHUFF_OK;
+    if (!in || !in_off || !out || !out_len) return arg_fail("NULL array");
+    if (in_off[n] > in_size) return arg_fail("in_off[n] > in_size");
+    return pipelined(false, in, in_size, in_off, n, nullptr, out, out_size, out_len, status, device, chunk_bytes);
+}
 
 HHUFF_API int hhuff_decode_batch_host(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len,
                                       uint32_t n, const uint32_t* is_name_bits, uint8_t* out, uint64_t out_size,

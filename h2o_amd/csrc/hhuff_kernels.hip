@@ -1252,10 +1252,10 @@ static int pick_encode(uint64_t in_size, uint32_t n) {
 
 hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
                          const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
-                         uint8_t* status, hipStream_t stream) {
+                         uint8_t* status, hipStream_t stream, uint64_t sel_bytes) {
     if (n == 0) return hipSuccess;
     DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status};
-    const int v = pick_decode(in_size, n);
+    const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n);
     const int grid = grid_for(v, current_device(), n);
     switch (v) {
         case kDecS: hipLaunchKernelGGL(DEC_S, dim3(grid), dim3(HHUFF_DSW * 64), 0, stream, A); break;
@@ -1266,9 +1266,11 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
 }
 
 hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
-                         uint8_t* out, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, hipStream_t stream) {
+                         uint8_t* out, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, hipStream_t stream,
+                         uint64_t sel_bytes) {
     if (n == 0) return hipSuccess;
     EncArgs A{in, in_size, in_off, in_len, n, out, out_off, out_len, status};
+    if (sel_bytes) in_size = sel_bytes;  // variant selection only; A keeps the addressable size
 #ifdef HHUFF_ENCODE_CHUNKED
     if (in_len == nullptr && out_off == nullptr) {  // contiguous implicit layout: byte-balanced chunks
         const uint64_t mean = in_size / n;

@@ -6,9 +6,13 @@
 namespace hhuff {
 hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
                          const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
-                         uint8_t* status, hipStream_t stream);
+                         uint8_t* status, hipStream_t stream, uint64_t sel_bytes = 0);
 hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
-                         uint8_t* out, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, hipStream_t stream);
+                         uint8_t* out, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, hipStream_t stream,
+                         uint64_t sel_bytes = 0);
+// sel_bytes: bytes the batch's strings span, used only to pick the kernel variant from the mean string
+// length (0 = in_size).  Chunked callers pass `in` shifted back by the chunk base so that absolute
+// offsets address the chunk; in_size is then absolute and sel_bytes carries the chunk's own span.
 hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
                           const uint8_t* first_bytes, uint32_t prefix_bits, const uint32_t* raw_bits, uint8_t* out,
                           const uint32_t* out_off, uint32_t* out_len, hipStream_t stream);

@@ -109,6 +109,21 @@ int hhuff_encode_batch_host(const uint8_t *in, uint64_t in_size, const uint32_t 
                             uint32_t n, uint8_t *out, uint64_t out_size, const uint32_t *out_off, uint32_t *out_len,
                             uint8_t *status, int device);
 
+/* (3b) Pipelined host path (the socket-buffer -> pinned -> device -> pinned -> pool staging of
+ *     SURVEY f3; replaces the caller-side copies around lib/http2/hpack.c:240-241).  Contiguous layout
+ *     (in_off[n + 1], implicit output slots) only.  The batch is cut into chunks of about
+ *     `chunk_bytes` input bytes (0 = 64 MiB) at multiples of 32 strings; chunks flow through three
+ *     streams so that host staging copies, H2D, kernels and D2H of different chunks overlap.  Caller
+ *     buffers already pinned (hipHostMalloc / hipHostRegister) are DMA'd directly.  Synchronous; the
+ *     results equal hhuff_*_batch_host's.  hhuff_*_batch_host take this path by themselves for
+ *     contiguous batches of 128 MiB and more. */
+int hhuff_decode_batch_host_pipelined(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, uint32_t n,
+                                      const uint32_t *is_name_bits, uint8_t *out, uint64_t out_size,
+                                      uint32_t *out_len, uint8_t *status, int device, uint64_t chunk_bytes);
+int hhuff_encode_batch_host_pipelined(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, uint32_t n,
+                                      uint8_t *out, uint64_t out_size, uint32_t *out_len, uint8_t *status,
+                                      int device, uint64_t chunk_bytes);
+
 /* ---------------------------------------------------------------------------------------------
  * (4) library info
  * ------------------------------------------------------------------------------------------- */
