@@ -56,6 +56,9 @@ def lib():
         L.hhuff_encode_batch_host.restype = ctypes.c_int
         L.hhuff_encode_batch_host.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint64,
                                               _vp, _vp, _vp, ctypes.c_int]
+        L.hhuff_decode_literals.restype = ctypes.c_int
+        L.hhuff_decode_literals.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint, ctypes.c_uint,
+                                            _vp, _vp, _vp, _vp, _vp, _vp, _vp]
         L.hhuff_decode_batch_host_pipelined.restype = ctypes.c_int
         L.hhuff_decode_batch_host_pipelined.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, _vp,
                                                         ctypes.c_uint64, _vp, _vp, ctypes.c_int, ctypes.c_uint64]
@@ -72,7 +75,7 @@ def lib():
 
 # symbols include/hhuff.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decode_batch", "hhuff_encode_batch",
-            "hhuff_flatten_batch",
+            "hhuff_flatten_batch", "hhuff_decode_literals",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string",
             "hhuff_grid_size")
@@ -180,6 +183,30 @@ def flatten_batch(data, in_off, n, prefix_bits=7, in_len=None, first_bytes=None,
                                      _dp(raw_bits), _dp(out), _dp(out_off), _dp(out_len), _stream(stream)),
            "hhuff_flatten_batch")
     return out, out_len
+
+
+LIT_QPACK = 1
+
+
+def decode_literals(data, lit_off, lit_end, n, prefix_bits=7, qpack=False, is_name_bits=None, out=None, in_size=None,
+                    stream=None):
+    """Batched HPACK decode_string / QPACK literal decode on device tensors.
+    Returns (out, out_len, pay_off, consumed, status); decoded bytes at out[floor(8 * pay_off / 5)]."""
+    import torch
+
+    dev = data.device
+    in_size = data.numel() if in_size is None else in_size
+    if out is None:
+        out = torch.empty(decode_slot_size(in_size), dtype=torch.uint8, device=dev)
+    m = max(n, 1)
+    out_len = torch.empty(m, dtype=torch.int32, device=dev)
+    pay_off = torch.empty(m, dtype=torch.int32, device=dev)
+    consumed = torch.empty(m, dtype=torch.int32, device=dev)
+    status = torch.empty(m, dtype=torch.uint8, device=dev)
+    _check(lib().hhuff_decode_literals(_dp(data), in_size, _dp(lit_off), _dp(lit_end), n, prefix_bits,
+                                       LIT_QPACK if qpack else 0, _dp(is_name_bits), _dp(out), _dp(out_len),
+                                       _dp(pay_off), _dp(consumed), _dp(status), _stream(stream)), "hhuff_decode_literals")
+    return out, out_len, pay_off, consumed, status
 
 
 # ---------------------------------------------------------------------------------------------------

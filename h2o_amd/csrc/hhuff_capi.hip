@@ -134,6 +134,25 @@ HHUFF_API int hhuff_flatten_batch(const uint8_t* in, uint64_t in_size, const uin
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "flatten launch");
 }
 
+HHUFF_API int hhuff_decode_literals(const uint8_t* in, uint64_t in_size, const uint32_t* lit_off, const uint32_t* lit_end,
+                                    uint32_t n, unsigned prefix_bits, unsigned flags, const uint32_t* is_name_bits,
+                                    uint8_t* out, uint32_t* out_len, uint32_t* pay_off, uint32_t* consumed,
+                                    uint8_t* status, void* stream) {
+    int rc = check_batch(in, lit_off, n, out, out_len);
+    if (rc) return rc;
+    if (n && (!lit_end || !pay_off || !consumed || !status)) return arg_fail("NULL array");
+    if (prefix_bits < 1 || prefix_bits > 7) return arg_fail("prefix_bits must be in 1..7");
+    if (n == 0) return HHUFF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    void* ws = nullptr;  // Huffman payload lengths, stream-ordered scratch
+    HIP_TRY(hipMallocAsync(&ws, (size_t)n * 4, s), "hipMallocAsync");
+    hipError_t e = hhuff::launch_literals(in, in_size, lit_off, lit_end, n, prefix_bits, flags, is_name_bits, out, out_len,
+                                          pay_off, consumed, status, (uint32_t*)ws, s);
+    hipError_t f = hipFreeAsync(ws, s);
+    if (e != hipSuccess) return hip_fail(e, "literal launch");
+    return f == hipSuccess ? HHUFF_OK : hip_fail(f, "hipFreeAsync");
+}
+
 // ---------------------------------------------------------------------------------------------------
 // (1) h2o per-string symbols: a batch of one on the thread's stream, synchronously
 // device/pinned layout: [meta 32 B: u32 in_off[2], out_len, is_name word, u8 status][input][output]

@@ -22,6 +22,8 @@
 namespace hhuff {
 
 __device__ const uint32_t g_dec_lut[1u << HHUFF_LUT_BITS] = HHUFF_DEC_LUT_INIT;
+__device__ const uint32_t g_name_invalid[8] = HHUFF_NAME_INVALID_INIT;    // raw-literal validity bitmaps
+__device__ const uint32_t g_value_invalid[8] = HHUFF_VALUE_INVALID_INIT;  // (hpack.c:171-180, 200-209)
 __device__ const uint32_t g_kinfo[31] = HHUFF_ONES_KINFO_INIT;
 __device__ const uint32_t g_ones[HHUFF_ONES_NENT] = HHUFF_ONES_ENT_INIT;
 __device__ const uint32_t g_enc_code[256] = HHUFF_ENC_CODE_INIT;
@@ -1149,6 +1151,152 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
 }
 
 // ------------------------------------------------------------------------------------------------
+// String literals in header blocks: HPACK decode_string (hpack.c:223-261) and QPACK
+// decode_header_{name,value}_literal (qpack.c:559-629).  Literal i starts at in[lit_off[i]]: the H flag
+// at bit prefix_bits of that byte, the length as a prefix integer (h2o_hpack_decode_int, hpack.c:52-83),
+// then the payload, all before in[lit_end[i]].  Three launches: parse the headers (payload offset and
+// Huffman length per literal), the Huffman decode kernel over (payload, length) pairs, then a fix-up
+// that validates and copies the raw literals (h2o_hpack_validate_header_name / _value, hpack.c:163-221)
+// and folds the header verdicts into out_len / status.
+// ------------------------------------------------------------------------------------------------
+struct LitArgs {
+    const uint8_t* in;
+    uint64_t in_size;
+    const uint32_t* lit_off;
+    const uint32_t* lit_end;
+    uint32_t n;
+    uint32_t prefix_bits;
+    uint32_t flags;
+    const uint32_t* is_name_bits;
+    uint8_t* out;
+    uint32_t* out_len;
+    uint32_t* pay_off;
+    uint32_t* consumed;
+    uint8_t* status;
+    uint32_t* huff_len;  // workspace: Huffman payload length (0 for raw literals and errors)
+};
+
+enum : uint32_t { kLitIncomplete = 1, kLitBadInt = 2, kLitTruncated = 3, kLitHuffman = 4, kLitUpper = 5, kLitTooLong = 6 };
+
+// header of literal i -> verdict (0 = ok); hdr = header bytes, len = payload bytes, huff = H flag
+__device__ __forceinline__ uint32_t lit_header(const LitArgs& A, uint32_t i, bool& huff, uint32_t& hdr, uint32_t& len) {
+    const uint64_t off = A.lit_off[i];
+    const uint64_t end = min((uint64_t)A.lit_end[i], A.in_size);
+    huff = false;
+    hdr = 0;
+    len = 0;
+    if (off >= end) return kLitIncomplete;
+    const uint32_t p = A.prefix_bits;
+    const uint32_t b0 = A.in[off];
+    huff = ((b0 >> p) & 1u) != 0;
+    const uint64_t pmax = (1u << p) - 1u;
+    uint64_t v = b0 & pmax, q = off + 1;
+    if (v == pmax) {
+        bool done = false;
+        uint32_t shift = 0;
+        for (; shift < 56; shift += 7) {
+            if (q == end) return kLitIncomplete;
+            const uint32_t b = A.in[q++];
+            v += (uint64_t)(b & 127u) << shift;
+            if (!(b & 128u)) {
+                done = true;
+                break;
+            }
+        }
+        if (!done) {  // the 9th octet (hpack.c:75-81)
+            if (q == end) return kLitIncomplete;
+            const uint32_t b = A.in[q];
+            if (b & 128u) return kLitBadInt;
+            v += (uint64_t)(b & 127u) << shift;
+            ++q;
+            if (v > 0x7FFFFFFFFFFFFFFFull) return kLitBadInt;
+        }
+    }
+    if (v > end - q) return kLitTruncated;
+    if (v > kMaxStrLen) return kLitTooLong;
+    hdr = (uint32_t)(q - off);
+    len = (uint32_t)v;
+    return 0;
+}
+
+__global__ void literal_parse_kernel(LitArgs A) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        bool huff;
+        uint32_t hdr, len;
+        const uint32_t v = lit_header(A, (uint32_t)i, huff, hdr, len);
+        A.pay_off[i] = A.lit_off[i] + hdr;
+        A.huff_len[i] = (v == 0 && huff) ? len : 0u;
+        A.consumed[i] = v == 0 ? hdr + len : 0u;
+    }
+}
+
+__device__ __forceinline__ bool pseudo_token(const uint8_t* s, uint32_t len) {  // lib/common/token_table.h
+    const char* tok[6] = {":authority", ":method", ":path", ":protocol", ":scheme", ":status"};
+    const uint32_t tl[6] = {10, 7, 5, 9, 7, 7};
+    for (int k = 0; k < 6; ++k) {
+        if (tl[k] != len) continue;
+        bool eq = true;
+        for (uint32_t j = 0; j < len && eq; ++j) eq = s[j] == (uint8_t)tok[k][j];
+        if (eq) return true;
+    }
+    return false;
+}
+
+__global__ void literal_fix_kernel(LitArgs A) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        bool huff;
+        uint32_t hdr, len;
+        const uint32_t v = lit_header(A, (uint32_t)i, huff, hdr, len);
+        if (v) {
+            A.out_len[i] = kFailLen;
+            A.status[i] = (uint8_t)(kStatusFail | (v << 2));
+            continue;
+        }
+        if (huff) {  // the Huffman kernel already wrote out_len / status
+            if (A.status[i] & kStatusFail) {
+                A.status[i] = (uint8_t)(kStatusFail | (kLitHuffman << 2));
+                A.consumed[i] = 0;
+            }
+            continue;
+        }
+        const bool is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) != 0 : false;
+        const uint8_t* src = A.in + A.lit_off[i] + hdr;
+        uint8_t* dst = A.out + ((uint64_t)(A.lit_off[i] + hdr) * 8u) / 5u;
+        uint32_t soft = 0;
+        bool upper = false;
+        if (is_name) {
+            const bool skip = (A.flags & 1u) ? pseudo_token(src, len) : (len != 0 && src[0] == ':');
+            if (!skip) {
+                if (len == 0) soft = 0x1;
+                for (uint32_t j = 0; j < len && !upper; ++j) {
+                    const uint32_t c = src[j];
+                    if ((g_name_invalid[c >> 5] >> (c & 31)) & 1u) {
+                        if (c - 'A' < 26u) upper = true;
+                        else soft = 0x1;
+                    }
+                }
+            }
+        } else {
+            bool bad = len != 0 && (src[0] == ' ' || src[0] == '\t' || src[len - 1] == ' ' || src[len - 1] == '\t');
+            for (uint32_t j = 0; j < len && !bad; ++j) {
+                const uint32_t c = src[j];
+                bad = ((g_value_invalid[c >> 5] >> (c & 31)) & 1u) != 0;
+            }
+            soft = bad ? 0x2 : 0u;
+        }
+        if (upper) {
+            A.out_len[i] = kFailLen;
+            A.status[i] = (uint8_t)(soft | kStatusFail | (kLitUpper << 2));
+            A.consumed[i] = 0;
+            continue;
+        }
+        for (uint32_t j = 0; j < len; ++j) dst[j] = src[j];
+        A.out_len[i] = len;
+        A.status[i] = (uint8_t)soft;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // launch configuration (LDS per workgroup in brackets)
 //   decode staged:        16 waves/WG, 3 KiB in + 4.5 KiB out per wave   [~158 KiB, 1 WG/CU]
 //   decode staged (long):  6 waves/WG, 8 KiB in + 12.9 KiB out per wave [~144 KiB, 1 WG/CU]
@@ -1329,6 +1477,23 @@ hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* i
     }
     const int grid = grid_for(kFlatD, current_device(), n);
     hipLaunchKernelGGL(FLAT_D, dim3(grid), dim3(256), 0, stream, A);
+    return hipGetLastError();
+}
+
+hipError_t launch_literals(const uint8_t* in, uint64_t in_size, const uint32_t* lit_off, const uint32_t* lit_end, uint32_t n,
+                           uint32_t prefix_bits, uint32_t flags, const uint32_t* is_name_bits, uint8_t* out,
+                           uint32_t* out_len, uint32_t* pay_off, uint32_t* consumed, uint8_t* status, uint32_t* huff_len,
+                           hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    LitArgs A{in, in_size, lit_off, lit_end, n, prefix_bits, flags, is_name_bits, out, out_len, pay_off, consumed, status,
+              huff_len};
+    const uint32_t blocks = min((n + 255u) / 256u, 4096u);
+    hipLaunchKernelGGL(literal_parse_kernel, dim3(blocks), dim3(256), 0, stream, A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = launch_decode(in, in_size, pay_off, huff_len, n, is_name_bits, out, nullptr, out_len, status, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(literal_fix_kernel, dim3(blocks), dim3(256), 0, stream, A);
     return hipGetLastError();
 }
 

@@ -16,5 +16,9 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
 hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
                           const uint8_t* first_bytes, uint32_t prefix_bits, const uint32_t* raw_bits, uint8_t* out,
                           const uint32_t* out_off, uint32_t* out_len, hipStream_t stream);
+hipError_t launch_literals(const uint8_t* in, uint64_t in_size, const uint32_t* lit_off, const uint32_t* lit_end, uint32_t n,
+                           uint32_t prefix_bits, uint32_t flags, const uint32_t* is_name_bits, uint8_t* out,
+                           uint32_t* out_len, uint32_t* pay_off, uint32_t* consumed, uint8_t* status, uint32_t* huff_len,
+                           hipStream_t stream);
 int grid_size(int device, int which);
 }  // namespace hhuff

@@ -109,6 +109,30 @@ int hhuff_encode_batch_host(const uint8_t *in, uint64_t in_size, const uint32_t 
                             uint32_t n, uint8_t *out, uint64_t out_size, const uint32_t *out_off, uint32_t *out_len,
                             uint8_t *status, int device);
 
+/* (2b) Batched string-literal decode: HPACK decode_string (lib/http2/hpack.c:223-261) and
+ *      QPACK decode_header_value_literal / decode_header_name_literal (lib/http3/qpack.c:559-629),
+ *      minus the memory pool.  Literal i starts at in[lit_off[i]] -- its first byte carries the H flag
+ *      at bit prefix_bits and the length as a prefix_bits-bit prefix integer (h2o_hpack_decode_int,
+ *      hpack.c:52-83) -- and must end by in[lit_end[i]] (the walker's src_end).  Huffman payloads are
+ *      decoded as h2o_hpack_decode_huffman does; raw payloads are copied and validated with
+ *      h2o_hpack_validate_header_name / _value (hpack.c:163-221).  Raw names skip validation when they
+ *      start with ':' (HPACK) or, with HHUFF_LIT_QPACK, when h2o_lookup_token knows them (qpack.c:585).
+ *      Outputs: pay_off[i] = offset of the payload in `in`; decoded bytes at out + floor(8 pay_off[i] / 5)
+ *      (out sized floor(8 in_size / 5) + 16); out_len[i] (HHUFF_FAIL_LEN on failure); consumed[i] =
+ *      header + payload bytes, how far the walker's cursor advances (0 on failure); status[i] = soft
+ *      bits (0x1 name, 0x2 value) | on failure HHUFF_STATUS_FAIL | verdict << 2 (HHUFF_LIT_*).
+ *      Device arrays, asynchronous on `stream`; uses stream-ordered scratch (4 n bytes). */
+#define HHUFF_LIT_QPACK 1u
+#define HHUFF_LIT_INCOMPLETE 1 /* no byte, or the length integer runs past lit_end (H2O_HTTP2_ERROR_INCOMPLETE) */
+#define HHUFF_LIT_BAD_INT 2    /* length integer overflow (H2O_HTTP2_ERROR_COMPRESSION from decode_int) */
+#define HHUFF_LIT_TRUNCATED 3  /* length > bytes left before lit_end */
+#define HHUFF_LIT_HUFFMAN 4    /* h2o_hpack_decode_huffman returned SIZE_MAX */
+#define HHUFF_LIT_UPPERCASE 5  /* raw name with an upper-case letter (validate_header_name returned 0) */
+#define HHUFF_LIT_TOO_LONG 6   /* payload of 2^29 bytes or more (this library's per-string limit) */
+int hhuff_decode_literals(const uint8_t *in, uint64_t in_size, const uint32_t *lit_off, const uint32_t *lit_end,
+                          uint32_t n, unsigned prefix_bits, unsigned flags, const uint32_t *is_name_bits, uint8_t *out,
+                          uint32_t *out_len, uint32_t *pay_off, uint32_t *consumed, uint8_t *status, void *stream);
+
 /* (3b) Pipelined host path (the socket-buffer -> pinned -> device -> pinned -> pool staging of
  *     SURVEY f3; replaces the caller-side copies around lib/http2/hpack.c:240-241).  Contiguous layout
  *     (in_off[n + 1], implicit output slots) only.  The batch is cut into chunks of about

@@ -21,7 +21,9 @@
 
 typedef struct {
     const uint8_t *in;
-    const uint32_t *in_off, *in_len, *is_name_bits, *out_off, *raw_bits;
+    const uint32_t *in_off, *in_len, *is_name_bits, *out_off, *raw_bits, *lit_end;
+    uint32_t *pay_off, *consumed;
+    unsigned flags;
     const uint8_t *first_bytes;
     unsigned prefix_bits;
     uint8_t *out;
@@ -84,6 +86,27 @@ static void *ORC_FN(flatten_worker)(void *arg)
     return NULL;
 }
 
+#ifdef ORC_CODEC_LITERAL
+/* literal i starts at in[in_off[i]] and may extend to in[lit_end[i]]; decoded bytes at
+ * out + floor(8 * pay_off[i] / 5); status = soft bits | 0x80 | verdict << 2 on failure */
+static void *ORC_FN(literal_worker)(void *arg)
+{
+    ORC_FN(job_t) *j = (ORC_FN(job_t) *)arg;
+    for (uint32_t i = j->begin; i < j->end; ++i) {
+        int is_name = j->is_name_bits ? (int)((j->is_name_bits[i >> 5] >> (i & 31)) & 1u) : 0;
+        unsigned soft = 0;
+        uint32_t hdr, consumed, olen;
+        int code = ORC_CODEC_LITERAL(j->in + j->in_off[i], j->in + j->lit_end[i], j->prefix_bits, is_name,
+                                     (int)(j->flags & 1u), j->out, j->in_off[i], &hdr, &consumed, &olen, &soft);
+        j->out_len[i] = code ? 0xFFFFFFFFu : olen;
+        j->pay_off[i] = j->in_off[i] + hdr;
+        j->consumed[i] = code ? 0u : consumed;
+        j->status[i] = (uint8_t)(soft | (code ? 0x80u | ((unsigned)code << 2) : 0u));
+    }
+    return NULL;
+}
+#endif
+
 static int ORC_FN(run)(void *(*fn)(void *), const ORC_FN(job_t) * proto, uint32_t n, int nthreads)
 {
     if (nthreads < 1)
@@ -142,3 +165,17 @@ ORC_BATCH_API int ORC_FN(flatten_batch)(const uint8_t *in, const uint32_t *in_of
     p.raw_bits = raw_bits, p.out = out, p.out_off = out_off, p.out_len = out_len;
     return ORC_FN(run)(ORC_FN(flatten_worker), &p, n, nthreads);
 }
+
+#ifdef ORC_CODEC_LITERAL
+ORC_BATCH_API int ORC_FN(literals_batch)(const uint8_t *in, const uint32_t *lit_off, const uint32_t *lit_end, uint32_t n,
+                                         unsigned prefix_bits, unsigned flags, const uint32_t *is_name_bits, uint8_t *out,
+                                         uint32_t *out_len, uint32_t *pay_off, uint32_t *consumed, uint8_t *status,
+                                         int nthreads)
+{
+    ORC_FN(job_t) p = {0};
+    p.in = in, p.in_off = lit_off, p.lit_end = lit_end, p.prefix_bits = prefix_bits, p.flags = flags;
+    p.is_name_bits = is_name_bits, p.out = out, p.out_len = out_len, p.pay_off = pay_off, p.consumed = consumed;
+    p.status = status;
+    return ORC_FN(run)(ORC_FN(literal_worker), &p, n, nthreads);
+}
+#endif

@@ -14,6 +14,11 @@ Fixture sets (numpy .npz, arrays only, no pickles):
                    re-decoded by the reference, plus the plain bytes decoded as (mostly invalid) Huffman
   adversarial.npz  hand-built decode edge cases (padding, EOS, truncation, long codes, names/values)
   framing.npz      HPACK h2o_hpack_encode_string and QPACK flatten_string (prefix 3/5/7) outputs
+  literals.npz     string literals as they sit in header blocks: every literal of the fuzz corpus's
+                   HPACK blocks plus hand-built edge cases (raw names/values to validate, bad and
+                   truncated integers, invalid Huffman), and QPACK name literals (prefix 3/5) -- the
+                   reference's decode_int / decode_huffman / validators / h2o_lookup_token composed as
+                   decode_string and decode_header_{name,value}_literal call them (oracle/ref_shim.c)
 
 Usage:  python3 oracle/gen_golden.py            (rewrites tests/golden/)
 """
@@ -315,6 +320,142 @@ def framing_set(seed=11):
                 int_values=np.asarray(ints, np.uint64), int_out=iod, int_out_off=ioo)
 
 
+def block_literals(block):
+    """-> list of (offset of the literal's first byte, is_name) for every string literal of a block"""
+    out, p = [], 0
+    while p < len(block):
+        c = block[p]
+        if c & 0x80:
+            _, p = _int(block, p, 7)
+            if p is None:
+                break
+            continue
+        if c & 0x40:
+            idx, p = _int(block, p, 6)
+        elif c & 0x20:
+            _, p = _int(block, p, 5)
+            if p is None:
+                break
+            continue
+        else:
+            idx, p = _int(block, p, 4)
+        if p is None:
+            break
+        for is_name in ((True, False) if idx == 0 else (False,)):
+            if p >= len(block):
+                return out
+            out.append((p, is_name))
+            n, q = _int(block, p, 7)
+            if n is None or q + n > len(block):
+                return out
+            p = q + n
+    return out
+
+
+def _lit(first_hi, prefix, huff, payload, r=None):
+    """literal bytes: first byte's bits above the H flag, H flag at bit `prefix`, prefix-int length"""
+    head = bytes([(first_hi & ~((2 << prefix) - 1) & 0xFF) | ((1 << prefix) if huff else 0)])
+    enc = O.ref().encode_int(len(payload), prefix, head[0])
+    return enc + payload
+
+
+def literals_set(seed=13):
+    r = O.ref()
+    rng = np.random.default_rng(seed)
+    buf, offs, ends, names = bytearray(), [], [], []
+    # (1) HPACK: the corpus's header blocks as they are
+    d = os.path.join(REF_ROOT, "fuzz", "http2-corpus")
+    for f in sorted(os.listdir(d)):
+        with open(os.path.join(d, f), "rb") as fh:
+            data = fh.read()
+        for blk in header_blocks(data):
+            base = len(buf)
+            lits = block_literals(blk)
+            if not lits:
+                continue
+            buf += blk
+            for p, nm in lits:
+                offs.append(base + p)
+                ends.append(base + len(blk))
+                names.append(nm)
+    n_corpus = len(offs)
+    # (2) HPACK edge cases, one block
+    huf = lambda s: huff_bits(s)  # noqa: E731
+    cases = [  # (is_name, literal bytes)
+        (True, _lit(0, 7, False, b"Content-Type")), (True, _lit(0, 7, False, b"x y")), (True, _lit(0, 7, False, b"")),
+        (True, _lit(0, 7, False, b":authority")), (True, _lit(0, 7, False, b":custom")),
+        (True, _lit(0, 7, False, b"a B")), (True, _lit(0, 7, False, b"ab\x00c")), (True, _lit(0, 7, False, b"ok-name")),
+        (False, _lit(0, 7, False, b" lead")), (False, _lit(0, 7, False, b"trail\t")), (False, _lit(0, 7, False, b"")),
+        (False, _lit(0, 7, False, b"\x01bad")), (False, _lit(0, 7, False, b"del\x7f")), (False, _lit(0, 7, False, b"fine")),
+        (False, _lit(0, 7, False, bytes(range(0x80, 0x100)))),
+        (True, _lit(0, 7, True, huf(b"UPPER"))), (True, _lit(0, 7, True, huf(b":upper-OK"))), (True, _lit(0, 7, True, b"")),
+        (False, _lit(0, 7, True, huf(b" sp "))), (False, _lit(0, 7, True, b"\xff\xff\xff\xff")),
+        (False, _lit(0, 7, True, huf(b"www.example.com")[:-1])), (False, _lit(0, 7, True, huf(b"A" * 300))),
+        (False, bytes([0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0x01])),  # 9th octet continuation
+        (False, bytes([0x7F, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0x7F])),  # > INT64_MAX? (value check)
+        (False, bytes([0x05]) + b"abc"),  # length past the block end (TRUNCATED) -- last before the tail
+    ]
+    base = len(buf)
+    blk = bytearray()
+    for nm, b in cases[:-1]:
+        offs.append(base + len(blk))
+        names.append(nm)
+        blk += b
+    offs.append(base + len(blk))
+    names.append(cases[-1][0])
+    blk += cases[-1][1]
+    buf += blk
+    ends += [base + len(blk)] * len(cases)
+    # truncated integer at the very end of a block, and an empty tail
+    base = len(buf)
+    buf += bytes([0x7F, 0x80])
+    offs += [base, base + 2]
+    ends += [base + 2, base + 2]
+    names += [False, False]
+    n_hpack = len(offs)
+    # (3) QPACK name literals with prefix 3 and 5 (and values with 7): raw / Huffman, tokens
+    syms, p = synth.header_alphabet()
+    q_off = {3: [], 5: [], 7: []}
+    q_end = {3: [], 5: [], 7: []}
+    q_name = {3: [], 5: [], 7: []}
+    qbuf = bytearray()
+    pool = [b":path", b":status", b":custom", b"content-type", b"Accept", b"x-a b", b""]
+    for i in range(1500):
+        pb = int(rng.choice([3, 5, 7]))
+        nm = pb != 7 or rng.random() < 0.3
+        k = rng.random()
+        if k < 0.3:
+            s = pool[int(rng.integers(0, len(pool)))]
+        else:
+            s = bytes(rng.choice(syms, int(rng.integers(0, 40)), p=p))
+        huff = rng.random() < 0.5
+        lit = _lit(int(rng.integers(0, 256)), pb, huff, huf(s) if huff else s)
+        q_off[pb].append(len(qbuf))
+        qbuf += lit
+        q_end[pb].append(len(qbuf))
+        q_name[pb].append(nm)
+    res = dict(lit_in=np.frombuffer(bytes(buf), np.uint8), lit_off=np.asarray(offs, np.uint32),
+               lit_end=np.asarray(ends, np.uint32), lit_names=synth.bits_from_bools(np.asarray(names, bool)),
+               n_corpus=np.asarray([n_corpus], np.uint32), q_in=np.frombuffer(bytes(qbuf), np.uint8))
+    lit_in = res["lit_in"]
+    out, ol, po, cons, st = r.literals_batch(lit_in, res["lit_off"], res["lit_end"], n_hpack, 7,
+                                             is_name_bits=res["lit_names"])
+    slots = (po.astype(np.uint64) * 8) // 5
+    res.update(h_out_len=ol, h_pay_off=po, h_consumed=cons, h_status=st,
+               h_out=np.frombuffer(b"".join(out[int(a):int(a) + int(L)].tobytes() for a, L in zip(slots, ol)
+                                            if L != 0xFFFFFFFF), np.uint8))
+    for pb in (3, 5, 7):
+        qo, qe = np.asarray(q_off[pb], np.uint32), np.asarray(q_end[pb], np.uint32)
+        qn = synth.bits_from_bools(np.asarray(q_name[pb], bool))
+        out, ol, po, cons, st = r.literals_batch(res["q_in"], qo, qe, len(qo), pb, qpack=True, is_name_bits=qn)
+        slots = (po.astype(np.uint64) * 8) // 5
+        res.update({"q%d_off" % pb: qo, "q%d_end" % pb: qe, "q%d_names" % pb: qn, "q%d_out_len" % pb: ol,
+                    "q%d_pay_off" % pb: po, "q%d_consumed" % pb: cons, "q%d_status" % pb: st,
+                    "q%d_out" % pb: np.frombuffer(b"".join(out[int(a):int(a) + int(L)].tobytes()
+                                                           for a, L in zip(slots, ol) if L != 0xFFFFFFFF), np.uint8)})
+    return res
+
+
 def main():
     if not O.ref_available():
         sys.exit("oracle/_ref/libh2oref.so missing: run `make -C oracle` where /root/reference exists")
@@ -328,6 +469,7 @@ def main():
         sets["random_" + cfg] = random_set(cfg, n, seed)
     sets["adversarial"] = adversarial_set()
     sets["framing"] = framing_set()
+    sets["literals"] = literals_set()
     for name, arrays in sets.items():
         path = os.path.join(GOLDEN, name + ".npz")
         np.savez_compressed(path, **arrays)

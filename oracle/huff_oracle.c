@@ -193,10 +193,93 @@ size_t orc_flatten_string(uint8_t *dst, const uint8_t *s, size_t len, unsigned p
     return head_len + hl;
 }
 
+/* ---- string literals (decode_string hpack.c:223-261; QPACK qpack.c:559-629 without the pool) ---- */
+
+/* h2o_hpack_validate_header_name (hpack.c:163-193): 0 = upper-case letter (hard error) */
+static int orc_validate_name(unsigned *soft, const uint8_t *s, size_t len)
+{
+    if (len == 0) {
+        *soft |= ORC_SOFT_NAME;
+        return 1;
+    }
+    for (; len != 0; ++s, --len) {
+        if (!orc_name_valid[*s]) {
+            if ((unsigned)(*s - 'A') < 26u)
+                return 0;
+            *soft |= ORC_SOFT_NAME;
+        }
+    }
+    return 1;
+}
+
+/* h2o_hpack_validate_header_value (hpack.c:195-221) */
+static void orc_validate_value(unsigned *soft, const uint8_t *s, size_t len)
+{
+    int bad = !orc_value_ws_ok((const char *)s, len);
+    for (size_t i = 0; !bad && i < len; ++i)
+        bad = !orc_value_valid[s[i]];
+    if (bad)
+        *soft |= ORC_SOFT_VALUE;
+}
+
+/* QPACK raw names skip validation when h2o_lookup_token finds them (qpack.c:585); the only tokens
+ * the validator would flag are the pseudo-header names (lib/common/token_table.h) */
+static int orc_is_pseudo_token(const uint8_t *s, size_t len)
+{
+    static const char *const tok[] = {":authority", ":method", ":path", ":protocol", ":scheme", ":status"};
+    for (size_t k = 0; k < sizeof(tok) / sizeof(tok[0]); ++k)
+        if (strlen(tok[k]) == len && memcmp(tok[k], s, len) == 0)
+            return 1;
+    return 0;
+}
+
+int orc_decode_literal(const uint8_t *lit, const uint8_t *end, unsigned prefix_bits, int is_name, int qpack,
+                       uint8_t *out, uint64_t lit_pos, uint32_t *hdr, uint32_t *consumed, uint32_t *out_len,
+                       unsigned *soft)
+{
+    const uint8_t *p = lit;
+    *hdr = 0;
+    *consumed = 0;
+    *out_len = ORC_FAIL_LEN;
+    if (p >= end)
+        return ORC_LIT_INCOMPLETE;
+    int huff = (*p >> prefix_bits) & 1;
+    int64_t len = orc_decode_int(&p, end, prefix_bits);
+    if (len == ORC_INT_INCOMPLETE)
+        return ORC_LIT_INCOMPLETE;
+    if (len < 0)
+        return ORC_LIT_BAD_INT;
+    if (len > end - p)
+        return ORC_LIT_TRUNCATED;
+    if (len > (int64_t)ORC_MAX_STR)
+        return ORC_LIT_TOO_LONG;
+    *hdr = (uint32_t)(p - lit);
+    uint8_t *dst = out + ((lit_pos + *hdr) * 8u) / 5u;
+    if (huff) {
+        size_t r = orc_decode_huffman((char *)dst, soft, p, (size_t)len, is_name);
+        if (r == SIZE_MAX)
+            return ORC_LIT_HUFFMAN;
+        *out_len = (uint32_t)r;
+    } else {
+        if (is_name) {
+            int skip = qpack ? orc_is_pseudo_token(p, (size_t)len) : (len != 0 && p[0] == ':');
+            if (!skip && !orc_validate_name(soft, p, (size_t)len))
+                return ORC_LIT_UPPERCASE;
+        } else {
+            orc_validate_value(soft, p, (size_t)len);
+        }
+        memcpy(dst, p, (size_t)len);
+        *out_len = (uint32_t)len;
+    }
+    *consumed = *hdr + (uint32_t)len;
+    return 0;
+}
+
 /* ---- batch drivers (same array contract as include/hhuff.h) ---------------------------------- */
 
 #define ORC_CODEC_DECODE orc_decode_huffman
 #define ORC_CODEC_ENCODE orc_encode_huffman
 #define ORC_CODEC_FLATTEN orc_flatten_string
+#define ORC_CODEC_LITERAL orc_decode_literal
 #define ORC_BATCH_PREFIX orc
 #include "batch_driver.h"

@@ -9,6 +9,14 @@
 #define ORC_INT_INCOMPLETE (-255) /* H2O_HTTP2_ERROR_INCOMPLETE, include/h2o/http2_common.h:57 */
 #define ORC_INT_COMPRESSION (-9) /* H2O_HTTP2_ERROR_COMPRESSION, include/h2o/http2_common.h:49 */
 #define ORC_FAIL_LEN 0xFFFFFFFFu
+#define ORC_MAX_STR ((1u << 29) - 1) /* per-string limit of the HIP path (include/hhuff.h) */
+/* string-literal verdicts (include/hhuff.h HHUFF_LIT_*) */
+#define ORC_LIT_INCOMPLETE 1
+#define ORC_LIT_BAD_INT 2
+#define ORC_LIT_TRUNCATED 3
+#define ORC_LIT_HUFFMAN 4
+#define ORC_LIT_UPPERCASE 5
+#define ORC_LIT_TOO_LONG 6
 #define ORC_STATUS_FAIL 0x80u
 
 size_t orc_decode_huffman(char *dst, unsigned *soft_errors, const uint8_t *src, size_t len, int is_name);
@@ -26,3 +34,9 @@ int orc_encode_batch(const uint8_t *in, const uint32_t *in_off, const uint32_t *
 int orc_flatten_batch(const uint8_t *in, const uint32_t *in_off, const uint32_t *in_len, uint32_t n,
                       const uint8_t *first_bytes, unsigned prefix_bits, const uint32_t *raw_bits, uint8_t *out,
                       const uint32_t *out_off, uint32_t *out_len, int nthreads);
+int orc_decode_literal(const uint8_t *lit, const uint8_t *end, unsigned prefix_bits, int is_name, int qpack,
+                       uint8_t *out, uint64_t lit_pos, uint32_t *hdr, uint32_t *consumed, uint32_t *out_len,
+                       unsigned *soft);
+int orc_literals_batch(const uint8_t *in, const uint32_t *lit_off, const uint32_t *lit_end, uint32_t n,
+                       unsigned prefix_bits, unsigned flags, const uint32_t *is_name_bits, uint8_t *out,
+                       uint32_t *out_len, uint32_t *pay_off, uint32_t *consumed, uint8_t *status, int nthreads);

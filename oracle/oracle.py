@@ -65,6 +65,10 @@ class _Codec:
             f = getattr(L, P + "_" + name)
             f.restype = ctypes.c_int
             f.argtypes = [_u8p, _u32p, _u32p, ctypes.c_uint32] + extra
+        f = getattr(L, P + "_literals_batch")
+        f.restype = ctypes.c_int
+        f.argtypes = [_u8p, _u32p, _u32p, ctypes.c_uint32, ctypes.c_uint, ctypes.c_uint, _u32p, _u8p, _u32p, _u32p,
+                      _u32p, _u8p, ctypes.c_int]
 
     # ---- per-string (h2o signatures) ----
     def decode(self, src: bytes, is_name: bool = False, soft_in: int = 0):
@@ -148,6 +152,24 @@ class _Codec:
             _ptr(raw_bits, _u32p), _ptr(out, _u8p), _ptr(out_off, _u32p), _ptr(out_len, _u32p), nthreads)
         assert rc == 0
         return out, out_len
+
+    def literals_batch(self, data, lit_off, lit_end, n, prefix_bits, qpack=False, is_name_bits=None, out_size=None,
+                       nthreads=1):
+        """string literals (decode_string / QPACK literal): -> out, out_len, pay_off, consumed, status"""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        if out_size is None:
+            out_size = (data.size * 8) // 5 + 16
+        out = np.zeros(max(1, out_size), np.uint8)
+        out_len = np.zeros(n, np.uint32)
+        pay_off = np.zeros(n, np.uint32)
+        consumed = np.zeros(n, np.uint32)
+        status = np.zeros(n, np.uint8)
+        rc = getattr(self.lib, self.prefix + "_literals_batch")(
+            _ptr(data, _u8p), _ptr(lit_off, _u32p), _ptr(lit_end, _u32p), n, prefix_bits, 1 if qpack else 0,
+            _ptr(is_name_bits, _u32p), _ptr(out, _u8p), _ptr(out_len, _u32p), _ptr(pay_off, _u32p),
+            _ptr(consumed, _u32p), _ptr(status, _u8p), nthreads)
+        assert rc == 0
+        return out, out_len, pay_off, consumed, status
 
 
 _oracle = None

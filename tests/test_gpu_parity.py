@@ -319,6 +319,59 @@ def test_pipelined_host_path(torch_cuda, pinned):
 
 
 # ------------------------------------------------------------------------------------------------
+# string literals in header blocks (HPACK decode_string, QPACK literal decode)
+# ------------------------------------------------------------------------------------------------
+def gpu_literals(torch, data, off, end, n, pb, qpack, names):
+    from h2o_amd import codec
+
+    o, ol, po, cons, st = codec.decode_literals(_dev(torch, data), _dev(torch, off), _dev(torch, end), n, pb, qpack=qpack,
+                                                is_name_bits=_dev(torch, names), in_size=int(np.asarray(data).size))
+    torch.cuda.synchronize()
+    return (_host(o, np.uint8), _host(ol, np.uint32)[:n], _host(po, np.uint32)[:n], _host(cons, np.uint32)[:n],
+            _host(st, np.uint8)[:n])
+
+
+def test_literals_golden(torch_cuda):
+    from test_oracle_golden import literal_cases, literal_concat
+
+    g = load_golden("literals")
+    for name, data, off, end, pb, qp, names, exp, n in literal_cases(g):
+        out, ol, po, cons, st = gpu_literals(torch_cuda, data, off, end, n, pb, qp, names)
+        np.testing.assert_array_equal(ol, exp["out_len"], err_msg=name)
+        np.testing.assert_array_equal(po, exp["pay_off"], err_msg=name)
+        np.testing.assert_array_equal(cons, exp["consumed"], err_msg=name)
+        np.testing.assert_array_equal(st, exp["status"], err_msg=name)
+        assert literal_concat(out, po, ol) == exp["out"].tobytes(), name
+
+
+def test_literals_random_blocks_vs_oracle(torch_cuda, oracle_codec):
+    """200K literals in synthetic header blocks: Huffman and raw, names and values, every alignment"""
+    rng = np.random.default_rng(29)
+    b = synth.make_batch("c2", n=200000, seed=31, adversarial_frac=0.03)
+    strings = synth.unpack(b["data"], b["off"])
+    names = rng.random(len(strings)) < 0.4
+    huff = rng.random(len(strings)) < 0.6
+    buf, offs = bytearray(), []
+    for s, h in zip(strings, huff):
+        payload = oracle_codec.encode(s) if h else None
+        if payload is None:
+            payload, h = s, False
+        offs.append(len(buf))
+        buf += oracle_codec.encode_int(len(payload), 7, 0x80 if h else 0) + payload
+    data = np.frombuffer(bytes(buf), np.uint8)
+    off = np.asarray(offs, np.uint32)
+    end = np.full(len(offs), len(buf), np.uint32)
+    nb = synth.bits_from_bools(names)
+    n = len(offs)
+    o = oracle_codec.literals_batch(data, off, end, n, 7, is_name_bits=nb, nthreads=8)
+    gdev = gpu_literals(torch_cuda, data, off, end, n, 7, False, nb)
+    for a, c in zip(gdev[1:], o[1:]):
+        np.testing.assert_array_equal(a, c)
+    from test_oracle_golden import literal_concat
+    assert literal_concat(gdev[0], gdev[2], gdev[1]) == literal_concat(o[0], o[2], o[1])
+
+
+# ------------------------------------------------------------------------------------------------
 # string-literal framing (HPACK h2o_hpack_encode_string, QPACK flatten_string)
 # ------------------------------------------------------------------------------------------------
 def gpu_flatten(torch, data, off, n, prefix_bits, in_len=None, first=None, raw_bits=None, out_off=None, out_size=None):

@@ -104,3 +104,40 @@ def test_oracle_matches_reference_directly():
                             is_name_bits=b["is_name_bits"])
         np.testing.assert_array_equal(d1[1], d2[1])
         np.testing.assert_array_equal(d1[2], d2[2])
+
+
+# ------------------------------------------------------------------------------------------------
+# string literals (decode_string / QPACK literal decode), tests/golden/literals.npz
+# ------------------------------------------------------------------------------------------------
+def literal_cases(g):
+    """(name, in, lit_off, lit_end, prefix_bits, qpack, names, expected dict) for every literal set"""
+    n = len(g["h_out_len"])
+    yield ("hpack", g["lit_in"], g["lit_off"], g["lit_end"], 7, False, g["lit_names"],
+           dict(out_len=g["h_out_len"], pay_off=g["h_pay_off"], consumed=g["h_consumed"], status=g["h_status"],
+                out=g["h_out"]), n)
+    for pb in (3, 5, 7):
+        k = "q%d_" % pb
+        yield ("qpack%d" % pb, g["q_in"], g[k + "off"], g[k + "end"], pb, True, g[k + "names"],
+               dict(out_len=g[k + "out_len"], pay_off=g[k + "pay_off"], consumed=g[k + "consumed"],
+                    status=g[k + "status"], out=g[k + "out"]), len(g[k + "off"]))
+
+
+def literal_concat(out, pay_off, out_len):
+    slots = (pay_off.astype(np.uint64) * 8) // 5
+    return b"".join(out[int(a):int(a) + int(L)].tobytes() for a, L in zip(slots, out_len) if L != 0xFFFFFFFF)
+
+
+def test_oracle_literals_match_golden(oracle_codec):
+    g = load_golden("literals")
+    assert int(g["n_corpus"][0]) > 40000  # every literal of the fuzz corpus's HPACK blocks
+    for name, data, off, end, pb, qp, names, exp, n in literal_cases(g):
+        out, ol, po, cons, st = oracle_codec.literals_batch(data, off, end, n, pb, qpack=qp, is_name_bits=names,
+                                                            nthreads=4)
+        np.testing.assert_array_equal(ol, exp["out_len"], err_msg=name)
+        np.testing.assert_array_equal(po, exp["pay_off"], err_msg=name)
+        np.testing.assert_array_equal(cons, exp["consumed"], err_msg=name)
+        np.testing.assert_array_equal(st, exp["status"], err_msg=name)
+        assert literal_concat(out, po, ol) == exp["out"].tobytes(), name
+    # every verdict the API defines is exercised by the fixture
+    codes = set(((g["h_status"][g["h_status"] >= 0x80] >> 2) & 7).tolist())
+    assert {1, 2, 3, 4, 5} <= codes

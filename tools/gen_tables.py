@@ -336,6 +336,14 @@ def oracle_header(lens, codes, fsm):
     out.append(fmt_array(lens, 32, "{}"))
     out.append("};")
     out.append("")
+    out.append("/* raw-literal validity: h2o_hpack_validate_header_name / _value tables (hpack.c:171-180, 200-209) */")
+    out.append("static const uint8_t orc_name_valid[256] = {")
+    out.append(fmt_array([1 if c in NAME_VALID else 0 for c in range(256)], 32, "{}"))
+    out.append("};")
+    out.append("static const uint8_t orc_value_valid[256] = {")
+    out.append(fmt_array([1 if c in VALUE_VALID else 0 for c in range(256)], 32, "{}"))
+    out.append("};")
+    out.append("")
     out.append("/* nibble FSM: [state][nibble] = next_state | flags << 8 | sym << 16 (hpack_huffman_table.h:89+) */")
     out.append("static const uint32_t orc_fsm[256][16] = {")
     for row in fsm:
