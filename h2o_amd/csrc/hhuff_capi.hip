@@ -144,8 +144,8 @@ HHUFF_API int hhuff_decode_literals(const uint8_t* in, uint64_t in_size, const u
     if (prefix_bits < 1 || prefix_bits > 7) return arg_fail("prefix_bits must be in 1..7");
     if (n == 0) return HHUFF_OK;
     hipStream_t s = (hipStream_t)stream;
-    void* ws = nullptr;  // Huffman payload lengths, stream-ordered scratch
-    HIP_TRY(hipMallocAsync(&ws, (size_t)n * 4, s), "hipMallocAsync");
+    void* ws = nullptr;  // Huffman payload lengths + per-literal verdict bytes, stream-ordered scratch
+    HIP_TRY(hipMallocAsync(&ws, (size_t)n * 5, s), "hipMallocAsync");
     hipError_t e = hhuff::launch_literals(in, in_size, lit_off, lit_end, n, prefix_bits, flags, is_name_bits, out, out_len,
                                           pay_off, consumed, status, (uint32_t*)ws, s);
     hipError_t f = hipFreeAsync(ws, s);

@@ -1174,6 +1174,7 @@ struct LitArgs {
     uint32_t* consumed;
     uint8_t* status;
     uint32_t* huff_len;  // workspace: Huffman payload length (0 for raw literals and errors)
+    uint8_t* code;       // workspace: verdict | H flag << 3 | soft bits << 4
 };
 
 enum : uint32_t { kLitIncomplete = 1, kLitBadInt = 2, kLitTruncated = 3, kLitHuffman = 4, kLitUpper = 5, kLitTooLong = 6 };
@@ -1219,17 +1220,6 @@ __device__ __forceinline__ uint32_t lit_header(const LitArgs& A, uint32_t i, boo
     return 0;
 }
 
-__global__ void literal_parse_kernel(LitArgs A) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n; i += (uint64_t)gridDim.x * blockDim.x) {
-        bool huff;
-        uint32_t hdr, len;
-        const uint32_t v = lit_header(A, (uint32_t)i, huff, hdr, len);
-        A.pay_off[i] = A.lit_off[i] + hdr;
-        A.huff_len[i] = (v == 0 && huff) ? len : 0u;
-        A.consumed[i] = v == 0 ? hdr + len : 0u;
-    }
-}
-
 __device__ __forceinline__ bool pseudo_token(const uint8_t* s, uint32_t len) {  // lib/common/token_table.h
     const char* tok[6] = {":authority", ":method", ":path", ":protocol", ":scheme", ":status"};
     const uint32_t tl[6] = {10, 7, 5, 9, 7, 7};
@@ -1242,57 +1232,80 @@ __device__ __forceinline__ bool pseudo_token(const uint8_t* s, uint32_t len) {  
     return false;
 }
 
-__global__ void literal_fix_kernel(LitArgs A) {
+// Pass 1: headers; raw payloads are validated and copied here (they skip the Huffman kernel, which
+// sees length 0 for them).  code[i] = verdict | H flag << 3 | soft bits << 4 for the fix-up.
+__global__ void literal_parse_kernel(LitArgs A) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n; i += (uint64_t)gridDim.x * blockDim.x) {
         bool huff;
         uint32_t hdr, len;
-        const uint32_t v = lit_header(A, (uint32_t)i, huff, hdr, len);
-        if (v) {
-            A.out_len[i] = kFailLen;
-            A.status[i] = (uint8_t)(kStatusFail | (v << 2));
-            continue;
-        }
-        if (huff) {  // the Huffman kernel already wrote out_len / status
-            if (A.status[i] & kStatusFail) {
-                A.status[i] = (uint8_t)(kStatusFail | (kLitHuffman << 2));
-                A.consumed[i] = 0;
-            }
-            continue;
-        }
-        const bool is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) != 0 : false;
-        const uint8_t* src = A.in + A.lit_off[i] + hdr;
-        uint8_t* dst = A.out + ((uint64_t)(A.lit_off[i] + hdr) * 8u) / 5u;
+        uint32_t v = lit_header(A, (uint32_t)i, huff, hdr, len);
         uint32_t soft = 0;
-        bool upper = false;
-        if (is_name) {
-            const bool skip = (A.flags & 1u) ? pseudo_token(src, len) : (len != 0 && src[0] == ':');
-            if (!skip) {
-                if (len == 0) soft = 0x1;
-                for (uint32_t j = 0; j < len && !upper; ++j) {
-                    const uint32_t c = src[j];
-                    if ((g_name_invalid[c >> 5] >> (c & 31)) & 1u) {
-                        if (c - 'A' < 26u) upper = true;
-                        else soft = 0x1;
-                    }
+        if (v == 0 && !huff) {
+            const bool is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) != 0 : false;
+            const uint64_t s0 = (uint64_t)A.lit_off[i] + hdr;
+            const uint8_t* src = A.in + s0;
+            const bool skip = is_name && ((A.flags & 1u) ? pseudo_token(src, len) : (len != 0 && src[0] == ':'));
+            const uint32_t* inval = is_name ? g_name_invalid : g_value_invalid;
+            uint8_t* dst = A.out + (s0 * 8u) / 5u;
+            // 16-byte aligned loads, no early exit: the loads of a long raw literal stay in flight together
+            bool anybad = false, softbad = false, upper = false;
+            const uint64_t a0 = s0 & ~15ull, e0 = s0 + len;
+            for (uint64_t a = a0; a < e0; a += 16) {
+                uint4 w4;
+                if (a + 16 <= A.in_size) {
+                    w4 = *reinterpret_cast<const uint4*>(A.in + a);
+                } else {
+                    uint32_t w[4] = {0, 0, 0, 0};
+                    for (uint32_t k = 0; k < 16; ++k)
+                        if (a + k < A.in_size) w[k >> 2] |= (uint32_t)A.in[a + k] << (8 * (k & 3));
+                    w4 = make_uint4(w[0], w[1], w[2], w[3]);
+                }
+                const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+                for (uint32_t k = 0; k < 16; ++k) {
+                    const uint64_t pos = a + k;
+                    if (pos < s0 || pos >= e0) continue;
+                    const uint32_t c = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+                    const bool bad = ((inval[c >> 5] >> (c & 31)) & 1u) != 0;
+                    const bool up = bad && (c - 'A' < 26u);
+                    anybad |= bad;
+                    softbad |= bad && !up && !upper;  // names: only what precedes the first upper-case letter
+                    upper |= up;
+                    dst[pos - s0] = (uint8_t)c;
                 }
             }
-        } else {
-            bool bad = len != 0 && (src[0] == ' ' || src[0] == '\t' || src[len - 1] == ' ' || src[len - 1] == '\t');
-            for (uint32_t j = 0; j < len && !bad; ++j) {
-                const uint32_t c = src[j];
-                bad = ((g_value_invalid[c >> 5] >> (c & 31)) & 1u) != 0;
+            if (is_name) {
+                if (!skip) {  // h2o_hpack_validate_header_name: empty -> soft; upper case -> hard error
+                    soft = (len == 0 || softbad) ? 0x1 : 0u;
+                    if (upper) v = kLitUpper;
+                }
+            } else {  // h2o_hpack_validate_header_value, with the whitespace rule (hpack.c:110-115)
+                const bool ws = len != 0 && (src[0] == ' ' || src[0] == '\t' || src[len - 1] == ' ' || src[len - 1] == '\t');
+                soft = (anybad || ws) ? 0x2 : 0u;
             }
-            soft = bad ? 0x2 : 0u;
         }
-        if (upper) {
+        A.pay_off[i] = A.lit_off[i] + hdr;
+        A.huff_len[i] = (v == 0 && huff) ? len : 0u;
+        A.consumed[i] = v == 0 ? hdr + len : 0u;
+        A.code[i] = (uint8_t)(v | (huff ? 8u : 0u) | (soft << 4));
+    }
+}
+
+// Pass 3: fold the header / raw verdicts into out_len and status (the Huffman kernel ran in between).
+__global__ void literal_fix_kernel(LitArgs A) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t c = A.code[i];
+        const uint32_t v = c & 7u, soft = c >> 4;
+        if (v) {
             A.out_len[i] = kFailLen;
-            A.status[i] = (uint8_t)(soft | kStatusFail | (kLitUpper << 2));
+            A.status[i] = (uint8_t)(soft | kStatusFail | (v << 2));
+        } else if (!(c & 8u)) {
+            A.out_len[i] = A.consumed[i] - (A.pay_off[i] - A.lit_off[i]);
+            A.status[i] = (uint8_t)soft;
+        } else if (A.status[i] & kStatusFail) {  // h2o_hpack_decode_huffman returned SIZE_MAX
+            A.status[i] = (uint8_t)(kStatusFail | (kLitHuffman << 2));
             A.consumed[i] = 0;
-            continue;
         }
-        for (uint32_t j = 0; j < len; ++j) dst[j] = src[j];
-        A.out_len[i] = len;
-        A.status[i] = (uint8_t)soft;
     }
 }
 
@@ -1486,7 +1499,7 @@ hipError_t launch_literals(const uint8_t* in, uint64_t in_size, const uint32_t* 
                            hipStream_t stream) {
     if (n == 0) return hipSuccess;
     LitArgs A{in, in_size, lit_off, lit_end, n, prefix_bits, flags, is_name_bits, out, out_len, pay_off, consumed, status,
-              huff_len};
+              huff_len, reinterpret_cast<uint8_t*>(huff_len + n)};
     const uint32_t blocks = min((n + 255u) / 256u, 4096u);
     hipLaunchKernelGGL(literal_parse_kernel, dim3(blocks), dim3(256), 0, stream, A);
     hipError_t e = hipGetLastError();

@@ -121,7 +121,7 @@ int hhuff_encode_batch_host(const uint8_t *in, uint64_t in_size, const uint32_t 
  *      (out sized floor(8 in_size / 5) + 16); out_len[i] (HHUFF_FAIL_LEN on failure); consumed[i] =
  *      header + payload bytes, how far the walker's cursor advances (0 on failure); status[i] = soft
  *      bits (0x1 name, 0x2 value) | on failure HHUFF_STATUS_FAIL | verdict << 2 (HHUFF_LIT_*).
- *      Device arrays, asynchronous on `stream`; uses stream-ordered scratch (4 n bytes). */
+ *      Device arrays, asynchronous on `stream`; uses stream-ordered scratch (5 n bytes). */
 #define HHUFF_LIT_QPACK 1u
 #define HHUFF_LIT_INCOMPLETE 1 /* no byte, or the length integer runs past lit_end (H2O_HTTP2_ERROR_INCOMPLETE) */
 #define HHUFF_LIT_BAD_INT 2    /* length integer overflow (H2O_HTTP2_ERROR_COMPRESSION from decode_int) */

@@ -385,6 +385,7 @@ def literals_set(seed=13):
         (True, _lit(0, 7, False, b"Content-Type")), (True, _lit(0, 7, False, b"x y")), (True, _lit(0, 7, False, b"")),
         (True, _lit(0, 7, False, b":authority")), (True, _lit(0, 7, False, b":custom")),
         (True, _lit(0, 7, False, b"a B")), (True, _lit(0, 7, False, b"ab\x00c")), (True, _lit(0, 7, False, b"ok-name")),
+        (True, _lit(0, 7, False, b"A b")), (True, _lit(0, 7, False, b"a\x01B c")), (True, _lit(0, 7, False, b"Zz")),
         (False, _lit(0, 7, False, b" lead")), (False, _lit(0, 7, False, b"trail\t")), (False, _lit(0, 7, False, b"")),
         (False, _lit(0, 7, False, b"\x01bad")), (False, _lit(0, 7, False, b"del\x7f")), (False, _lit(0, 7, False, b"fine")),
         (False, _lit(0, 7, False, bytes(range(0x80, 0x100)))),

@@ -3,6 +3,8 @@
   c2  1M strings mean 32 B, decode only
   c3  1M strings Zipf 8..512 B, encode + decode round trip, P / (t_enc + t_dec)
   c5  512K QPACK values mean 512 B (cookie/URI charset), encode only with flatten_string(prefix 7) framing
+  lit 16M c4 strings framed as HPACK literals (h2o_hpack_encode_string), then decoded as literals
+      (decode_string: header integer, Huffman or raw + validation); round trip checked on the device
 Prints one JSON line per config.  Device-resident, HIP-event timing on the launch stream."""
 import json
 import os
@@ -44,14 +46,60 @@ def packed_huffman(torch, codec, b):
     return huff, h_off.to(torch.int32), int(idx.numel()), H, int(lens[idx].sum().item())
 
 
+def literals_line(torch, codec, synth):
+    b = synth.make_batch_torch("c4", seed=9)
+    n, P = b["n"], int(b["total"])
+    off32 = b["off"].to(torch.int32)
+    f_out = torch.empty(P + 11 * n + 16, dtype=torch.uint8, device="cuda")
+    f_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    codec.flatten_batch(b["data"], off32, n, 7, out=f_out, out_len=f_len, in_size=P)  # h2o_hpack_encode_string
+    # pack the literals back to back, as they sit in header blocks
+    fl = f_len.to(torch.int64)
+    dense_off = torch.zeros(n + 1, dtype=torch.int64, device="cuda")
+    dense_off[1:] = torch.cumsum(fl, 0)
+    W = int(dense_off[-1].item())
+    src = torch.repeat_interleave(b["off"][:-1] + 11 * torch.arange(n, device="cuda"), fl)
+    src = src + torch.arange(W, device="cuda") - torch.repeat_interleave(dense_off[:-1], fl)
+    wire = torch.empty(W + 16, dtype=torch.uint8, device="cuda")
+    wire[:W] = f_out[src]
+    f_out = wire
+    lit_off = dense_off[:-1].to(torch.int32)
+    lit_end = dense_off[1:].to(torch.int32)
+    names = b["is_name_bits"]
+    out = torch.empty((W * 8) // 5 + 16, dtype=torch.uint8, device="cuda")
+    res = {}
+
+    def run():
+        res["r"] = codec.decode_literals(f_out, lit_off, lit_end, n, 7, is_name_bits=names, out=out, in_size=W)
+
+    t = timed(torch, run)
+    o, ol, po, cons, st = res["r"]
+    ok = ol != -1
+    # round trip on the device: every successfully decoded literal reproduces its plain string
+    lens = (b["off"][1:] - b["off"][:-1])
+    slot = (po.to(torch.int64) * 8) // 5
+    seg = torch.repeat_interleave(torch.arange(n, device="cuda"), lens)
+    pos = torch.arange(P, device="cuda") - torch.repeat_interleave(b["off"][:-1], lens)
+    got = o[torch.repeat_interleave(slot, lens) + pos]
+    good_str = ok & (ol.to(torch.int64) == lens)
+    match = bool((got[good_str[seg]] == b["data"][good_str[seg]]).all())
+    return {"config": "lit", "literals": n, "plain_bytes": P, "wire_bytes": int(f_len.to(torch.int64).sum().item()),
+            "decode_literals_ms": round(t, 4), "decode_literals_gibps": round(P / GIB / (t * 1e-3), 2),
+            "ok_literals": int(ok.sum().item()), "round_trip_match": match,
+            "consumed_matches_wire": bool((cons[ok].to(torch.int64) == f_len[ok].to(torch.int64)).all())}
+
+
 def main():
     import torch
 
     from h2o_amd import codec, synth
 
     torch.cuda.set_device(0)
-    cfgs = sys.argv[1:] or ["c2", "c3", "c5"]
+    cfgs = sys.argv[1:] or ["c2", "c3", "c5", "lit"]
     for cfg in cfgs:
+        if cfg == "lit":
+            print(json.dumps(literals_line(torch, codec, synth)), flush=True)
+            continue
         b = synth.make_batch_torch(cfg, seed=7)
         n, P = b["n"], int(b["total"])
         off32 = b["off"].to(torch.int32)
@@ -73,6 +121,8 @@ def main():
                                                                 status=e_st, in_size=P))
                 line.update(encode_ms=round(t_enc, 4), encode_gibps=round(P / GIB / (t_enc * 1e-3), 2),
                             round_trip_gibps=round(P / GIB / ((t_enc + t_dec) * 1e-3), 2))
+        elif cfg == "lit":
+            pass
         else:
             f_out = torch.empty(P + 11 * n + 16, dtype=torch.uint8, device="cuda")
             f_len = torch.empty(n, dtype=torch.int32, device="cuda")
