@@ -311,11 +311,17 @@ __device__ __forceinline__ DecResult decode_staged_lane_i(const uint32_t* stage,
 // pushing c positive.  x2 = stage[q+2] is fetched one step ahead, so only the LUT read is on the
 // step's dependency chain.  Two steps per vote.
 // ---------------------------------------------------------------------------------------------------
+#ifndef HHUFF_DEC_B16  // A/B knob: one 2-byte output store per decode step instead of two byte stores.
+#define HHUFF_DEC_B16 0  // Off: correct, but odd-address ds_write_b16 is slow on gfx950 (c4 decode 1.01 -> 1.48 ms)
+#endif
 typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(size_t)(const lds_u8*)p; }
 __device__ __forceinline__ void lds_st8(uint32_t addr, uint32_t v) { *(lds_u8*)(size_t)addr = (uint8_t)v; }
+// 2-byte store at any byte address (gfx950 LDS honours unaligned ds_write_b16: tools/probe/lds_unaligned.hip)
+__device__ __forceinline__ void lds_st16(uint32_t addr, uint32_t v) { *(lds_u16*)(size_t)addr = (uint16_t)v; }
 __device__ __forceinline__ uint32_t sel_bits(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 
 __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage, uint32_t start, uint32_t len,
@@ -330,7 +336,8 @@ __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage
     const uint32_t o0 = lds_addr(obuf) + op0, trash = lds_addr(obuf) + trash_off;
     uint32_t o = o0, acc1 = 0, acc2 = 0, accl = 0, fail = 0;
     int32_t prog = 0;
-    auto step = [&]() {
+    uint32_t first = 0;  // first decoded byte, kept in a register (HHUFF_DEC_B16 fix-up below)
+    auto step = [&](bool cap) {
         const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
         const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
         const int32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
@@ -338,8 +345,16 @@ __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage
         const uint32_t m1 = (uint32_t)((s1 & ~(int32_t)e) >> 31);         // first code fits, not LONG
         const uint32_t m2 = (uint32_t)((s2 & (int32_t)(e << 1)) >> 31);  // HAS2 and both fit
         int32_t cons = (int32_t)sel_bits(m2, (uint32_t)L12, m1 & (uint32_t)L1);
+#if HHUFF_DEC_B16
+        // both symbol bytes in one store; with one symbol taken the second byte is garbage one past it,
+        // overwritten by the next step -- or, at the string's end, possibly on the next string's first
+        // byte, which every lane restores from `first` after the loop
+        lds_st16(sel_bits(m1, o, trash), e);
+#else
         lds_st8(sel_bits(m1, o - m2, trash), e >> 8);  // second symbol, or onto the first one's byte
         lds_st8(sel_bits(m1, o, trash), e);
+#endif
+        if (cap) first = m1 ? (e & 0xFFu) : first;
         o = o - m1 - m2;
         acc1 |= e & m1;
         acc2 |= e & m2;
@@ -356,6 +371,7 @@ __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage
                 const uint32_t okm = fits & ~eos;
                 fail |= fits & eos & 1u;  // EOS inside the string (hpack.c:88-89)
                 lds_st8(sel_bits(okm, o, trash), le);
+                if (cap) first = okm ? (le & 0xFFu) : first;
                 o -= okm;
                 accl |= le & okm;
                 consl = okm & (uint32_t)L;
@@ -373,11 +389,15 @@ __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage
         x2 = st[q + 2];
         prog = cons;
     };
+    step(true);
     for (;;) {
-        step();
-        step();
+        step(false);
+        step(false);
         if (!__any(prog != 0)) break;
     }
+#if HHUFF_DEC_B16
+    lds_st8(o != o0 ? o0 : trash, first);  // every lane's garbage byte is down by now (lock step)
+#endif
     DecResult r;
     const uint32_t R = ~(uint32_t)c;  // string bits left (meaningless for parked lanes, which fail)
     const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
