@@ -544,6 +544,11 @@ __device__ __forceinline__ uint32_t encode_staged_lane(const uint32_t* stage, ui
 // Same contract as encode_staged_lane, with a wave-uniform trip count: `jmax` = the largest number of
 // input dwords over the wave's lanes, so the loop needs no vote; lanes that finished or failed run with
 // every byte masked out (their table entries are {0, 0}).  The first / last dword masks are precomputed.
+#ifndef HHUFF_ENC_PAIRS  // A/B knob: fused encode path for codes <= 16 bits as two 32-bit pairs (else <= 8 bits)
+#define HHUFF_ENC_PAIRS 1
+#endif
+constexpr uint32_t kFusedMaxBits = HHUFF_ENC_PAIRS ? 16u : 8u;
+
 // Encode the stage bytes [start, start + len) with the first code bit landing at bit `startbit` of the
 // LDS output stage (MSB-first dwords, OR-ed in, so neighbouring chunks may share a dword).  The trip
 // count jmax is wave-uniform (>= this lane's dword count).  `limit`: fail as soon as the code bits
@@ -573,10 +578,10 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint32_t* stage, uint32_t
         const uint2 e1 = enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)];
         const uint2 e2 = enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)];
         const uint2 e3 = enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)];
-        const bool lng = max(max(e0.y, e1.y), max(e2.y, e3.y)) > 8;
+        const bool lng = max(max(e0.y, e1.y), max(e2.y, e3.y)) > kFusedMaxBits;
         const uint32_t n = e0.y + e1.y + e2.y + e3.y;
         const bool over = tb + n >= limit;
-        if (__any(lng && !over)) {  // a code longer than 8 bits: byte by byte (wave-uniform detour)
+        if (__any(lng && !over)) {  // a code too long for the fused path: byte by byte (wave-uniform detour)
             if (lng && !over) {
                 const uint2 ek[4] = {e0, e1, e2, e3};
 #pragma unroll
@@ -596,11 +601,29 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint32_t* stage, uint32_t
         fail = fail || over;
         live = live && !over;
         const bool put = live && !lng;
+#if HHUFF_ENC_PAIRS
+        // codes <= 16 bits: two 32-bit pairs, each inserted and (at most one word) emitted in turn
+        const uint32_t p01 = put ? (e0.x << e1.y | e1.x) : 0u, n01 = put ? e0.y + e1.y : 0u;
+        const uint32_t p23 = put ? (e2.x << e3.y | e3.x) : 0u, n23 = put ? e2.y + e3.y : 0u;
+        {
+            acc |= (uint64_t)p01 << ((64u - an - n01) & 63u);
+            an += n01;
+            const uint32_t e = an >= 32 ? 1u : 0u;
+            atomicOr(&obuf32[opw], e ? bswap32((uint32_t)(acc >> 32)) : 0u);
+            acc <<= 32u * e;
+            an -= 32u * e;
+            opw += e;
+        }
+        acc |= (uint64_t)p23 << ((64u - an - n23) & 63u);
+        an += n23;
+        tb += n01 + n23;
+#else
         const uint32_t c = put ? ((((e0.x << e1.y | e1.x) << e2.y | e2.x) << e3.y) | e3.x) : 0u;
         const uint32_t nn = put ? n : 0u;
         acc |= (uint64_t)c << ((64u - an - nn) & 63u);
         an += nn;
         tb += nn;
+#endif
         const uint32_t e = an >= 32 ? 1u : 0u;
         atomicOr(&obuf32[opw], e ? bswap32((uint32_t)(acc >> 32)) : 0u);
         acc <<= 32u * e;
