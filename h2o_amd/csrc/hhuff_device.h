@@ -311,6 +311,9 @@ __device__ __forceinline__ DecResult decode_staged_lane_i(const uint32_t* stage,
 // pushing c positive.  x2 = stage[q+2] is fetched one step ahead, so only the LUT read is on the
 // step's dependency chain.  Two steps per vote.
 // ---------------------------------------------------------------------------------------------------
+#ifndef HHUFF_DEC_X2  // A/B knob: two dependent LUT lookups per decode step (up to 4 symbols)
+#define HHUFF_DEC_X2 1
+#endif
 #ifndef HHUFF_DEC_B16  // A/B knob: one 2-byte output store per decode step instead of two byte stores.
 #define HHUFF_DEC_B16 0  // Off: correct, but odd-address ds_write_b16 is slow on gfx950 (c4 decode 1.01 -> 1.48 ms)
 #endif
@@ -358,6 +361,23 @@ __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage
         o = o - m1 - m2;
         acc1 |= e & m1;
         acc2 |= e & m2;
+#if HHUFF_DEC_X2
+        {  // second lookup on the same 32-bit window, after what the first one took (<= 13 bits): up to
+           // 4 symbols per step.  Nothing taken first -> same window, same entry, nothing taken again.
+            const uint32_t wb = w << cons;
+            const uint32_t eb = T.lut[wb >> (32 - HHUFF_LUT_BITS)];
+            const int32_t cb = c + cons;
+            const int32_t L1b = (eb >> 16) & 15u, L12b = (eb >> 20) & 15u;
+            const uint32_t m1b = (uint32_t)(((L1b + cb) & ~(int32_t)eb) >> 31);
+            const uint32_t m2b = (uint32_t)(((L12b + cb) & (int32_t)(eb << 1)) >> 31);
+            lds_st8(sel_bits(m1b, o - m2b, trash), eb >> 8);
+            lds_st8(sel_bits(m1b, o, trash), eb);
+            o = o - m1b - m2b;
+            acc1 |= eb & m1b;
+            acc2 |= eb & m2b;
+            cons += (int32_t)sel_bits(m2b, (uint32_t)L12b, m1b & (uint32_t)L1b);
+        }
+#endif
         const bool lact = (s1 & (int32_t)e) < 0;  // LONG entry and >= LUT_BITS + 1 bits left
         uint32_t consl = 0;
         if (__builtin_amdgcn_ballot_w64(lact) != 0) {  // wave-uniform: codes longer than the window, EOS
