@@ -294,20 +294,28 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, P_ok, tor
     np_ = __import__("numpy")
     res = {}
     for kind in ("pinned", "pageable"):
+        def hbuf(count, dt):
+            if kind == "pinned":
+                return torch.empty(count, dtype=dt).pin_memory().numpy()
+            return np_.empty(count, {torch.uint8: np_.uint8, torch.int32: np_.int32}[dt])
+
         if kind == "pinned":
             src_p, src_h = h_plain.numpy(), h_huff.numpy()
-            out_e = torch.empty(P + 16, dtype=torch.uint8).pin_memory().numpy()
-            out_d = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8).pin_memory().numpy()
         else:
             src_p, src_h = h_plain.numpy().copy(), h_huff.numpy().copy()
-            out_e, out_d = np_.empty(P + 16, np_.uint8), np_.empty(codec.decode_slot_size(H), np_.uint8)
+        out_e, out_d = hbuf(P + 16, torch.uint8), hbuf(codec.decode_slot_size(H), torch.uint8)
+        el, es = hbuf(n, torch.int32).view(np_.uint32), hbuf(n, torch.uint8)
+        dl, ds = hbuf(n_ok, torch.int32).view(np_.uint32), hbuf(n_ok, torch.uint8)
         off_np, hoff_np = h_off.numpy().view(np_.uint32), h_hoff.numpy().view(np_.uint32)
         names_np = h_names.numpy().view(np_.uint32)
+        if kind == "pageable":
+            off_np, hoff_np, names_np = off_np.copy(), hoff_np.copy(), names_np.copy()
         ts = []
         for _ in range(reps + 1):
             t0 = time.perf_counter()
-            codec.encode_batch_host_pipelined(src_p, off_np, n, out=out_e)
-            codec.decode_batch_host_pipelined(src_h, hoff_np, n_ok, is_name_bits=names_np, out=out_d)
+            codec.encode_batch_host_pipelined(src_p, off_np, n, out=out_e, out_len=el, status=es)
+            codec.decode_batch_host_pipelined(src_h, hoff_np, n_ok, is_name_bits=names_np, out=out_d, out_len=dl,
+                                              status=ds)
             ts.append(time.perf_counter() - t0)
         res[kind] = min(ts[1:])
     t = res["pinned"]

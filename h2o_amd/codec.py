@@ -244,26 +244,27 @@ def encode_batch_host(data, in_off, n, in_len=None, out_off=None, out_size=None,
     return out, out_len[:n], status[:n]
 
 
-def decode_batch_host_pipelined(data, in_off, n, is_name_bits=None, out=None, chunk_bytes=0, device=0):
-    """Pipelined host decode (contiguous layout).  `out` may be a caller buffer (e.g. pinned memory)."""
+def decode_batch_host_pipelined(data, in_off, n, is_name_bits=None, out=None, chunk_bytes=0, device=0, out_len=None,
+                                status=None):
+    """Pipelined host decode (contiguous layout).  Caller buffers may be pinned memory (DMA'd in place)."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     if out is None:
         out = np.zeros(decode_slot_size(data.size), np.uint8)
-    out_len = np.zeros(max(1, n), np.uint32)
-    status = np.zeros(max(1, n), np.uint8)
+    out_len = np.zeros(max(1, n), np.uint32) if out_len is None else out_len
+    status = np.zeros(max(1, n), np.uint8) if status is None else status
     _check(lib().hhuff_decode_batch_host_pipelined(_hp(data), data.size, _hp(in_off), n, _hp(is_name_bits), _hp(out),
                                                    out.size, _hp(out_len), _hp(status), device, chunk_bytes),
            "hhuff_decode_batch_host_pipelined")
     return out, out_len[:n], status[:n]
 
 
-def encode_batch_host_pipelined(data, in_off, n, out=None, chunk_bytes=0, device=0):
+def encode_batch_host_pipelined(data, in_off, n, out=None, chunk_bytes=0, device=0, out_len=None, status=None):
     """Pipelined host encode (contiguous layout, output slot = in_off)."""
     data = np.ascontiguousarray(data, dtype=np.uint8)
     if out is None:
         out = np.zeros(data.size + 16, np.uint8)
-    out_len = np.zeros(max(1, n), np.uint32)
-    status = np.zeros(max(1, n), np.uint8)
+    out_len = np.zeros(max(1, n), np.uint32) if out_len is None else out_len
+    status = np.zeros(max(1, n), np.uint8) if status is None else status
     _check(lib().hhuff_encode_batch_host_pipelined(_hp(data), data.size, _hp(in_off), n, _hp(out), out.size,
                                                    _hp(out_len), _hp(status), device, chunk_bytes),
            "hhuff_encode_batch_host_pipelined")

@@ -394,6 +394,8 @@ int pipelined(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* 
     rc = P.bind(c.dev);
     if (rc) return rc;
     const bool pin_in = is_pinned(in), pin_out = is_pinned(out);
+    const bool pin_meta = is_pinned(in_off) && is_pinned(out_len) && (!status || is_pinned(status)) &&
+                          (!is_name_bits || is_pinned(is_name_bits));  // offsets/lengths DMA'd in place
     auto slot_of = [&](uint64_t pos) { return decode ? (pos * 8) / 5 : pos; };  // implicit output slot
     // chunk boundaries: multiples of 32 strings, about chunk_bytes of input each
     std::vector<uint64_t> cut{0};
@@ -409,8 +411,10 @@ int pipelined(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* 
         if (!x.busy) return HHUFF_OK;
         HIP_TRY(hipStreamSynchronize(x.s), "sync");
         if (!pin_out && x.out_n) par_copy(out + x.out_lo, x.h + x.h_out, x.out_n);
-        memcpy(out_len + x.i0, x.h + x.h_len, x.m * 4);
-        if (status) memcpy(status + x.i0, x.h + x.h_st, x.m);
+        if (!pin_meta) {
+            par_copy(out_len + x.i0, x.h + x.h_len, x.m * 4);
+            if (status) par_copy(status + x.i0, x.h + x.h_st, x.m);
+        }
         x.busy = false;
         return HHUFF_OK;
     };
@@ -439,10 +443,17 @@ int pipelined(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* 
             par_copy(x.h + o_in, in + base, nbytes);
             HIP_TRY(hipMemcpyAsync(x.d + o_in, x.h + o_in, nbytes, hipMemcpyHostToDevice, x.s), "H2D in");
         }
-        memcpy(x.h + o_off, in_off + i0, (m + 1) * 4);
-        if (nw) memcpy(x.h + o_nm, is_name_bits + i0 / 32, nw * 4);
-        HIP_TRY(hipMemcpyAsync(x.d + o_off, x.h + o_off, (o_nm - o_off) + nw * 4, hipMemcpyHostToDevice, x.s),
-                "H2D offsets");
+        if (pin_meta) {
+            HIP_TRY(hipMemcpyAsync(x.d + o_off, in_off + i0, (m + 1) * 4, hipMemcpyHostToDevice, x.s), "H2D offsets");
+            if (nw)
+                HIP_TRY(hipMemcpyAsync(x.d + o_nm, is_name_bits + i0 / 32, nw * 4, hipMemcpyHostToDevice, x.s),
+                        "H2D names");
+        } else {
+            par_copy(x.h + o_off, in_off + i0, (m + 1) * 4);
+            if (nw) memcpy(x.h + o_nm, is_name_bits + i0 / 32, nw * 4);
+            HIP_TRY(hipMemcpyAsync(x.d + o_off, x.h + o_off, (o_nm - o_off) + nw * 4, hipMemcpyHostToDevice, x.s),
+                    "H2D offsets");
+        }
         const uint8_t* d_in = x.d + o_in - base;  // absolute offsets address the chunk
         uint8_t* d_out = x.d + o_out - obase;
         const uint32_t* d_off = reinterpret_cast<const uint32_t*>(x.d + o_off);
@@ -467,7 +478,12 @@ int pipelined(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* 
             else
                 HIP_TRY(hipMemcpyAsync(x.h + o_out, d_out + olo, x.out_n, hipMemcpyDeviceToHost, x.s), "D2H out");
         }
-        HIP_TRY(hipMemcpyAsync(x.h + o_len, x.d + o_len, o_st + m - o_len, hipMemcpyDeviceToHost, x.s), "D2H len");
+        if (pin_meta) {
+            HIP_TRY(hipMemcpyAsync(out_len + i0, x.d + o_len, m * 4, hipMemcpyDeviceToHost, x.s), "D2H len");
+            if (status) HIP_TRY(hipMemcpyAsync(status + i0, x.d + o_st, m, hipMemcpyDeviceToHost, x.s), "D2H status");
+        } else {
+            HIP_TRY(hipMemcpyAsync(x.h + o_len, x.d + o_len, o_st + m - o_len, hipMemcpyDeviceToHost, x.s), "D2H len");
+        }
         x.busy = true;
     }
     for (auto& x : P.slot) {
