@@ -311,6 +311,9 @@ __device__ __forceinline__ DecResult decode_staged_lane_i(const uint32_t* stage,
 // pushing c positive.  x2 = stage[q+2] is fetched one step ahead, so only the LUT read is on the
 // step's dependency chain.  Two steps per vote.
 // ---------------------------------------------------------------------------------------------------
+#ifndef HHUFF_DEC_LONG2  // A/B knob: look for long codes every other decode step only
+#define HHUFF_DEC_LONG2 1
+#endif
 #ifndef HHUFF_DEC_X2  // A/B knob: two dependent LUT lookups per decode step (up to 4 symbols)
 #define HHUFF_DEC_X2 1
 #endif
@@ -340,7 +343,7 @@ __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage
     uint32_t o = o0, acc1 = 0, acc2 = 0, accl = 0, fail = 0;
     int32_t prog = 0;
     uint32_t first = 0;  // first decoded byte, kept in a register (HHUFF_DEC_B16 fix-up below)
-    auto step = [&](bool cap) {
+    auto step = [&](bool cap, bool longchk) {
         const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
         const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
         const int32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
@@ -380,7 +383,9 @@ __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage
 #endif
         const bool lact = (s1 & (int32_t)e) < 0;  // LONG entry and >= LUT_BITS + 1 bits left
         uint32_t consl = 0;
-        if (__builtin_amdgcn_ballot_w64(lact) != 0) {  // wave-uniform: codes longer than the window, EOS
+        // wave-uniform detour for codes longer than the window and EOS; with HHUFF_DEC_LONG2 only every
+        // other step looks (a lane parked on a long code for one step retries it on the next)
+        if ((!HHUFF_DEC_LONG2 || longchk) && __builtin_amdgcn_ballot_w64(lact) != 0) {
             if (lact) {
                 const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
                 const uint32_t ki = T.kinfo[k];
@@ -409,10 +414,10 @@ __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage
         x2 = st[q + 2];
         prog = cons;
     };
-    step(true);
+    step(true, true);
     for (;;) {
-        step(false);
-        step(false);
+        step(false, false);
+        step(false, true);
         if (!__any(prog != 0)) break;
     }
 #if HHUFF_DEC_B16
