@@ -356,7 +356,7 @@ __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage
         // overwritten by the next step -- or, at the string's end, possibly on the next string's first
         // byte, which every lane restores from `first` after the loop
         lds_st16(sel_bits(m1, o, trash), e);
-#else
+#elif !defined(HHUFF_ABL_V5_NOWRITE)  // ablation: drop the output stores (wrong output, timing only)
         lds_st8(sel_bits(m1, o - m2, trash), e >> 8);  // second symbol, or onto the first one's byte
         lds_st8(sel_bits(m1, o, trash), e);
 #endif
@@ -373,8 +373,10 @@ __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage
             const int32_t L1b = (eb >> 16) & 15u, L12b = (eb >> 20) & 15u;
             const uint32_t m1b = (uint32_t)(((L1b + cb) & ~(int32_t)eb) >> 31);
             const uint32_t m2b = (uint32_t)(((L12b + cb) & (int32_t)(eb << 1)) >> 31);
+#ifndef HHUFF_ABL_V5_NOWRITE
             lds_st8(sel_bits(m1b, o - m2b, trash), eb >> 8);
             lds_st8(sel_bits(m1b, o, trash), eb);
+#endif
             o = o - m1b - m2b;
             acc1 |= eb & m1b;
             acc2 |= eb & m2b;
@@ -429,6 +431,293 @@ __device__ __forceinline__ DecResult decode_staged_lane_v5(const uint32_t* stage
     r.ok = active && !fail && R <= 7 && (w | (0xFFFFFFFFu >> (R & 31u))) == 0xFFFFFFFFu;
     r.len = o - o0;
     r.flags = ((acc1 >> 24) | (acc2 >> 26) | (accl >> 14)) & 3u;
+    r.status = 0;
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Staged decode, v6 step: v5's window, LUT and take-masks, but the decoded bytes collect in a register
+// accumulator (lo:hi, `pend` bytes pending, pend <= 3 between steps) and leave as ONE ds_or_b32 per step
+// into the zeroed output stage at dword granularity, instead of four predicated ds_write_b8 (two per
+// lookup).  The accumulator starts `op0 & 3` bytes into its dword, so a lane only ever ORs non-zero
+// bits into its own bytes [op0, op0 + count): neighbouring slots that share a dword do not interfere.
+// LDS instructions per step: 2 LUT reads + 1 stage read + 1 OR (v5: 2 + 1 + 4 byte stores).
+// The caller zeroes the stage bytes the lanes may touch before the call.
+// ---------------------------------------------------------------------------------------------------
+#ifndef HHUFF_DEC_ACC  // A/B knob: 1 = v6 register-accumulated output, 0 = v5 byte stores
+#define HHUFF_DEC_ACC 0
+#endif
+typedef __attribute__((address_space(3))) uint32_t lds_u32w;
+
+__device__ __forceinline__ void lds_or32(uint32_t addr, uint32_t v) {
+    __hip_atomic_fetch_or((lds_u32w*)(size_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+struct OutAcc {  // pending output bytes, first byte in bits 0..7 of lo
+    uint32_t lo, hi, pend, addr;
+    // insert n <= 4 bytes (b, first byte in bits 0..7, bits above 8n zero), then emit one dword if >= 4 pend
+    __device__ __forceinline__ void put(uint32_t b, uint32_t n) {
+        const uint64_t v = (uint64_t)b << (8u * pend);  // pend <= 3
+        lo |= (uint32_t)v;
+        hi |= (uint32_t)(v >> 32);
+        pend += n;
+        const uint32_t em = 0u - (pend >> 2);  // pend >= 4 (pend <= 7)
+#ifndef HHUFF_ABL_V6_NOOR
+        lds_or32(addr, lo & em);
+#else
+        asm volatile("" ::"v"(lo & em), "v"(addr));
+#endif
+        lo = sel_bits(em, hi, lo);
+        hi &= ~em;
+        pend -= em & 4u;
+        addr += em & 4u;
+    }
+    __device__ __forceinline__ void flush() {
+        if (pend) lds_or32(addr, lo);
+    }
+};
+
+__device__ __forceinline__ DecResult decode_staged_lane_v6(const uint32_t* stage, uint32_t start, uint32_t len,
+                                                           bool active, uint8_t* obuf, uint32_t op0, const DecTables& T) {
+    const lds_u32* st = (const lds_u32*)stage;
+    int32_t pm = (int32_t)(8u * start) - 1;
+    const int32_t end = (int32_t)(8u * (start + len));
+    int32_t c = active ? pm - end : 0x40000000;
+    int32_t q = pm >> 5;
+    uint32_t x0 = st[q], x1 = st[q + 1], x2 = st[q + 2];
+    const uint32_t ob = lds_addr(obuf) + op0;
+    OutAcc acc{0u, 0u, ob & 3u, ob & ~3u};
+    uint32_t acc1 = 0, acc2 = 0, accl = 0, fail = 0, cnt = 0;
+    int32_t prog = 0;
+    auto step = [&](bool longchk) {
+        const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+        const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+        const int32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+        const int32_t s1 = L1 + c, s2 = L12 + c;
+        const uint32_t m1 = (uint32_t)((s1 & ~(int32_t)e) >> 31);         // first code fits, not LONG
+        const uint32_t m2 = (uint32_t)((s2 & (int32_t)(e << 1)) >> 31);  // HAS2 and both fit
+        int32_t cons = (int32_t)sel_bits(m2, (uint32_t)L12, m1 & (uint32_t)L1);
+        acc1 |= e & m1;
+        acc2 |= e & m2;
+        const uint32_t n1 = (m1 & 1u) + (m2 & 1u);
+        uint32_t bytes = e & ((m1 & 0xFFu) | (m2 & 0xFF00u));
+        uint32_t n = n1;
+#if HHUFF_DEC_X2
+        {  // second lookup on the same 32-bit window, after what the first one took (<= 13 bits)
+            const uint32_t wb = w << cons;
+            const uint32_t eb = T.lut[wb >> (32 - HHUFF_LUT_BITS)];
+            const int32_t cb = c + cons;
+            const int32_t L1b = (eb >> 16) & 15u, L12b = (eb >> 20) & 15u;
+            const uint32_t m1b = (uint32_t)(((L1b + cb) & ~(int32_t)eb) >> 31);
+            const uint32_t m2b = (uint32_t)(((L12b + cb) & (int32_t)(eb << 1)) >> 31);
+            acc1 |= eb & m1b;
+            acc2 |= eb & m2b;
+            bytes |= (eb & ((m1b & 0xFFu) | (m2b & 0xFF00u))) << (8u * n1);
+            n += (m1b & 1u) + (m2b & 1u);
+            cons += (int32_t)sel_bits(m2b, (uint32_t)L12b, m1b & (uint32_t)L1b);
+        }
+#endif
+        acc.put(bytes, n);
+        cnt += n;
+        const bool lact = (s1 & (int32_t)e) < 0;  // LONG entry and >= LUT_BITS + 1 bits left
+        uint32_t consl = 0;
+        if ((!HHUFF_DEC_LONG2 || longchk) && __builtin_amdgcn_ballot_w64(lact) != 0) {
+            if (lact) {
+                const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                const uint32_t ki = T.kinfo[k];
+                const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                const int32_t L = (le >> 9) & 31u;
+                const uint32_t fits = (uint32_t)((L + c) >> 31);
+                const uint32_t eos = (le & 0x1FFu) == kEos ? 0xFFFFFFFFu : 0u;
+                const uint32_t okm = fits & ~eos;
+                fail |= fits & eos & 1u;  // EOS inside the string (hpack.c:88-89)
+                acc.put(le & okm & 0xFFu, okm & 1u);
+                cnt += okm & 1u;
+                accl |= le & okm;
+                consl = okm & (uint32_t)L;
+                c = (int32_t)sel_bits(okm, (uint32_t)c, 0x40000000u);  // park: EOS, or a code that cannot fit
+            }
+        }
+        cons |= (int32_t)consl;  // LONG lanes took no window symbol, so cons was 0 there
+        c += cons;
+        pm += cons;
+        const int32_t qn = pm >> 5;
+        const bool adv = qn != q;
+        x0 = adv ? x1 : x0;
+        x1 = adv ? x2 : x1;
+        q = qn;
+        x2 = st[q + 2];
+        prog = cons;
+    };
+    step(true);
+    for (;;) {
+        step(false);
+        step(true);
+        if (!__any(prog != 0)) break;
+    }
+    acc.flush();
+    DecResult r;
+    const uint32_t R = ~(uint32_t)c;
+    const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+    r.ok = active && !fail && R <= 7 && (w | (0xFFFFFFFFu >> (R & 31u))) == 0xFFFFFFFFu;
+    r.len = cnt;
+    r.flags = ((acc1 >> 24) | (acc2 >> 26) | (accl >> 14)) & 3u;
+    r.status = 0;
+    return r;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Staged decode, v7: a BULK phase and a TAIL phase (same results as decode_core).
+// Bulk steps run only for lanes with >= 27 string bits left (pm < lim = end - 26; inactive and parked
+// lanes have lim = INT_MIN), so everything both lookups of a step hold lies inside the string: there are
+// no end-of-string take-masks, the entry says what to take -- [29:28] symbol count, L12 bits (none for
+// LONG) -- and flag bits of absent symbols are zero, so `accb |= e` collects them.  Lanes below lim are
+// switched off (exec mask) until the bulk loop drains; then v5's checked step finishes every lane
+// (<= 26 bits, at most ~3 steps).  Bulk VALU per step is about half of v5's.  Codes longer than the
+// window take the same wave-uniform detour (fit checked against `end`; EOS or a code that cannot fit
+// parks the lane, which then fails).
+// ---------------------------------------------------------------------------------------------------
+#ifndef HHUFF_DEC_BULK  // A/B knob: 1 = v7 bulk + tail decode, 0 = v5 / v6
+#define HHUFF_DEC_BULK 1
+#endif
+
+__device__ __forceinline__ DecResult decode_staged_lane_v7(const uint32_t* stage, uint32_t start, uint32_t len,
+                                                           bool active, uint8_t* obuf, uint32_t op0, uint32_t trash_off,
+                                                           const DecTables& T) {
+    const lds_u32* st = (const lds_u32*)stage;
+    int32_t pm = (int32_t)(8u * start) - 1;
+    const int32_t end = (int32_t)(8u * (start + len));
+    int32_t q = pm >> 5;
+    uint32_t x0 = st[q], x1 = st[q + 1], x2 = st[q + 2];
+    const uint32_t o0 = lds_addr(obuf) + op0, trash = lds_addr(obuf) + trash_off;  // trash: 4 lane-private bytes
+    uint32_t o = o0, accb = 0, acc1 = 0, acc2 = 0, accl = 0, fail = 0, parked = active ? 0u : 1u;
+    int32_t lim = active ? end - 26 : (int32_t)0x80000000;
+
+    // ---- bulk ----
+    auto advance = [&](int32_t cons) {
+        pm += cons;
+        const int32_t qn = pm >> 5;
+        const bool adv = qn != q;
+        x0 = adv ? x1 : x0;
+        x1 = adv ? x2 : x1;
+        q = qn;
+        x2 = st[q + 2];
+    };
+    auto bstep = [&](bool longchk) {
+        if (pm < lim) {
+            const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+            const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+            const uint32_t sl = (uint32_t)((int32_t)e >> 31);         // LONG: nothing taken from the window
+            const uint32_t h2 = (uint32_t)((int32_t)(e << 1) >> 31);  // HAS2
+            lds_st8(sel_bits(sl, trash, o), e);
+            lds_st8(sel_bits(h2, o, trash - 1u) + 1u, e >> 8);
+            o += (e >> 28) & 3u;
+            accb |= e;
+            uint32_t cons = ((e >> 20) & 15u) & ~sl;
+            {
+                const uint32_t wb = w << cons;
+                const uint32_t eb = T.lut[wb >> (32 - HHUFF_LUT_BITS)];
+                const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
+                const uint32_t h2b = (uint32_t)((int32_t)(eb << 1) >> 31);
+                lds_st8(sel_bits(slb, trash, o), eb);
+                lds_st8(sel_bits(h2b, o, trash - 1u) + 1u, eb >> 8);
+                o += (eb >> 28) & 3u;
+                accb |= eb;
+                cons += ((eb >> 20) & 15u) & ~slb;
+            }
+            if ((!HHUFF_DEC_LONG2 || longchk) && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
+                if (sl) {
+                    const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                    const uint32_t ki = T.kinfo[k];
+                    const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                    const int32_t L = (le >> 9) & 31u;
+                    const uint32_t fits = (uint32_t)((L + pm - end) >> 31);
+                    const uint32_t eos = (le & 0x1FFu) == kEos ? 0xFFFFFFFFu : 0u;
+                    const uint32_t okm = fits & ~eos;
+                    fail |= fits & eos & 1u;  // EOS inside the string (hpack.c:88-89)
+                    lds_st8(sel_bits(okm, o, trash), le);
+                    o -= okm;
+                    accl |= le & okm;
+                    cons = okm & (uint32_t)L;
+                    parked |= ~okm & 1u;
+                    lim = (int32_t)sel_bits(okm, (uint32_t)lim, 0x80000000u);
+                }
+            }
+            advance((int32_t)cons);
+        }
+    };
+    for (;;) {
+        bstep(false);
+        bstep(true);
+        if (!__any(pm < lim)) break;
+    }
+
+    // ---- tail: v5's checked step ----
+    int32_t c = parked ? 0x40000000 : pm - end;
+    int32_t prog = 0;
+    auto step = [&](bool longchk) {
+        const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+        const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+        const int32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+        const int32_t s1 = L1 + c, s2 = L12 + c;
+        const uint32_t m1 = (uint32_t)((s1 & ~(int32_t)e) >> 31);
+        const uint32_t m2 = (uint32_t)((s2 & (int32_t)(e << 1)) >> 31);
+        int32_t cons = (int32_t)sel_bits(m2, (uint32_t)L12, m1 & (uint32_t)L1);
+        lds_st8(sel_bits(m1, o - m2, trash), e >> 8);
+        lds_st8(sel_bits(m1, o, trash), e);
+        o = o - m1 - m2;
+        acc1 |= e & m1;
+        acc2 |= e & m2;
+        {
+            const uint32_t wb = w << cons;
+            const uint32_t eb = T.lut[wb >> (32 - HHUFF_LUT_BITS)];
+            const int32_t cb = c + cons;
+            const int32_t L1b = (eb >> 16) & 15u, L12b = (eb >> 20) & 15u;
+            const uint32_t m1b = (uint32_t)(((L1b + cb) & ~(int32_t)eb) >> 31);
+            const uint32_t m2b = (uint32_t)(((L12b + cb) & (int32_t)(eb << 1)) >> 31);
+            lds_st8(sel_bits(m1b, o - m2b, trash), eb >> 8);
+            lds_st8(sel_bits(m1b, o, trash), eb);
+            o = o - m1b - m2b;
+            acc1 |= eb & m1b;
+            acc2 |= eb & m2b;
+            cons += (int32_t)sel_bits(m2b, (uint32_t)L12b, m1b & (uint32_t)L1b);
+        }
+        const bool lact = (s1 & (int32_t)e) < 0;
+        uint32_t consl = 0;
+        if ((!HHUFF_DEC_LONG2 || longchk) && __builtin_amdgcn_ballot_w64(lact) != 0) {
+            if (lact) {
+                const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                const uint32_t ki = T.kinfo[k];
+                const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                const int32_t L = (le >> 9) & 31u;
+                const uint32_t fits = (uint32_t)((L + c) >> 31);
+                const uint32_t eos = (le & 0x1FFu) == kEos ? 0xFFFFFFFFu : 0u;
+                const uint32_t okm = fits & ~eos;
+                fail |= fits & eos & 1u;
+                lds_st8(sel_bits(okm, o, trash), le);
+                o -= okm;
+                accl |= le & okm;
+                consl = okm & (uint32_t)L;
+                c = (int32_t)sel_bits(okm, (uint32_t)c, 0x40000000u);
+            }
+        }
+        cons |= (int32_t)consl;
+        c += cons;
+        advance(cons);
+        prog = cons;
+    };
+    step(true);
+    for (;;) {  // the vote follows a long-code step: a lane with no progress there is finished
+        step(false);
+        step(true);
+        if (!__any(prog != 0)) break;
+    }
+    DecResult r;
+    const uint32_t R = ~(uint32_t)c;
+    const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+    r.ok = active && !fail && R <= 7 && (w | (0xFFFFFFFFu >> (R & 31u))) == 0xFFFFFFFFu;
+    r.len = o - o0;
+    r.flags = ((accb >> 24) | (accb >> 26) | (acc1 >> 24) | (acc2 >> 26) | (accl >> 14)) & 3u;
     r.status = 0;
     return r;
 }

@@ -335,6 +335,15 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
 #if HHUFF_DEC_I
             const DecResult r =
                 decode_staged_lane_i(stage, last, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
+#elif HHUFF_DEC_BULK
+            (void)last;
+            const DecResult r = decode_staged_lane_v7(stage, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
+#elif HHUFF_DEC_ACC
+            (void)last;
+            for (uint32_t k = (uint32_t)lane * 16u; k < cur.ospan + 4u; k += 64u * 16u)  // OR target: zeroed
+                *reinterpret_cast<uint4*>(obuf + k) = make_uint4(0u, 0u, 0u, 0u);
+            wave_lds_sync();
+            const DecResult r = decode_staged_lane_v6(stage, rel, t.len, act, obuf, cur.op0, T);
 #else
             (void)last;
             const DecResult r = decode_staged_lane_v5(stage, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);

@@ -51,8 +51,10 @@ def test_window_lut_matches_tree():
         syms = _tree_decode(format(w, "0%db" % G.LUT_BITS), root)
         if not syms:
             assert e >> 31 and (e >> 16) & 15 == G.LUT_BITS + 1 and (e >> 20) & 15 == G.LUT_BITS + 1
+            assert (e >> 28) & 3 == 0
             continue
         assert not e >> 31
+        assert (e >> 28) & 3 == min(len(syms), 2)
         s1, l1 = syms[0]
         assert e & 0xFF == s1 and (e >> 16) & 15 == l1
         assert (e >> 24) & 1 == (s1 not in G.NAME_VALID) and (e >> 25) & 1 == (s1 not in G.VALUE_VALID)
