@@ -592,6 +592,16 @@ __device__ __forceinline__ DecResult decode_staged_lane_v7(const uint32_t* stage
     const uint32_t o0 = lds_addr(obuf) + op0, trash = lds_addr(obuf) + trash_off;  // trash: 4 lane-private bytes
     uint32_t o = o0, accb = 0, acc1 = 0, acc2 = 0, accl = 0, fail = 0, parked = active ? 0u : 1u;
     int32_t lim = active ? end - 26 : (int32_t)0x80000000;
+#ifdef HHUFF_ABL_DEC_NOSTEP  // ablation: no decoding at all (wrong output, timing of the tile overhead)
+    {
+        DecResult r0;
+        r0.ok = active;
+        r0.len = len;
+        r0.flags = 0;
+        r0.status = 0;
+        if (__any(active)) return r0;
+    }
+#endif
 
     // ---- bulk ----
     auto advance = [&](int32_t cons) {
@@ -960,6 +970,125 @@ __device__ __forceinline__ uint32_t encode_staged_lane_u(const uint32_t* stage, 
     const uint32_t tb = encode_chunk(stage, last, start, len, active, obuf32, 8u * opb, enc, jmax,
                                      active ? 8 * len - 7 : 0xFFFFFFFFu, true);
     return tb == kFailLen ? kFailLen : (tb + 7) >> 3;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Encode v2: stateless bit placement + a bulk phase (same results as encode_core).
+// The output stage holds the code stream as MSB-first u32 words (bit 31 of word k = stream bit 32k), so
+// n <= 64 code bits land at absolute stage bit tb with at most three ds_or_b32 and no accumulator:
+// left-align them in 64 bits, shift right by tb % 32 for words k, k+1, and the bits shifted out go to
+// word k+2 (only when tb % 32 + n > 64).  OR is order-free, so there is no emit state to carry and no
+// per-step flush; the caller byte-swaps the stage's words once before copying out.
+// A lane's dwords split into a head (the first dword, when the string does not start on it), whole
+// dwords (bulk: no byte masks, one placement of all four codes when each is <= 16 bits), and a tail (the
+// last, partial dword).  Head and tail use the masked lookups (entries 256..511 are zero); bulk steps
+// run for lanes inside their whole-dword range with the others switched off (exec mask).
+// ---------------------------------------------------------------------------------------------------
+#ifndef HHUFF_ENC_V2  // A/B knob: 1 = encode v2 (stateless placement, bulk phase), 0 = encode_chunk
+#define HHUFF_ENC_V2 1
+#endif
+
+__device__ __forceinline__ void place_bits(uint32_t obase, uint32_t tb, uint64_t c, uint32_t n) {
+    const uint64_t t = c << ((64u - n) & 63u);  // left-aligned (n == 0 needs c == 0)
+    const uint32_t sh = tb & 31u;
+    const uint64_t u = t >> sh;
+    const uint32_t a = obase + ((tb >> 3) & ~3u);
+#ifdef HHUFF_ABL_ENC_NOOR  // ablation: no output (wrong output, timing only)
+    asm volatile("" ::"v"(a), "v"((uint32_t)(u >> 32)), "v"((uint32_t)u), "v"((uint32_t)t << (32u - sh)));
+#else
+    lds_or32(a, (uint32_t)(u >> 32));
+    lds_or32(a + 4u, (uint32_t)u);
+    if (sh + n > 64u) lds_or32(a + 8u, (uint32_t)t << (32u - sh));  // sh > 0 here
+#endif
+}
+
+struct EncV2 {
+    const uint2* enc;
+    uint32_t obase;  // LDS byte address of the MSB-first output stage
+    uint32_t tb;     // next stage bit
+    uint32_t tlim;   // stage bit at which the string fails (~0: no limit)
+    bool live, fail;
+    // four table entries of one input dword; `on`: this lane has these bytes
+    __device__ __forceinline__ void put4(uint2 e0, uint2 e1, uint2 e2, uint2 e3, bool on) {
+        const uint32_t n01 = e0.y + e1.y, n23 = e2.y + e3.y, n = n01 + n23;
+        const bool lng = max(max(e0.y, e1.y), max(e2.y, e3.y)) > 16u;
+        const bool over = on && live && tb + n >= tlim;
+        fail = fail || over;
+        live = live && !over;
+        const bool put = on && live;
+        if (__any(put && lng)) {  // a code longer than 16 bits: two placements of 64-bit pairs
+            if (put && lng) {
+                place_bits(obase, tb, (uint64_t)e0.x << e1.y | e1.x, n01);
+                place_bits(obase, tb + n01, (uint64_t)e2.x << e3.y | e3.x, n23);
+            }
+        }
+        const bool f = put && !lng;
+        const uint32_t p01 = e0.x << e1.y | e1.x, p23 = e2.x << e3.y | e3.x;
+        const uint64_t cc = f ? ((uint64_t)p01 << n23 | p23) : 0ull;
+        place_bits(obase, tb, cc, f ? n : 0u);
+        tb += put ? n : 0u;
+    }
+};
+
+// Encode stage bytes [start, start + len) to stage bit `startbit` of the MSB-first output stage at LDS
+// byte address `obase`.  `limit`, `pad`: as encode_chunk.  Returns the code bits or kFailLen.
+__device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
+                                                    bool active, uint32_t obase, uint32_t startbit,
+                                                    const uint2* __restrict__ enc, uint32_t limit, bool pad) {
+    const uint32_t end = start + len;
+    const uint32_t a0 = start & ~3u;
+    const uint32_t ndw = active ? (end - a0 + 3u) >> 2 : 0u;
+    const uint32_t jf = (start & 3u) ? 1u : 0u;            // whole dwords: [jf, jl)
+    const uint32_t jl = active ? (end - a0) >> 2 : 0u;
+    const uint32_t mfirst = 0xFFFFFFFFu << (8u * (start & 3u));
+    const uint32_t mlast = (uint32_t)(0xFFFFFFFFull >> ((32u - 8u * (end & 3u)) & 31u));
+    EncV2 E{enc, obase, startbit, limit == 0xFFFFFFFFu ? 0xFFFFFFFFu : startbit + limit, active, false};
+    auto masked = [&](uint32_t j, bool on) {  // one dword with byte masks (head / tail)
+        const uint32_t w = stage[min(a0 + 4u * j, last) >> 2];
+        uint32_t vm = j == 0 ? mfirst : 0xFFFFFFFFu;
+        vm &= (j + 1 == ndw) ? mlast : 0xFFFFFFFFu;
+        vm = on ? vm : 0u;
+        const uint32_t iw = ~vm & 0x01010101u;
+        E.put4(enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0400u)], enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)],
+               enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)], enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)], on);
+    };
+#ifdef HHUFF_ABL_ENC_NOSTEP  // ablation: no encoding at all (wrong output, timing of the tile overhead)
+    if (active) return len;
+#endif
+    masked(0, active && jf != 0);  // head
+    const uint32_t* sw = stage + (a0 >> 2);
+    const uint32_t jlast = (last >> 2) - (a0 >> 2);  // stage reads are clamped to the span
+    uint32_t wn = sw[min(jf, jlast)];                 // next whole dword, read one step ahead
+    for (uint32_t j = 0;; ++j) {                      // bulk
+        if (!__any(E.live && j < jl)) break;
+        if (E.live && j >= jf && j < jl) {
+            const uint32_t w = wn;
+            wn = sw[min(j + 1u, jlast)];
+#ifdef HHUFF_ABL_ENC_NOTAB  // ablation: table entries from registers (wrong output, timing only)
+            E.put4(make_uint2(w & 0x3Fu, 6u), make_uint2((w >> 8) & 0x1Fu, 5u), make_uint2((w >> 16) & 0x3Fu, 6u),
+                   make_uint2((w >> 24) & 0x7Fu, 7u), true);
+#else
+            E.put4(enc[w & 0xFFu], enc[(w >> 8) & 0xFFu], enc[(w >> 16) & 0xFFu], enc[w >> 24], true);
+#endif
+        }
+    }
+    masked(jl, active && (end & 3u) != 0 && jl >= jf);  // tail
+    if (E.fail || !active) return kFailLen;
+    const uint32_t tbits = E.tb - startbit;
+    if (pad) {  // fill the last byte with ones (EOS prefix, hpack.c:795-798)
+        const uint32_t p = (0u - tbits) & 7u;
+        place_bits(obase, E.tb, (1ull << p) - 1ull, p);
+    }
+    return tbits;
+}
+
+// Byte-swap the words of an MSB-first output stage [0, bytes) in place (one wave; bytes % 16 == 0).
+__device__ __forceinline__ void stage_bswap(uint32_t* obuf32, uint32_t bytes, int lane) {
+    for (uint32_t k = (uint32_t)lane * 16u; k < bytes; k += 64u * 16u) {
+        uint4 v = *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(obuf32) + k);
+        v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(obuf32) + k) = v;
+    }
 }
 
 // Code bits of the stage bytes [start, start + len) (pass 1 of the proportional-lane encode).

@@ -503,6 +503,12 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
             const uint32_t last = cur.span ? cur.span - 4u : 0u;
 #ifdef HHUFF_ENC_VOTE_LOOP
             const uint32_t r = encode_staged_lane(stage, last, rel, t.len, act, obuf32, cur.op0, s_enc);
+#elif HHUFF_ENC_V2
+            const uint32_t tb = encode_chunk_v2(stage, last, rel, t.len, act, lds_addr(obuf32), 8u * cur.op0, s_enc,
+                                                act ? 8 * t.len - 7 : 0xFFFFFFFFu, true);
+            const uint32_t r = tb == kFailLen ? kFailLen : (tb + 7) >> 3;
+            wave_lds_sync();
+            stage_bswap(obuf32, (cur.ospan + 15u) & ~15u, lane);
 #else
             const uint32_t jmax = wave_max_u32(act ? ((rel + t.len - (rel & ~3u) + 3u) >> 2) : 0u);
             const uint32_t r = encode_staged_lane_u(stage, last, rel, t.len, act, obuf32, cur.op0, s_enc, jmax);
