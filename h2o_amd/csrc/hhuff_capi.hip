@@ -528,6 +528,14 @@ HHUFF_API int hhuff_encode_batch_host(const uint8_t* in, uint64_t in_size, const
 // ---------------------------------------------------------------------------------------------------
 // (4) info
 // ---------------------------------------------------------------------------------------------------
+#ifdef HHUFF_PROFILE  // profile builds: per-phase cycle sums of the staged kernels (tools/ab.py prof)
+namespace hhuff {
+hipError_t read_prof(unsigned long long* out16, bool reset);
+}
+HHUFF_API int hhuff_debug_prof(unsigned long long* out16, int reset) {
+    return hhuff::read_prof(out16, reset != 0) == hipSuccess ? 0 : -1;
+}
+#endif
 HHUFF_API const char* hhuff_version(void) { return "hhuff 0.1.0 (gfx950)"; }
 HHUFF_API const char* hhuff_last_error_string(void) { return t_err; }
 HHUFF_API int hhuff_grid_size(int device, int which) {

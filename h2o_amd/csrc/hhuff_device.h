@@ -35,6 +35,37 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 __device__ __forceinline__ uint64_t dec_slot(uint32_t x) { return ((uint64_t)x * 8u) / 5u; }
 
 // ---------------------------------------------------------------------------------------------------
+// wave helpers
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+// exclusive prefix sum over the wave
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (lane >= o) x += y;
+    }
+    return x - v;
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+
+// ---------------------------------------------------------------------------------------------------
 // Byte sources.  word(a) returns the little-endian dword at 4-aligned position a.
 // ---------------------------------------------------------------------------------------------------
 struct LdsSource {  // a wave's staged input span; positions relative to the 16-aligned span start
@@ -1028,7 +1059,43 @@ struct EncV2 {
         place_bits(obase, tb, cc, f ? n : 0u);
         tb += put ? n : 0u;
     }
+    // Same with every per-lane predicate an all-ones / zero mask in a VGPR (no exec-mask juggling on
+    // the SALU): `onm` = this lane has these four bytes; `livem` mirrors `live`.
+    uint32_t livem, failm;
+    __device__ __forceinline__ void put4m(uint2 e0, uint2 e1, uint2 e2, uint2 e3, uint32_t onm) {
+        const uint32_t n01 = e0.y + e1.y, n23 = e2.y + e3.y, n = n01 + n23;
+        const uint32_t mx = max(max(e0.y, e1.y), max(e2.y, e3.y));
+        const uint32_t lngm = (uint32_t)((int32_t)(16u - mx) >> 31);                 // a code > 16 bits
+        const uint32_t overm = onm & livem & ~(uint32_t)((int32_t)(tb + n - tlim) >> 31);  // tb + n >= tlim
+        failm |= overm;
+        livem &= ~overm;
+        const uint32_t putm = onm & livem;
+        if (__builtin_amdgcn_ballot_w64((putm & lngm) != 0u) != 0) {
+            if (putm & lngm) {
+                place_bits(obase, tb, (uint64_t)e0.x << e1.y | e1.x, n01);
+                place_bits(obase, tb + n01, (uint64_t)e2.x << e3.y | e3.x, n23);
+            }
+        }
+        const uint32_t fm = putm & ~lngm;
+        const uint32_t p01 = e0.x << e1.y | e1.x, p23 = e2.x << e3.y | e3.x;
+        const uint64_t cc = ((uint64_t)p01 << n23 | p23) & ((uint64_t)fm << 32 | fm);
+        const uint32_t nf = n & fm;
+        const uint64_t t = cc << ((64u - nf) & 63u);
+        const uint32_t sh = tb & 31u;
+        const uint64_t u = t >> sh;
+        const uint32_t a = obase + ((tb >> 3) & ~3u);
+        lds_or32(a, (uint32_t)(u >> 32));
+        lds_or32(a + 4u, (uint32_t)u);
+        if (__builtin_amdgcn_ballot_w64(sh + nf > 64u) != 0) {
+            if (sh + nf > 64u) lds_or32(a + 8u, (uint32_t)t << (32u - sh));
+        }
+        tb += n & putm;
+    }
 };
+
+#ifndef HHUFF_ENC_PRED  // A/B knob: 1 = predicated bulk loop with a uniform trip count, 0 = exec-masked
+#define HHUFF_ENC_PRED 1
+#endif
 
 // Encode stage bytes [start, start + len) to stage bit `startbit` of the MSB-first output stage at LDS
 // byte address `obase`.  `limit`, `pad`: as encode_chunk.  Returns the code bits or kFailLen.
@@ -1042,7 +1109,9 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
     const uint32_t jl = active ? (end - a0) >> 2 : 0u;
     const uint32_t mfirst = 0xFFFFFFFFu << (8u * (start & 3u));
     const uint32_t mlast = (uint32_t)(0xFFFFFFFFull >> ((32u - 8u * (end & 3u)) & 31u));
-    EncV2 E{enc, obase, startbit, limit == 0xFFFFFFFFu ? 0xFFFFFFFFu : startbit + limit, active, false};
+    // tlim < 2^31 keeps tb + n - tlim a signed quantity (stage bits are < 2^20)
+    EncV2 E{enc, obase, startbit, limit >= 0x40000000u ? 0x7FFFFFFFu : startbit + limit, active, false,
+            active ? 0xFFFFFFFFu : 0u, 0u};
     auto masked = [&](uint32_t j, bool on) {  // one dword with byte masks (head / tail)
         const uint32_t w = stage[min(a0 + 4u * j, last) >> 2];
         uint32_t vm = j == 0 ? mfirst : 0xFFFFFFFFu;
@@ -1058,6 +1127,26 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
     masked(0, active && jf != 0);  // head
     const uint32_t* sw = stage + (a0 >> 2);
     const uint32_t jlast = (last >> 2) - (a0 >> 2);  // stage reads are clamped to the span
+#if HHUFF_ENC_PRED
+    E.livem = E.live ? 0xFFFFFFFFu : 0u;
+    {
+        const uint32_t jend = wave_max_u32(E.live ? jl : 0u);  // uniform trip count: no vote per step
+        uint32_t wn = sw[min(0u, jlast)];
+        for (uint32_t j = 0; j < jend; ++j) {  // bulk
+            const uint32_t w = wn;
+            wn = sw[min(j + 1u, jlast)];
+            const uint32_t onm = ~(uint32_t)((int32_t)((j - jf) | (jl - 1u - j)) >> 31);  // jf <= j < jl
+#ifdef HHUFF_ABL_ENC_NOTAB
+            E.put4m(make_uint2(w & 0x3Fu, 6u), make_uint2((w >> 8) & 0x1Fu, 5u), make_uint2((w >> 16) & 0x3Fu, 6u),
+                    make_uint2((w >> 24) & 0x7Fu, 7u), onm);
+#else
+            E.put4m(enc[w & 0xFFu], enc[(w >> 8) & 0xFFu], enc[(w >> 16) & 0xFFu], enc[w >> 24], onm);
+#endif
+        }
+    }
+    E.live = E.livem != 0u;
+    E.fail = E.fail || E.failm != 0u;
+#else
     uint32_t wn = sw[min(jf, jlast)];                 // next whole dword, read one step ahead
     for (uint32_t j = 0;; ++j) {                      // bulk
         if (!__any(E.live && j < jl)) break;
@@ -1072,6 +1161,7 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
 #endif
         }
     }
+#endif
     masked(jl, active && (end & 3u) != 0 && jl >= jf);  // tail
     if (E.fail || !active) return kFailLen;
     const uint32_t tbits = E.tb - startbit;
@@ -1110,36 +1200,6 @@ __device__ __forceinline__ uint32_t chunk_code_bits(const uint32_t* stage, uint3
               enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)].y + enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)].y;
     }
     return tb;
-}
-
-// ---------------------------------------------------------------------------------------------------
-// wave helpers
-// ---------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
-}
-// exclusive prefix sum over the wave
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-        if (lane >= o) x += y;
-    }
-    return x - v;
-}
-
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 }  // namespace hhuff

@@ -89,6 +89,38 @@ constexpr bool kSpanPrefetch = true;
 #endif
 constexpr bool kDecSwap = !HHUFF_DEC_I;
 
+// Commit the next tile's prefetched span to the input stage as soon as the current tile's steps are
+// done, BEFORE the current tile's output stores: the commit's vmcnt wait then covers only loads issued
+// a whole tile ago (the counter also counts stores, so committing after them waited for their writes).
+#ifndef HHUFF_EARLY_COMMIT  // A/B knob
+#define HHUFF_EARLY_COMMIT 0  // measured neutral (c4: 0.728 vs 0.729 ms decode)
+#endif
+constexpr bool kEarlyCommit = HHUFF_EARLY_COMMIT;
+
+// Phase timing (profile builds only, -DHHUFF_PROFILE): shader cycles per phase summed over waves,
+// read back with hhuff_debug_prof() (tools/ab.py prof).  s_memtime costs a little itself.
+#ifdef HHUFF_PROFILE
+__device__ unsigned long long g_prof[2][8];
+#define PROF_DECL                                      \
+    uint64_t prof_t = __builtin_readcyclecounter();    \
+    uint64_t prof_a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define PROF_MARK(k)                                          \
+    do {                                                      \
+        const uint64_t prof_n = __builtin_readcyclecounter(); \
+        prof_a[k] += prof_n - prof_t;                         \
+        prof_t = prof_n;                                      \
+    } while (0)
+#define PROF_FLUSH(kern) \
+    if (lane == 0)       \
+        for (int prof_k = 0; prof_k < 8; ++prof_k) atomicAdd(&g_prof[kern][prof_k], (unsigned long long)prof_a[prof_k]);
+#else
+#define PROF_DECL
+#define PROF_MARK(k) \
+    do {             \
+    } while (0)
+#define PROF_FLUSH(kern)
+#endif
+
 struct TileIn {  // per-lane prefetched fields of one tile
     uint32_t s, len, name_word, dst;
 };
@@ -155,6 +187,11 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
 
 // Write LDS bytes [0, ospan) to global [gbase, gbase + ospan) (gbase 16-aligned), keeping only the
 // global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
+// Write LDS bytes [0, ospan) to global [gbase, gbase + ospan) (gbase 16-aligned), keeping only the
+// global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
+// (Measured: batching the LDS reads of all chunks, or taking the edge bytes from the loaded registers,
+// made the c4 decode 3.5 % slower -- register pressure / code size in the 16-wave staged kernels.)
+template <int NCH>
 __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds, uint32_t ospan,
                                             uint64_t keep_lo, uint64_t keep_hi, int lane) {
     for (uint32_t k = (uint32_t)lane * 16u; k < ospan; k += 64u * 16u) {
@@ -310,6 +347,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
     if (base + stride < A.n) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
     if (cur.fits) pf.template commit<kDecSwap>(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+    PROF_DECL
     for (;;) {
         const uint64_t nbase = base + stride;
         const bool have_next = nbase < A.n;
@@ -327,6 +365,8 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         const bool is_name = t.valid && A.is_name_bits ? ((cur_name >> (t.i & 31)) & 1u) : false;
         uint32_t ol = 0;
         uint8_t st = 0;
+        bool committed = false;
+        PROF_MARK(0);  // plan + issue of the next tiles
         if (cur.fits) {
             wave_lds_sync();
             const bool act = t.valid && t.len <= kMaxStrLen;
@@ -337,6 +377,9 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
                 decode_staged_lane_i(stage, last, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
 #elif HHUFF_DEC_BULK
             (void)last;
+#ifdef HHUFF_ABL_REPEAT  // ablation: run the step loop twice (same output; times the steps alone)
+            (void)decode_staged_lane_v7(stage, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
+#endif
             const DecResult r = decode_staged_lane_v7(stage, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
 #elif HHUFF_DEC_ACC
             (void)last;
@@ -348,6 +391,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
             (void)last;
             const DecResult r = decode_staged_lane_v5(stage, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
 #endif
+            PROF_MARK(1);  // steps
             if (t.valid && t.len > kMaxStrLen) {
                 ol = kFailLen;
                 st = kStatusTooLong;
@@ -360,22 +404,39 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
                 st = kStatusFail;
             }
             wave_lds_sync();
+            PROF_MARK(2);  // verdicts
+            if (kEarlyCommit && have_next && nxt.fits) {  // the input stage is free: fill it before our stores
+                if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+                pf.template commit<kDecSwap>(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+                committed = true;
+            }
+            PROF_MARK(3);  // commit of the next span
+#ifdef HHUFF_ABL_NOCOPY  // ablation: no output copy (timing only)
+            if (region && A.n == 0) {
+#else
             if (region) {
-                region_copy(A.out, cur.obase, obuf, cur.ospan, cur.olo, cur.ohi, lane);
+#endif
+                region_copy<(OUT_STAGE + 1023) / 1024>(A.out, cur.obase, obuf, cur.ospan, cur.olo, cur.ohi, lane);
             } else if (t.valid && ol != kFailLen) {
                 lane_copy(A.out + cur.dst_g, obuf + cur.op0, ol);
             }
             wave_lds_sync();
+            PROF_MARK(4);  // output copy
         } else if (t.valid) {
             const uint64_t d = A.out_off ? cur.dst_g : dec_slot(t.s);
             decode_direct(A, t.s, t.len, is_name, A.out + d, T, ol, st);
+            PROF_MARK(6);  // direct path
         }
         if (t.valid) {
             A.out_len[t.i] = ol;
             A.status[t.i] = st;
         }
-        if (!have_next) break;
-        if (nxt.fits) {
+        PROF_MARK(5);  // lengths / statuses
+        if (!have_next) {
+            PROF_FLUSH(0);
+            break;
+        }
+        if (nxt.fits && !committed) {
             if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
             pf.template commit<kDecSwap>(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
         }
@@ -482,6 +543,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
     if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
     if (base + stride < A.n) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
     if (cur.fits) pf.commit(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+    PROF_DECL
     for (;;) {
         const uint64_t nbase = base + stride;
         const bool have_next = nbase < A.n;
@@ -494,6 +556,8 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
         // ---- the current tile ----
         const Tile& t = cur.t;
         uint32_t ol = kFailLen;
+        bool committed = false;
+        PROF_MARK(0);
         if (cur.fits) {
             for (uint32_t k = (uint32_t)lane * 16u; k < cur.ospan + 16u; k += 64u * 16u)
                 *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(obuf32) + k) = make_uint4(0u, 0u, 0u, 0u);
@@ -504,9 +568,14 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
 #ifdef HHUFF_ENC_VOTE_LOOP
             const uint32_t r = encode_staged_lane(stage, last, rel, t.len, act, obuf32, cur.op0, s_enc);
 #elif HHUFF_ENC_V2
+#ifdef HHUFF_ABL_REPEAT
+            (void)encode_chunk_v2(stage, last, rel, t.len, act, lds_addr(obuf32), 8u * cur.op0, s_enc,
+                                  act ? 8 * t.len - 7 : 0xFFFFFFFFu, true);
+#endif
             const uint32_t tb = encode_chunk_v2(stage, last, rel, t.len, act, lds_addr(obuf32), 8u * cur.op0, s_enc,
                                                 act ? 8 * t.len - 7 : 0xFFFFFFFFu, true);
             const uint32_t r = tb == kFailLen ? kFailLen : (tb + 7) >> 3;
+            PROF_MARK(1);
             wave_lds_sync();
             stage_bswap(obuf32, (cur.ospan + 15u) & ~15u, lane);
 #else
@@ -515,20 +584,37 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
 #endif
             if (act) ol = r;
             wave_lds_sync();
+            PROF_MARK(2);
+            if (kEarlyCommit && have_next && nxt.fits) {  // the input stage is free: fill it before our stores
+                if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+                pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+                committed = true;
+            }
+            PROF_MARK(3);
+#ifdef HHUFF_ABL_NOCOPY
+            if (region && A.n == 0) {
+#else
             if (region) {
-                region_copy(A.out, cur.a0, obuf, cur.ospan, t.lo, t.hi, lane);
+#endif
+                region_copy<(STAGE + 1023) / 1024>(A.out, cur.a0, obuf, cur.ospan, t.lo, t.hi, lane);
             } else if (t.valid && ol != kFailLen) {
                 lane_copy(A.out + cur.dst_g, obuf + cur.op0, ol);
             }
             wave_lds_sync();
+            PROF_MARK(4);
         } else if (t.valid && t.len <= kMaxStrLen) {
             RegSink sink;
             sink.init(A.out + (A.out_off ? cur.dst_g : (uint64_t)t.s));
             ol = encode_core(GlobalSource{A.in, A.in_size}, t.s, t.len, sink, s_enc);
+            PROF_MARK(6);
         }
         if (t.valid) finish_encode(A, t.i, t.len, ol);
-        if (!have_next) break;
-        if (nxt.fits) {
+        PROF_MARK(5);
+        if (!have_next) {
+            PROF_FLUSH(1);
+            break;
+        }
+        if (nxt.fits && !committed) {
             if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
             pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
         }
@@ -671,7 +757,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
             }
             ol = (uint32_t)__shfl((int)res, (int)L, 64);
             wave_lds_sync();
-            region_copy(A.out, cur.a0, obuf, cur.span, cur.lo, cur.hi, lane);
+            region_copy<(STAGE + 1023) / 1024>(A.out, cur.a0, obuf, cur.span, cur.lo, cur.hi, lane);
             wave_lds_sync();
         } else if (own && len <= kMaxStrLen) {
             RegSink sink;
@@ -902,7 +988,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_chunked_kernel(EncArgs A, u
             finish_encode(A, (uint32_t)t0 + j, len, ok ? (T + 7u) >> 3 : kFailLen);
         }
         wave_lds_sync();
-        region_copy(A.out, a0, reinterpret_cast<const uint8_t*>(obuf32), span, lo, hi, lane);
+        region_copy<(STAGE + 1023) / 1024>(A.out, a0, reinterpret_cast<const uint8_t*>(obuf32), span, lo, hi, lane);
         wave_lds_sync();
     }
 }
@@ -1135,7 +1221,7 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
             const uint32_t res = ok ? hn + (huff ? hlen : lj) : kFailLen;
             ol = (uint32_t)__shfl((int)res, (int)L, 64);
             wave_lds_sync();
-            region_copy(A.out, ob, obuf, ospan, olo, ohi, lane);
+            region_copy<(OSTAGE + 1023) / 1024>(A.out, ob, obuf, ospan, olo, ohi, lane);
             wave_lds_sync();
         } else if (own && len <= kMaxStrLen) {  // tile larger than the stage: one string per lane from global
             const GlobalSource src{A.in, A.in_size};
@@ -1528,3 +1614,16 @@ hipError_t launch_literals(const uint8_t* in, uint64_t in_size, const uint32_t* 
 int grid_size(int device, int which) { return grid_for(which == 0 ? kDecS : kEncS, device, 0xFFFFFFFFu); }
 
 }  // namespace hhuff
+
+#ifdef HHUFF_PROFILE
+namespace hhuff {
+hipError_t read_prof(unsigned long long* out16, bool reset) {
+    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prof), sizeof(g_prof));
+    if (e == hipSuccess && reset) {
+        static const unsigned long long z[16] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(g_prof));
+    }
+    return e;
+}
+}  // namespace hhuff
+#endif

@@ -112,6 +112,27 @@ def run(names, cfg="c4", rounds=5, steps=10):
             if ref is None:
                 ref = chk
             assert chk == ref or nm.startswith("x_"), (nm, chk, ref)  # x_*: ablation builds, output not checked
+    # profile builds (-DHHUFF_PROFILE): per-phase shader cycles of one launch of each kernel
+    phases = ["plan+issue", "steps", "verdicts/bswap", "commit", "out copy", "len/status", "direct", "-"]
+    for nm in names:
+        L = libs[nm]
+        if not hasattr(L, "hhuff_debug_prof"):
+            continue
+        buf = (ctypes.c_ulonglong * 16)()
+        L.hhuff_debug_prof(buf, 1)
+        for kind in ("dec", "enc"):
+            if kind == "enc":
+                L.hhuff_encode_batch(b["data"].data_ptr(), P, off32.data_ptr(), None, n, e_out.data_ptr(), None,
+                                     e_len.data_ptr(), e_st.data_ptr(), s)
+            else:
+                L.hhuff_decode_batch(huff.data_ptr(), H, hoff.data_ptr(), None, n_ok, None, d_out.data_ptr(), None,
+                                     d_len.data_ptr(), d_st.data_ptr(), s)
+            torch.cuda.synchronize()
+            L.hhuff_debug_prof(buf, 1)
+            row = list(buf)[0:8] if kind == "dec" else list(buf)[8:16]
+            tot = float(sum(row)) or 1.0
+            print(json.dumps({"build": nm, "kernel": kind, "cycles_per_wave": round(tot / 4096),
+                              "phases": {phases[k]: round(row[k] / tot, 4) for k in range(8) if row[k]}}))
     for nm in names:
         e = sorted(res[nm]["enc"])
         d = sorted(res[nm]["dec"])
