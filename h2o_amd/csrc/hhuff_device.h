@@ -37,6 +37,14 @@ __device__ __forceinline__ uint64_t dec_slot(uint32_t x) { return ((uint64_t)x *
 // ---------------------------------------------------------------------------------------------------
 // wave helpers
 // ---------------------------------------------------------------------------------------------------
+// Wave-wide reductions and scan with DPP (row shifts within 16-lane rows, then row broadcasts across
+// them): no LDS / ds_bpermute traffic and no per-lane address registers.  The results of the
+// reductions are read from lane 63, so they are wave-uniform (SGPR) values.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, ROW_MASK, 0xF, false);
+}
+#ifdef HHUFF_SHFL_REDUCE  // A/B knob: ds_bpermute (__shfl_xor / __shfl_up) reductions and scan
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
@@ -47,15 +55,49 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
     return v;
 }
-// exclusive prefix sum over the wave
-__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
-    uint32_t x = v;
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = (int)__lane_id();
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-        if (lane >= o) x += y;
+        const uint32_t y = (uint32_t)__shfl_up((int)v, o, 64);
+        if (lane >= o) v += y;
     }
-    return x - v;
+    return v;
+}
+#else
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, dpp<0x111>(v, v));  // row_shr:1 (lanes without a source keep their own value)
+    v = min(v, dpp<0x112>(v, v));  // row_shr:2
+    v = min(v, dpp<0x114>(v, v));  // row_shr:4
+    v = min(v, dpp<0x118>(v, v));  // row_shr:8: lane 15 of each row holds the row's minimum
+    v = min(v, dpp<0x142, 0xA>(v, v));  // row_bcast:15
+    v = min(v, dpp<0x143, 0xC>(v, v));  // row_bcast:31: lane 63 holds the wave's minimum
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = max(v, dpp<0x111>(v, v));
+    v = max(v, dpp<0x112>(v, v));
+    v = max(v, dpp<0x114>(v, v));
+    v = max(v, dpp<0x118>(v, v));
+    v = max(v, dpp<0x142, 0xA>(v, v));
+    v = max(v, dpp<0x143, 0xC>(v, v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// inclusive prefix sum over the wave (lane 63 holds the total)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    v += dpp<0x111>(0u, v);
+    v += dpp<0x112>(0u, v);
+    v += dpp<0x114>(0u, v);
+    v += dpp<0x118>(0u, v);
+    v += dpp<0x142, 0xA>(0u, v);
+    v += dpp<0x143, 0xC>(0u, v);
+    return v;
+}
+#endif
+// exclusive prefix sum over the wave
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, int lane) {
+    (void)lane;
+    return wave_incl_scan(v) - v;
 }
 
 __device__ __forceinline__ void wave_lds_sync() {

@@ -156,11 +156,14 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
     uint4 v[NCH];
     __device__ __forceinline__ void issue(const uint8_t* __restrict__ in, uint64_t in_size, uint32_t a0, uint32_t span,
                                           int lane) {
+        // bytes readable from a0 on, clamped to 32 bits (a0 <= in_size): every test below is 32-bit
+        const uint64_t av = in_size > (uint64_t)a0 ? in_size - a0 : 0u;
+        const uint32_t avail = av > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)av;
+        const uint8_t* src = in + a0;
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
             const uint32_t k = (uint32_t)c * 1024u + (uint32_t)lane * 16u;
-            const uint64_t g = (uint64_t)a0 + k;
-            if (k < span && g + 16 <= in_size) v[c] = *reinterpret_cast<const uint4*>(in + g);
+            if (k < span && k + 16u <= avail) v[c] = *reinterpret_cast<const uint4*>(src + k);
         }
     }
     template <bool kSwap = false>  // kSwap: store big-endian dwords (the v5 decode window reads them)
@@ -309,69 +312,78 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     uint64_t base = ((uint64_t)blockIdx.x * WAVES + wave) * 64;
     if (base >= A.n) return;
 
-    // per-tile layout: input span and output stage extent
+    // per-tile layout: input span and output stage extent.  Per lane: the string and its stage offset;
+    // wave-uniform (SGPRs): the tile's input span [lo, hi) and everything derived from it.
     struct Plan {
-        Tile t;
-        uint32_t a0, span, op0, ospan;
-        uint64_t obase, olo, ohi, dst_g;
-        bool fits;
+        uint32_t s, len, op0;    // per lane
+        uint32_t lo, hi, ospan;  // wave-uniform
+        uint64_t dst_g;          // explicit destinations
+        bool valid, fits;
+        __device__ __forceinline__ uint32_t a0() const { return lo & ~15u; }
+        __device__ __forceinline__ uint32_t span() const { return hi > lo ? ((hi + 15u) & ~15u) - a0() : 0u; }
+        __device__ __forceinline__ uint64_t olo() const { return dec_slot(lo); }
+        __device__ __forceinline__ uint64_t ohi() const { return dec_slot(hi); }
+        __device__ __forceinline__ uint64_t obase() const { return olo() & ~15ull; }
     };
     auto plan = [&](uint64_t b, const TileIn& ti) {
         Plan P;
-        P.t = finish_tile(b, lane, A.n, ti, pairs);
-        const Tile& t = P.t;
-        P.a0 = t.lo & ~15u;
-        P.span = t.hi > t.lo ? ((t.hi + 15u) & ~15u) - P.a0 : 0u;
-        P.obase = P.olo = P.ohi = P.dst_g = 0;
+        const Tile t = finish_tile(b, lane, A.n, ti, pairs);
+        P.s = t.s;
+        P.len = t.len;
+        P.valid = t.valid;
+        P.lo = __builtin_amdgcn_readfirstlane(t.lo);
+        P.hi = __builtin_amdgcn_readfirstlane(t.hi);
+        P.dst_g = 0;
         if (region) {
-            P.olo = dec_slot(t.lo);
-            P.ohi = dec_slot(t.hi);
-            P.obase = P.olo & ~15ull;
-            P.ospan = t.hi > t.lo ? (uint32_t)(P.ohi - P.obase) : 0u;
-            P.op0 = t.len ? (uint32_t)(dec_slot(t.s) - P.obase) : 0u;
+            P.ospan = P.hi > P.lo ? (uint32_t)(P.ohi() - P.obase()) : 0u;
+            P.op0 = t.len ? (uint32_t)(dec_slot(t.s) - P.obase()) : 0u;
         } else {
             P.dst_g = A.out_off ? (uint64_t)ti.dst : dec_slot(t.s);
             const uint32_t cap = t.valid ? (uint32_t)(((uint64_t)min(t.len, kMaxStrLen) * 8u) / 5u) + 3u : 0u;
             const uint32_t pre = wave_excl_scan(cap, lane);
-            P.ospan = __shfl(pre + cap, 63, 64);
+            P.ospan = (uint32_t)__builtin_amdgcn_readlane((int)(pre + cap), 63);
             P.op0 = pre + ((uint32_t)(((uintptr_t)A.out + P.dst_g) - pre) & 3u);
         }
-        P.fits = P.span <= IN_STAGE && P.ospan <= OUT_STAGE;
+        P.fits = P.span() <= IN_STAGE && P.ospan <= OUT_STAGE;
         return P;
     };
 
+    // Software pipeline over the wave's tiles (cur = being decoded, nxt = span prefetched into registers,
+    // ti = offsets of the tile after).  Every wait on a global load sits between the current tile's steps
+    // and its stores: the vmcnt counter also counts stores, so a load consumed right after the previous
+    // tile's stores would wait for their writes to land.
     SpanPrefetch<(IN_STAGE + 1023) / 1024> pf;
     TileIn ti = issue_tile(base, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
     Plan cur = plan(base, ti);
     uint32_t cur_name = ti.name_word;
-    if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
-    if (base + stride < A.n) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
-    if (cur.fits) pf.template commit<kDecSwap>(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+    if (cur.fits) pf.issue(A.in, A.in_size, cur.a0(), cur.span(), lane);
+    bool have_next = base + stride < A.n;
+    if (have_next) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
+    if (cur.fits) pf.template commit<kDecSwap>(stage, A.in, A.in_size, cur.a0(), cur.span(), lane);
+    Plan nxt;
+    uint32_t nxt_name = 0;
+    if (have_next) {
+        nxt = plan(base + stride, ti);
+        nxt_name = ti.name_word;
+        if (nxt.fits) pf.issue(A.in, A.in_size, nxt.a0(), nxt.span(), lane);
+        if (base + 2 * stride < A.n)
+            ti = issue_tile(base + 2 * stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
+    }
     PROF_DECL
     for (;;) {
         const uint64_t nbase = base + stride;
-        const bool have_next = nbase < A.n;
-        Plan nxt;
-        uint32_t nxt_name = 0;
-        if (have_next) {
-            nxt = plan(nbase, ti);
-            nxt_name = ti.name_word;
-            if (kSpanPrefetch && nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
-            if (nbase + stride < A.n)
-                ti = issue_tile(nbase + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
-        }
-        // ---- the current tile ----
-        const Tile& t = cur.t;
-        const bool is_name = t.valid && A.is_name_bits ? ((cur_name >> (t.i & 31)) & 1u) : false;
+        // ---- the current tile: steps and verdicts ----
+        const Plan& t = cur;
+        const uint32_t ti_i = (uint32_t)base + (uint32_t)lane;
+        const bool is_name = t.valid && A.is_name_bits ? ((cur_name >> (ti_i & 31)) & 1u) : false;
         uint32_t ol = 0;
         uint8_t st = 0;
-        bool committed = false;
-        PROF_MARK(0);  // plan + issue of the next tiles
+        PROF_MARK(0);
         if (cur.fits) {
             wave_lds_sync();
             const bool act = t.valid && t.len <= kMaxStrLen;
-            const uint32_t rel = t.len ? t.s - cur.a0 : 0u;
-            const uint32_t last = cur.span ? cur.span - 4u : 0u;
+            const uint32_t rel = t.len ? t.s - cur.a0() : 0u;
+            const uint32_t last = cur.span() ? cur.span() - 4u : 0u;
 #if HHUFF_DEC_I
             const DecResult r =
                 decode_staged_lane_i(stage, last, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
@@ -405,43 +417,54 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
             }
             wave_lds_sync();
             PROF_MARK(2);  // verdicts
-            if (kEarlyCommit && have_next && nxt.fits) {  // the input stage is free: fill it before our stores
-                if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
-                pf.template commit<kDecSwap>(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
-                committed = true;
-            }
-            PROF_MARK(3);  // commit of the next span
-#ifdef HHUFF_ABL_NOCOPY  // ablation: no output copy (timing only)
-            if (region && A.n == 0) {
-#else
-            if (region) {
-#endif
-                region_copy<(OUT_STAGE + 1023) / 1024>(A.out, cur.obase, obuf, cur.ospan, cur.olo, cur.ohi, lane);
-            } else if (t.valid && ol != kFailLen) {
-                lane_copy(A.out + cur.dst_g, obuf + cur.op0, ol);
-            }
-            wave_lds_sync();
-            PROF_MARK(4);  // output copy
         } else if (t.valid) {
             const uint64_t d = A.out_off ? cur.dst_g : dec_slot(t.s);
             decode_direct(A, t.s, t.len, is_name, A.out + d, T, ol, st);
             PROF_MARK(6);  // direct path
         }
-        if (t.valid) {
-            A.out_len[t.i] = ol;
-            A.status[t.i] = st;
+        // ---- the next tile: commit its span (the input stage is free), plan + prefetch the one after ----
+        Plan nn;
+        uint32_t nn_name = 0;
+        bool have_nn = false;
+        if (have_next) {
+            if (nxt.fits) pf.template commit<kDecSwap>(stage, A.in, A.in_size, nxt.a0(), nxt.span(), lane);
+            have_nn = nbase + stride < A.n;
+            if (have_nn) {
+                nn = plan(nbase + stride, ti);
+                nn_name = ti.name_word;
+                if (nn.fits) pf.issue(A.in, A.in_size, nn.a0(), nn.span(), lane);
+                if (nbase + 2 * stride < A.n)
+                    ti = issue_tile(nbase + 2 * stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
+            }
         }
-        PROF_MARK(5);  // lengths / statuses
+        PROF_MARK(3);  // commit + plan
+        // ---- the current tile: stores ----
+        if (cur.fits) {
+#ifdef HHUFF_ABL_NOCOPY  // ablation: no output copy (timing only)
+            if (region && A.n == 0) {
+#else
+            if (region) {
+#endif
+                region_copy<(OUT_STAGE + 1023) / 1024>(A.out, cur.obase(), obuf, cur.ospan, cur.olo(), cur.ohi(), lane);
+            } else if (t.valid && ol != kFailLen) {
+                lane_copy(A.out + cur.dst_g, obuf + cur.op0, ol);
+            }
+            wave_lds_sync();
+        }
+        if (t.valid) {
+            A.out_len[ti_i] = ol;
+            A.status[ti_i] = st;
+        }
+        PROF_MARK(4);  // stores
         if (!have_next) {
             PROF_FLUSH(0);
             break;
         }
-        if (nxt.fits && !committed) {
-            if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
-            pf.template commit<kDecSwap>(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
-        }
         cur = nxt;
         cur_name = nxt_name;
+        nxt = nn;
+        nxt_name = nn_name;
+        have_next = have_nn;
         base = nbase;
     }
 }
@@ -530,7 +553,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
             P.dst_g = A.out_off ? (uint64_t)ti.dst : (uint64_t)t.s;
             const uint32_t cap = t.valid ? min(t.len, kMaxStrLen) + 3u : 0u;
             const uint32_t pre = wave_excl_scan(cap, lane);
-            P.ospan = __shfl(pre + cap, 63, 64);
+            P.ospan = (uint32_t)__builtin_amdgcn_readlane((int)(pre + cap), 63);
             P.op0 = pre + ((uint32_t)(((uintptr_t)A.out + P.dst_g) - pre) & 3u);
         }
         P.fits = P.span <= STAGE && P.ospan <= STAGE;
