@@ -12,7 +12,8 @@ Multi-GPU (torchrun, one process per GPU, RCCL): each rank owns an independent s
 
 Extra JSON fields: per-direction rates, `roofline` for the dominant kernel (decode; algorithmic bytes
 B_dec = H + P_ok + 9 N_ok + 4 + ceil(N_ok / 8) per launch over its HIP-event duration), and
-`cpu_baseline` (oracle restatement of h2o's CPU path on this host's cores, rank 0 only).
+`cpu_baseline` (h2o's CPU path -- the reference's hpack.c compiled, or the restatement -- on this host's
+cores, rank 0 only).
 """
 import argparse
 import json
@@ -35,7 +36,7 @@ def parse():
     ap.add_argument("--config", default="c4")
     ap.add_argument("--n", type=int, default=None, help="strings per rank (default: the config's N)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=1 << 21, help="strings in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=0, help="strings in the CPU-baseline sample (0: the whole batch)")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--only", choices=["encode", "decode"], default=None, help="profile one direction")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
@@ -328,32 +329,46 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, P_ok, tor
 
 
 def cpu_baseline(b, args, np):
-    """h2o's CPU path (oracle restatement, same algorithm as lib/http2/hpack.c) on this host's cores, on a
-    bounded sample (the first `cpu_sample` strings of rank 0's batch), encode + decode like one step."""
+    """h2o's own CPU path on this host's cores, timed like one step (encode all strings, then decode the
+    compressible ones).  kind "reference": oracle/_ref/libh2oref.so, the reference's lib/http2/hpack.c
+    compiled where it lies (it travels with the tree); kind "port": the clean-room restatement when the
+    reference build is absent.  Multi-threaded over a bounded sample of rank 0's batch (default: all
+    of it, ~10-30 s of CPU work), contiguous per-thread ranges; plus a single-thread rate on a smaller
+    sample."""
     from oracle import oracle as O
 
-    o = O.oracle()
-    m = min(args.cpu_sample, b["n"])
+    kind = "reference" if O.ref_available() else "port"
+    codec = O.ref() if kind == "reference" else O.oracle()
+    m = min(args.cpu_sample, b["n"]) if args.cpu_sample else b["n"]
     off = b["off"][:m + 1].cpu().numpy().astype(np.uint32)
     data = b["data"][:int(off[-1])].cpu().numpy()
     names = b["is_name_bits"][:(m + 31) // 32].cpu().numpy().view(np.uint32)
     threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-    enc, el, _ = o.encode_batch(data, off, m, nthreads=threads)  # also produces the decode input
-    ok = el != O.FAIL
-    hl = np.where(ok, el, 0).astype(np.uint32)
-    starts = off[:-1].copy()
-    best = None
-    for _ in range(3):
-        t0 = time.perf_counter()
-        o.encode_batch(data, off, m, nthreads=threads)
-        t1 = time.perf_counter()
-        o.decode_batch(enc, starts, m, in_len=hl, is_name_bits=names, nthreads=threads)
-        t2 = time.perf_counter()
-        best = (t2 - t0) if best is None else min(best, t2 - t0)
-    P = float(off[-1])
-    return {"value": round(P / GIB / best, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": "%d strings (%.1f MB) of rank 0's batch, encode + decode, best of 3, %d threads"
-                      % (m, P / 1e6, threads)}
+
+    def rate(mm, nthreads, reps):
+        o = off[:mm + 1]
+        d = data[:int(o[-1])]
+        enc, el, _ = codec.encode_batch(d, o, mm, nthreads=nthreads)  # also produces the decode input
+        hl = np.where(el != O.FAIL, el, 0).astype(np.uint32)
+        starts = o[:-1].copy()
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            codec.encode_batch(d, o, mm, nthreads=nthreads)
+            codec.decode_batch(enc, starts, mm, in_len=hl, is_name_bits=names, nthreads=nthreads)
+            t = time.perf_counter() - t0
+            best = t if best is None else min(best, t)
+        return float(o[-1]) / GIB / best, float(o[-1])
+
+    v, P = rate(m, threads, 3)
+    m1 = min(m, 1 << 18)
+    v1, P1 = rate(m1, 1, 3)
+    return {"value": round(v, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": "%d strings (%.1f MB) of rank 0's batch, encode + decode, best of 3, %d threads "
+                      "(%s)" % (m, P / 1e6, threads, "oracle/_ref: lib/http2/hpack.c compiled" if kind == "reference"
+                                else "clean-room restatement"),
+            "single_thread_value": round(v1, 4),
+            "single_thread_sample": "%d strings (%.1f MB), 1 thread" % (m1, P1 / 1e6)}
 
 
 if __name__ == "__main__":
