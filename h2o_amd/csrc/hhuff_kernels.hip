@@ -188,8 +188,14 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
     }
 };
 
+#ifndef HHUFF_COPY_V2  // A/B knob: 0 = LDS byte reads at the edges; N = N chunks per round, register edges
+#define HHUFF_COPY_V2 0  // measured: register edges 5 % slower (c4 decode 0.7125 -> 0.7485 ms)
+#endif
 // Write LDS bytes [0, ospan) to global [gbase, gbase + ospan) (gbase 16-aligned), keeping only the
 // global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
+#ifndef HHUFF_COPY_V2  // A/B knob: 0 = LDS byte reads at the edges; N = N chunks per round, register edges
+#define HHUFF_COPY_V2 0  // measured: register edges 5 % slower (c4 decode 0.7125 -> 0.7485 ms)
+#endif
 // Write LDS bytes [0, ospan) to global [gbase, gbase + ospan) (gbase 16-aligned), keeping only the
 // global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
 // (Measured: batching the LDS reads of all chunks, or taking the edge bytes from the loaded registers,
@@ -197,6 +203,38 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
 template <int NCH>
 __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds, uint32_t ospan,
                                             uint64_t keep_lo, uint64_t keep_hi, int lane) {
+#if HHUFF_COPY_V2
+    // two 1-KiB chunks per round: both LDS reads are issued before the stores, and the two edge chunks
+    // of the region take their bytes from the loaded registers (no LDS round trip per byte)
+    constexpr int CP = HHUFF_COPY_V2;  // chunks per round
+#pragma unroll
+    for (int c0 = 0; c0 < NCH; c0 += CP) {
+        uint4 v[CP];
+#pragma unroll
+        for (int d = 0; d < CP; ++d) {
+            const uint32_t k = (uint32_t)(c0 + d) * 1024u + (uint32_t)lane * 16u;
+            if (c0 + d < NCH && k < ospan) v[d] = *reinterpret_cast<const uint4*>(lds + k);
+        }
+#pragma unroll
+        for (int d = 0; d < CP; ++d) {
+            const uint32_t k = (uint32_t)(c0 + d) * 1024u + (uint32_t)lane * 16u;
+            if (c0 + d >= NCH || k >= ospan) continue;
+            const uint64_t g = gbase + k;
+            if (g >= keep_lo && g + 16 <= keep_hi) {
+                *reinterpret_cast<uint4*>(out + g) = v[d];
+            } else {
+                const int64_t rl = (int64_t)keep_lo - (int64_t)g, rh = (int64_t)keep_hi - (int64_t)g;
+                const uint32_t blo = (uint32_t)min(max(rl, (int64_t)0), (int64_t)16);
+                const uint32_t bhi = (uint32_t)min(max(rh, (int64_t)0), (int64_t)16);
+                const uint32_t m = ((1u << bhi) - 1u) & ~((1u << blo) - 1u);  // bytes [blo, bhi) are ours
+                const uint32_t w[4] = {v[d].x, v[d].y, v[d].z, v[d].w};
+#pragma unroll
+                for (uint32_t b = 0; b < 16; ++b)
+                    if ((m >> b) & 1u) out[g + b] = (uint8_t)(w[b >> 2] >> (8u * (b & 3u)));
+            }
+        }
+    }
+#else
     for (uint32_t k = (uint32_t)lane * 16u; k < ospan; k += 64u * 16u) {
         const uint64_t g = gbase + k;
         if (g >= keep_lo && g + 16 <= keep_hi) {
@@ -206,6 +244,7 @@ __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t 
                 if (g + b >= keep_lo && g + b < keep_hi) out[g + b] = lds[k + b];
         }
     }
+#endif
 }
 
 // Copy `n` bytes from LDS `src` to global `dst`, where src == dst (mod 4).
