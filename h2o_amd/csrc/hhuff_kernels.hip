@@ -193,11 +193,6 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
 #endif
 // Write LDS bytes [0, ospan) to global [gbase, gbase + ospan) (gbase 16-aligned), keeping only the
 // global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
-#ifndef HHUFF_COPY_V2  // A/B knob: 0 = LDS byte reads at the edges; N = N chunks per round, register edges
-#define HHUFF_COPY_V2 0  // measured: register edges 5 % slower (c4 decode 0.7125 -> 0.7485 ms)
-#endif
-// Write LDS bytes [0, ospan) to global [gbase, gbase + ospan) (gbase 16-aligned), keeping only the
-// global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
 // (Measured: batching the LDS reads of all chunks, or taking the edge bytes from the loaded registers,
 // made the c4 decode 3.5 % slower -- register pressure / code size in the 16-wave staged kernels.)
 template <int NCH>
