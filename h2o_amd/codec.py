@@ -65,6 +65,11 @@ def lib():
         L.hhuff_encode_batch_host_pipelined.restype = ctypes.c_int
         L.hhuff_encode_batch_host_pipelined.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, ctypes.c_uint64,
                                                         _vp, _vp, ctypes.c_int, ctypes.c_uint64]
+        L.hhuff_hpack_scratch_size.restype = ctypes.c_uint64
+        L.hhuff_hpack_scratch_size.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        L.hhuff_hpack_decode_blocks.restype = ctypes.c_int
+        L.hhuff_hpack_decode_blocks.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp,
+                                                _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]
         L.hhuff_version.restype = ctypes.c_char_p
         L.hhuff_last_error_string.restype = ctypes.c_char_p
         L.hhuff_grid_size.restype = ctypes.c_int
@@ -75,7 +80,7 @@ def lib():
 
 # symbols include/hhuff.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decode_batch", "hhuff_encode_batch",
-            "hhuff_flatten_batch", "hhuff_decode_literals",
+            "hhuff_flatten_batch", "hhuff_decode_literals", "hhuff_hpack_decode_blocks", "hhuff_hpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string",
             "hhuff_grid_size")
@@ -207,6 +212,57 @@ def decode_literals(data, lit_off, lit_end, n, prefix_bits=7, qpack=False, is_na
                                        LIT_QPACK if qpack else 0, _dp(is_name_bits), _dp(out), _dp(out_len),
                                        _dp(pay_off), _dp(consumed), _dp(status), _stream(stream)), "hhuff_decode_literals")
     return out, out_len, pay_off, consumed, status
+
+
+BLK_ARENA = -300
+BLK_SKIPPED = -301
+ERR_PROTOCOL = -1
+ERR_COMPRESSION = -9
+
+
+def default_arena_off(blk_off, table_size=4096):
+    """u64 arena slice offsets per block (torch, on blk_off's device): a block of L bytes gets
+    floor(8 L / 5) + (L / 4 + 1) * (table_size + 64) bytes -- literals expand at most 8/5, and an indexed
+    field (>= 1 byte) copies at most one table entry"""
+    import torch
+
+    L = (blk_off[1:].to(torch.int64) & 0xFFFFFFFF) - (blk_off[:-1].to(torch.int64) & 0xFFFFFFFF)
+    cap = (L * 8) // 5 + (L // 4 + 1) * (table_size + 64)
+    out = torch.zeros(L.numel() + 1, dtype=torch.int64, device=blk_off.device)
+    out[1:] = torch.cumsum(cap, 0)
+    return out
+
+
+def hpack_decode_blocks(data, blk_off, conn_first, table_size=4096, arena_off=None, in_size=None, stream=None):
+    """HPACK header blocks (include/hhuff.h hhuff_hpack_decode_blocks) on device tensors: blk_off / conn_first
+    int32 tensors (u32 bits), arena_off int64.  Returns a dict of device tensors: arena, name_off, name_len,
+    value_off, value_len, fflags (per field slot), nfields, bstatus (per block)."""
+    import torch
+
+    dev = data.device
+    in_size = data.numel() if in_size is None else in_size
+    nblk = blk_off.numel() - 1
+    nconn = conn_first.numel() - 1
+    if arena_off is None:
+        arena_off = default_arena_off(blk_off, table_size)
+    nslots = max(1, int(blk_off[-1].item()) & 0xFFFFFFFF)
+    r = dict(arena=torch.empty(max(1, int(arena_off[-1].item())), dtype=torch.uint8, device=dev),
+             name_off=torch.empty(nslots, dtype=torch.int32, device=dev),
+             name_len=torch.empty(nslots, dtype=torch.int32, device=dev),
+             value_off=torch.empty(nslots, dtype=torch.int32, device=dev),
+             value_len=torch.empty(nslots, dtype=torch.int32, device=dev),
+             fflags=torch.empty(nslots, dtype=torch.uint8, device=dev),
+             nfields=torch.empty(max(1, nblk), dtype=torch.int32, device=dev),
+             bstatus=torch.empty(max(1, nblk), dtype=torch.int32, device=dev))
+    ss = int(lib().hhuff_hpack_scratch_size(nconn, table_size))
+    scratch = torch.empty(max(16, ss), dtype=torch.uint8, device=dev)
+    _check(lib().hhuff_hpack_decode_blocks(_dp(data), in_size, _dp(blk_off), _dp(conn_first), nconn, table_size,
+                                           _dp(r["arena"]), _dp(arena_off), _dp(r["name_off"]), _dp(r["name_len"]),
+                                           _dp(r["value_off"]), _dp(r["value_len"]), _dp(r["fflags"]), _dp(r["nfields"]),
+                                           _dp(r["bstatus"]), _dp(scratch), scratch.numel(), _stream(stream)),
+           "hhuff_hpack_decode_blocks")
+    r["scratch"] = scratch  # keep alive until the stream has run the launch
+    return r
 
 
 # ---------------------------------------------------------------------------------------------------

@@ -153,6 +153,27 @@ HHUFF_API int hhuff_decode_literals(const uint8_t* in, uint64_t in_size, const u
     return f == hipSuccess ? HHUFF_OK : hip_fail(f, "hipFreeAsync");
 }
 
+HHUFF_API uint64_t hhuff_hpack_scratch_size(uint32_t nconn, uint32_t table_size) {
+    return (uint64_t)nconn * hhuff::hpack_conn_scratch(table_size);
+}
+
+HHUFF_API int hhuff_hpack_decode_blocks(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off,
+                                        const uint32_t* conn_first, uint32_t nconn, uint32_t table_size, uint8_t* arena,
+                                        const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len,
+                                        uint32_t* value_off, uint32_t* value_len, uint8_t* fflags, uint32_t* nfields,
+                                        int32_t* bstatus, void* scratch, uint64_t scratch_size, void* stream) {
+    if (nconn == 0) return HHUFF_OK;
+    if (!in || !blk_off || !conn_first || !arena || !arena_off || !name_off || !name_len || !value_off || !value_len ||
+        !fflags || !nfields || !bstatus || !scratch)
+        return arg_fail("NULL array");
+    if (scratch_size < hhuff_hpack_scratch_size(nconn, table_size)) return arg_fail("scratch smaller than hhuff_hpack_scratch_size");
+    if (((uintptr_t)scratch & 15u) != 0) return arg_fail("scratch must be 16-byte aligned");
+    hipError_t e = hhuff::launch_hpack_blocks(in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off,
+                                              name_len, value_off, value_len, fflags, nfields, bstatus,
+                                              (uint8_t*)scratch, (hipStream_t)stream);
+    return e == hipSuccess ? HHUFF_OK : hip_fail(e, "hpack block launch");
+}
+
 // ---------------------------------------------------------------------------------------------------
 // (1) h2o per-string symbols: a batch of one on the thread's stream, synchronously
 // device/pinned layout: [meta 32 B: u32 in_off[2], out_len, is_name word, u8 status][input][output]

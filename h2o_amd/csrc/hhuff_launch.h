@@ -20,5 +20,12 @@ hipError_t launch_literals(const uint8_t* in, uint64_t in_size, const uint32_t* 
                            uint32_t prefix_bits, uint32_t flags, const uint32_t* is_name_bits, uint8_t* out,
                            uint32_t* out_len, uint32_t* pay_off, uint32_t* consumed, uint8_t* status, uint32_t* huff_len,
                            hipStream_t stream);
+// HPACK header blocks (f4): see include/hhuff.h hhuff_hpack_decode_blocks; scratch = nconn x
+// hpack_conn_scratch(table_size) bytes of device memory
+uint64_t hpack_conn_scratch(uint32_t table_size);
+hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off, const uint32_t* conn_first,
+                               uint32_t nconn, uint32_t table_size, uint8_t* arena, const uint64_t* arena_off,
+                               uint32_t* name_off, uint32_t* name_len, uint32_t* value_off, uint32_t* value_len,
+                               uint8_t* fflags, uint32_t* nfields, int32_t* bstatus, uint8_t* scratch, hipStream_t stream);
 int grid_size(int device, int which);
 }  // namespace hhuff

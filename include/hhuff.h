@@ -133,6 +133,35 @@ int hhuff_decode_literals(const uint8_t *in, uint64_t in_size, const uint32_t *l
                           uint32_t n, unsigned prefix_bits, unsigned flags, const uint32_t *is_name_bits, uint8_t *out,
                           uint32_t *out_len, uint32_t *pay_off, uint32_t *consumed, uint8_t *status, void *stream);
 
+/* (2c) HPACK header blocks: h2o_hpack_decode_header (lib/http2/hpack.c:319-435) applied field
+ *      after field over each block, as h2o_hpack_parse_request loops over a block (hpack.c:513-527), with
+ *      one dynamic table per connection whose blocks are decoded in order.  One GPU lane per connection.
+ *        block b        in[blk_off[b] .. blk_off[b+1])      (blocks packed back to back; blk_off has nblk+1)
+ *        connection c   blocks conn_first[c] .. conn_first[c+1]-1   (conn_first has nconn+1 entries)
+ *        table_size     SETTINGS_HEADER_TABLE_SIZE of every connection: the table's initial and maximum
+ *                       capacity (hpack_capacity = hpack_max_capacity, lib/http2/connection.c:1844;
+ *                       h2o's default 4096)
+ *        arena          decoded names and values; block b writes arena[arena_off[b] .. arena_off[b+1])
+ *                       (u64 offsets); every field's name is written, then its value
+ *      Per field f of block b (f in blk_off[b] .. blk_off[b] + nfields[b] - 1: a block of L bytes holds at
+ *      most L fields, so field slots reuse the block's byte offsets): name_off/name_len/value_off/
+ *      value_len (arena offsets, u32) and fflags = its soft-error bits (HHUFF_SOFT_NAME / _VALUE: the
+ *      field's H2O_HTTP2_ERROR_INVALID_HEADER_CHAR).  Per block: nfields[b] and bstatus[b] = 0, or the
+ *      hard error that stopped it: -9 H2O_HTTP2_ERROR_COMPRESSION, -1 H2O_HTTP2_ERROR_PROTOCOL (upper-case
+ *      raw name), HHUFF_BLK_ARENA (a string does not fit the block's arena slice: a Huffman literal needs
+ *      floor(8 len / 5) bytes free, a raw one len, an indexed one its size), or HHUFF_BLK_SKIPPED (an
+ *      earlier block of the connection failed: h2o drops the connection).  Fields before the error stand.
+ *      Device arrays; scratch = device memory of hhuff_hpack_scratch_size(nconn, table_size) bytes (the
+ *      dynamic tables); asynchronous on `stream`. */
+#define HHUFF_BLK_ARENA (-300)
+#define HHUFF_BLK_SKIPPED (-301)
+uint64_t hhuff_hpack_scratch_size(uint32_t nconn, uint32_t table_size);
+int hhuff_hpack_decode_blocks(const uint8_t *in, uint64_t in_size, const uint32_t *blk_off, const uint32_t *conn_first,
+                              uint32_t nconn, uint32_t table_size, uint8_t *arena, const uint64_t *arena_off,
+                              uint32_t *name_off, uint32_t *name_len, uint32_t *value_off, uint32_t *value_len,
+                              uint8_t *fflags, uint32_t *nfields, int32_t *bstatus, void *scratch, uint64_t scratch_size,
+                              void *stream);
+
 /* (3b) Pipelined host path (the socket-buffer -> pinned -> device -> pinned -> pool staging of
  *     SURVEY f3; replaces the caller-side copies around lib/http2/hpack.c:240-241).  Contiguous layout
  *     (in_off[n + 1], implicit output slots) only.  The batch is cut into chunks of about

@@ -14,6 +14,10 @@ Fixture sets (numpy .npz, arrays only, no pickles):
                    re-decoded by the reference, plus the plain bytes decoded as (mostly invalid) Huffman
   adversarial.npz  hand-built decode edge cases (padding, EOS, truncation, long codes, names/values)
   framing.npz      HPACK h2o_hpack_encode_string and QPACK flatten_string (prefix 3/5/7) outputs
+  blocks.npz       header blocks (f4): the fuzz corpus's connections, the unit test's request sequences,
+                   a static-table sweep and synthetic connections (h2o_amd/hpack_synth.py), decoded by
+                   h2o_hpack_decode_header field after field with a table per connection (4096 bytes);
+  blocks_256.npz   the unit test's response blocks and synthetic connections with a 256-byte table
   literals.npz     string literals as they sit in header blocks: every literal of the fuzz corpus's
                    HPACK blocks plus hand-built edge cases (raw names/values to validate, bad and
                    truncated integers, invalid Huffman), and QPACK name literals (prefix 3/5) -- the
@@ -457,7 +461,90 @@ def literals_set(seed=13):
     return res
 
 
+# ------------------------------------------------------------------------------------------------
+# header blocks (f4): h2o_hpack_decode_header over whole blocks, one dynamic table per connection
+# ------------------------------------------------------------------------------------------------
+# request sequences of the reference's unit test (t/00unit/lib/http2/hpack.c:287-296: RFC 7541 C.3 / C.4)
+UNIT_REQUESTS = [
+    [b"\x82\x86\x84\x41\x0f\x77\x77\x77\x2e\x65\x78\x61\x6d\x70\x6c\x65\x2e\x63\x6f\x6d",
+     b"\x82\x86\x84\xbe\x58\x08\x6e\x6f\x2d\x63\x61\x63\x68\x65",
+     b"\x82\x87\x85\xbf\x40\x0a\x63\x75\x73\x74\x6f\x6d\x2d\x6b\x65\x79\x0c\x63\x75\x73\x74"
+     b"\x6f\x6d\x2d\x76\x61\x6c\x75\x65"],
+    [b"\x82\x86\x84\x41\x8c\xf1\xe3\xc2\xe5\xf2\x3a\x6b\xa0\xab\x90\xf4\xff",
+     b"\x82\x86\x84\xbe\x58\x86\xa8\xeb\x10\x64\x9c\xbf",
+     b"\x82\x87\x85\xbf\x40\x88\x25\xa8\x49\xe9\x5b\xa9\x7d\x7f\x89\x25\xa8\x49\xe9\x5b\xb8\xe8\xb4\xbf"],
+]
+# response blocks of the same test with a 256-byte table (:309-331, including the disabled vectors)
+UNIT_RESPONSES_256 = [
+    [b"\x08\x03\x33\x30\x32\x58\x85\xae\xc3\x77\x1a\x4b\x61\x96\xd0\x7a\xbe\x94\x10"
+     b"\x54\xd4\x44\xa8\x20\x05\x95\x04\x0b\x81\x66\xe0\x82\xa6\x2d\x1b\xff\x6e\x91"
+     b"\x9d\x29\xad\x17\x18\x63\xc7\x8f\x0b\x97\xc8\xe9\xae\x82\xae\x43\xd3",
+     b"\x08\x03\x33\x30\x37\xc0\xbf\xbe"],
+    [b"\x48\x03\x33\x30\x37\xc1\xc0\xbf",
+     b"\x88\xc1\x61\x1d\x4d\x6f\x6e\x2c\x20\x32\x31\x20\x4f\x63\x74\x20\x32\x30\x31\x33\x20\x32\x30\x3a"
+     b"\x31\x33\x3a\x32\x32\x20\x47\x4d\x54\xc0\x5a\x04\x67\x7a\x69\x70\x77\x38\x66\x6f\x6f\x3d\x41\x53"
+     b"\x44\x4a\x4b\x48\x51\x4b\x42\x5a\x58\x4f\x51\x57\x45\x4f\x50\x49\x55\x41\x58\x51\x57\x45\x4f\x49"
+     b"\x55\x3b\x20\x6d\x61\x78\x2d\x61\x67\x65\x3d\x33\x36\x30\x30\x3b\x20\x76\x65\x72\x73\x69\x6f\x6e\x3d\x31"],
+]
+
+
+def soft_code(bits):
+    """what h2o_hpack_decode_header reports for a field's soft errors: its err_desc names the name
+    error when there is one (hpack.c:427-431): 1 name, 2 value only, 0 none"""
+    bits = np.asarray(bits)
+    return np.where(bits & 1, 1, np.where(bits & 2, 2, 0)).astype(np.uint8)
+
+
+def blocks_set(conns, table_size):
+    from h2o_amd import hpack_synth as HS
+
+    b = HS.pack_connections(conns, table_size)
+    r = O.ref().hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], table_size)
+    nb = len(b["blk_off"]) - 1
+    names, values, soft = [], [], []
+    for bi in range(nb):
+        s = int(b["blk_off"][bi])
+        for f in range(s, s + int(r["nfields"][bi])):
+            names.append(r["arena"][r["name_off"][f]:r["name_off"][f] + r["name_len"][f]].tobytes())
+            values.append(r["arena"][r["value_off"][f]:r["value_off"][f] + r["value_len"][f]].tobytes())
+            soft.append(r["fflags"][f])
+    nd, no = pack(names)
+    vd, vo = pack(values)
+    return dict(data=b["data"], blk_off=b["blk_off"], conn_first=b["conn_first"],
+                table_size=np.asarray([table_size], np.uint32), nfields=r["nfields"][:nb], bstatus=r["bstatus"][:nb],
+                fld_name=nd, fld_name_off=no, fld_value=vd, fld_value_off=vo, fld_soft=np.asarray(soft, np.uint8))
+
+
+def blocks_sets():
+    from h2o_amd import hpack_synth as HS
+
+    d = os.path.join(REF_ROOT, "fuzz", "http2-corpus")
+    corpus = []
+    for fn in sorted(os.listdir(d)):
+        blocks = header_blocks(open(os.path.join(d, fn), "rb").read())
+        if blocks:
+            corpus.append(blocks)
+    static_sweep = [[b"".join(HS.encode_int(i, 7, 0x80) for i in range(1, 62))]]
+    syn = HS.make_connections(2500, seed=21, adversarial_frac=0.25)
+    syn_conns = [[syn["data"][syn["blk_off"][k]:syn["blk_off"][k + 1]].tobytes()
+                  for k in range(syn["conn_first"][c], syn["conn_first"][c + 1])] for c in range(len(syn["conn_first"]) - 1)]
+    s256 = HS.make_connections(400, seed=22, table_size=256, adversarial_frac=0.25)
+    s256_conns = [[s256["data"][s256["blk_off"][k]:s256["blk_off"][k + 1]].tobytes()
+                   for k in range(s256["conn_first"][c], s256["conn_first"][c + 1])]
+                  for c in range(len(s256["conn_first"]) - 1)]
+    out = {"blocks": blocks_set(UNIT_REQUESTS + static_sweep + corpus + syn_conns, 4096),
+           "blocks_256": blocks_set(UNIT_RESPONSES_256 + s256_conns, 256)}
+    for k, v in out.items():
+        print("%-12s connections %5d  blocks %6d  fields %7d  errors %d" % (
+            k, len(v["conn_first"]) - 1, len(v["blk_off"]) - 1, int(v["nfields"].sum()), int((v["bstatus"] != 0).sum())))
+    return out
+
+
 def main():
+    if "--only-blocks" in sys.argv:
+        for name, arrays in blocks_sets().items():
+            np.savez_compressed(os.path.join(GOLDEN, name + ".npz"), **arrays)
+        return
     if not O.ref_available():
         sys.exit("oracle/_ref/libh2oref.so missing: run `make -C oracle` where /root/reference exists")
     os.makedirs(GOLDEN, exist_ok=True)
@@ -471,6 +558,7 @@ def main():
     sets["adversarial"] = adversarial_set()
     sets["framing"] = framing_set()
     sets["literals"] = literals_set()
+    sets.update(blocks_sets())
     for name, arrays in sets.items():
         path = os.path.join(GOLDEN, name + ".npz")
         np.savez_compressed(path, **arrays)

@@ -1,0 +1,301 @@
+/*
+ * ORACLE -- TEST INFRASTRUCTURE ONLY.  Clean-room CPU restatement of HPACK header-block decoding
+ * (SURVEY.md 8 f4): h2o_hpack_decode_header (lib/http2/hpack.c:319-435) applied field after field over
+ * each header block the way h2o_hpack_parse_request loops over it (hpack.c:513-527), with one dynamic
+ * table per connection (header_table_add :277-317, header_table_evict_one :263-275, size updates
+ * :352-366).  Strings go through decode_string's semantics (hpack.c:223-261), restated in
+ * huff_oracle.c.  Output contract: include/hhuff.h hhuff_hpack_decode_blocks.
+ */
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "huff_oracle.h"
+#include "huff_tables.h"
+
+#define ENTRY_OVERHEAD 32u /* HEADER_TABLE_ENTRY_SIZE_OFFSET, hpack.c:30 */
+#define STATIC_COUNT 61u   /* HEADER_TABLE_OFFSET - 1, hpack.c:27 */
+
+typedef struct {
+    uint8_t *name, *value;
+    uint32_t nlen, vlen;
+    unsigned soft;
+} orc_entry_t;
+
+typedef struct {
+    orc_entry_t *e; /* e[0] is the newest entry (dynamic index 62) */
+    uint32_t num, cap_entries;
+    uint64_t size, capacity, max_capacity;
+} orc_table_t;
+
+static void tbl_evict_one(orc_table_t *t)
+{
+    orc_entry_t *x = &t->e[--t->num];
+    t->size -= (uint64_t)x->nlen + x->vlen + ENTRY_OVERHEAD;
+    free(x->name);
+    free(x->value);
+    memset(x, 0, sizeof(*x));
+}
+
+/* header_table_add with max_num_entries = SIZE_MAX (hpack.c:413) */
+static void tbl_add(orc_table_t *t, const uint8_t *name, uint32_t nlen, const uint8_t *value, uint32_t vlen,
+                    unsigned soft)
+{
+    uint64_t add = (uint64_t)nlen + vlen + ENTRY_OVERHEAD;
+    while (t->num != 0 && t->size + add > t->capacity)
+        tbl_evict_one(t);
+    if (t->num == 0 && add > t->capacity)
+        return; /* does not fit an empty table: not added */
+    if (t->num == t->cap_entries) {
+        uint32_t nc = t->cap_entries ? 2 * t->cap_entries : 16;
+        t->e = (orc_entry_t *)realloc(t->e, nc * sizeof(orc_entry_t));
+        t->cap_entries = nc;
+    }
+    memmove(t->e + 1, t->e, t->num * sizeof(orc_entry_t));
+    orc_entry_t *x = &t->e[0];
+    x->name = (uint8_t *)malloc(nlen + 1);
+    x->value = (uint8_t *)malloc(vlen + 1);
+    memcpy(x->name, name, nlen);
+    memcpy(x->value, value, vlen);
+    x->nlen = nlen;
+    x->vlen = vlen;
+    x->soft = soft;
+    t->size += add;
+    ++t->num;
+}
+
+static void tbl_free(orc_table_t *t)
+{
+    while (t->num)
+        tbl_evict_one(t);
+    free(t->e);
+}
+
+typedef struct {
+    uint8_t *arena;
+    uint64_t cur, end;
+} orc_arena_t;
+
+enum { STR_OK = 0, STR_FAIL = 1, STR_UPPER = 2, STR_ARENA = 3 };
+
+/* decode_string (hpack.c:223-261) into the arena; *off / *len the decoded bytes */
+static int orc_block_string(const uint8_t **src, const uint8_t *end, int is_name, unsigned *soft, orc_arena_t *A,
+                            uint32_t *off, uint32_t *len)
+{
+    if (*src >= end)
+        return STR_FAIL;
+    int huff = (**src & 0x80) != 0;
+    int64_t n = orc_decode_int(src, end, 7);
+    if (n < 0 || n > end - *src)
+        return STR_FAIL;
+    if (huff) {
+        if (A->cur + ((uint64_t)n * 8u) / 5u > A->end)
+            return STR_ARENA;
+        size_t r = orc_decode_huffman((char *)A->arena + A->cur, soft, *src, (size_t)n, is_name);
+        if (r == SIZE_MAX)
+            return STR_FAIL;
+        *len = (uint32_t)r;
+    } else {
+        if (is_name) {
+            if ((n == 0 || **src != ':') && !orc_validate_header_name(soft, *src, (size_t)n))
+                return STR_UPPER;
+        } else {
+            orc_validate_header_value(soft, *src, (size_t)n);
+        }
+        if (A->cur + (uint64_t)n > A->end)
+            return STR_ARENA;
+        memcpy(A->arena + A->cur, *src, (size_t)n);
+        *len = (uint32_t)n;
+    }
+    *off = (uint32_t)A->cur;
+    A->cur += *len;
+    *src += n;
+    return STR_OK;
+}
+
+static int orc_block_copy(orc_arena_t *A, const uint8_t *s, uint32_t n, uint32_t *off)
+{
+    if (A->cur + n > A->end)
+        return STR_ARENA;
+    memcpy(A->arena + A->cur, s, n);
+    *off = (uint32_t)A->cur;
+    A->cur += n;
+    return STR_OK;
+}
+
+/* one field (h2o_hpack_decode_header, hpack.c:319-435): 0 / ORC_ERR_INVALID_CHAR = a field was
+ * produced; otherwise a hard error (ORC_ERR_COMPRESSION / ORC_ERR_PROTOCOL / ORC_BLK_ARENA) */
+static int orc_block_field(orc_table_t *t, const uint8_t **src, const uint8_t *end, orc_arena_t *A, uint32_t *noff,
+                           uint32_t *nlen, uint32_t *voff, uint32_t *vlen, unsigned *soft_out)
+{
+    int64_t index = 0;
+    int value_indexed = 0, do_index = 0;
+    for (;;) {
+        if (*src >= end)
+            return ORC_ERR_COMPRESSION;
+        uint8_t b = **src;
+        if (b >= 128) { /* indexed */
+            if ((index = orc_decode_int(src, end, 7)) <= 0)
+                return ORC_ERR_COMPRESSION;
+            value_indexed = 1;
+        } else if (b >= 64) { /* literal with incremental indexing */
+            if (b == 64)
+                ++*src;
+            else if ((index = orc_decode_int(src, end, 6)) <= 0)
+                return ORC_ERR_COMPRESSION;
+            do_index = 1;
+        } else if (b < 32) { /* literal without indexing / never indexed */
+            if ((b & 0xf) == 0)
+                ++*src;
+            else if ((index = orc_decode_int(src, end, 4)) <= 0)
+                return ORC_ERR_COMPRESSION;
+        } else { /* dynamic table size update */
+            int64_t cap = orc_decode_int(src, end, 5);
+            if (cap < 0 || (uint64_t)cap > t->max_capacity)
+                return ORC_ERR_COMPRESSION;
+            t->capacity = (uint64_t)cap;
+            while (t->num != 0 && t->size > t->capacity)
+                tbl_evict_one(t);
+            continue;
+        }
+        break;
+    }
+    unsigned soft = 0;
+    int r;
+    const orc_entry_t *ent = NULL;
+    if (index > 0) {
+        if ((uint64_t)index <= STATIC_COUNT) {
+            const char *n = orc_static_name[index];
+            if ((r = orc_block_copy(A, (const uint8_t *)n, (uint32_t)strlen(n), noff)) != STR_OK)
+                return ORC_BLK_ARENA;
+            *nlen = (uint32_t)strlen(n);
+            if (value_indexed) {
+                const char *v = orc_static_value[index];
+                if ((r = orc_block_copy(A, (const uint8_t *)v, (uint32_t)strlen(v), voff)) != STR_OK)
+                    return ORC_BLK_ARENA;
+                *vlen = (uint32_t)strlen(v);
+            }
+        } else if ((uint64_t)index - STATIC_COUNT - 1 < t->num) {
+            ent = &t->e[index - STATIC_COUNT - 1];
+            soft = ent->soft;
+            if (orc_block_copy(A, ent->name, ent->nlen, noff) != STR_OK)
+                return ORC_BLK_ARENA;
+            *nlen = ent->nlen;
+            if (value_indexed) {
+                if (orc_block_copy(A, ent->value, ent->vlen, voff) != STR_OK)
+                    return ORC_BLK_ARENA;
+                *vlen = ent->vlen;
+            }
+        } else {
+            return ORC_ERR_COMPRESSION;
+        }
+    } else {
+        r = orc_block_string(src, end, 1, &soft, A, noff, nlen);
+        if (r == STR_ARENA)
+            return ORC_BLK_ARENA;
+        if (r != STR_OK)
+            return r == STR_UPPER ? ORC_ERR_PROTOCOL : ORC_ERR_COMPRESSION;
+    }
+    if (!value_indexed) {
+        soft &= ~ORC_SOFT_VALUE;
+        r = orc_block_string(src, end, 0, &soft, A, voff, vlen);
+        if (r == STR_ARENA)
+            return ORC_BLK_ARENA;
+        if (r != STR_OK)
+            return ORC_ERR_COMPRESSION;
+    }
+    if (do_index)
+        tbl_add(t, A->arena + *noff, *nlen, A->arena + *voff, *vlen, soft);
+    *soft_out = soft;
+    return soft ? ORC_ERR_INVALID_CHAR : 0;
+}
+
+typedef struct {
+    const uint8_t *in;
+    const uint32_t *blk_off, *conn_first;
+    uint32_t c_begin, c_end, table_size;
+    uint8_t *arena;
+    const uint64_t *arena_off;
+    uint32_t *name_off, *name_len, *value_off, *value_len, *nfields;
+    uint8_t *fflags;
+    int32_t *bstatus;
+} orc_blk_job_t;
+
+static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
+{
+    orc_table_t t = {NULL, 0, 0, 0, j->table_size, j->table_size};
+    int failed = 0;
+    for (uint32_t b = j->conn_first[c]; b < j->conn_first[c + 1]; ++b) {
+        j->nfields[b] = 0;
+        if (failed) {
+            j->bstatus[b] = ORC_BLK_SKIPPED;
+            continue;
+        }
+        const uint8_t *p = j->in + j->blk_off[b], *end = j->in + j->blk_off[b + 1];
+        orc_arena_t A = {j->arena, j->arena_off[b], j->arena_off[b + 1]};
+        uint32_t nf = 0, slot = j->blk_off[b];
+        int st = 0;
+        while (p != end) {
+            uint32_t no = 0, nl = 0, vo = 0, vl = 0;
+            unsigned soft = 0;
+            int rc = orc_block_field(&t, &p, end, &A, &no, &nl, &vo, &vl, &soft);
+            if (rc != 0 && rc != ORC_ERR_INVALID_CHAR) {
+                st = rc;
+                break;
+            }
+            j->name_off[slot + nf] = no;
+            j->name_len[slot + nf] = nl;
+            j->value_off[slot + nf] = vo;
+            j->value_len[slot + nf] = vl;
+            j->fflags[slot + nf] = (uint8_t)soft;
+            ++nf;
+        }
+        j->nfields[b] = nf;
+        j->bstatus[b] = st;
+        failed = st != 0;
+    }
+    tbl_free(&t);
+}
+
+static void *orc_blk_worker(void *arg)
+{
+    const orc_blk_job_t *j = (const orc_blk_job_t *)arg;
+    for (uint32_t c = j->c_begin; c < j->c_end; ++c)
+        orc_hpack_connection(j, c);
+    return NULL;
+}
+
+int orc_hpack_decode_blocks(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
+                            uint32_t table_size, uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off,
+                            uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,
+                            uint32_t *nfields, int32_t *bstatus, int nthreads)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if ((uint32_t)nthreads > nconn)
+        nthreads = nconn ? (int)nconn : 1;
+    orc_blk_job_t *jobs = (orc_blk_job_t *)calloc((size_t)nthreads, sizeof(*jobs));
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(*th));
+    if (!jobs || !th) {
+        free(jobs);
+        free(th);
+        return -1;
+    }
+    for (int k = 0; k < nthreads; ++k) {
+        orc_blk_job_t *j = &jobs[k];
+        j->in = in, j->blk_off = blk_off, j->conn_first = conn_first, j->table_size = table_size;
+        j->arena = arena, j->arena_off = arena_off, j->name_off = name_off, j->name_len = name_len;
+        j->value_off = value_off, j->value_len = value_len, j->fflags = fflags, j->nfields = nfields;
+        j->bstatus = bstatus;
+        j->c_begin = (uint32_t)(((uint64_t)nconn * k) / nthreads);
+        j->c_end = (uint32_t)(((uint64_t)nconn * (k + 1)) / nthreads);
+    }
+    for (int k = 1; k < nthreads; ++k)
+        pthread_create(&th[k], NULL, orc_blk_worker, &jobs[k]);
+    orc_blk_worker(&jobs[0]);
+    for (int k = 1; k < nthreads; ++k)
+        pthread_join(th[k], NULL);
+    free(jobs);
+    free(th);
+    return 0;
+}

@@ -222,6 +222,9 @@ static void orc_validate_value(unsigned *soft, const uint8_t *s, size_t len)
         *soft |= ORC_SOFT_VALUE;
 }
 
+int orc_validate_header_name(unsigned *soft, const uint8_t *s, size_t len) { return orc_validate_name(soft, s, len); }
+void orc_validate_header_value(unsigned *soft, const uint8_t *s, size_t len) { orc_validate_value(soft, s, len); }
+
 /* QPACK raw names skip validation when h2o_lookup_token finds them (qpack.c:585); the only tokens
  * the validator would flag are the pseudo-header names (lib/common/token_table.h) */
 static int orc_is_pseudo_token(const uint8_t *s, size_t len)

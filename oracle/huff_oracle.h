@@ -18,6 +18,12 @@
 #define ORC_LIT_UPPERCASE 5
 #define ORC_LIT_TOO_LONG 6
 #define ORC_STATUS_FAIL 0x80u
+/* header blocks (f4): h2o return codes (include/h2o/http2_common.h:41, :49, :55) and the batch's own */
+#define ORC_ERR_PROTOCOL (-1)
+#define ORC_ERR_COMPRESSION (-9)
+#define ORC_ERR_INVALID_CHAR (-254)
+#define ORC_BLK_ARENA (-300)   /* HHUFF_BLK_ARENA: the block's arena slice is too small */
+#define ORC_BLK_SKIPPED (-301) /* HHUFF_BLK_SKIPPED: an earlier block of the connection failed */
 
 size_t orc_decode_huffman(char *dst, unsigned *soft_errors, const uint8_t *src, size_t len, int is_name);
 size_t orc_encode_huffman(uint8_t *dst, const uint8_t *src, size_t len);
@@ -40,3 +46,11 @@ int orc_decode_literal(const uint8_t *lit, const uint8_t *end, unsigned prefix_b
 int orc_literals_batch(const uint8_t *in, const uint32_t *lit_off, const uint32_t *lit_end, uint32_t n,
                        unsigned prefix_bits, unsigned flags, const uint32_t *is_name_bits, uint8_t *out,
                        uint32_t *out_len, uint32_t *pay_off, uint32_t *consumed, uint8_t *status, int nthreads);
+
+/* raw-literal validators (h2o_hpack_validate_header_name / _value, hpack.c:163-221) */
+int orc_validate_header_name(unsigned *soft, const uint8_t *s, size_t len);
+void orc_validate_header_value(unsigned *soft, const uint8_t *s, size_t len);
+int orc_hpack_decode_blocks(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
+                            uint32_t table_size, uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off,
+                            uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,
+                            uint32_t *nfields, int32_t *bstatus, int nthreads);

@@ -65,6 +65,10 @@ class _Codec:
             f = getattr(L, P + "_" + name)
             f.restype = ctypes.c_int
             f.argtypes = [_u8p, _u32p, _u32p, ctypes.c_uint32] + extra
+        f = getattr(L, P + "_hpack_decode_blocks")
+        f.restype = ctypes.c_int
+        f.argtypes = [_u8p, _u32p, _u32p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.POINTER(ctypes.c_uint64),
+                      _u32p, _u32p, _u32p, _u32p, _u8p, _u32p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
         f = getattr(L, P + "_literals_batch")
         f.restype = ctypes.c_int
         f.argtypes = [_u8p, _u32p, _u32p, ctypes.c_uint32, ctypes.c_uint, ctypes.c_uint, _u32p, _u8p, _u32p, _u32p,
@@ -170,6 +174,42 @@ class _Codec:
             _ptr(consumed, _u32p), _ptr(status, _u8p), nthreads)
         assert rc == 0
         return out, out_len, pay_off, consumed, status
+
+
+    def hpack_decode_blocks(self, data, blk_off, conn_first, table_size=4096, arena_off=None, nthreads=1):
+        """HPACK header blocks (include/hhuff.h hhuff_hpack_decode_blocks contract) -> dict of arrays:
+        arena, name_off, name_len, value_off, value_len, fflags (per field slot), nfields, bstatus (per block)"""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        blk_off = np.ascontiguousarray(blk_off, dtype=np.uint32)
+        conn_first = np.ascontiguousarray(conn_first, dtype=np.uint32)
+        nb = blk_off.size - 1
+        if arena_off is None:
+            arena_off = default_arena_off(blk_off, table_size)
+        arena_off = np.ascontiguousarray(arena_off, dtype=np.uint64)
+        nslots = max(1, int(blk_off[-1]))
+        r = dict(arena=np.zeros(max(1, int(arena_off[-1])), np.uint8),
+                 name_off=np.zeros(nslots, np.uint32), name_len=np.zeros(nslots, np.uint32),
+                 value_off=np.zeros(nslots, np.uint32), value_len=np.zeros(nslots, np.uint32),
+                 fflags=np.zeros(nslots, np.uint8), nfields=np.zeros(max(1, nb), np.uint32),
+                 bstatus=np.zeros(max(1, nb), np.int32))
+        rc = getattr(self.lib, self.prefix + "_hpack_decode_blocks")(
+            _ptr(data, _u8p), _ptr(blk_off, _u32p), _ptr(conn_first, _u32p), conn_first.size - 1, table_size,
+            _ptr(r["arena"], _u8p), arena_off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+            _ptr(r["name_off"], _u32p), _ptr(r["name_len"], _u32p), _ptr(r["value_off"], _u32p),
+            _ptr(r["value_len"], _u32p), _ptr(r["fflags"], _u8p), _ptr(r["nfields"], _u32p),
+            r["bstatus"].ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), nthreads)
+        assert rc == 0
+        return r
+
+
+def default_arena_off(blk_off, table_size=4096):
+    """A block of L bytes produces at most L fields; each field's name + value is at most 8/5 of its
+    literal bytes or a copy of one table entry (<= table_size bytes): a generous bound per block."""
+    L = np.diff(np.asarray(blk_off, dtype=np.uint64))
+    cap = (L * 8) // 5 + (L // 4 + 1) * np.uint64(table_size + 64)  # = h2o_amd.codec.default_arena_off
+    out = np.zeros(L.size + 1, np.uint64)
+    out[1:] = np.cumsum(cap)
+    return out
 
 
 _oracle = None

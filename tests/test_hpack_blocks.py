@@ -1,0 +1,175 @@
+"""HPACK header blocks: h2o_hpack_decode_header over whole blocks with a dynamic table per
+connection.  CPU: the restatement (oracle/hpack_block.c) against the reference's outputs (tests/golden/
+blocks*.npz, written by oracle/gen_golden.py from h2o's own decoder) and, where oracle/_ref exists, against
+the reference directly on fresh synthetic connections.  GPU: hhuff_hpack_decode_blocks through the C-ABI
+against the same fixtures (bit-exact names, values, soft-error codes, field counts, block statuses) and
+against the restatement field by field (arena offsets and full soft bits included)."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from h2o_amd import hpack_synth as HS
+
+BLOCK_SETS = ["blocks", "blocks_256"]
+
+
+def soft_code(bits):
+    """the reference reports one soft error per field (err_desc, hpack.c:427-431): name first"""
+    bits = np.asarray(bits)
+    return np.where(bits & 1, 1, np.where(bits & 2, 2, 0)).astype(np.uint8)
+
+
+def fields_of(res, blk_off, nblk):
+    """-> (names, values, soft bits) of every decoded field, in block order"""
+    names, values, soft = [], [], []
+    a = res["arena"]
+    for b in range(nblk):
+        s = int(blk_off[b])
+        for f in range(s, s + int(res["nfields"][b])):
+            no, nl, vo, vl = (int(res[k][f]) for k in ("name_off", "name_len", "value_off", "value_len"))
+            names.append(a[no:no + nl].tobytes())
+            values.append(a[vo:vo + vl].tobytes())
+            soft.append(int(res["fflags"][f]))
+    return names, values, np.asarray(soft, np.uint8)
+
+
+def expected_fields(g):
+    n = len(g["fld_name_off"]) - 1
+    names = [g["fld_name"][g["fld_name_off"][i]:g["fld_name_off"][i + 1]].tobytes() for i in range(n)]
+    values = [g["fld_value"][g["fld_value_off"][i]:g["fld_value_off"][i + 1]].tobytes() for i in range(n)]
+    return names, values, g["fld_soft"]
+
+
+def check_against_golden(res, g):
+    nblk = len(g["blk_off"]) - 1
+    np.testing.assert_array_equal(np.asarray(res["nfields"][:nblk], np.uint32), g["nfields"])
+    np.testing.assert_array_equal(np.asarray(res["bstatus"][:nblk], np.int32), g["bstatus"])
+    names, values, soft = fields_of(res, g["blk_off"], nblk)
+    en, ev, es = expected_fields(g)
+    assert names == en
+    assert values == ev
+    np.testing.assert_array_equal(soft_code(soft), es)
+
+
+@pytest.mark.parametrize("name", BLOCK_SETS)
+def test_restatement_matches_reference_fixtures(oracle_codec, name):
+    g = load_golden(name)
+    res = oracle_codec.hpack_decode_blocks(g["data"], g["blk_off"], g["conn_first"], int(g["table_size"][0]),
+                                           nthreads=8)
+    check_against_golden(res, g)
+
+
+def test_fixtures_cover_the_paths():
+    g = load_golden("blocks")
+    st = set(int(x) for x in g["bstatus"])
+    assert {0, -9, -1, -301} <= st  # ok, COMPRESSION, PROTOCOL, skipped after an error
+    assert (g["fld_soft"] == 1).any() and (g["fld_soft"] == 2).any()
+    assert int(g["nfields"].sum()) > 100000
+    # the static-table sweep: indices 1..61 decode to RFC 7541 Appendix A (checked by the reference)
+    en, ev, _ = expected_fields(g)
+    from h2o_amd import tables
+
+    k = int(g["nfields"][:6].sum())  # 6 request blocks of the unit test come first, then the sweep
+    assert list(zip(en[k:k + 61], ev[k:k + 61])) == list(tables.STATIC_TABLE)
+
+
+def test_restatement_matches_compiled_reference_on_fresh_connections():
+    from oracle import oracle as O
+
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    for seed, ts in ((31, 4096), (32, 256), (33, 0), (34, 65536)):
+        b = HS.make_connections(600, seed=seed, table_size=ts, adversarial_frac=0.3)
+        ro = O.oracle().hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], ts)
+        rr = O.ref().hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], ts)
+        nblk = len(b["blk_off"]) - 1
+        np.testing.assert_array_equal(ro["nfields"][:nblk], rr["nfields"][:nblk])
+        np.testing.assert_array_equal(ro["bstatus"][:nblk], rr["bstatus"][:nblk])
+        a, b2 = fields_of(ro, b["blk_off"], nblk), fields_of(rr, b["blk_off"], nblk)
+        assert a[0] == b2[0] and a[1] == b2[1]
+        np.testing.assert_array_equal(soft_code(a[2]), b2[2])
+
+
+# ---------------------------------------------------------------------------------------------------
+# GPU
+# ---------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def gpu_blocks(torch, data, blk_off, conn_first, table_size, arena_off=None):
+    from h2o_amd import codec
+
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
+    d = dev(data if data.size else np.zeros(1, np.uint8))
+    ao = None if arena_off is None else dev(np.asarray(arena_off, np.uint64).view(np.int64))
+    r = codec.hpack_decode_blocks(d, dev(blk_off.view(np.int32)), dev(conn_first.view(np.int32)), table_size,
+                                  arena_off=ao, in_size=int(data.size))
+    torch.cuda.synchronize()
+    out = {}
+    for k, v in r.items():
+        if k == "scratch":
+            continue
+        a = v.cpu().numpy()
+        out[k] = a.view(np.uint32) if k in ("name_off", "name_len", "value_off", "value_len", "nfields") else a
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", BLOCK_SETS)
+def test_gpu_matches_reference_fixtures(torch_cuda, name):
+    g = load_golden(name)
+    res = gpu_blocks(torch_cuda, g["data"], g["blk_off"], g["conn_first"], int(g["table_size"][0]))
+    check_against_golden(res, g)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,table_size", [(41, 4096), (42, 256), (43, 0), (44, 65536)])
+def test_gpu_matches_restatement_field_by_field(torch_cuda, oracle_codec, seed, table_size):
+    b = HS.make_connections(3000, seed=seed, table_size=table_size, adversarial_frac=0.3)
+    ro = oracle_codec.hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], table_size, nthreads=8)
+    rg = gpu_blocks(torch_cuda, b["data"], b["blk_off"], b["conn_first"], table_size)
+    nblk = len(b["blk_off"]) - 1
+    np.testing.assert_array_equal(rg["nfields"][:nblk], ro["nfields"][:nblk])
+    np.testing.assert_array_equal(rg["bstatus"][:nblk], ro["bstatus"][:nblk])
+    for b_ in range(nblk):  # same arena offsets, lengths and full soft bits in every used slot
+        s, n = int(b["blk_off"][b_]), int(ro["nfields"][b_])
+        for k in ("name_off", "name_len", "value_off", "value_len", "fflags"):
+            np.testing.assert_array_equal(rg[k][s:s + n], ro[k][s:s + n], err_msg="%s block %d" % (k, b_))
+    ga, oa = fields_of(rg, b["blk_off"], nblk), fields_of(ro, b["blk_off"], nblk)
+    assert ga[0] == oa[0] and ga[1] == oa[1]
+
+
+@pytest.mark.gpu
+def test_gpu_arena_limit_matches_restatement(torch_cuda, oracle_codec):
+    """tight arena slices: HHUFF_BLK_ARENA exactly where the restatement reports it"""
+    b = HS.make_connections(800, seed=45, adversarial_frac=0.1)
+    L = np.diff(b["blk_off"].astype(np.uint64))
+    rng = np.random.default_rng(46)
+    cap = (L * rng.uniform(0.3, 1.6, size=L.size)).astype(np.uint64)
+    ao = np.zeros(L.size + 1, np.uint64)
+    ao[1:] = np.cumsum(cap)
+    ro = oracle_codec.hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], 4096, arena_off=ao)
+    rg = gpu_blocks(torch_cuda, b["data"], b["blk_off"], b["conn_first"], 4096, arena_off=ao)
+    nblk = L.size
+    assert (ro["bstatus"][:nblk] == -300).any()
+    np.testing.assert_array_equal(rg["bstatus"][:nblk], ro["bstatus"][:nblk])
+    np.testing.assert_array_equal(rg["nfields"][:nblk], ro["nfields"][:nblk])
+    ga, oa = fields_of(rg, b["blk_off"], nblk), fields_of(ro, b["blk_off"], nblk)
+    assert ga[0] == oa[0] and ga[1] == oa[1]
+    np.testing.assert_array_equal(ga[2], oa[2])
+
+
+@pytest.mark.gpu
+def test_gpu_empty_and_degenerate_batches(torch_cuda, oracle_codec):
+    conns = [[], [b""], [b"\x82", b""], [b"\x20"], [b"\x3f\xe1\x1f"], [b"\x80"], [b"\xbe"]]
+    b = HS.pack_connections(conns)
+    ro = oracle_codec.hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], 4096)
+    rg = gpu_blocks(torch_cuda, b["data"], b["blk_off"], b["conn_first"], 4096)
+    nblk = len(b["blk_off"]) - 1
+    np.testing.assert_array_equal(rg["bstatus"][:nblk], ro["bstatus"][:nblk])
+    np.testing.assert_array_equal(rg["nfields"][:nblk], ro["nfields"][:nblk])

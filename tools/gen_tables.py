@@ -52,6 +52,37 @@ F_UPPER = 32
 
 LUT_BITS = 13  # GPU decode window
 
+# RFC 7541 Appendix A static table (index 1..61): (name, value).  The reference holds the same table in
+# lib/common/token_table.h (h2o_hpack_static_table); tests/test_hpack_blocks.py checks every index
+# against the reference's decoding of it.
+STATIC_TABLE = [
+    (":authority", ""), (":method", "GET"), (":method", "POST"), (":path", "/"), (":path", "/index.html"),
+    (":scheme", "http"), (":scheme", "https"), (":status", "200"), (":status", "204"), (":status", "206"),
+    (":status", "304"), (":status", "400"), (":status", "404"), (":status", "500"), ("accept-charset", ""),
+    ("accept-encoding", "gzip, deflate"), ("accept-language", ""), ("accept-ranges", ""), ("accept", ""),
+    ("access-control-allow-origin", ""), ("age", ""), ("allow", ""), ("authorization", ""),
+    ("cache-control", ""), ("content-disposition", ""), ("content-encoding", ""), ("content-language", ""),
+    ("content-length", ""), ("content-location", ""), ("content-range", ""), ("content-type", ""),
+    ("cookie", ""), ("date", ""), ("etag", ""), ("expect", ""), ("expires", ""), ("from", ""), ("host", ""),
+    ("if-match", ""), ("if-modified-since", ""), ("if-none-match", ""), ("if-range", ""),
+    ("if-unmodified-since", ""), ("last-modified", ""), ("link", ""), ("location", ""), ("max-forwards", ""),
+    ("proxy-authenticate", ""), ("proxy-authorization", ""), ("range", ""), ("referer", ""), ("refresh", ""),
+    ("retry-after", ""), ("server", ""), ("set-cookie", ""), ("strict-transport-security", ""),
+    ("transfer-encoding", ""), ("user-agent", ""), ("vary", ""), ("via", ""), ("www-authenticate", ""),
+]
+assert len(STATIC_TABLE) == 61
+
+
+def static_arrays():
+    """-> (bytes of all names and values back to back, [name_off, name_len, value_off, value_len] * 61)"""
+    blob, ent = bytearray(), []
+    for n, v in STATIC_TABLE:
+        ent += [len(blob), len(n)]
+        blob += n.encode()
+        ent += [len(blob), len(v)]
+        blob += v.encode()
+    return bytes(blob), ent
+
 
 def code_lengths():
     lens = [ord(c) - ord("A") + 5 for c in _RFC7541_LENGTHS]
@@ -320,6 +351,15 @@ def product_header(lens, codes, order, lut, longt):
     out.append("#define HHUFF_NAME_INVALID_INIT { %s }" % ", ".join("0x%08xu" % w for w in name_inv))
     out.append("#define HHUFF_VALUE_INVALID_INIT { %s }" % ", ".join("0x%08xu" % w for w in value_inv))
     out.append("")
+    blob, ent = static_arrays()
+    out.append("/* RFC 7541 Appendix A static table: names and values back to back, and per index 1..61")
+    out.append(" * {name_off, name_len, value_off, value_len} into them */")
+    out.append("#define HHUFF_STATIC_NBYTES %d" % len(blob))
+    out.append("#define HHUFF_STATIC_BYTES_INIT { \\")
+    out.append(fmt_array(list(blob), 24, "{}").replace("\n", " \\\n") + " \\\n}")
+    out.append("#define HHUFF_STATIC_ENT_INIT { \\")
+    out.append(fmt_array(ent, 16, "{}").replace("\n", " \\\n") + " \\\n}")
+    out.append("")
     return "\n".join(out)
 
 
@@ -351,6 +391,12 @@ def oracle_header(lens, codes, fsm):
         out.append("    {" + ", ".join("0x%06x" % v for v in row) + "},")
     out.append("};")
     out.append("")
+    out.append("/* RFC 7541 Appendix A static table, indices 1..61 (entry 0 unused) */")
+    out.append("static const char *const orc_static_name[62] = {\"\",")
+    out.append(",\n".join('    "%s"' % n for n, _ in STATIC_TABLE) + "};")
+    out.append("static const char *const orc_static_value[62] = {\"\",")
+    out.append(",\n".join('    "%s"' % v for _, v in STATIC_TABLE) + "};")
+    out.append("")
     return "\n".join(out)
 
 
@@ -362,6 +408,7 @@ def python_module(lens, codes):
         '"""',
         "ENC_CODE = (%s)" % ", ".join(str(c) for c in codes[:256]),
         "ENC_NBITS = (%s)" % ", ".join(str(l) for l in lens[:256]),
+        "STATIC_TABLE = %r" % (tuple((n.encode(), v.encode()) for n, v in STATIC_TABLE),),
         "EOS_CODE = %d" % codes[EOS],
         "EOS_NBITS = %d" % lens[EOS],
         "NAME_VALID = frozenset((%s))" % ", ".join(str(c) for c in sorted(NAME_VALID)),
