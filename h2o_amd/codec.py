@@ -69,7 +69,8 @@ def lib():
         L.hhuff_hpack_scratch_size.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         L.hhuff_hpack_decode_blocks.restype = ctypes.c_int
         L.hhuff_hpack_decode_blocks.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp,
-                                                _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64, _vp]
+                                                _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64,
+                                                ctypes.c_uint, _vp]
         L.hhuff_version.restype = ctypes.c_char_p
         L.hhuff_last_error_string.restype = ctypes.c_char_p
         L.hhuff_grid_size.restype = ctypes.c_int
@@ -233,7 +234,11 @@ def default_arena_off(blk_off, table_size=4096):
     return out
 
 
-def hpack_decode_blocks(data, blk_off, conn_first, table_size=4096, arena_off=None, in_size=None, stream=None):
+BLK_CONTINUE = 1
+
+
+def hpack_decode_blocks(data, blk_off, conn_first, table_size=4096, arena_off=None, in_size=None, stream=None,
+                        scratch=None, cont=False):
     """HPACK header blocks (include/hhuff.h hhuff_hpack_decode_blocks) on device tensors: blk_off / conn_first
     int32 tensors (u32 bits), arena_off int64.  Returns a dict of device tensors: arena, name_off, name_len,
     value_off, value_len, fflags (per field slot), nfields, bstatus (per block)."""
@@ -255,11 +260,13 @@ def hpack_decode_blocks(data, blk_off, conn_first, table_size=4096, arena_off=No
              nfields=torch.empty(max(1, nblk), dtype=torch.int32, device=dev),
              bstatus=torch.empty(max(1, nblk), dtype=torch.int32, device=dev))
     ss = int(lib().hhuff_hpack_scratch_size(nconn, table_size))
-    scratch = torch.empty(max(16, ss), dtype=torch.uint8, device=dev)
+    if scratch is None:  # pass the previous call's r["scratch"] back with cont=True to carry the tables over
+        scratch = torch.empty(max(16, ss), dtype=torch.uint8, device=dev)
     _check(lib().hhuff_hpack_decode_blocks(_dp(data), in_size, _dp(blk_off), _dp(conn_first), nconn, table_size,
                                            _dp(r["arena"]), _dp(arena_off), _dp(r["name_off"]), _dp(r["name_len"]),
                                            _dp(r["value_off"]), _dp(r["value_len"]), _dp(r["fflags"]), _dp(r["nfields"]),
-                                           _dp(r["bstatus"]), _dp(scratch), scratch.numel(), _stream(stream)),
+                                           _dp(r["bstatus"]), _dp(scratch), scratch.numel(),
+                                           BLK_CONTINUE if cont else 0, _stream(stream)),
            "hhuff_hpack_decode_blocks")
     r["scratch"] = scratch  # keep alive until the stream has run the launch
     return r

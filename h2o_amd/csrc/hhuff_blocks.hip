@@ -52,6 +52,13 @@ struct BlkArgs {
     int32_t* bstatus;
     uint8_t* scratch;
     uint64_t conn_scratch;  // bytes of scratch per connection
+    uint32_t flags;         // HHUFF_BLK_CONTINUE: start from the tables the previous call left in scratch
+};
+
+// per-connection scratch: [TableState 32 B][byte ring, table_size rounded to 16][entry ring]
+struct TableState {
+    uint32_t start, num, whead, failed;
+    uint64_t size, cap;
 };
 
 // h2o_hpack_decode_int (hpack.c:52-83) at in[*p], bounded by end
@@ -284,9 +291,20 @@ __global__ __launch_bounds__(256) void hpack_blocks_kernel(BlkArgs A) {
     const uint32_t R = A.table_size, E = A.table_size / kEntryOverhead + 1;
     for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < A.nconn; c += (uint64_t)gridDim.x * blockDim.x) {
         uint8_t* scr = A.scratch + c * A.conn_scratch;
-        DynTable t{scr, reinterpret_cast<uint4*>(scr + ((R + 15u) & ~15u)), R, E, 0u, 0u, 0u, 0u, A.table_size,
+        TableState* ts = reinterpret_cast<TableState*>(scr);
+        uint8_t* ring = scr + sizeof(TableState);
+        DynTable t{ring, reinterpret_cast<uint4*>(ring + ((R + 15u) & ~15u)), R, E, 0u, 0u, 0u, 0u, A.table_size,
                    A.table_size};
         bool failed = false;
+        if (A.flags & HHUFF_BLK_CONTINUE) {
+            const TableState s0 = *ts;
+            t.start = s0.start;
+            t.num = s0.num;
+            t.whead = s0.whead;
+            t.size = s0.size;
+            t.cap = s0.cap;
+            failed = s0.failed != 0;
+        }
         for (uint32_t b = A.conn_first[c]; b < A.conn_first[c + 1]; ++b) {
             A.nfields[b] = 0;
             if (failed) {
@@ -318,21 +336,23 @@ __global__ __launch_bounds__(256) void hpack_blocks_kernel(BlkArgs A) {
             A.bstatus[b] = st;
             failed = st != 0;
         }
+        *ts = TableState{t.start, t.num, t.whead, failed ? 1u : 0u, t.size, t.cap};
     }
 }
 
 uint64_t hpack_conn_scratch(uint32_t table_size) {
     const uint64_t R = ((uint64_t)table_size + 15u) & ~15ull;
-    return R + 16ull * (table_size / kEntryOverhead + 1u);
+    return sizeof(TableState) + R + 16ull * (table_size / kEntryOverhead + 1u);
 }
 
 hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off, const uint32_t* conn_first,
                                uint32_t nconn, uint32_t table_size, uint8_t* arena, const uint64_t* arena_off,
                                uint32_t* name_off, uint32_t* name_len, uint32_t* value_off, uint32_t* value_len,
-                               uint8_t* fflags, uint32_t* nfields, int32_t* bstatus, uint8_t* scratch, hipStream_t stream) {
+                               uint8_t* fflags, uint32_t* nfields, int32_t* bstatus, uint8_t* scratch, uint32_t flags,
+                               hipStream_t stream) {
     if (nconn == 0) return hipSuccess;
     BlkArgs A{in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len, value_off,
-              value_len, fflags, nfields, bstatus, scratch, hpack_conn_scratch(table_size)};
+              value_len, fflags, nfields, bstatus, scratch, hpack_conn_scratch(table_size), flags};
     const uint32_t blocks = min((nconn + 255u) / 256u, 65535u);
     hipLaunchKernelGGL(hpack_blocks_kernel, dim3(blocks), dim3(256), 0, stream, A);
     return hipGetLastError();

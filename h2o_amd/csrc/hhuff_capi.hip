@@ -161,7 +161,8 @@ HHUFF_API int hhuff_hpack_decode_blocks(const uint8_t* in, uint64_t in_size, con
                                         const uint32_t* conn_first, uint32_t nconn, uint32_t table_size, uint8_t* arena,
                                         const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len,
                                         uint32_t* value_off, uint32_t* value_len, uint8_t* fflags, uint32_t* nfields,
-                                        int32_t* bstatus, void* scratch, uint64_t scratch_size, void* stream) {
+                                        int32_t* bstatus, void* scratch, uint64_t scratch_size, unsigned flags,
+                                        void* stream) {
     if (nconn == 0) return HHUFF_OK;
     if (!in || !blk_off || !conn_first || !arena || !arena_off || !name_off || !name_len || !value_off || !value_len ||
         !fflags || !nfields || !bstatus || !scratch)
@@ -170,7 +171,7 @@ HHUFF_API int hhuff_hpack_decode_blocks(const uint8_t* in, uint64_t in_size, con
     if (((uintptr_t)scratch & 15u) != 0) return arg_fail("scratch must be 16-byte aligned");
     hipError_t e = hhuff::launch_hpack_blocks(in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off,
                                               name_len, value_off, value_len, fflags, nfields, bstatus,
-                                              (uint8_t*)scratch, (hipStream_t)stream);
+                                              (uint8_t*)scratch, flags, (hipStream_t)stream);
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "hpack block launch");
 }
 

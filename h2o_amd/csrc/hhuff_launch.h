@@ -26,6 +26,7 @@ uint64_t hpack_conn_scratch(uint32_t table_size);
 hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off, const uint32_t* conn_first,
                                uint32_t nconn, uint32_t table_size, uint8_t* arena, const uint64_t* arena_off,
                                uint32_t* name_off, uint32_t* name_len, uint32_t* value_off, uint32_t* value_len,
-                               uint8_t* fflags, uint32_t* nfields, int32_t* bstatus, uint8_t* scratch, hipStream_t stream);
+                               uint8_t* fflags, uint32_t* nfields, int32_t* bstatus, uint8_t* scratch, uint32_t flags,
+                               hipStream_t stream);
 int grid_size(int device, int which);
 }  // namespace hhuff

@@ -152,7 +152,11 @@ int hhuff_decode_literals(const uint8_t *in, uint64_t in_size, const uint32_t *l
  *      floor(8 len / 5) bytes free, a raw one len, an indexed one its size), or HHUFF_BLK_SKIPPED (an
  *      earlier block of the connection failed: h2o drops the connection).  Fields before the error stand.
  *      Device arrays; scratch = device memory of hhuff_hpack_scratch_size(nconn, table_size) bytes (the
- *      dynamic tables); asynchronous on `stream`. */
+ *      dynamic tables, 16-byte aligned), kept by the caller between calls for HHUFF_BLK_CONTINUE;
+ *      asynchronous on `stream`. */
+#define HHUFF_BLK_CONTINUE 1u /* flags: the tables (and failed state) the previous call left in scratch
+                                 carry over -- connection c of this call is connection c of that one; without
+                                 it every connection starts with an empty table */
 #define HHUFF_BLK_ARENA (-300)
 #define HHUFF_BLK_SKIPPED (-301)
 uint64_t hhuff_hpack_scratch_size(uint32_t nconn, uint32_t table_size);
@@ -160,7 +164,7 @@ int hhuff_hpack_decode_blocks(const uint8_t *in, uint64_t in_size, const uint32_
                               uint32_t nconn, uint32_t table_size, uint8_t *arena, const uint64_t *arena_off,
                               uint32_t *name_off, uint32_t *name_len, uint32_t *value_off, uint32_t *value_len,
                               uint8_t *fflags, uint32_t *nfields, int32_t *bstatus, void *scratch, uint64_t scratch_size,
-                              void *stream);
+                              unsigned flags, void *stream);
 
 /* (3b) Pipelined host path (the socket-buffer -> pinned -> device -> pinned -> pool staging of
  *     SURVEY f3; replaces the caller-side copies around lib/http2/hpack.c:240-241).  Contiguous layout

@@ -173,3 +173,65 @@ def test_gpu_empty_and_degenerate_batches(torch_cuda, oracle_codec):
     nblk = len(b["blk_off"]) - 1
     np.testing.assert_array_equal(rg["bstatus"][:nblk], ro["bstatus"][:nblk])
     np.testing.assert_array_equal(rg["nfields"][:nblk], ro["nfields"][:nblk])
+
+
+@pytest.mark.gpu
+def test_gpu_tables_carry_over_between_calls(torch_cuda, oracle_codec):
+    """HHUFF_BLK_CONTINUE: each connection's blocks split over two calls sharing the scratch decode exactly
+    like one call over all of them (dynamic tables and the failed state persist)"""
+    from h2o_amd import codec
+
+    b = HS.make_connections(2000, seed=47, adversarial_frac=0.2)
+    conns = [[b["data"][b["blk_off"][k]:b["blk_off"][k + 1]].tobytes()
+              for k in range(b["conn_first"][c], b["conn_first"][c + 1])] for c in range(len(b["conn_first"]) - 1)]
+    first = HS.pack_connections([cb[:len(cb) // 2] for cb in conns])
+    second = HS.pack_connections([cb[len(cb) // 2:] for cb in conns])
+    ro = oracle_codec.hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], 4096)
+    want = fields_of(ro, b["blk_off"], len(b["blk_off"]) - 1)
+    torch = torch_cuda
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
+    got, st, nf = ([], [], []), [], []
+    scratch = None
+    for part, cont in ((first, False), (second, True)):
+        r = codec.hpack_decode_blocks(dev(part["data"] if part["data"].size else np.zeros(1, np.uint8)),
+                                      dev(part["blk_off"].view(np.int32)), dev(part["conn_first"].view(np.int32)),
+                                      4096, in_size=int(part["data"].size), scratch=scratch, cont=cont)
+        torch.cuda.synchronize()
+        scratch = r["scratch"]
+        h = {k: v.cpu().numpy() for k, v in r.items() if k != "scratch"}
+        for k in ("name_off", "name_len", "value_off", "value_len", "nfields"):
+            h[k] = h[k].view(np.uint32)
+        nb = len(part["blk_off"]) - 1
+        st.append((part, h["bstatus"][:nb], h["nfields"][:nb]))
+        f = fields_of(h, part["blk_off"], nb)
+        got[0].extend(f[0])
+        got[1].extend(f[1])
+    # reassemble per connection in the original block order and compare statuses and fields
+    exp_status = []
+    for c, cb in enumerate(conns):
+        k0 = int(b["conn_first"][c])
+        exp_status += list(ro["bstatus"][k0:k0 + len(cb)])
+    got_status = []
+    p1, s1, _ = st[0]
+    p2, s2, _ = st[1]
+    for c, cb in enumerate(conns):
+        got_status += list(s1[p1["conn_first"][c]:p1["conn_first"][c + 1]])
+        got_status += list(s2[p2["conn_first"][c]:p2["conn_first"][c + 1]])
+    assert got_status == exp_status
+    # fields: compare as per-connection multisets of the ordered lists (calls interleave connections)
+    def per_conn(part_stats, fields):
+        out, i = {}, 0
+        for part, _, nfields in part_stats:
+            for c in range(len(part["conn_first"]) - 1):
+                for k in range(part["conn_first"][c], part["conn_first"][c + 1]):
+                    n = int(nfields[k])
+                    out.setdefault(c, []).extend(zip(fields[0][i:i + n], fields[1][i:i + n]))
+                    i += n
+        return out
+    exp, i = {}, 0
+    for c in range(len(conns)):
+        for k in range(b["conn_first"][c], b["conn_first"][c + 1]):
+            n = int(ro["nfields"][k])
+            exp.setdefault(c, []).extend(zip(want[0][i:i + n], want[1][i:i + n]))
+            i += n
+    assert per_conn(st, got) == exp

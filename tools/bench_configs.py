@@ -3,12 +3,16 @@
   c2  1M strings mean 32 B, decode only
   c3  1M strings Zipf 8..512 B, encode + decode round trip, P / (t_enc + t_dec)
   c5  512K QPACK values mean 512 B (cookie/URI charset), encode only with flatten_string(prefix 7) framing
+  blocks[N]  f4: N synthetic HPACK connections (default 65536), header blocks decoded with a dynamic
+      table per connection; CPU baselines: the reference (1 thread) and the restatement (16 threads)
   lit 16M c4 strings framed as HPACK literals (h2o_hpack_encode_string), then decoded as literals
       (decode_string: header integer, Huffman or raw + validation); round trip checked on the device
 Prints one JSON line per config.  Device-resident, HIP-event timing on the launch stream."""
 import json
 import os
 import sys
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -89,6 +93,60 @@ def literals_line(torch, codec, synth):
             "consumed_matches_wire": bool((cons[ok].to(torch.int64) == f_len[ok].to(torch.int64)).all())}
 
 
+def blocks_line(torch, codec, nconn=65536):
+    """f4: HPACK header blocks of synthetic browser-like connections (h2o_amd/hpack_synth.py, 1-8 requests
+    each, 1 % adversarial), decoded with a dynamic table per connection; the CPU baselines run the same
+    batch through the reference's h2o_hpack_decode_header (oracle/_ref, 1 thread) and the restatement
+    (16 threads)"""
+    import time
+
+    from h2o_amd import hpack_synth as HS
+
+    b = HS.make_connections(nconn, seed=5, adversarial_frac=0.01)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
+    d, bo, cf = dev(b["data"]), dev(b["blk_off"].view(np.int32)), dev(b["conn_first"].view(np.int32))
+    ao = codec.default_arena_off(bo)
+    res = {}
+
+    def run():
+        res["r"] = codec.hpack_decode_blocks(d, bo, cf, 4096, arena_off=ao, in_size=int(b["data"].size))
+
+    t = timed(torch, run, steps=10, warmup=2)
+    r = res["r"]
+    nblk = len(b["blk_off"]) - 1
+    nf = int(r["nfields"][:nblk].to(torch.int64).sum().item())
+    out_bytes = int((r["name_len"].to(torch.int64) * 0).sum().item())
+    ok = int((r["bstatus"][:nblk] == 0).sum().item())
+    W = int(b["data"].size)
+    line = {"config": "blocks", "connections": nconn, "blocks": nblk, "fields": nf, "block_bytes": W, "ok_blocks": ok,
+            "decode_ms": round(t, 4), "blocks_per_s": round(nblk / (t * 1e-3), 1),
+            "fields_per_s": round(nf / (t * 1e-3), 1), "block_gibps": round(W / GIB / (t * 1e-3), 3)}
+    del out_bytes
+    try:
+        sys.path.insert(0, ROOT)
+        from oracle import oracle as O
+
+        cpu = {}
+        if O.ref_available():
+            m = min(nconn, 4096)
+            k = int(b["conn_first"][m])
+            sub = (b["data"][:int(b["blk_off"][k])], b["blk_off"][:k + 1], b["conn_first"][:m + 1])
+            t0 = time.perf_counter()
+            O.ref().hpack_decode_blocks(*sub, 4096)
+            dt = time.perf_counter() - t0
+            cpu["reference_1thread_blocks_per_s"] = round(k / dt, 1)
+            cpu["reference_1thread_gibps"] = round(int(sub[1][-1]) / GIB / dt, 4)
+        threads = min(16, len(os.sched_getaffinity(0)))
+        t0 = time.perf_counter()
+        O.oracle().hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], 4096, nthreads=threads)
+        dt = time.perf_counter() - t0
+        cpu["restatement_%dthreads_blocks_per_s" % threads] = round(nblk / dt, 1)
+        line["cpu"] = cpu
+    except Exception as e:  # the CPU baseline is a report, not a gate
+        line["cpu_error"] = str(e)
+    return line
+
+
 def main():
     import torch
 
@@ -99,6 +157,10 @@ def main():
     for cfg in cfgs:
         if cfg == "lit":
             print(json.dumps(literals_line(torch, codec, synth)), flush=True)
+            continue
+        if cfg.startswith("blocks"):
+            n = int(cfg[6:]) if len(cfg) > 6 else 65536
+            print(json.dumps(blocks_line(torch, codec, n)), flush=True)
             continue
         b = synth.make_batch_torch(cfg, seed=7)
         n, P = b["n"], int(b["total"])
