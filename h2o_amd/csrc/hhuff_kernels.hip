@@ -15,6 +15,7 @@
 // Reference semantics: lib/http2/hpack.c:117-156 (decode), :774-804 (encode); see hhuff_device.h.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <mutex>
 
 #include "hhuff_device.h"
 #include "hhuff_launch.h"
@@ -188,6 +189,9 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
     }
 };
 
+#ifndef HHUFF_DEFER_EDGES  // A/B knob: region edges written by edge_fix_kernel after the staged kernels
+#define HHUFF_DEFER_EDGES 1
+#endif
 #ifndef HHUFF_COPY_V2  // A/B knob: 0 = LDS byte reads at the edges; N = N chunks per round, register edges
 #define HHUFF_COPY_V2 0  // measured: register edges 5 % slower (c4 decode 0.7125 -> 0.7485 ms)
 #endif
@@ -242,6 +246,58 @@ __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t 
 #endif
 }
 
+// Deferred region edges.  Writing the (at most two) 16-byte chunks a tile's output region shares with
+// its neighbours byte by byte costs a serial LDS round trip per byte; measured, it was 11 % of both c4
+// kernels.  Instead the tile writes every whole chunk with 16-B stores, and the lanes holding its first
+// and last chunk record them {bytes, address, byte range} in `rec` (2 per tile) straight from their
+// registers; edge_fix_kernel writes the recorded byte ranges after the kernel (neighbouring tiles'
+// ranges in one chunk are disjoint, so dword / byte stores suffice).
+struct EdgeRec {
+    uint4 v;
+    uint4 m;  // {address lo, address hi, lo, hi}: bytes [lo, hi) of the chunk are ours (lo >= hi: none)
+};
+
+__device__ __forceinline__ void region_copy_deferred(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds,
+                                                     uint32_t ospan, uint64_t keep_lo, uint64_t keep_hi, int lane,
+                                                     EdgeRec* __restrict__ rec) {
+    const uint32_t kl = ospan ? (ospan - 1u) & ~15u : 0u;  // the last chunk
+    for (uint32_t k = (uint32_t)lane * 16u; k < ospan; k += 64u * 16u) {
+        const uint64_t g = gbase + k;
+        const uint4 v = *reinterpret_cast<const uint4*>(lds + k);
+        const bool full = g >= keep_lo && g + 16 <= keep_hi;
+        if (full) *reinterpret_cast<uint4*>(out + g) = v;
+        if (k == 0 || k == kl) {
+            const uint32_t lo = keep_lo > g ? (uint32_t)(keep_lo - g) : 0u;
+            const uint32_t hi = keep_hi - g < 16 ? (uint32_t)(keep_hi - g) : 16u;
+            EdgeRec* r = rec + (k == 0 ? 0 : 1);
+            r->v = v;
+            r->m = make_uint4((uint32_t)g, (uint32_t)(g >> 32), full ? 0u : lo, full ? 0u : hi);
+            if (kl == 0) rec[1].m = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    if (ospan == 0 && lane == 0) {
+        rec[0].m = make_uint4(0u, 0u, 0u, 0u);
+        rec[1].m = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+// one thread per (record, dword)
+__global__ void edge_fix_kernel(uint8_t* __restrict__ out, const EdgeRec* __restrict__ rec, uint64_t nrec) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 4 * nrec; i += (uint64_t)gridDim.x * blockDim.x) {
+        const EdgeRec& r = rec[i >> 2];
+        const uint4 m = r.m;
+        const uint32_t w = (uint32_t)(i & 3), lo = max(m.z, 4u * w), hi = min(m.w, 4u * w + 4u);
+        if (lo >= hi) continue;
+        const uint32_t word = reinterpret_cast<const uint32_t*>(&r.v)[w];
+        uint8_t* g = out + (((uint64_t)m.y << 32) | m.x);
+        if (hi - lo == 4) {
+            *reinterpret_cast<uint32_t*>(g + lo) = word;
+        } else {
+            for (uint32_t x = lo; x < hi; ++x) g[x] = (uint8_t)(word >> (8u * (x & 3u)));
+        }
+    }
+}
+
 // Copy `n` bytes from LDS `src` to global `dst`, where src == dst (mod 4).
 __device__ __forceinline__ void lane_copy(uint8_t* __restrict__ dst, const uint8_t* src, uint32_t n) {
     uint32_t head = (4u - ((uint32_t)(uintptr_t)dst & 3u)) & 3u;
@@ -287,6 +343,7 @@ struct DecArgs {
     const uint32_t* out_off;
     uint32_t* out_len;
     uint8_t* status;
+    EdgeRec* edges;  // region layout: 2 records per 64-string tile (deferred edges), or NULL
 };
 
 __device__ __forceinline__ void load_dec_tables(uint32_t* s_lut, uint32_t* s_kinfo, uint32_t* s_ones, int nthreads) {
@@ -479,11 +536,18 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
 #else
             if (region) {
 #endif
-                region_copy<(OUT_STAGE + 1023) / 1024>(A.out, cur.obase(), obuf, cur.ospan, cur.olo(), cur.ohi(), lane);
+                if (A.edges)
+                    region_copy_deferred(A.out, cur.obase(), obuf, cur.ospan, cur.olo(), cur.ohi(), lane,
+                                         A.edges + 2 * (base >> 6));
+                else
+                    region_copy<(OUT_STAGE + 1023) / 1024>(A.out, cur.obase(), obuf, cur.ospan, cur.olo(), cur.ohi(), lane);
             } else if (t.valid && ol != kFailLen) {
                 lane_copy(A.out + cur.dst_g, obuf + cur.op0, ol);
             }
             wave_lds_sync();
+        } else if (A.edges && lane == 0) {  // direct path: no edges to defer
+            A.edges[2 * (base >> 6)].m = make_uint4(0u, 0u, 0u, 0u);
+            A.edges[2 * (base >> 6) + 1].m = make_uint4(0u, 0u, 0u, 0u);
         }
         if (t.valid) {
             A.out_len[ti_i] = ol;
@@ -538,6 +602,7 @@ struct EncArgs {
     const uint32_t* out_off;
     uint32_t* out_len;
     uint8_t* status;
+    EdgeRec* edges;  // region layout, encode_staged_kernel: 2 records per 64-string tile, or NULL
 };
 
 __device__ __forceinline__ void load_enc_table(uint2* s_enc, int nthreads) {
@@ -653,7 +718,10 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
 #else
             if (region) {
 #endif
-                region_copy<(STAGE + 1023) / 1024>(A.out, cur.a0, obuf, cur.ospan, t.lo, t.hi, lane);
+                if (A.edges)
+                    region_copy_deferred(A.out, cur.a0, obuf, cur.ospan, t.lo, t.hi, lane, A.edges + 2 * (base >> 6));
+                else
+                    region_copy<(STAGE + 1023) / 1024>(A.out, cur.a0, obuf, cur.ospan, t.lo, t.hi, lane);
             } else if (t.valid && ol != kFailLen) {
                 lane_copy(A.out + cur.dst_g, obuf + cur.op0, ol);
             }
@@ -664,6 +732,10 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
             sink.init(A.out + (A.out_off ? cur.dst_g : (uint64_t)t.s));
             ol = encode_core(GlobalSource{A.in, A.in_size}, t.s, t.len, sink, s_enc);
             PROF_MARK(6);
+        }
+        if (!cur.fits && A.edges && lane == 0) {  // direct path: no edges to defer
+            A.edges[2 * (base >> 6)].m = make_uint4(0u, 0u, 0u, 0u);
+            A.edges[2 * (base >> 6) + 1].m = make_uint4(0u, 0u, 0u, 0u);
         }
         if (t.valid) finish_encode(A, t.i, t.len, ol);
         PROF_MARK(5);
@@ -1558,6 +1630,46 @@ static int pick_decode(uint64_t in_size, uint32_t n) {
 #ifndef HHUFF_ENC_PL_K  // strings per tile (0 = from the mean length)
 #define HHUFF_ENC_PL_K 0
 #endif
+static uint64_t edge_recs(uint32_t n) { return 2 * (((uint64_t)n + 63) / 64); }
+
+// Edge records come from a library-owned stream-ordered pool that keeps its memory between calls (the
+// default pool's release threshold of 0 would hand it back to the driver at every synchronisation).
+static hipError_t alloc_edges(EdgeRec** p, uint32_t n, hipStream_t stream) {
+    static std::mutex mu;
+    static hipMemPool_t pools[64] = {};
+    const int dev = current_device();
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    hipMemPool_t pool;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (!pools[dev]) {
+            hipMemPoolProps props = {};
+            props.allocType = hipMemAllocationTypePinned;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = dev;
+            hipError_t e = hipMemPoolCreate(&pools[dev], &props);
+            if (e != hipSuccess) return e;
+            uint64_t keep = ~0ull;
+            (void)hipMemPoolSetAttribute(pools[dev], hipMemPoolAttrReleaseThreshold, &keep);
+        }
+        pool = pools[dev];
+    }
+    return hipMallocFromPoolAsync((void**)p, edge_recs(n) * sizeof(EdgeRec), pool, stream);
+}
+
+// after a staged kernel launched with deferred edges: write them, release the records (stream order)
+static hipError_t finish_deferred(uint8_t* out, EdgeRec* edges, uint32_t n, hipStream_t stream) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) {
+        const uint64_t nrec = edge_recs(n);
+        const uint32_t blocks = (uint32_t)min((4 * nrec + 255) / 256, (uint64_t)8192);
+        hipLaunchKernelGGL(edge_fix_kernel, dim3(blocks), dim3(256), 0, stream, out, edges, nrec);
+        e = hipGetLastError();
+    }
+    const hipError_t f = hipFreeAsync(edges, stream);
+    return e != hipSuccess ? e : f;
+}
+
 static bool use_pl_encode(uint64_t in_size, uint32_t n) {
     const uint64_t mean = n ? in_size / n : 0;
     return HHUFF_ENC_PL >= 0 && mean >= (uint64_t)HHUFF_ENC_PL;
@@ -1573,22 +1685,27 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
                          const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
                          uint8_t* status, hipStream_t stream, uint64_t sel_bytes) {
     if (n == 0) return hipSuccess;
-    DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status};
+    DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr};
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n);
     const int grid = grid_for(v, current_device(), n);
+    const bool defer = HHUFF_DEFER_EDGES && v != kDecD && in_len == nullptr && out_off == nullptr;
+    if (defer) {
+        hipError_t e = alloc_edges(&A.edges, n, stream);
+        if (e != hipSuccess) return e;
+    }
     switch (v) {
         case kDecS: hipLaunchKernelGGL(DEC_S, dim3(grid), dim3(HHUFF_DSW * 64), 0, stream, A); break;
         case kDecL: hipLaunchKernelGGL(DEC_L, dim3(grid), dim3(384), 0, stream, A); break;
         default: hipLaunchKernelGGL(DEC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }
-    return hipGetLastError();
+    return defer ? finish_deferred(out, A.edges, n, stream) : hipGetLastError();
 }
 
 hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
                          uint8_t* out, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, hipStream_t stream,
                          uint64_t sel_bytes) {
     if (n == 0) return hipSuccess;
-    EncArgs A{in, in_size, in_off, in_len, n, out, out_off, out_len, status};
+    EncArgs A{in, in_size, in_off, in_len, n, out, out_off, out_len, status, nullptr};
     if (sel_bytes) in_size = sel_bytes;  // variant selection only; A keeps the addressable size
 #ifdef HHUFF_ENCODE_CHUNKED
     if (in_len == nullptr && out_off == nullptr) {  // contiguous implicit layout: byte-balanced chunks
@@ -1622,12 +1739,17 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     }
     const int v = pick_encode(in_size, n);
     const int grid = grid_for(v, current_device(), n);
+    const bool defer = HHUFF_DEFER_EDGES && v != kEncD && in_len == nullptr && out_off == nullptr;
+    if (defer) {
+        hipError_t e = alloc_edges(&A.edges, n, stream);
+        if (e != hipSuccess) return e;
+    }
     switch (v) {
         case kEncS: hipLaunchKernelGGL(ENC_S, dim3(grid), dim3(1024), 0, stream, A); break;
         case kEncL: hipLaunchKernelGGL(ENC_L, dim3(grid), dim3(512), 0, stream, A); break;
         default: hipLaunchKernelGGL(ENC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }
-    return hipGetLastError();
+    return defer ? finish_deferred(out, A.edges, n, stream) : hipGetLastError();
 }
 
 hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
