@@ -76,14 +76,17 @@ def pmc_traffic(args):
                         for r in csv.DictReader(open(os.path.join(root, f))):
                             if "hhuff::" not in r["Kernel_Name"]:
                                 continue
-                            k = "decode" if "decode" in r["Kernel_Name"] else "encode"
+                            nm = r["Kernel_Name"]
+                            k = "decode" if "decode" in nm else "encode" if "encode" in nm else "edge_fix" if "edge_fix" in nm else None
+                            if k is None:
+                                continue
                             vals.setdefault((k, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
         except Exception:
             return {}
         finally:
             shutil.rmtree(d, ignore_errors=True)
     out = {}
-    for k in ("decode", "encode"):
+    for k in ("decode", "encode", "edge_fix"):
         f, w = vals.get((k, "FETCH_SIZE")), vals.get((k, "WRITE_SIZE"))
         if f and w:
             out[k] = (2.0 * sum(f) / len(f) + sum(w) / len(w)) * 1024.0

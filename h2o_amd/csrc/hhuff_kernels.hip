@@ -590,6 +590,320 @@ __global__ __launch_bounds__(WAVES * 64) void decode_direct_kernel(DecArgs A) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Streaming decode (long and mixed lengths).  The staged kernels give a tile of 64 strings one lane
+// each and run it as long as its longest string; with Zipf-like lengths (c3) a tile idles most of its
+// lanes, and strings longer than a stage share fall back to decode_direct_kernel.  Here every lane owns
+// one string at a time and a private window: NW input dwords and an OUT-byte output buffer in LDS.
+// A round
+//   1. gives idle lanes the next strings of the wave's batch (waves take batches of 64 from a global
+//      counter, so waves finish together too);
+//   2. loads each lane's next window: NW dwords from its current byte (dword-aligned), byte-swapped;
+//   3. runs v7 bulk steps as far as the window allows (or to 27 bits before the string end) and, where
+//      the string ends inside the window, v5's checked tail with the padding rule (hpack.c:132-133);
+//   4. flushes the lane's whole output chunks with 16-B stores at 16-B aligned destinations -- the LDS
+//      buffer holds byte g of the output at offset g % 16 -- and carries the partial last chunk over;
+//      a string's first (head) and last (tail) chunks are written byte / dword-wise, only the bytes it
+//      produced, so neighbouring slots are never touched.
+// Lanes share nothing but the tables: no barriers, and a lane never waits for another lane's string.
+// Same results as decode_core (hpack.c:117-156) for every layout (implicit slots, pairs, explicit dst).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint4 load16_bounded(const uint8_t* __restrict__ in, uint64_t in_size, uint64_t a) {
+    if (a + 16 <= in_size) {
+        typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-B load
+        const u32x4a v = *reinterpret_cast<const u32x4a*>(in + a);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll 1
+    for (uint32_t b = 0; b < 16; ++b)
+        if (a + b < in_size) w[b >> 2] |= (uint32_t)in[a + b] << (8u * (b & 3u));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// bytes [lo, hi) of the 16-B LDS chunk `c` to global `g` (16-B aligned): dword stores where whole
+__device__ __forceinline__ void store_range16(uint8_t* __restrict__ g, const uint8_t* c, uint32_t lo, uint32_t hi) {
+    const uint4 v = *reinterpret_cast<const uint4*>(c);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t bl = max(lo, 4u * k), bh = min(hi, 4u * k + 4u);
+        if (bl >= bh) continue;
+        if (bh - bl == 4u) {
+            *reinterpret_cast<uint32_t*>(g + 4u * k) = w[k];
+        } else {
+            for (uint32_t x = bl; x < bh; ++x) g[x] = (uint8_t)(w[k] >> (8u * (x & 3u)));
+        }
+    }
+}
+
+template <int WAVES, int NW, int OUT>
+__global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, unsigned long long* __restrict__ counter) {
+    static_assert(NW >= 8 && NW % 4 == 0 && OUT % 16 == 0, "window shape");
+    // per round a lane consumes <= 32 (NW - 2) bits: <= 32 (NW - 2) / 5 symbols after <= 15 carried bytes,
+    // plus the byte the second-symbol store may touch; the last byte of the buffer is the trash byte
+    static_assert(15 + (32 * (NW - 2)) / 5 + 2 < OUT, "output buffer too small for a window");
+    constexpr uint32_t kWS = NW + 1;  // odd dword stride: lanes at the same q hit distinct banks
+    struct __attribute__((aligned(16))) Smem {
+        uint32_t lut[1u << HHUFF_LUT_BITS];
+        uint32_t kinfo[32];
+        uint32_t ones[(HHUFF_ONES_NENT + 3) & ~3];
+        uint8_t out[WAVES * 64][OUT];
+        uint32_t win[WAVES * 64][kWS];  // [0]: the dword before the window (read, never used)
+    };
+    __shared__ Smem sm;
+    load_dec_tables(sm.lut, sm.kinfo, sm.ones, WAVES * 64);
+    __syncthreads();
+    const DecTables T{sm.lut, sm.kinfo, sm.ones};
+    const int lane = threadIdx.x & 63;
+    uint32_t* win = &sm.win[threadIdx.x][1];
+    const lds_u32* st = (const lds_u32*)win;
+    uint8_t* obuf = sm.out[threadIdx.x];
+    const uint32_t ob = lds_addr(obuf), trash = ob + OUT - 1u;
+    constexpr int32_t kLimW = 32 * (NW - 2) - 30;  // bulk steps start below this window bit
+    constexpr int32_t kFinal = 32 * (NW - 2);      // a string ending at or before this bit ends in the window
+
+    // per-lane string state
+    bool busy = false, head = false, is_name = false;
+    uint32_t i = 0, s = 0, len = 0, P = 0, ocnt = 0, flags = 0, first = 0, lastb = 0, fail = 0;
+    uint64_t dst = 0;
+    // wave batch
+    uint64_t bnext = 0, bend = 0;
+    bool qdone = false;
+
+    for (;;) {
+        // ---- 1. idle lanes take strings ----
+        for (int it = 0; it < 2; ++it) {
+            const uint64_t need = __builtin_amdgcn_ballot_w64(!busy);
+            if (need == 0) break;
+            if (bnext >= bend) {
+                if (qdone) break;
+                uint64_t b = 0;
+                if (lane == 0) b = atomicAdd(counter, 64ull);
+                b = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
+                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+                if (b >= A.n) {
+                    qdone = true;
+                    break;
+                }
+                bnext = b;
+                bend = min(b + 64u, (uint64_t)A.n);
+            }
+            const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            if (!busy && bnext + rank < bend) {
+                i = (uint32_t)(bnext + rank);
+                s = A.in_off[i];
+                len = A.in_len ? A.in_len[i] : A.in_off[i + 1] - s;
+                is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) : false;
+                dst = A.out_off ? (uint64_t)A.out_off[i] : dec_slot(s);
+                if (len > kMaxStrLen) {
+                    A.out_len[i] = kFailLen;
+                    A.status[i] = kStatusTooLong;
+                } else {
+                    busy = true;
+                    head = (dst & 15u) != 0;
+                    P = ocnt = flags = first = lastb = fail = 0;
+                }
+            }
+            bnext = min(bend, bnext + (uint64_t)__builtin_popcountll(need));
+        }
+        if (!__any(busy)) {
+            if (qdone) break;
+            continue;
+        }
+
+        // ---- 2. the lane's window: NW dwords from its current byte (dword-aligned) ----
+        const uint64_t cur = (uint64_t)s + (P >> 3);
+        const uint64_t wb = cur & ~3ull;
+        if (busy) {
+#pragma unroll
+            for (int j = 0; j < NW / 4; ++j) {
+                const uint4 x = load16_bounded(A.in, A.in_size, wb + 16u * j);
+                win[4 * j + 0] = bswap32(x.x);
+                win[4 * j + 1] = bswap32(x.y);
+                win[4 * j + 2] = bswap32(x.z);
+                win[4 * j + 3] = bswap32(x.w);
+            }
+        }
+        const uint64_t rem = (uint64_t)len * 8u - P;  // string bits left
+        int32_t pm = busy ? (int32_t)(8u * (uint32_t)(cur - wb) + (P & 7u)) - 1 : -1;
+        const int32_t pm0 = pm;
+        const int32_t end = busy ? (int32_t)min((uint64_t)(pm + 1) + rem, (uint64_t)0x40000000u) : 0;
+        const bool fin = busy && end <= kFinal;
+        const uint32_t h0 = (uint32_t)((dst + ocnt) & 15u);  // buffer offset of this round's first byte
+        uint32_t o = ob + h0;
+        int32_t q = pm >> 5;
+        uint32_t x0 = st[q], x1 = st[q + 1], x2 = st[q + 2];
+        uint32_t accb = 0, acc1 = 0, acc2 = 0, accl = 0, parked = busy ? 0u : 1u;
+        int32_t lim = busy ? min(end - 26, kLimW) : (int32_t)0x80000000;
+        auto advance = [&](int32_t cons) {
+            pm += cons;
+            const int32_t qn = pm >> 5;
+            const bool adv = qn != q;
+            x0 = adv ? x1 : x0;
+            x1 = adv ? x2 : x1;
+            q = qn;
+            x2 = st[q + 2];
+        };
+
+        // ---- 3a. bulk (decode_staged_lane_v7's step) ----
+        auto bstep = [&](bool longchk) {
+            if (pm < lim) {
+                const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+                const uint32_t sl = (uint32_t)((int32_t)e >> 31);
+                const uint32_t h2 = (uint32_t)((int32_t)(e << 1) >> 31);
+                lds_st8(sel_bits(sl, trash, o), e);
+                lds_st8(sel_bits(h2, o, trash - 1u) + 1u, e >> 8);
+                o += (e >> 28) & 3u;
+                accb |= e;
+                uint32_t cons = ((e >> 20) & 15u) & ~sl;
+                {
+                    const uint32_t wb2 = w << cons;
+                    const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
+                    const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
+                    const uint32_t h2b = (uint32_t)((int32_t)(eb << 1) >> 31);
+                    lds_st8(sel_bits(slb, trash, o), eb);
+                    lds_st8(sel_bits(h2b, o, trash - 1u) + 1u, eb >> 8);
+                    o += (eb >> 28) & 3u;
+                    accb |= eb;
+                    cons += ((eb >> 20) & 15u) & ~slb;
+                }
+                if ((!HHUFF_DEC_LONG2 || longchk) && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
+                    if (sl) {
+                        const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                        const uint32_t ki = T.kinfo[k];
+                        const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                        const int32_t L = (le >> 9) & 31u;
+                        const uint32_t fits = (uint32_t)((L + pm - end) >> 31);
+                        const uint32_t eos = (le & 0x1FFu) == kEos ? 0xFFFFFFFFu : 0u;
+                        const uint32_t okm = fits & ~eos;
+                        fail |= fits & eos & 1u;  // EOS inside the string (hpack.c:88-89)
+                        lds_st8(sel_bits(okm, o, trash), le);
+                        o -= okm;
+                        accl |= le & okm;
+                        cons = okm & (uint32_t)L;
+                        parked |= ~okm & 1u;
+                        lim = (int32_t)sel_bits(okm, (uint32_t)lim, 0x80000000u);
+                    }
+                }
+                advance((int32_t)cons);
+            }
+        };
+        for (;;) {
+            bstep(false);
+            bstep(true);
+            if (!__any(pm < lim)) break;
+        }
+
+        // ---- 3b. tail: lanes whose string ends in this window ----
+        int32_t c = (fin && !parked) ? pm - end : 0x40000000;
+        if (__any(fin)) {
+            int32_t prog = 0;
+            auto step = [&](bool longchk) {
+                const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+                const int32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+                const int32_t s1 = L1 + c, s2 = L12 + c;
+                const uint32_t m1 = (uint32_t)((s1 & ~(int32_t)e) >> 31);
+                const uint32_t m2 = (uint32_t)((s2 & (int32_t)(e << 1)) >> 31);
+                int32_t cons = (int32_t)sel_bits(m2, (uint32_t)L12, m1 & (uint32_t)L1);
+                lds_st8(sel_bits(m1, o - m2, trash), e >> 8);
+                lds_st8(sel_bits(m1, o, trash), e);
+                o = o - m1 - m2;
+                acc1 |= e & m1;
+                acc2 |= e & m2;
+                {
+                    const uint32_t wb2 = w << cons;
+                    const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
+                    const int32_t cb = c + cons;
+                    const int32_t L1b = (eb >> 16) & 15u, L12b = (eb >> 20) & 15u;
+                    const uint32_t m1b = (uint32_t)(((L1b + cb) & ~(int32_t)eb) >> 31);
+                    const uint32_t m2b = (uint32_t)(((L12b + cb) & (int32_t)(eb << 1)) >> 31);
+                    lds_st8(sel_bits(m1b, o - m2b, trash), eb >> 8);
+                    lds_st8(sel_bits(m1b, o, trash), eb);
+                    o = o - m1b - m2b;
+                    acc1 |= eb & m1b;
+                    acc2 |= eb & m2b;
+                    cons += (int32_t)sel_bits(m2b, (uint32_t)L12b, m1b & (uint32_t)L1b);
+                }
+                const bool lact = (s1 & (int32_t)e) < 0;
+                uint32_t consl = 0;
+                if ((!HHUFF_DEC_LONG2 || longchk) && __builtin_amdgcn_ballot_w64(lact) != 0) {
+                    if (lact) {
+                        const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                        const uint32_t ki = T.kinfo[k];
+                        const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                        const int32_t L = (le >> 9) & 31u;
+                        const uint32_t fits = (uint32_t)((L + c) >> 31);
+                        const uint32_t eos = (le & 0x1FFu) == kEos ? 0xFFFFFFFFu : 0u;
+                        const uint32_t okm = fits & ~eos;
+                        fail |= fits & eos & 1u;
+                        lds_st8(sel_bits(okm, o, trash), le);
+                        o -= okm;
+                        accl |= le & okm;
+                        consl = okm & (uint32_t)L;
+                        c = (int32_t)sel_bits(okm, (uint32_t)c, 0x40000000u);
+                    }
+                }
+                cons |= (int32_t)consl;
+                c += cons;
+                advance(cons);
+                prog = cons;
+            };
+            step(true);
+            for (;;) {
+                step(false);
+                step(true);
+                if (!__any(prog != 0)) break;
+            }
+        }
+
+        // ---- 4. flush whole chunks, carry the partial one; finish strings ----
+        if (busy) {
+            flags |= ((accb >> 24) | (accb >> 26) | (acc1 >> 24) | (acc2 >> 26) | (accl >> 14)) & 3u;
+            const uint32_t nb = o - ob;  // buffer bytes: h0 carried (or, at a string's start, foreign) + produced
+            const uint32_t made = nb - h0;
+            if (made) {
+                if (ocnt == 0) first = obuf[h0];
+                lastb = obuf[nb - 1u];
+            }
+            const bool done = parked || fin;
+            const bool ok = fin && !parked && !fail && [&] {
+                const uint32_t R = ~(uint32_t)c;
+                const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                return R <= 7 && (w | (0xFFFFFFFFu >> (R & 31u))) == 0xFFFFFFFFu;
+            }();
+            uint8_t* gchunk = A.out + ((dst + ocnt) & ~15ull);
+            const uint32_t hs = (uint32_t)(dst & 15u);  // head chunk: the string's bytes start here
+            if (!done || ok) {  // a failed string's output is unspecified: skip its last stores
+                const uint32_t nfull = nb >> 4;
+                for (uint32_t k = 0; k < nfull; ++k) {
+                    if (head && k == 0)
+                        store_range16(gchunk, obuf, hs, 16u);
+                    else
+                        *reinterpret_cast<uint4*>(gchunk + 16u * k) = *reinterpret_cast<const uint4*>(obuf + 16u * k);
+                }
+                head = head && nfull == 0;
+                const uint32_t part = nb & 15u;
+                if (done) {
+                    if (part > (head ? hs : 0u)) store_range16(gchunk + 16u * nfull, obuf + 16u * nfull, head ? hs : 0u, part);
+                } else if (nfull) {
+                    *reinterpret_cast<uint4*>(obuf) = *reinterpret_cast<const uint4*>(obuf + 16u * nfull);
+                }
+            }
+            ocnt += made;
+            P += (uint32_t)(pm - pm0);
+            if (done) {
+                A.out_len[i] = ok ? ocnt : kFailLen;
+                A.status[i] = ok ? soft_bits(is_name, ocnt, flags, first, lastb) : kStatusFail;
+                busy = false;
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // encode
 // ------------------------------------------------------------------------------------------------
 struct EncArgs {
@@ -1555,6 +1869,12 @@ __global__ void literal_fix_kernel(LitArgs A) {
 #define DEC_S decode_staged_kernel<HHUFF_DSW, 3072, 4608>
 #define DEC_L decode_staged_kernel<6, 8192, 12928>
 #define DEC_D decode_direct_kernel<4>
+#ifndef HHUFF_DTW  // streaming decode shape: waves per block, window dwords, output bytes per lane
+#define HHUFF_DTW 8    // measured (c3 / u400 decode, ms): 12,12,96: 0.335 / 0.621; 16,8,64: 0.390 / 0.783;
+#define HHUFF_DTNW 16  // 8,16,112: 0.316 / 0.527
+#define HHUFF_DTOUT 112
+#endif
+#define DEC_T decode_stream_kernel<HHUFF_DTW, HHUFF_DTNW, HHUFF_DTOUT>
 #define ENC_S encode_staged_kernel<16, 3584>
 #define ENC_L encode_staged_kernel<8, 8192>
 #define ENC_D encode_direct_kernel<4>
@@ -1564,13 +1884,14 @@ __global__ void literal_fix_kernel(LitArgs A) {
 #define ENC_C encode_chunked_kernel<12, 4096, 128>
 #define ENC_CL encode_chunked_kernel<8, 8192, 64>
 
-enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncC, kEncCL, kEncP, kFlatP, kNumVariants };
+enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncC, kEncCL, kEncP, kFlatP, kDecT, kNumVariants };
 
 static const void* variant_fn(int v) {
     switch (v) {
         case kDecS: return (const void*)DEC_S;
         case kDecL: return (const void*)DEC_L;
         case kDecD: return (const void*)DEC_D;
+        case kDecT: return (const void*)DEC_T;
         case kEncS: return (const void*)ENC_S;
         case kEncL: return (const void*)ENC_L;
         case kFlatD: return (const void*)FLAT_D;
@@ -1584,6 +1905,7 @@ static const void* variant_fn(int v) {
 static int variant_threads(int v) {
     switch (v) {
         case kDecS: return HHUFF_DSW * 64;
+        case kDecT: return HHUFF_DTW * 64;
         case kEncS: return 1024;
         case kDecL: return 384;
         case kEncL: return 512;
@@ -1618,11 +1940,15 @@ static int current_device() {
     return dev;
 }
 
+#ifndef HHUFF_FORCE_DEC  // A/B knob: force a decode variant (kDecS / kDecL / kDecD / kDecT), -1 = by mean length
+#define HHUFF_FORCE_DEC -1
+#endif
 static int pick_decode(uint64_t in_size, uint32_t n) {
+    if (HHUFF_FORCE_DEC >= 0) return HHUFF_FORCE_DEC;
     const uint64_t mean = n ? in_size / n : 0;  // in_size bounds the bytes the batch can address
     if (mean <= 40) return kDecS;
     if (mean <= 128) return kDecL;
-    return kDecD;
+    return kDecT;  // u400: 2.35 ms (kDecL, tiles past the stage go direct) -> 0.53 ms
 }
 #ifndef HHUFF_ENC_PL  // A/B knobs: proportional-lane encode from this mean string length up (0 = always)
 #define HHUFF_ENC_PL 53
@@ -1634,7 +1960,7 @@ static uint64_t edge_recs(uint32_t n) { return 2 * (((uint64_t)n + 63) / 64); }
 
 // Edge records come from a library-owned stream-ordered pool that keeps its memory between calls (the
 // default pool's release threshold of 0 would hand it back to the driver at every synchronisation).
-static hipError_t alloc_edges(EdgeRec** p, uint32_t n, hipStream_t stream) {
+static hipError_t pool_alloc(void** p, uint64_t bytes, hipStream_t stream) {
     static std::mutex mu;
     static hipMemPool_t pools[64] = {};
     const int dev = current_device();
@@ -1654,7 +1980,10 @@ static hipError_t alloc_edges(EdgeRec** p, uint32_t n, hipStream_t stream) {
         }
         pool = pools[dev];
     }
-    return hipMallocFromPoolAsync((void**)p, edge_recs(n) * sizeof(EdgeRec), pool, stream);
+    return hipMallocFromPoolAsync(p, bytes, pool, stream);
+}
+static hipError_t alloc_edges(EdgeRec** p, uint32_t n, hipStream_t stream) {
+    return pool_alloc((void**)p, edge_recs(n) * sizeof(EdgeRec), stream);
 }
 
 // after a staged kernel launched with deferred edges: write them, release the records (stream order)
@@ -1688,10 +2017,24 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr};
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n);
     const int grid = grid_for(v, current_device(), n);
-    const bool defer = HHUFF_DEFER_EDGES && v != kDecD && in_len == nullptr && out_off == nullptr;
+    const bool defer = HHUFF_DEFER_EDGES && (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr;
     if (defer) {
         hipError_t e = alloc_edges(&A.edges, n, stream);
         if (e != hipSuccess) return e;
+    }
+    if (v == kDecT) {  // work counter for the waves' string batches
+        unsigned long long* ctr = nullptr;
+        hipError_t e = pool_alloc((void**)&ctr, sizeof(*ctr), stream);
+        if (e == hipSuccess) e = hipMemsetAsync(ctr, 0, sizeof(*ctr), stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(DEC_T, dim3(grid), dim3(HHUFF_DTW * 64), 0, stream, A, ctr);
+            e = hipGetLastError();
+        }
+        if (ctr) {
+            const hipError_t f = hipFreeAsync(ctr, stream);
+            if (e == hipSuccess) e = f;
+        }
+        return e;
     }
     switch (v) {
         case kDecS: hipLaunchKernelGGL(DEC_S, dim3(grid), dim3(HHUFF_DSW * 64), 0, stream, A); break;

@@ -201,6 +201,71 @@ def test_contiguous_mixed_lengths_proportional_lanes(torch_cuda, oracle_codec):
     assert len(ok) > 1000 and (np.diff(off)[ok] > 400).sum() > 100
 
 
+def test_streaming_decode_long_mixed(torch_cuda, oracle_codec):
+    """decode with mean Huffman length > 128 B (decode_stream_kernel): packed wire layout and pairs,
+    strings of 0..6000 B crossing many windows, long codes and EOS at every offset, invalid padding,
+    name validation; the plain bytes decoded as (mostly invalid) Huffman too"""
+    rng = np.random.default_rng(21)
+    syms, p = synth.header_alphabet()
+    strings = []
+    for i in range(5000):
+        L = int(rng.choice([0, 1, 2, 7, 40, 130, 400, 900, 2500, 6000], p=[.03, .03, .03, .06, .15, .25, .2, .15, .07, .03]))
+        kind = rng.random()
+        if kind < 0.1:  # long codes only (8..28-bit codes): windows end inside long codes
+            s = bytes(rng.choice(np.frombuffer(b"{}~^|<>\\\x00\x7f\xfe", np.uint8), L))
+        elif kind < 0.15:
+            s = bytes(rng.integers(0, 256, L, dtype=np.uint8))
+        else:
+            s = bytes(rng.choice(syms, L, p=p))
+        strings.append(s)
+    data, off = synth.pack(strings)
+    n = len(strings)
+    o_out, o_len, _ = oracle_codec.encode_batch(data, off, n, nthreads=8)
+    ok = np.nonzero(o_len != FAIL)[0]
+    huff = [o_out[int(off[i]):int(off[i]) + int(o_len[i])].tobytes() for i in ok]
+    # corrupt some: truncate, flip a bit, append an EOS (30 ones) / a zero byte (bad padding)
+    for j in rng.choice(len(huff), len(huff) // 20, replace=False):
+        h = bytearray(huff[j])
+        k = int(rng.integers(4))
+        if k == 0 and len(h) > 1:
+            h = h[:int(rng.integers(1, len(h)))]
+        elif k == 1 and h:
+            h[int(rng.integers(len(h)))] ^= 1 << int(rng.integers(8))
+        elif k == 2:
+            h += b"\xff\xff\xff\xff"
+        else:
+            h += b"\x00"
+        huff[j] = bytes(h)
+    hdata, hoff = synth.pack(huff)
+    m = len(huff)
+    assert hdata.size // m > 128  # mean length selects the streaming kernel
+    names = synth.bits_from_bools(rng.random(m) < 0.3)
+    g = gpu_decode(torch_cuda, hdata, hoff, m, is_name_bits=names)
+    o = oracle_codec.decode_batch(hdata, hoff, m, is_name_bits=names, nthreads=8)
+    np.testing.assert_array_equal(g[1], o[1])
+    np.testing.assert_array_equal(g[2], o[2])
+    slots = (hoff[:m].astype(np.uint64) * 8) // 5
+    assert compact(g[0], slots, g[1]) == compact(o[0], slots, o[1])
+    good = np.nonzero(g[1] != FAIL)[0]
+    assert len(good) > 0.9 * m and (np.diff(hoff)[good] > 1000).sum() > 100
+    # pairs layout over the same bytes (every other string, reversed), implicit slots
+    idx = np.arange(m)[::-2].copy()
+    starts, lens = hoff[idx].astype(np.uint32), np.diff(hoff)[idx].astype(np.uint32)
+    g = gpu_decode(torch_cuda, hdata, starts, len(idx), in_len=lens)
+    o = oracle_codec.decode_batch(hdata, starts, len(idx), in_len=lens, nthreads=8)
+    np.testing.assert_array_equal(g[1], o[1])
+    np.testing.assert_array_equal(g[2], o[2])
+    sl = (starts.astype(np.uint64) * 8) // 5
+    assert compact(g[0], sl, g[1]) == compact(o[0], sl, o[1])
+    # the plain strings as Huffman input
+    g = gpu_decode(torch_cuda, data, off, n)
+    o = oracle_codec.decode_batch(data, off, n, nthreads=8)
+    np.testing.assert_array_equal(g[1], o[1])
+    np.testing.assert_array_equal(g[2], o[2])
+    slots = (off[:n].astype(np.uint64) * 8) // 5
+    assert compact(g[0], slots, g[1]) == compact(o[0], slots, o[1])
+
+
 # ------------------------------------------------------------------------------------------------
 # per-string h2o symbols and the host batch API
 # ------------------------------------------------------------------------------------------------
