@@ -71,6 +71,12 @@ def lib():
         L.hhuff_hpack_decode_blocks.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp,
                                                 _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64,
                                                 ctypes.c_uint, _vp]
+        L.hhuff_qpack_scratch_size.restype = ctypes.c_uint64
+        L.hhuff_qpack_scratch_size.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
+        L.hhuff_qpack_decode.restype = ctypes.c_int
+        L.hhuff_qpack_decode.argtypes = ([_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32,
+                                          ctypes.c_uint32, ctypes.c_uint64] + [_vp] * 15 +
+                                         [ctypes.c_uint64, ctypes.c_uint, _vp])
         L.hhuff_version.restype = ctypes.c_char_p
         L.hhuff_last_error_string.restype = ctypes.c_char_p
         L.hhuff_grid_size.restype = ctypes.c_int
@@ -82,6 +88,7 @@ def lib():
 # symbols include/hhuff.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decode_batch", "hhuff_encode_batch",
             "hhuff_flatten_batch", "hhuff_decode_literals", "hhuff_hpack_decode_blocks", "hhuff_hpack_scratch_size",
+            "hhuff_qpack_decode", "hhuff_qpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string",
             "hhuff_grid_size")
@@ -269,6 +276,46 @@ def hpack_decode_blocks(data, blk_off, conn_first, table_size=4096, arena_off=No
                                            BLK_CONTINUE if cont else 0, _stream(stream)),
            "hhuff_hpack_decode_blocks")
     r["scratch"] = scratch  # keep alive until the stream has run the launch
+    return r
+
+
+QPK_CONTINUE = 1
+
+
+def qpack_decode(data, enc_off, enc_len, sec_off, conn_first, nsec, header_table_size=4096, max_blocked=100,
+                 num_blocked=None, arena_off=None, in_size=None, stream=None, scratch=None, cont=False):
+    """QPACK decoder step (include/hhuff.h hhuff_qpack_decode) on device tensors: enc_off / enc_len (per
+    connection), sec_off / conn_first / num_blocked int32 tensors (u32 bits), arena_off int64; nsec =
+    conn_first[-1] as a host int.  Returns a dict of device tensors: arena, name_off, name_len, value_off,
+    value_len, fflags (per field slot), nfields, sstatus, req_insert_count (per section), enc_status,
+    enc_consumed, insert_count (per connection), and the scratch holding the tables (pass it back with
+    cont=True for the next step)."""
+    import torch
+
+    dev = data.device
+    in_size = data.numel() if in_size is None else in_size
+    nconn = conn_first.numel() - 1
+    if arena_off is None:
+        arena_off = default_arena_off(sec_off, header_table_size)
+    nslots = max(1, int(sec_off[-1].item()) & 0xFFFFFFFF)
+    i32 = lambda n: torch.empty(max(1, n), dtype=torch.int32, device=dev)  # noqa: E731
+    r = dict(arena=torch.empty(max(1, int(arena_off[-1].item())), dtype=torch.uint8, device=dev),
+             name_off=i32(nslots), name_len=i32(nslots), value_off=i32(nslots), value_len=i32(nslots),
+             fflags=torch.empty(nslots, dtype=torch.uint8, device=dev), nfields=i32(nsec), sstatus=i32(nsec),
+             req_insert_count=torch.empty(max(1, nsec), dtype=torch.int64, device=dev), enc_status=i32(nconn),
+             enc_consumed=i32(nconn), insert_count=torch.empty(max(1, nconn), dtype=torch.int64, device=dev))
+    ss = int(lib().hhuff_qpack_scratch_size(nconn, header_table_size))
+    if scratch is None:
+        scratch = torch.empty(max(16, ss), dtype=torch.uint8, device=dev)
+    _check(lib().hhuff_qpack_decode(_dp(data), in_size, _dp(enc_off), _dp(enc_len), _dp(sec_off), _dp(conn_first),
+                                    nconn, nsec, header_table_size, max_blocked,
+                                    None if num_blocked is None else _dp(num_blocked), _dp(r["arena"]), _dp(arena_off),
+                                    _dp(r["name_off"]), _dp(r["name_len"]), _dp(r["value_off"]), _dp(r["value_len"]),
+                                    _dp(r["fflags"]), _dp(r["nfields"]), _dp(r["sstatus"]), _dp(r["req_insert_count"]),
+                                    _dp(r["enc_status"]), _dp(r["enc_consumed"]), _dp(r["insert_count"]), _dp(scratch),
+                                    scratch.numel(), QPK_CONTINUE if cont else 0, _stream(stream)),
+           "hhuff_qpack_decode")
+    r["scratch"] = scratch
     return r
 
 

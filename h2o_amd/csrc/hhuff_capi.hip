@@ -175,6 +175,36 @@ HHUFF_API int hhuff_hpack_decode_blocks(const uint8_t* in, uint64_t in_size, con
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "hpack block launch");
 }
 
+HHUFF_API uint64_t hhuff_qpack_scratch_size(uint32_t nconn, uint32_t header_table_size) {
+    return (uint64_t)nconn * hhuff::qpack_conn_scratch(header_table_size);
+}
+
+HHUFF_API int hhuff_qpack_decode(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off, const uint32_t* enc_len,
+                                 const uint32_t* sec_off, const uint32_t* conn_first, uint32_t nconn, uint32_t nsec,
+                                 uint32_t header_table_size, uint64_t max_blocked, const uint32_t* num_blocked,
+                                 uint8_t* arena, const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len,
+                                 uint32_t* value_off, uint32_t* value_len, uint8_t* fflags, uint32_t* nfields,
+                                 int32_t* sstatus, uint64_t* req_insert_count, int32_t* enc_status,
+                                 uint32_t* enc_consumed, uint64_t* insert_count, void* scratch, uint64_t scratch_size,
+                                 unsigned flags, void* stream) {
+    if (nconn == 0) return HHUFF_OK;
+    if (!in || !enc_off || !enc_len || !sec_off || !conn_first || !enc_status || !enc_consumed || !insert_count ||
+        !scratch)
+        return arg_fail("NULL array");
+    if (nsec && (!arena || !arena_off || !name_off || !name_len || !value_off || !value_len || !fflags || !nfields ||
+                 !sstatus || !req_insert_count))
+        return arg_fail("NULL array");
+    if (header_table_size > (1u << 30)) return arg_fail("header_table_size above 2^30");
+    if (scratch_size < hhuff_qpack_scratch_size(nconn, header_table_size))
+        return arg_fail("scratch smaller than hhuff_qpack_scratch_size");
+    if (((uintptr_t)scratch & 15u) != 0) return arg_fail("scratch must be 16-byte aligned");
+    hipError_t e = hhuff::launch_qpack(in, in_size, enc_off, enc_len, sec_off, conn_first, nconn, nsec,
+                                       header_table_size, max_blocked, num_blocked, arena, arena_off, name_off, name_len,
+                                       value_off, value_len, fflags, nfields, sstatus, req_insert_count, enc_status,
+                                       enc_consumed, insert_count, (uint8_t*)scratch, flags, (hipStream_t)stream);
+    return e == hipSuccess ? HHUFF_OK : hip_fail(e, "qpack launch");
+}
+
 // ---------------------------------------------------------------------------------------------------
 // (1) h2o per-string symbols: a batch of one on the thread's stream, synchronously
 // device/pinned layout: [meta 32 B: u32 in_off[2], out_len, is_name word, u8 status][input][output]

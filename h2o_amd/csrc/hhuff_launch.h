@@ -28,5 +28,15 @@ hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32
                                uint32_t* name_off, uint32_t* name_len, uint32_t* value_off, uint32_t* value_len,
                                uint8_t* fflags, uint32_t* nfields, int32_t* bstatus, uint8_t* scratch, uint32_t flags,
                                hipStream_t stream);
+// QPACK decoder (f4): see include/hhuff.h hhuff_qpack_decode; scratch = nconn x
+// qpack_conn_scratch(header_table_size) bytes of device memory
+uint64_t qpack_conn_scratch(uint32_t header_table_size);
+hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off, const uint32_t* enc_len,
+                        const uint32_t* sec_off, const uint32_t* conn_first, uint32_t nconn, uint32_t nsec,
+                        uint32_t header_table_size, uint64_t max_blocked, const uint32_t* num_blocked, uint8_t* arena,
+                        const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len, uint32_t* value_off,
+                        uint32_t* value_len, uint8_t* fflags, uint32_t* nfields, int32_t* sstatus,
+                        uint64_t* req_insert_count, int32_t* enc_status, uint32_t* enc_consumed, uint64_t* insert_count,
+                        uint8_t* scratch, uint32_t flags, hipStream_t stream);
 int grid_size(int device, int which);
 }  // namespace hhuff

@@ -1,0 +1,691 @@
+// QPACK decoding on the GPU (QPACK half): h2o's QPACK decoder, lib/http3/qpack.c.
+//   encoder stream  h2o_qpack_decoder_handle_input (:420-485) -- insert with static / dynamic name
+//                   reference (:289-348), insert with a literal name (:352-393), duplicate (:395-406),
+//                   set dynamic table capacity (:408-418) -- into one dynamic table per connection
+//                   (header_table_insert :166-190, header_table_evict :153-164)
+//   field sections  h2o_qpack_parse_request's reading of a section (:830-858): parse_decode_context
+//                   (:754-799), check_decode_context_blocked (:801-820), then decode_header (:652-752)
+//                   field after field (resolve_static / resolve_dynamic / _postbase :506-557, literals
+//                   :559-629)
+//
+// Decomposition.  Unlike HPACK, a QPACK field section never changes the dynamic table: only the encoder
+// stream does.  So a step runs in two launches on the stream:
+//   qpack_encoder_kernel   one lane per connection applies its encoder-stream bytes, in order;
+//   qpack_sections_kernel  one lane per field SECTION (many per connection) decodes it against the table
+//                          the first launch left -- the wide, parallel part.
+// The table lives in per-connection scratch in HBM: a byte ring of 2 x header_table_size bytes and an
+// entry ring of header_table_size / 32 + 1 records {byte offset, name length, value length, soft bits},
+// oldest first, absolute index = base_offset + position as in h2o (base_offset starts at 1, :143).
+// Live entries hold at most max_size <= header_table_size bytes, so the free part of the byte ring is
+// always >= header_table_size bytes: a new entry is written (Huffman-decoded straight into the ring,
+// or copied from the static table, the input or a live entry -- its own name source included) before
+// the eviction it causes is booked, without ever touching a live byte.  Writes stop at
+// header_table_size bytes; anything longer fails the reference's size check anyway (:278-281).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "hhuff_device.h"
+#include "hhuff.h"
+#include "hhuff_launch.h"
+
+namespace hhuff {
+namespace {
+__device__ const uint32_t q_dec_lut[1u << HHUFF_LUT_BITS] = HHUFF_DEC_LUT_INIT;
+__device__ const uint32_t q_kinfo[31] = HHUFF_ONES_KINFO_INIT;
+__device__ const uint32_t q_ones[HHUFF_ONES_NENT] = HHUFF_ONES_ENT_INIT;
+__device__ const uint32_t q_name_invalid[8] = HHUFF_NAME_INVALID_INIT;
+__device__ const uint32_t q_value_invalid[8] = HHUFF_VALUE_INVALID_INIT;
+__device__ const uint8_t q_static_bytes[HHUFF_QSTATIC_NBYTES] = HHUFF_QSTATIC_BYTES_INIT;
+__device__ const uint16_t q_static_ent[99 * 4] = HHUFF_QSTATIC_ENT_INIT;
+
+constexpr uint32_t kQStaticCount = 99;  // h2o_qpack_static_table (include/h2o/token_table.h)
+constexpr int32_t kDF = HHUFF_QPK_DECOMPRESSION_FAILED;
+constexpr int32_t kQIncomplete = -1;       // H2O_HTTP3_ERROR_INCOMPLETE (http3_common.h:77)
+constexpr int32_t kErrInvalidChar = -254;  // H2O_HTTP2_ERROR_INVALID_HEADER_CHAR
+constexpr uint32_t kEntryOverhead = 32;    // HEADER_ENTRY_SIZE_OFFSET (qpack.c:32)
+constexpr int64_t kQuicIntMax = 4611686018427387903LL;  // PTLS_QUICINT_MAX
+constexpr int64_t kIntIncomplete = -255, kIntBad = -9;
+}  // namespace
+
+struct QpkArgs {
+    const uint8_t* in;
+    uint64_t in_size;
+    const uint32_t *enc_off, *enc_len, *sec_off, *conn_first, *num_blocked;
+    uint32_t nconn, nsec, T;  // T = header_table_size
+    uint64_t max_blocked;
+    uint8_t* arena;
+    const uint64_t* arena_off;
+    uint32_t *name_off, *name_len, *value_off, *value_len;
+    uint8_t* fflags;
+    uint32_t* nfields;
+    int32_t* sstatus;
+    uint64_t* req_insert_count;
+    int32_t* enc_status;
+    uint32_t* enc_consumed;
+    uint64_t* insert_count;
+    uint8_t* scratch;
+    uint64_t conn_scratch;
+    uint32_t flags;
+};
+
+// per-connection scratch: [QState 64 B][byte ring RB = max(2T, 16) rounded to 16][entry ring E x 16 B]
+struct QState {
+    int64_t base_offset;
+    uint64_t total_inserts, num_bytes, max_size;
+    uint32_t start, num, whead, failed;
+    uint32_t pad[4];
+};
+static_assert(sizeof(QState) == 64, "QState layout");
+
+__host__ __device__ __forceinline__ uint32_t qpk_ring_bytes(uint32_t T) {
+    const uint32_t r = 2u * T < 16u ? 16u : 2u * T;
+    return (r + 15u) & ~15u;
+}
+
+// h2o_hpack_decode_int (lib/http2/hpack.c:52-83) at in[p], bounded by end
+__device__ int64_t q_hpack_int(const uint8_t* __restrict__ in, uint64_t& p, uint64_t end, uint32_t prefix_bits) {
+    if (p >= end) return kIntIncomplete;
+    const uint64_t pmax = (1u << prefix_bits) - 1u;
+    uint64_t v = in[p++] & pmax;
+    if (v != pmax) return (int64_t)v;
+    uint32_t shift = 0;
+    for (; shift < 56; shift += 7) {
+        if (p == end) return kIntIncomplete;
+        const uint32_t b = in[p++];
+        v += (uint64_t)(b & 127u) << shift;
+        if (!(b & 128u)) return (int64_t)v;
+    }
+    if (p == end) return kIntIncomplete;
+    if (in[p] & 128u) return kIntBad;
+    v += (uint64_t)(in[p++] & 127u) << shift;
+    if (v > 0x7FFFFFFFFFFFFFFFull) return kIntBad;
+    return (int64_t)v;
+}
+
+// decode_int (qpack.c:215-220): 0, kQIncomplete or kDF
+__device__ __forceinline__ int32_t q_int(int64_t& v, const uint8_t* in, uint64_t& p, uint64_t end, uint32_t prefix) {
+    v = q_hpack_int(in, p, end, prefix);
+    if (v < 0) return v == kIntIncomplete ? kQIncomplete : kDF;
+    return 0;
+}
+
+// h2o_hpack_validate_header_name (hpack.c:163-192): false on an upper-case letter, soft name bit otherwise
+template <class Get>
+__device__ bool q_valid_name(Get get, uint64_t n, uint32_t& soft) {
+    bool bad = n == 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint32_t c = get(i);
+        if ((q_name_invalid[c >> 5] >> (c & 31)) & 1u) {
+            if (c - 'A' < 26u) return false;
+            bad = true;
+        }
+    }
+    if (bad) soft |= 0x1u;
+    return true;
+}
+
+// h2o_hpack_validate_header_value (hpack.c:194-221) with the whole-value rule (:110-115)
+template <class Get>
+__device__ void q_valid_value(Get get, uint64_t n, uint32_t& soft) {
+    bool bad = false;
+    if (n != 0) {
+        const uint32_t f = get(0), l = get(n - 1);
+        bad = f == ' ' || f == '\t' || l == ' ' || l == '\t';
+    }
+    for (uint64_t i = 0; !bad && i < n; ++i) {
+        const uint32_t c = get(i);
+        bad = ((q_value_invalid[c >> 5] >> (c & 31)) & 1u) != 0;
+    }
+    if (bad) soft |= 0x2u;
+}
+
+// h2o_lookup_token on a raw name (qpack.c:585) can only change a verdict for the pseudo-header tokens
+// (every other token is a valid lower-case name): :authority :method :path :protocol :scheme :status
+template <class Get>
+__device__ bool q_pseudo_token(Get get, uint64_t n) {
+    if (n < 5 || n > 10 || get(0) != ':') return false;
+    const char* const tok[6] = {":authority", ":method", ":path", ":protocol", ":scheme", ":status"};
+    const uint8_t len[6] = {10, 7, 5, 9, 7, 7};
+    for (int k = 0; k < 6; ++k) {
+        if (len[k] != n) continue;
+        bool eq = true;
+        for (uint64_t i = 1; eq && i < n; ++i) eq = get(i) == (uint8_t)tok[k][i];
+        if (eq) return true;
+    }
+    return false;
+}
+
+// sink with first / last byte tracking over a RegSink (soft bits need them, hpack.c:136-152)
+struct ArenaSinkFL {
+    RegSink s;
+    uint32_t first, last;
+    __device__ __forceinline__ void put1(uint32_t b) {
+        first = s.cnt == 0 ? (b & 0xFFu) : first;
+        last = b & 0xFFu;
+        s.put1(b);
+    }
+    __device__ __forceinline__ void put12(uint32_t syms, bool two) {
+        first = s.cnt == 0 ? (syms & 0xFFu) : first;
+        last = (two ? (syms >> 8) : syms) & 0xFFu;
+        s.put12(syms, two);
+    }
+    __device__ __forceinline__ uint32_t count() const { return s.count(); }
+};
+
+// byte-ring sink: writes the first `cap` bytes at ring[pos...] (wrapping), counts them all
+struct RingSinkFL {
+    uint8_t* ring;
+    uint32_t RB, pos, cnt, cap, first, last;
+    __device__ __forceinline__ void put1(uint32_t b) {
+        b &= 0xFFu;
+        first = cnt == 0 ? b : first;
+        last = b;
+        if (cnt < cap) {
+            ring[pos] = (uint8_t)b;
+            pos = pos + 1 == RB ? 0u : pos + 1;
+        }
+        ++cnt;
+    }
+    __device__ __forceinline__ void put12(uint32_t syms, bool two) {
+        put1(syms);
+        if (two) put1(syms >> 8);
+    }
+    __device__ __forceinline__ uint32_t count() const { return cnt; }
+};
+
+struct QTable {  // one connection's table, as the kernels see it
+    uint8_t* ring;
+    uint4* ent;  // {byte offset, name length, value length, soft bits}
+    uint32_t RB, E;
+    QState s;
+    __device__ __forceinline__ uint4 get(uint32_t k) const {  // k-th oldest live entry
+        uint32_t i = s.start + k;
+        return ent[i >= E ? i - E : i];
+    }
+    __device__ __forceinline__ int64_t total() const { return s.base_offset + (int64_t)s.num; }  // :321-324
+    __device__ __forceinline__ bool resolve_abs(int64_t index, uint4& e) const {  // resolve_dynamic_abs :201-213
+        if (index < s.base_offset || index - s.base_offset >= (int64_t)s.num) return false;
+        e = get((uint32_t)(index - s.base_offset));
+        return true;
+    }
+    __device__ __forceinline__ uint32_t at(uint32_t off) const {  // off < 2 RB
+        return ring[off >= RB ? off - RB : off];
+    }
+    __device__ void evict(uint64_t delta) {  // header_table_evict (:153-164)
+        while (s.num != 0 && s.num_bytes + delta > s.max_size) {
+            const uint4 e = get(0);
+            s.num_bytes -= (uint64_t)e.y + e.z + kEntryOverhead;
+            s.start = s.start + 1 == E ? 0u : s.start + 1;
+            --s.num;
+            ++s.base_offset;
+        }
+    }
+    // book an entry whose nlen + vlen bytes were written at ring[w0...] (header_table_insert :166-190)
+    __device__ void commit(uint32_t w0, uint32_t nlen, uint32_t vlen, uint32_t soft) {
+        const uint64_t add = (uint64_t)nlen + vlen + kEntryOverhead;
+        evict(add);
+        const uint32_t i = s.start + s.num;
+        ent[i >= E ? i - E : i] = make_uint4(w0, nlen, vlen, soft);
+        ++s.num;
+        s.num_bytes += add;
+        ++s.total_inserts;
+        s.whead = (uint32_t)(((uint64_t)w0 + nlen + vlen) % RB);
+    }
+};
+
+// writes n bytes get(0..n-1) at ring[pos...], at most `room` of them
+template <class Get>
+__device__ void ring_put(QTable& t, uint32_t pos, Get get, uint64_t n, uint32_t room) {
+    const uint64_t m = n < room ? n : room;
+    for (uint64_t i = 0; i < m; ++i) {
+        t.ring[pos] = (uint8_t)get(i);
+        pos = pos + 1 == t.RB ? 0u : pos + 1;
+    }
+}
+
+// the value half of an insert (decode_value_and_insert :273-287) once the name sits at ring[w0, +nlen)
+__device__ int32_t q_value_and_insert(QTable& t, const QpkArgs& A, uint32_t w0, uint64_t nlen, uint32_t soft,
+                                      bool vhuff, uint64_t vp, uint64_t vlen, const DecTables& T) {
+    const uint32_t cap = A.T;
+    const uint32_t room = nlen < cap ? cap - (uint32_t)nlen : 0u;
+    const uint32_t vpos = (uint32_t)(((uint64_t)w0 + (nlen < cap ? nlen : cap)) % t.RB);
+    uint64_t r;
+    if (vhuff) {
+        if (vlen > kMaxStrLen) return kDF;
+        RingSinkFL sk{t.ring, t.RB, vpos, 0u, room, 0u, 0u};
+        const DecResult d = decode_core(GlobalSource{A.in, A.in_size}, (uint32_t)vp, (uint32_t)vlen, sk, T);
+        if (!d.ok) return kDF;
+        soft |= soft_bits(false, d.len, d.flags, sk.first, sk.last);
+        r = d.len;
+    } else {
+        const uint8_t* src = A.in + vp;
+        q_valid_value([&](uint64_t i) { return (uint32_t)src[i]; }, vlen, soft);
+        ring_put(t, vpos, [&](uint64_t i) { return (uint32_t)src[i]; }, vlen, room);
+        r = vlen;
+    }
+    if (nlen + r + kEntryOverhead > t.s.max_size) return kDF;  // header exceeds table size (:278-281)
+    t.commit(w0, (uint32_t)nlen, (uint32_t)r, soft);
+    return 0;
+}
+
+// h2o_qpack_decoder_handle_input (qpack.c:420-485) over in[p, end)
+__device__ int32_t q_handle_input(QTable& t, const QpkArgs& A, uint64_t p, uint64_t end, uint32_t& consumed,
+                                  uint64_t& insert_count, const DecTables& T) {
+    const uint8_t* in = A.in;
+    const uint64_t p0 = p;
+    uint64_t done = p;
+    const uint64_t old_total = t.s.total_inserts;
+    int32_t ret = 0;
+    insert_count = 0;
+    while (p != end && ret == 0) {
+        const uint32_t b = in[p];
+        switch (b >> 5) {
+            default: {  // insert with name reference (:430-444)
+                int64_t name_index, value_len;
+                const bool name_is_static = (b & 0x40u) != 0;
+                if ((ret = q_int(name_index, in, p, end, 6)) != 0) goto Exit;
+                if (p == end) goto Exit;
+                const bool vhuff = (in[p] & 0x80u) != 0;
+                if ((ret = q_int(value_len, in, p, end, 7)) != 0) goto Exit;
+                if (!((uint64_t)value_len <= end - p)) goto Exit;
+                const uint32_t w0 = t.s.whead;
+                if (name_is_static) {  // insert_token_header (:289-300): soft starts at 0
+                    if ((uint64_t)name_index >= kQStaticCount) {
+                        ret = kDF;
+                    } else {
+                        const uint32_t k = 4u * (uint32_t)name_index;
+                        const uint32_t no = q_static_ent[k], nl = q_static_ent[k + 1];
+                        ring_put(t, w0, [&](uint64_t i) { return (uint32_t)q_static_bytes[no + i]; }, nl, A.T);
+                        ret = q_value_and_insert(t, A, w0, nl, 0u, vhuff, p, (uint64_t)value_len, T);
+                    }
+                } else {  // dynamic (:335-348): token names carry no name bit, literal names keep theirs
+                    const int64_t base_index = t.total() - 1;
+                    uint4 e;
+                    if (name_index > base_index || !t.resolve_abs(base_index - name_index, e)) {
+                        ret = kDF;
+                    } else {
+                        ring_put(t, w0, [&](uint64_t i) { return t.at(e.x + (uint32_t)i); }, e.y, A.T);
+                        ret = q_value_and_insert(t, A, w0, e.y, e.w & 0x1u, vhuff, p, (uint64_t)value_len, T);
+                    }
+                }
+                p += (uint64_t)value_len;
+            } break;
+            case 2:
+            case 3: {  // insert without name reference (:446-462, :352-393)
+                int64_t name_len, value_len;
+                const bool nhuff = (b & 0x20u) != 0;
+                if ((ret = q_int(name_len, in, p, end, 5)) != 0) goto Exit;
+                if (!((uint64_t)name_len < end - p)) goto Exit;
+                const uint64_t qn = p;
+                p += (uint64_t)name_len;
+                const bool vhuff = (in[p] & 0x80u) != 0;
+                if ((ret = q_int(value_len, in, p, end, 7)) != 0) goto Exit;
+                if (!((uint64_t)value_len <= end - p)) goto Exit;
+                uint32_t soft = 0;
+                const uint32_t w0 = t.s.whead;
+                uint64_t nl = 0;
+                bool ok = true;
+                if (nhuff) {
+                    if ((uint64_t)name_len > kMaxStrLen) {
+                        ok = false;
+                    } else {
+                        RingSinkFL sk{t.ring, t.RB, w0, 0u, A.T, 0u, 0u};
+                        const DecResult d =
+                            decode_core(GlobalSource{A.in, A.in_size}, (uint32_t)qn, (uint32_t)name_len, sk, T);
+                        ok = d.ok;
+                        if (ok) soft |= soft_bits(true, d.len, d.flags, sk.first, sk.last);
+                        nl = d.len;
+                    }
+                } else {
+                    const uint8_t* src = in + qn;
+                    ok = q_valid_name([&](uint64_t i) { return (uint32_t)src[i]; }, (uint64_t)name_len, soft);
+                    if (ok) ring_put(t, w0, [&](uint64_t i) { return (uint32_t)src[i]; }, (uint64_t)name_len, A.T);
+                    nl = (uint64_t)name_len;
+                }
+                if (!ok) {
+                    ret = kDF;
+                } else {
+                    // a name h2o_lookup_token knows goes in as a token header with soft bits 0 (:383-384)
+                    if (soft && nl <= A.T && q_pseudo_token([&](uint64_t i) { return t.at(w0 + (uint32_t)i); }, nl))
+                        soft = 0;
+                    ret = q_value_and_insert(t, A, w0, nl, soft, vhuff, p, (uint64_t)value_len, T);
+                }
+                p += (uint64_t)value_len;
+            } break;
+            case 0: {  // duplicate (:463-468, :395-406)
+                int64_t index;
+                if ((ret = q_int(index, in, p, end, 5)) != 0) goto Exit;
+                if (index >= (int64_t)t.s.num) {
+                    ret = kDF;
+                } else {
+                    const uint4 e = t.get(t.s.num - 1u - (uint32_t)index);
+                    const uint32_t w0 = t.s.whead;
+                    ring_put(t, w0, [&](uint64_t i) { return t.at(e.x + (uint32_t)i); }, (uint64_t)e.y + e.z, A.T);
+                    t.commit(w0, e.y, e.z, e.w);
+                }
+            } break;
+            case 1: {  // set dynamic table capacity (:469-474, :408-418)
+                int64_t max_size;
+                if ((ret = q_int(max_size, in, p, end, 5)) != 0) goto Exit;
+                if (max_size > (int64_t)A.T) {
+                    ret = kDF;
+                } else {
+                    t.s.max_size = (uint64_t)max_size;
+                    t.evict(0);
+                }
+            } break;
+        }
+        done = p;
+    }
+Exit:
+    if (ret == kQIncomplete) ret = 0;
+    if (ret == 0 && old_total != t.s.total_inserts) insert_count = t.s.total_inserts;
+    consumed = (uint32_t)(done - p0);
+    return ret;
+}
+
+__device__ __forceinline__ QTable q_table(const QpkArgs& A, uint64_t c) {
+    uint8_t* scr = A.scratch + c * A.conn_scratch;
+    const uint32_t RB = qpk_ring_bytes(A.T);
+    uint8_t* ring = scr + sizeof(QState);
+    QTable t{ring, reinterpret_cast<uint4*>(ring + RB), RB, A.T / kEntryOverhead + 1u, {}};
+    t.s = *reinterpret_cast<const QState*>(scr);
+    return t;
+}
+
+__device__ __forceinline__ void load_dec_tables(uint32_t* s_lut, uint32_t* s_kinfo, uint32_t* s_ones) {
+    for (uint32_t k = threadIdx.x; k < (1u << HHUFF_LUT_BITS) / 4; k += blockDim.x)
+        reinterpret_cast<uint4*>(s_lut)[k] = reinterpret_cast<const uint4*>(q_dec_lut)[k];
+    for (uint32_t k = threadIdx.x; k < HHUFF_ONES_NENT; k += blockDim.x) s_ones[k] = q_ones[k];
+    if (threadIdx.x < 31) s_kinfo[threadIdx.x] = q_kinfo[threadIdx.x];
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void qpack_encoder_kernel(QpkArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
+    __shared__ uint32_t s_kinfo[32];
+    __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
+    load_dec_tables(s_lut, s_kinfo, s_ones);
+    const DecTables T{s_lut, s_kinfo, s_ones};
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < A.nconn; c += (uint64_t)gridDim.x * blockDim.x) {
+        QState* ps = reinterpret_cast<QState*>(A.scratch + c * A.conn_scratch);
+        if (!(A.flags & HHUFF_QPK_CONTINUE)) {  // h2o_qpack_create_decoder (:240-252)
+            QState s0{};
+            s0.base_offset = 1;
+            s0.max_size = A.T;
+            *ps = s0;
+        }
+        QTable t = q_table(A, c);
+        int32_t st = 0;
+        uint32_t consumed = 0;
+        uint64_t ic = 0;
+        if (t.s.failed) {
+            st = HHUFF_QPK_SKIPPED;
+        } else if (A.enc_len[c]) {
+            const uint64_t p = A.enc_off[c];
+            st = q_handle_input(t, A, p, p + A.enc_len[c], consumed, ic, T);
+            t.s.failed = st != 0;
+        }
+        A.enc_status[c] = st;
+        A.enc_consumed[c] = consumed;
+        A.insert_count[c] = ic;
+        *ps = t.s;
+    }
+}
+
+// ---- field sections ----
+
+struct QCtx {
+    int64_t ric, base;
+};
+
+// parse_decode_context (qpack.c:754-799)
+__device__ int32_t q_parse_context(const QTable& t, uint32_t max_entries, QCtx& ctx, const uint8_t* in, uint64_t& p,
+                                   uint64_t end) {
+    int64_t ric, delta;
+    if (q_int(ric, in, p, end, 8) != 0) return kDF;
+    if (ric > 0) {
+        if (max_entries == 0) return kDF;
+        const uint32_t full_range = 2 * max_entries;
+        const uint64_t max_value = t.s.total_inserts + max_entries;
+        const uint64_t rounded = max_value / full_range * full_range;
+        ric = (int64_t)((uint64_t)ric + rounded - 1);
+        if ((uint64_t)ric > max_value) {
+            if (ric <= (int64_t)full_range) return kDF;
+            ric -= full_range;
+        }
+        if (ric == 0) return kDF;
+        if (ric > kQuicIntMax) return kDF;
+    }
+    ctx.ric = ric;
+    if (p >= end) return kDF;
+    const bool sign = (in[p] & 0x80u) != 0;
+    if (q_int(delta, in, p, end, 7) != 0) return kDF;
+    if (delta > kQuicIntMax) return kDF;
+    ctx.base = sign ? ric - delta - 1 : ric + delta;
+    if (ctx.base < 0) return kDF;
+    return 0;
+}
+
+// resolve_dynamic / resolve_dynamic_postbase (qpack.c:523-557)
+__device__ bool q_dyn(const QTable& t, const QCtx& ctx, const uint8_t* in, uint64_t& p, uint64_t end, uint32_t prefix,
+                      bool postbase, uint4& e) {
+    int64_t off, index;
+    if (q_int(off, in, p, end, prefix) != 0) return false;
+    if (postbase) {
+        if (off > INT64_MAX - ctx.base - 1) return false;
+        index = ctx.base + off + 1;
+    } else {
+        if (off >= ctx.base) return false;
+        index = ctx.base - off;
+    }
+    if (ctx.ric < index) return false;
+    return t.resolve_abs(index, e);
+}
+
+struct QArena {
+    uint8_t* a;
+    uint64_t cur, end;
+};
+
+__device__ __forceinline__ int32_t q_copy_static(QArena& R, uint32_t so, uint32_t n, uint32_t& off) {
+    if (R.cur + n > R.end) return HHUFF_QPK_ARENA;
+    for (uint32_t i = 0; i < n; ++i) R.a[R.cur + i] = q_static_bytes[so + i];
+    off = (uint32_t)R.cur;
+    R.cur += n;
+    return 0;
+}
+
+__device__ __forceinline__ int32_t q_copy_ring(QArena& R, const QTable& t, uint32_t ro, uint32_t n, uint32_t& off) {
+    if (R.cur + n > R.end) return HHUFF_QPK_ARENA;
+    if (ro >= t.RB) ro -= t.RB;
+    for (uint32_t i = 0; i < n; ++i) {
+        R.a[R.cur + i] = t.ring[ro];
+        ro = ro + 1 == t.RB ? 0u : ro + 1;
+    }
+    off = (uint32_t)R.cur;
+    R.cur += n;
+    return 0;
+}
+
+// decode_header_value_literal (qpack.c:603-629) / decode_header_name_literal (:559-601, prefix 3)
+__device__ int32_t q_literal(const QpkArgs& A, QArena& R, uint32_t& soft, uint64_t& p, uint64_t end, bool is_name,
+                             uint32_t& off, uint32_t& len, const DecTables& T) {
+    const uint8_t* in = A.in;
+    if (!is_name && !(p < end)) return kDF;
+    const uint32_t prefix = is_name ? 3u : 7u;
+    const bool huff = ((in[p] >> prefix) & 1u) != 0;
+    int64_t n;
+    if (q_int(n, in, p, end, prefix) != 0) return kDF;
+    if ((int64_t)(end - p) < n) return kDF;
+    if (huff) {
+        if (R.cur + ((uint64_t)n * 8u) / 5u > R.end) return HHUFF_QPK_ARENA;
+        if ((uint64_t)n > kMaxStrLen) return kDF;
+        ArenaSinkFL sk{RegSink{}, 0u, 0u};
+        sk.s.init(R.a + R.cur);
+        const DecResult d = decode_core(GlobalSource{A.in, A.in_size}, (uint32_t)p, (uint32_t)n, sk, T);
+        if (!d.ok) return kDF;
+        sk.s.finish();
+        soft |= soft_bits(is_name, d.len, d.flags, sk.first, sk.last);
+        len = d.len;
+    } else {
+        const uint8_t* src = in + p;
+        auto get = [&](uint64_t i) { return (uint32_t)src[i]; };
+        if (is_name) {  // tokens are taken as they are; anything else is validated (:583-588)
+            if (!q_pseudo_token(get, (uint64_t)n) && !q_valid_name(get, (uint64_t)n, soft)) return kDF;
+        } else {
+            q_valid_value(get, (uint64_t)n, soft);
+        }
+        if (R.cur + (uint64_t)n > R.end) return HHUFF_QPK_ARENA;
+        for (int64_t i = 0; i < n; ++i) R.a[R.cur + i] = src[i];
+        len = (uint32_t)n;
+    }
+    off = (uint32_t)R.cur;
+    R.cur += len;
+    p += (uint64_t)n;
+    return 0;
+}
+
+// decode_header (qpack.c:652-752): 0 / kErrInvalidChar = a field was produced
+__device__ int32_t q_field(const QpkArgs& A, const QTable& t, const QCtx& ctx, uint64_t& p, uint64_t end, QArena& R,
+                           uint32_t& noff, uint32_t& nlen, uint32_t& voff, uint32_t& vlen, uint32_t& soft_out,
+                           const DecTables& T) {
+    const uint8_t* in = A.in;
+    uint32_t soft = 0;
+    int32_t r;
+    uint4 e;
+    const uint32_t kind = in[p] >> 4;
+    switch (kind) {
+        case 12:
+        case 13:
+        case 14:
+        case 15: {  // indexed field line, static (:659-669)
+            int64_t si;
+            if (q_int(si, in, p, end, 6) != 0 || (uint64_t)si >= kQStaticCount) return kDF;
+            const uint32_t k = 4u * (uint32_t)si;
+            nlen = q_static_ent[k + 1];
+            if ((r = q_copy_static(R, q_static_ent[k], nlen, noff)) != 0) return r;
+            vlen = q_static_ent[k + 3];
+            if ((r = q_copy_static(R, q_static_ent[k + 2], vlen, voff)) != 0) return r;
+        } break;
+        case 8:
+        case 9:
+        case 10:
+        case 11:  // indexed field line, dynamic (:670-682)
+        case 1:   // indexed field line, post-base (:713-722)
+            if (!q_dyn(t, ctx, in, p, end, kind == 1 ? 4u : 6u, kind == 1, e)) return kDF;
+            if ((r = q_copy_ring(R, t, e.x, e.y, noff)) != 0) return r;
+            if ((r = q_copy_ring(R, t, e.x + e.y, e.z, voff)) != 0) return r;
+            nlen = e.y;
+            vlen = e.z;
+            soft = e.w;
+            break;
+        case 5:
+        case 7: {  // literal field line, static name reference (:683-692)
+            int64_t si;
+            if (q_int(si, in, p, end, 4) != 0 || (uint64_t)si >= kQStaticCount) return kDF;
+            const uint32_t k = 4u * (uint32_t)si;
+            nlen = q_static_ent[k + 1];
+            if ((r = q_copy_static(R, q_static_ent[k], nlen, noff)) != 0) return r;
+            if ((r = q_literal(A, R, soft, p, end, false, voff, vlen, T)) != 0) return r;
+        } break;
+        case 4:
+        case 6:  // literal field line, dynamic name reference (:693-704)
+        case 0:  // literal field line, post-base name reference (:723-733)
+            if (!q_dyn(t, ctx, in, p, end, kind == 0 ? 3u : 4u, kind == 0, e)) return kDF;
+            if ((r = q_copy_ring(R, t, e.x, e.y, noff)) != 0) return r;
+            nlen = e.y;
+            soft = e.w & 0x1u;
+            if ((r = q_literal(A, R, soft, p, end, false, voff, vlen, T)) != 0) return r;
+            break;
+        default:  // 2, 3: literal field line with a literal name (:705-712)
+            if ((r = q_literal(A, R, soft, p, end, true, noff, nlen, T)) != 0) return r;
+            if ((r = q_literal(A, R, soft, p, end, false, voff, vlen, T)) != 0) return r;
+            break;
+    }
+    soft_out = soft;
+    return soft ? kErrInvalidChar : 0;
+}
+
+__global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
+    __shared__ uint32_t s_kinfo[32];
+    __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
+    load_dec_tables(s_lut, s_kinfo, s_ones);
+    const DecTables T{s_lut, s_kinfo, s_ones};
+    const uint32_t max_entries = A.T / kEntryOverhead;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < A.nsec; k += (uint64_t)gridDim.x * blockDim.x) {
+        // the section's connection: the last c with conn_first[c] <= k
+        uint32_t lo = 0, hi = A.nconn;  // invariant: conn_first[lo] <= k < conn_first[hi]
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (A.conn_first[mid] <= k)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        const QTable t = q_table(A, lo);
+        A.nfields[k] = 0;
+        A.req_insert_count[k] = 0;
+        if (t.s.failed) {
+            A.sstatus[k] = HHUFF_QPK_SKIPPED;
+            continue;
+        }
+        uint64_t p = A.sec_off[k];
+        const uint64_t end = A.sec_off[k + 1];
+        QCtx ctx{0, 0};
+        int32_t st = q_parse_context(t, max_entries, ctx, A.in, p, end);
+        if (st == 0) {
+            A.req_insert_count[k] = (uint64_t)ctx.ric;
+            // check_decode_context_blocked (:801-820)
+            const uint64_t nb = A.num_blocked ? A.num_blocked[lo] : 0u;
+            if (!(ctx.ric < t.total())) st = nb >= A.max_blocked ? kDF : HHUFF_QPK_BLOCKED;
+        }
+        QArena R{A.arena, A.arena_off[k], A.arena_off[k + 1]};
+        const uint32_t slot = A.sec_off[k];
+        uint32_t nf = 0;
+        while (st == 0 && p != end) {
+            uint32_t no = 0, nl = 0, vo = 0, vl = 0, soft = 0;
+            const int32_t rc = q_field(A, t, ctx, p, end, R, no, nl, vo, vl, soft, T);
+            if (rc != 0 && rc != kErrInvalidChar) {
+                st = rc;
+                break;
+            }
+            A.name_off[slot + nf] = no;
+            A.name_len[slot + nf] = nl;
+            A.value_off[slot + nf] = vo;
+            A.value_len[slot + nf] = vl;
+            A.fflags[slot + nf] = (uint8_t)soft;
+            ++nf;
+        }
+        A.nfields[k] = nf;
+        A.sstatus[k] = st;
+    }
+}
+
+uint64_t qpack_conn_scratch(uint32_t header_table_size) {
+    return sizeof(QState) + qpk_ring_bytes(header_table_size) + 16ull * (header_table_size / kEntryOverhead + 1u);
+}
+
+hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off, const uint32_t* enc_len,
+                        const uint32_t* sec_off, const uint32_t* conn_first, uint32_t nconn, uint32_t nsec,
+                        uint32_t header_table_size, uint64_t max_blocked, const uint32_t* num_blocked, uint8_t* arena,
+                        const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len, uint32_t* value_off,
+                        uint32_t* value_len, uint8_t* fflags, uint32_t* nfields, int32_t* sstatus,
+                        uint64_t* req_insert_count, int32_t* enc_status, uint32_t* enc_consumed, uint64_t* insert_count,
+                        uint8_t* scratch, uint32_t flags, hipStream_t stream) {
+    if (nconn == 0) return hipSuccess;
+    QpkArgs A{in, in_size, enc_off, enc_len, sec_off, conn_first, num_blocked, nconn, nsec, header_table_size,
+              max_blocked, arena, arena_off, name_off, name_len, value_off, value_len, fflags, nfields, sstatus,
+              req_insert_count, enc_status, enc_consumed, insert_count, scratch, qpack_conn_scratch(header_table_size),
+              flags};
+    hipLaunchKernelGGL(qpack_encoder_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || nsec == 0) return e;
+    hipLaunchKernelGGL(qpack_sections_kernel, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
+    return hipGetLastError();
+}
+
+}  // namespace hhuff

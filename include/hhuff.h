@@ -166,6 +166,50 @@ int hhuff_hpack_decode_blocks(const uint8_t *in, uint64_t in_size, const uint32_
                               uint8_t *fflags, uint32_t *nfields, int32_t *bstatus, void *scratch, uint64_t scratch_size,
                               unsigned flags, void *stream);
 
+/* (2d) QPACK decoder (QPACK half): h2o's QPACK decoder (lib/http3/qpack.c) for many
+ *      connections at once.  One call is one step of every connection c:
+ *        encoder stream  in[enc_off[c] .. + enc_len[c]): h2o_qpack_decoder_handle_input (qpack.c:420-485,
+ *                        decl. include/h2o/qpack.h) -- the caller's encoder-stream receive buffer, i.e. the
+ *                        bytes not consumed by the previous step followed by the new ones
+ *        field sections  conn_first[c] .. conn_first[c+1]-1, section k = in[sec_off[k] .. sec_off[k+1])
+ *                        (packed back to back): what h2o_qpack_parse_request (qpack.c:830-858) reads --
+ *                        parse_decode_context, check_decode_context_blocked, then decode_header field after
+ *                        field -- against the table as the connection's encoder stream left it
+ *        header_table_size  the decoder's SETTINGS_QPACK_MAX_TABLE_CAPACITY (h2o_qpack_create_decoder,
+ *                        qpack.c:240); max_blocked its blocked-streams limit; num_blocked[c] (NULL = 0) the
+ *                        caller's count of the connection's blocked streams (lib/http3/server.c:1544)
+ *      Per connection: enc_status[c] = 0, HHUFF_QPK_DECOMPRESSION_FAILED (h2o then closes the connection
+ *      with H2O_HTTP3_ERROR_QPACK_ENCODER_STREAM) or HHUFF_QPK_SKIPPED (an earlier step failed);
+ *      enc_consumed[c] = bytes of complete instructions consumed (the rest waits for more input);
+ *      insert_count[c] as handle_input reports it (the new Insert Count, 0 when nothing was inserted).
+ *      Per section k: sstatus[k] = 0, HHUFF_QPK_DECOMPRESSION_FAILED, HHUFF_QPK_BLOCKED (Required Insert
+ *      Count not reached and a blocked slot free: h2o parks the stream until more inserts arrive),
+ *      HHUFF_QPK_ARENA (a string does not fit arena[arena_off[k] .. arena_off[k+1]): a Huffman literal
+ *      needs floor(8 len / 5) bytes free, a raw one len, an indexed one its size) or HHUFF_QPK_SKIPPED;
+ *      req_insert_count[k] (decoded Required Insert Count, for the Section Acknowledgment); nfields[k]
+ *      fields in slots sec_off[k] .. + nfields[k] - 1: name_off/name_len/value_off/value_len (arena
+ *      offsets) and fflags = soft bits (HHUFF_SOFT_NAME / _VALUE: decode_header's
+ *      H2O_HTTP2_ERROR_INVALID_HEADER_CHAR).  Fields before an error stand.
+ *      Device arrays; scratch = hhuff_qpack_scratch_size(nconn, header_table_size) bytes of device memory
+ *      (16-byte aligned) that holds the tables: pass HHUFF_QPK_CONTINUE to carry them (and the failed
+ *      state) over from the previous call -- connection c of this call is connection c of that one;
+ *      without it every connection starts with a fresh decoder.  nsec = conn_first[nconn] (host copy).
+ *      Asynchronous on `stream` (two launches: encoder streams one lane per connection, then sections
+ *      one lane per section). */
+#define HHUFF_QPK_CONTINUE 1u
+#define HHUFF_QPK_DECOMPRESSION_FAILED 0x30200 /* H2O_HTTP3_ERROR_QPACK_DECOMPRESSION_FAILED, http3_common.h:73 */
+#define HHUFF_QPK_ARENA (-300)
+#define HHUFF_QPK_SKIPPED (-301)
+#define HHUFF_QPK_BLOCKED (-302)
+uint64_t hhuff_qpack_scratch_size(uint32_t nconn, uint32_t header_table_size);
+int hhuff_qpack_decode(const uint8_t *in, uint64_t in_size, const uint32_t *enc_off, const uint32_t *enc_len,
+                       const uint32_t *sec_off, const uint32_t *conn_first, uint32_t nconn, uint32_t nsec,
+                       uint32_t header_table_size, uint64_t max_blocked, const uint32_t *num_blocked, uint8_t *arena,
+                       const uint64_t *arena_off, uint32_t *name_off, uint32_t *name_len, uint32_t *value_off,
+                       uint32_t *value_len, uint8_t *fflags, uint32_t *nfields, int32_t *sstatus,
+                       uint64_t *req_insert_count, int32_t *enc_status, uint32_t *enc_consumed, uint64_t *insert_count,
+                       void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
+
 /* (3b) Pipelined host path (the socket-buffer -> pinned -> device -> pinned -> pool staging of
  *     SURVEY f3; replaces the caller-side copies around lib/http2/hpack.c:240-241).  Contiguous layout
  *     (in_off[n + 1], implicit output slots) only.  The batch is cut into chunks of about

@@ -540,7 +540,104 @@ def blocks_sets():
     return out
 
 
+QPACK_SESSIONS = [  # name, seed, connections, steps, header_table_size, max_blocked, adversarial fraction
+    ("q4096", 61, 300, 4, 4096, 4, 0.3),
+    ("q256", 62, 150, 3, 256, 2, 0.3),
+    ("q0", 63, 100, 2, 0, 0, 0.2),
+]
+
+
+def qpack_edge_session():
+    """hand-built connections (one step): empty inputs, truncated and bad instructions, the corner cases of
+    Required Insert Count / Base, post-base references, pseudo-header token names, raw upper-case names"""
+    from h2o_amd import qpack_synth as QS
+
+    q, i = QS.qstring, QS.encode_int
+    www = q(b"www.example.com")
+    conns = [
+        (b"", [b"", b"\x00", b"\x00\x00", b"\x00\x00\xd1", b"\x00\x80\xd1", b"\x00\x00\xff\x3f"]),
+        # insert :authority=www.example.com (static name 0), then read it back (RFC 9204 B.2 shape)
+        (i(0, 6, 0xC0) + www, [b"\x02\x00\x80", b"\x02\x80\x10", b"\x02\x81\x10", b"\x03\x00\x80",
+                               b"\x02\x00\x81", b"\x00\x00\x80", b"\x02\x00\x40" + q(b"v")]),
+        # literal-name inserts: token pseudo-header raw (soft dropped), odd chars (soft kept), upper case (fail)
+        (q(b":path", 5, 0x40, True) + q(b"/a", 7, 0, True) + q(b"x y", 5, 0x40, True) + q(b"v", 7, 0),
+         [b"\x03\x00\x80\x81", b"\x03\x00\x41" + q(b"\x01bad")]),
+        (q(b"X-Upper", 5, 0x40, True) + q(b"v", 7, 0), [b"\x00\x00\xd1"]),
+        # duplicate, capacity update to 0 (evicts all), capacity above the table size
+        (i(0, 6, 0xC0) + www + i(0, 5, 0x00) + i(0, 5, 0x20), [b"\x03\x00\x80", b"\x00\x00\xd1"]),
+        (i(5000, 5, 0x20), [b"\x00\x00\xd1"]),
+        # truncated instruction (waits for more input), then a section blocked on it
+        (i(0, 6, 0xC0) + www[:5], [b"\x02\x00\x80"]),
+        # entry larger than the table; dynamic name reference past the table
+        (q(b"x-big", 5, 0x40) + q(b"v" * 5000, 7, 0, True), []),
+        (i(7, 6, 0x80) + q(b"v"), []),
+        # literal lines: static name with Huffman / raw values, literal names Huffman / raw / empty
+        (b"", [b"\x00\x00\x51" + q(b"/index.html"), b"\x00\x00\x5f\x00" + q(b" lead", 7, 0, True),
+               b"\x00\x00" + q(b"custom-key", 3, 0x20) + q(b"custom-value"),
+               b"\x00\x00" + q(b"", 3, 0x20, True) + q(b"v"), b"\x00\x00" + q(b":status", 3, 0x20, True) + q(b"200"),
+               b"\x00\x00" + q(b"Upper", 3, 0x20, True) + q(b"v"), b"\x00\x00\x2f\xff\xff\xff\xff\xff\xff\xff\xff\xff\x7f"]),
+    ]
+    sec, sec_len, cf, enc = [], [], [0], []
+    for e, ss in conns:
+        sec += ss
+        sec_len += [len(x) for x in ss]
+        cf.append(len(sec_len))
+        enc.append(e)
+    sec_off = np.zeros(len(sec_len) + 1, np.uint64)
+    sec_off[1:] = np.cumsum(sec_len)
+    base = int(sec_off[-1])
+    enc_off = base + np.concatenate([[0], np.cumsum([len(e) for e in enc])[:-1]]).astype(np.uint64)
+    return [dict(data=np.frombuffer(b"".join(sec) + b"".join(enc), np.uint8).copy(), sec_off=sec_off.astype(np.uint32),
+                 conn_first=np.asarray(cf, np.uint32), enc_off=enc_off.astype(np.uint32),
+                 enc_len=np.asarray([len(e) for e in enc], np.uint32), header_table_size=4096)]
+
+
+def qpack_set():
+    """tests/golden/qpack.npz: QPACK decoder sessions run through the reference's own decoder (oracle/_ref,
+    qpack.c included: h2o_qpack_decoder_handle_input, parse_decode_context, check_decode_context_blocked,
+    decode_header); per session the step inputs and the reference's outputs"""
+    from h2o_amd import qpack_synth as QS
+
+    out = {}
+    sessions = [(n, QS.make_session(nc, steps=st, seed=sd, header_table_size=h, adversarial_frac=adv), nc, h, mb)
+                for n, sd, nc, st, h, mb, adv in QPACK_SESSIONS]
+    sessions.append(("qedge", qpack_edge_session(), 10, 4096, 2))
+    for name, steps, nconn, hts, mb in sessions:
+        sr = O.QpackSession(O.ref(), nconn, hts, mb)
+        nbl = (np.arange(nconn) % 6).astype(np.uint32)
+        out[name + "_meta"] = np.asarray([nconn, hts, mb, len(steps)], np.uint32)
+        out[name + "_num_blocked"] = nbl
+        for k, st in enumerate(steps):
+            ao = QS.arena_offsets(st["sec_off"], hts)
+            r = sr.step(st["data"], st["enc_off"], st["enc_len"], st["sec_off"], st["conn_first"], ao, nbl)
+            ns = len(st["sec_off"]) - 1
+            names, values, soft = [], [], []
+            for s_ in range(ns):
+                o = int(st["sec_off"][s_])
+                for f in range(o, o + int(r["nfields"][s_])):
+                    names.append(r["arena"][r["name_off"][f]:r["name_off"][f] + r["name_len"][f]].tobytes())
+                    values.append(r["arena"][r["value_off"][f]:r["value_off"][f] + r["value_len"][f]].tobytes())
+                    soft.append(r["fflags"][f])
+            nd, no = pack(names)
+            vd, vo = pack(values)
+            p = "%s_%d_" % (name, k)
+            for key in ("data", "sec_off", "conn_first", "enc_off", "enc_len"):
+                out[p + key] = st[key]
+            out[p + "arena_off"] = ao
+            for key in ("nfields", "sstatus", "req_insert_count"):
+                out[p + key] = r[key][:ns]
+            for key in ("enc_status", "enc_consumed", "insert_count"):
+                out[p + key] = r[key][:nconn]
+            out[p + "fld_name"], out[p + "fld_name_off"], out[p + "fld_value"], out[p + "fld_value_off"] = nd, no, vd, vo
+            out[p + "fld_soft"] = np.asarray(soft, np.uint8)
+        sr.close()
+    return out
+
+
 def main():
+    if "--only-qpack" in sys.argv:
+        np.savez_compressed(os.path.join(GOLDEN, "qpack.npz"), **qpack_set())
+        return
     if "--only-blocks" in sys.argv:
         for name, arrays in blocks_sets().items():
             np.savez_compressed(os.path.join(GOLDEN, name + ".npz"), **arrays)
@@ -559,6 +656,7 @@ def main():
     sets["framing"] = framing_set()
     sets["literals"] = literals_set()
     sets.update(blocks_sets())
+    sets["qpack"] = qpack_set()
     for name, arrays in sets.items():
         path = os.path.join(GOLDEN, name + ".npz")
         np.savez_compressed(path, **arrays)

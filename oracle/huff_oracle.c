@@ -236,6 +236,8 @@ static int orc_is_pseudo_token(const uint8_t *s, size_t len)
     return 0;
 }
 
+int orc_is_qpack_token(const uint8_t *s, size_t len) { return orc_is_pseudo_token(s, len); }
+
 int orc_decode_literal(const uint8_t *lit, const uint8_t *end, unsigned prefix_bits, int is_name, int qpack,
                        uint8_t *out, uint64_t lit_pos, uint32_t *hdr, uint32_t *consumed, uint32_t *out_len,
                        unsigned *soft)

@@ -24,6 +24,10 @@
 #define ORC_ERR_INVALID_CHAR (-254)
 #define ORC_BLK_ARENA (-300)   /* HHUFF_BLK_ARENA: the block's arena slice is too small */
 #define ORC_BLK_SKIPPED (-301) /* HHUFF_BLK_SKIPPED: an earlier block of the connection failed */
+/* QPACK decoder (f4, QPACK half): h2o's codes (include/h2o/http3_common.h:73, :77) and the batch's own */
+#define ORC_QPK_DECOMPRESSION_FAILED 0x30200 /* H2O_HTTP3_ERROR_QPACK_DECOMPRESSION_FAILED (app code 0x200) */
+#define ORC_QPK_INCOMPLETE (-1)              /* H2O_HTTP3_ERROR_INCOMPLETE */
+#define ORC_QPK_BLOCKED (-302) /* HHUFF_QPK_BLOCKED: Required Insert Count not reached (*blocked_ref != 0) */
 
 size_t orc_decode_huffman(char *dst, unsigned *soft_errors, const uint8_t *src, size_t len, int is_name);
 size_t orc_encode_huffman(uint8_t *dst, const uint8_t *src, size_t len);
@@ -50,6 +54,14 @@ int orc_literals_batch(const uint8_t *in, const uint32_t *lit_off, const uint32_
 /* raw-literal validators (h2o_hpack_validate_header_name / _value, hpack.c:163-221) */
 int orc_validate_header_name(unsigned *soft, const uint8_t *s, size_t len);
 void orc_validate_header_value(unsigned *soft, const uint8_t *s, size_t len);
+int orc_is_qpack_token(const uint8_t *s, size_t len);
+void *orc_qpack_open(uint32_t nconn, uint32_t header_table_size, uint64_t max_blocked);
+void orc_qpack_close(void *h);
+int orc_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, const uint32_t *enc_len, const uint32_t *sec_off,
+                   const uint32_t *conn_first, const uint32_t *num_blocked, uint8_t *arena, const uint64_t *arena_off,
+                   uint32_t *name_off, uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,
+                   uint32_t *nfields, int32_t *sstatus, uint64_t *req_insert_count, int32_t *enc_status,
+                   uint32_t *enc_consumed, uint64_t *insert_count);
 int orc_hpack_decode_blocks(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
                             uint32_t table_size, uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off,
                             uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,

@@ -202,6 +202,57 @@ class _Codec:
         return r
 
 
+class QpackSession:
+    """QPACK decoder session (include/hhuff.h hhuff_qpack_decode contract): one dynamic table per connection,
+    kept between step() calls.  codec = oracle() (restatement) or ref() (h2o's qpack.c)."""
+
+    def __init__(self, codec, nconn, header_table_size=4096, max_blocked=100):
+        L, P = codec.lib, codec.prefix
+        self._open, self._close, self._step = (getattr(L, P + "_qpack_open"), getattr(L, P + "_qpack_close"),
+                                               getattr(L, P + "_qpack_step"))
+        self._open.restype = ctypes.c_void_p
+        self._open.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
+        self._close.argtypes = [ctypes.c_void_p]
+        self._step.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 19
+        self.nconn = nconn
+        self.h = self._open(nconn, header_table_size, max_blocked)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._close(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def step(self, data, enc_off, enc_len, sec_off, conn_first, arena_off, num_blocked=None):
+        """-> dict: arena, name_off, name_len, value_off, value_len, fflags (per field slot), nfields, sstatus,
+        req_insert_count (per section), enc_status, enc_consumed, insert_count (per connection)"""
+        c = lambda a, t: np.ascontiguousarray(a, dtype=t)  # noqa: E731
+        data, enc_off, enc_len, sec_off, conn_first = (c(data, np.uint8), c(enc_off, np.uint32), c(enc_len, np.uint32),
+                                                       c(sec_off, np.uint32), c(conn_first, np.uint32))
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        arena_off = c(arena_off, np.uint64)
+        nb = None if num_blocked is None else c(num_blocked, np.uint32)
+        ns = sec_off.size - 1
+        nslots = max(1, int(sec_off[-1]))
+        nc = max(1, self.nconn)
+        r = dict(arena=np.zeros(max(1, int(arena_off[-1])), np.uint8),
+                 name_off=np.zeros(nslots, np.uint32), name_len=np.zeros(nslots, np.uint32),
+                 value_off=np.zeros(nslots, np.uint32), value_len=np.zeros(nslots, np.uint32),
+                 fflags=np.zeros(nslots, np.uint8), nfields=np.zeros(max(1, ns), np.uint32),
+                 sstatus=np.zeros(max(1, ns), np.int32), req_insert_count=np.zeros(max(1, ns), np.uint64),
+                 enc_status=np.zeros(nc, np.int32), enc_consumed=np.zeros(nc, np.uint32),
+                 insert_count=np.zeros(nc, np.uint64))
+        d = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+        rc = self._step(self.h, d(data), d(enc_off), d(enc_len), d(sec_off), d(conn_first), d(nb), d(r["arena"]),
+                        d(arena_off), d(r["name_off"]), d(r["name_len"]), d(r["value_off"]), d(r["value_len"]),
+                        d(r["fflags"]), d(r["nfields"]), d(r["sstatus"]), d(r["req_insert_count"]), d(r["enc_status"]),
+                        d(r["enc_consumed"]), d(r["insert_count"]))
+        assert rc == 0
+        return r
+
+
 def default_arena_off(blk_off, table_size=4096):
     """A block of L bytes produces at most L fields; each field's name + value is at most 8/5 of its
     literal bytes or a copy of one table entry (<= table_size bytes): a generous bound per block."""

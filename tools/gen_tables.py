@@ -72,11 +72,48 @@ STATIC_TABLE = [
 ]
 assert len(STATIC_TABLE) == 61
 
+# RFC 9204 Appendix A QPACK static table (index 0..98).  The reference holds the same table in
+# lib/common/token_table.h (h2o_qpack_static_table); tests/test_qpack.py checks every index against the
+# reference's decoding of it.
+QPACK_STATIC_TABLE = [
+    (":authority", ""), (":path", "/"), ("age", "0"), ("content-disposition", ""), ("content-length", "0"),
+    ("cookie", ""), ("date", ""), ("etag", ""), ("if-modified-since", ""), ("if-none-match", ""),
+    ("last-modified", ""), ("link", ""), ("location", ""), ("referer", ""), ("set-cookie", ""),
+    (":method", "CONNECT"), (":method", "DELETE"), (":method", "GET"), (":method", "HEAD"), (":method", "OPTIONS"),
+    (":method", "POST"), (":method", "PUT"), (":scheme", "http"), (":scheme", "https"), (":status", "103"),
+    (":status", "200"), (":status", "304"), (":status", "404"), (":status", "503"), ("accept", "*/*"),
+    ("accept", "application/dns-message"), ("accept-encoding", "gzip, deflate, br"), ("accept-ranges", "bytes"),
+    ("access-control-allow-headers", "cache-control"), ("access-control-allow-headers", "content-type"),
+    ("access-control-allow-origin", "*"), ("cache-control", "max-age=0"), ("cache-control", "max-age=2592000"),
+    ("cache-control", "max-age=604800"), ("cache-control", "no-cache"), ("cache-control", "no-store"),
+    ("cache-control", "public, max-age=31536000"), ("content-encoding", "br"), ("content-encoding", "gzip"),
+    ("content-type", "application/dns-message"), ("content-type", "application/javascript"),
+    ("content-type", "application/json"), ("content-type", "application/x-www-form-urlencoded"),
+    ("content-type", "image/gif"), ("content-type", "image/jpeg"), ("content-type", "image/png"),
+    ("content-type", "text/css"), ("content-type", "text/html; charset=utf-8"), ("content-type", "text/plain"),
+    ("content-type", "text/plain;charset=utf-8"), ("range", "bytes=0-"), ("strict-transport-security", "max-age=31536000"),
+    ("strict-transport-security", "max-age=31536000; includesubdomains"),
+    ("strict-transport-security", "max-age=31536000; includesubdomains; preload"), ("vary", "accept-encoding"),
+    ("vary", "origin"), ("x-content-type-options", "nosniff"), ("x-xss-protection", "1; mode=block"),
+    (":status", "100"), (":status", "204"), (":status", "206"), (":status", "302"), (":status", "400"),
+    (":status", "403"), (":status", "421"), (":status", "425"), (":status", "500"), ("accept-language", ""),
+    ("access-control-allow-credentials", "FALSE"), ("access-control-allow-credentials", "TRUE"),
+    ("access-control-allow-headers", "*"), ("access-control-allow-methods", "get"),
+    ("access-control-allow-methods", "get, post, options"), ("access-control-allow-methods", "options"),
+    ("access-control-expose-headers", "content-length"), ("access-control-request-headers", "content-type"),
+    ("access-control-request-method", "get"), ("access-control-request-method", "post"), ("alt-svc", "clear"),
+    ("authorization", ""), ("content-security-policy", "script-src 'none'; object-src 'none'; base-uri 'none'"),
+    ("early-data", "1"), ("expect-ct", ""), ("forwarded", ""), ("if-range", ""), ("origin", ""), ("purpose", "prefetch"),
+    ("server", ""), ("timing-allow-origin", "*"), ("upgrade-insecure-requests", "1"), ("user-agent", ""),
+    ("x-forwarded-for", ""), ("x-frame-options", "deny"), ("x-frame-options", "sameorigin"),
+]
+assert len(QPACK_STATIC_TABLE) == 99
 
-def static_arrays():
-    """-> (bytes of all names and values back to back, [name_off, name_len, value_off, value_len] * 61)"""
+
+def static_arrays(table=None):
+    """-> (bytes of all names and values back to back, [name_off, name_len, value_off, value_len] per entry)"""
     blob, ent = bytearray(), []
-    for n, v in STATIC_TABLE:
+    for n, v in (STATIC_TABLE if table is None else table):
         ent += [len(blob), len(n)]
         blob += n.encode()
         ent += [len(blob), len(v)]
@@ -360,6 +397,15 @@ def product_header(lens, codes, order, lut, longt):
     out.append("#define HHUFF_STATIC_ENT_INIT { \\")
     out.append(fmt_array(ent, 16, "{}").replace("\n", " \\\n") + " \\\n}")
     out.append("")
+    qblob, qent = static_arrays(QPACK_STATIC_TABLE)
+    out.append("/* RFC 9204 Appendix A QPACK static table: names and values back to back, and per index 0..98")
+    out.append(" * {name_off, name_len, value_off, value_len} into them */")
+    out.append("#define HHUFF_QSTATIC_NBYTES %d" % len(qblob))
+    out.append("#define HHUFF_QSTATIC_BYTES_INIT { \\")
+    out.append(fmt_array(list(qblob), 24, "{}").replace("\n", " \\\n") + " \\\n}")
+    out.append("#define HHUFF_QSTATIC_ENT_INIT { \\")
+    out.append(fmt_array(qent, 16, "{}").replace("\n", " \\\n") + " \\\n}")
+    out.append("")
     return "\n".join(out)
 
 
@@ -397,6 +443,12 @@ def oracle_header(lens, codes, fsm):
     out.append("static const char *const orc_static_value[62] = {\"\",")
     out.append(",\n".join('    "%s"' % v for _, v in STATIC_TABLE) + "};")
     out.append("")
+    out.append("/* RFC 9204 Appendix A QPACK static table, indices 0..98 */")
+    out.append("static const char *const orc_qpack_static_name[99] = {")
+    out.append(",\n".join('    "%s"' % n for n, _ in QPACK_STATIC_TABLE) + "};")
+    out.append("static const char *const orc_qpack_static_value[99] = {")
+    out.append(",\n".join('    "%s"' % v for _, v in QPACK_STATIC_TABLE) + "};")
+    out.append("")
     return "\n".join(out)
 
 
@@ -409,6 +461,7 @@ def python_module(lens, codes):
         "ENC_CODE = (%s)" % ", ".join(str(c) for c in codes[:256]),
         "ENC_NBITS = (%s)" % ", ".join(str(l) for l in lens[:256]),
         "STATIC_TABLE = %r" % (tuple((n.encode(), v.encode()) for n, v in STATIC_TABLE),),
+        "QPACK_STATIC_TABLE = %r" % (tuple((n.encode(), v.encode()) for n, v in QPACK_STATIC_TABLE),),
         "EOS_CODE = %d" % codes[EOS],
         "EOS_NBITS = %d" % lens[EOS],
         "NAME_VALID = frozenset((%s))" % ", ".join(str(c) for c in sorted(NAME_VALID)),
