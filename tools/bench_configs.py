@@ -147,6 +147,65 @@ def blocks_line(torch, codec, nconn=65536):
     return line
 
 
+def qpack_line(torch, codec, nconn=65536):
+    """f4 (QPACK half): one decoder step of synthetic HTTP/3 connections (h2o_amd/qpack_synth.py: 1-4 requests
+    each, encoder-stream inserts then field sections, 1 % adversarial) -- encoder streams one lane per
+    connection, then sections one lane per section; the CPU baselines run the same step through the
+    reference's h2o_qpack_decoder_handle_input + decode_header (oracle/_ref, 1 thread, first 4096
+    connections) and the restatement (1 thread)"""
+    import time
+
+    from h2o_amd import qpack_synth as QS
+
+    st = QS.make_session(nconn, steps=1, seed=9, adversarial_frac=0.01)[0]
+    L = np.diff(st["sec_off"].astype(np.uint64))  # arena slice: 8/5 per literal byte, 64x per line byte
+    ao_np = np.concatenate([[0], np.cumsum((L * 8) // 5 + L * np.uint64(64) + np.uint64(512))]).astype(np.uint64)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
+    u32 = lambda a: dev(np.asarray(a, np.uint32).view(np.int32))  # noqa: E731
+    d, eo, el, so, cf = dev(st["data"]), u32(st["enc_off"]), u32(st["enc_len"]), u32(st["sec_off"]), u32(st["conn_first"])
+    ao = dev(ao_np.view(np.int64))
+    nsec = int(st["conn_first"][-1])
+    scratch = torch.empty(int(codec.lib().hhuff_qpack_scratch_size(nconn, 4096)), dtype=torch.uint8, device="cuda")
+    res = {}
+
+    def run():
+        res["r"] = codec.qpack_decode(d, eo, el, so, cf, nsec, 4096, 100, arena_off=ao, in_size=int(st["data"].size),
+                                      scratch=scratch)
+
+    t = timed(torch, run, steps=10, warmup=2)
+    r = res["r"]
+    nf = int(r["nfields"][:nsec].to(torch.int64).sum().item())
+    W = int(st["data"].size)
+    line = {"config": "qpack", "connections": nconn, "sections": nsec, "fields": nf, "input_bytes": W,
+            "encoder_stream_bytes": int(st["enc_len"].sum()),
+            "ok_sections": int((r["sstatus"][:nsec] == 0).sum().item()),
+            "arena_short_sections": int((r["sstatus"][:nsec] == -300).sum().item()), "decode_ms": round(t, 4),
+            "sections_per_s": round(nsec / (t * 1e-3), 1), "fields_per_s": round(nf / (t * 1e-3), 1),
+            "input_gibps": round(W / GIB / (t * 1e-3), 3)}
+    try:
+        sys.path.insert(0, ROOT)
+        from oracle import oracle as O
+
+        cpu = {}
+        m = min(nconn, 4096)
+        k = int(st["conn_first"][m])
+        sub = dict(data=st["data"], enc_off=st["enc_off"][:m], enc_len=st["enc_len"][:m], sec_off=st["sec_off"][:k + 1],
+                   conn_first=st["conn_first"][:m + 1], arena_off=ao_np[:k + 1])
+        for kind, lib in (("reference", O.ref() if O.ref_available() else None), ("restatement", O.oracle())):
+            if lib is None:
+                continue
+            s = O.QpackSession(lib, m, 4096, 100)
+            t0 = time.perf_counter()
+            s.step(sub["data"], sub["enc_off"], sub["enc_len"], sub["sec_off"], sub["conn_first"], sub["arena_off"])
+            dt = time.perf_counter() - t0
+            s.close()
+            cpu[kind + "_1thread_sections_per_s"] = round(k / dt, 1)
+        line["cpu"] = cpu
+    except Exception as e:  # the CPU baseline is a report, not a gate
+        line["cpu_error"] = str(e)
+    return line
+
+
 def main():
     import torch
 
@@ -157,6 +216,10 @@ def main():
     for cfg in cfgs:
         if cfg == "lit":
             print(json.dumps(literals_line(torch, codec, synth)), flush=True)
+            continue
+        if cfg.startswith("qpack"):
+            n = int(cfg[5:]) if len(cfg) > 5 else 65536
+            print(json.dumps(qpack_line(torch, codec, n)), flush=True)
             continue
         if cfg.startswith("blocks"):
             n = int(cfg[6:]) if len(cfg) > 6 else 65536
