@@ -252,6 +252,27 @@ __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t 
 // and last chunk record them {bytes, address, byte range} in `rec` (2 per tile) straight from their
 // registers; edge_fix_kernel writes the recorded byte ranges after the kernel (neighbouring tiles'
 // ranges in one chunk are disjoint, so dword / byte stores suffice).
+// decode_select_kernel's verdict: which of the two kernels launched behind it does the work
+constexpr uint32_t kGateStaged = 0u, kGateStream = 1u;
+
+// The staged/stream verdict from decode_select_kernel's partial sums; called by one whole wave.
+// Prices (MI355X, tools/ab.py, ms per 1M strings of fixed length 64..120 B and c3): staged ~ 40 ps per
+// string + 1.07 ps per tile-padded byte (64 x the tile's longest string); stream ~ 184 ps per string +
+// 1.15 ps per byte.
+__device__ __forceinline__ uint32_t select_verdict(const uint64_t* __restrict__ part) {
+    constexpr uint32_t kB = 64;  // kSelBlocks
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t pad = part[lane], sum = part[kB + lane], cnt = part[2 * kB + lane];
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        pad += (uint64_t)__shfl_xor((long long)pad, d);
+        sum += (uint64_t)__shfl_xor((long long)sum, d);
+        cnt += (uint64_t)__shfl_xor((long long)cnt, d);
+    }
+    const double staged = 40.0 * (double)cnt + 1.07 * (double)pad, streamed = 184.0 * (double)cnt + 1.15 * (double)sum;
+    return streamed < staged ? kGateStream : kGateStaged;
+}
+
 struct EdgeRec {
     uint4 v;
     uint4 m;  // {address lo, address hi, lo, hi}: bytes [lo, hi) of the chunk are ours (lo >= hi: none)
@@ -282,7 +303,9 @@ __device__ __forceinline__ void region_copy_deferred(uint8_t* __restrict__ out, 
 }
 
 // one thread per (record, dword)
-__global__ void edge_fix_kernel(uint8_t* __restrict__ out, const EdgeRec* __restrict__ rec, uint64_t nrec) {
+__global__ void edge_fix_kernel(uint8_t* __restrict__ out, const EdgeRec* __restrict__ rec, uint64_t nrec,
+                                const uint32_t* __restrict__ gate) {
+    if (gate && *gate != kGateStaged) return;  // the staged kernel did not run: no records were written
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < 4 * nrec; i += (uint64_t)gridDim.x * blockDim.x) {
         const EdgeRec& r = rec[i >> 2];
         const uint4 m = r.m;
@@ -344,6 +367,8 @@ struct DecArgs {
     uint32_t* out_len;
     uint8_t* status;
     EdgeRec* edges;  // region layout: 2 records per 64-string tile (deferred edges), or NULL
+    uint32_t* gate;        // NULL, or the device-side kernel choice (kGate*), written by the staged kernel
+    const uint64_t* sel;   // decode_select_kernel's partial sums [3][kSelBlocks] (with gate)
 };
 
 __device__ __forceinline__ void load_dec_tables(uint32_t* s_lut, uint32_t* s_kinfo, uint32_t* s_ones, int nthreads) {
@@ -385,6 +410,18 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         uint32_t in[WAVES][IN_STAGE / 4];
         uint8_t out[WAVES][OUT_STAGE + 256];  // + a trash dword per lane
     };
+    if (A.gate) {  // mixed-length batch: price both kernels from the sampled tiles (decode_select_kernel)
+        __shared__ uint32_t verdict;
+        if (threadIdx.x < 64) {
+            const uint32_t g = select_verdict(A.sel);
+            if (threadIdx.x == 0) {
+                verdict = g;
+                if (blockIdx.x == 0) *A.gate = g;  // read by edge_fix_kernel and the stream kernel, launched after
+            }
+        }
+        __syncthreads();
+        if (verdict != kGateStaged) return;  // block-uniform
+    }
     __shared__ Smem sm;
     uint32_t* s_lut = sm.lut;
     uint32_t* s_kinfo = sm.kinfo;
@@ -650,6 +687,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
         uint8_t out[WAVES * 64][OUT];
         uint32_t win[WAVES * 64][kWS];  // [0]: the dword before the window (read, never used)
     };
+    if (A.gate && *A.gate != kGateStream) return;  // block-uniform: decode_select_kernel chose the staged kernel
     __shared__ Smem sm;
     load_dec_tables(sm.lut, sm.kinfo, sm.ones, WAVES * 64);
     __syncthreads();
@@ -1940,6 +1978,55 @@ static int current_device() {
     return dev;
 }
 
+#ifndef HHUFF_DEC_SELECT  // A/B knob: device-side staged/stream choice for mean lengths in (40, 128]
+#define HHUFF_DEC_SELECT 1
+#endif
+// Mixed lengths (Zipf 8..512 B): a staged tile of 64 strings runs as long as its longest
+// string, while the stream kernel pays a per-string setup but never waits for another lane.  Which is
+// faster depends on the length spread, and the lengths live in device memory: 64 one-wave blocks (on
+// different CUs, so the scattered first touches do not queue behind one CU's address translation)
+// sample 4 tiles each and write partial sums; the staged kernel, launched next, prices both kernels
+// from them in every block (select_verdict), runs or exits, and its block 0 publishes the verdict for
+// edge_fix_kernel and the stream kernel launched after it.  Block 0 here zeroes the work counter.
+constexpr uint32_t kSelBlocks = 64, kSelTiles = 4;  // 256 sampled tiles, spread over 64 CUs
+__global__ __launch_bounds__(64) void decode_select_kernel(DecArgs A, uint64_t* __restrict__ part,
+                                                           unsigned long long* __restrict__ counter) {
+    const uint64_t ntiles = ((uint64_t)A.n + 63) / 64;
+    const uint64_t S = ntiles < kSelBlocks * kSelTiles ? ntiles : kSelBlocks * kSelTiles;
+    const uint32_t lane = threadIdx.x;
+    uint32_t len[kSelTiles];
+    bool live[kSelTiles];
+#pragma unroll
+    for (uint32_t k = 0; k < kSelTiles; ++k) {  // independent coalesced loads, issued back to back
+        const uint64_t t = (uint64_t)blockIdx.x * kSelTiles + k;
+        const uint64_t i = (t < S ? t * ntiles / S : 0) * 64 + lane;
+        live[k] = t < S && i < A.n;
+        len[k] = live[k] ? (A.in_len ? A.in_len[i] : A.in_off[i + 1] - A.in_off[i]) : 0u;
+    }
+    uint64_t pad = 0, sum = 0, cnt = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kSelTiles; ++k) {
+        const uint32_t l = min(len[k], kMaxStrLen + 1u);  // a failing length costs no more than that
+        uint32_t mx = l;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+        pad += 64ull * mx;
+        sum += l;
+        cnt += live[k] ? 1u : 0u;
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        sum += (uint64_t)__shfl_xor((long long)sum, d);
+        cnt += (uint64_t)__shfl_xor((long long)cnt, d);
+    }
+    if (lane == 0) {
+        part[blockIdx.x] = pad;
+        part[kSelBlocks + blockIdx.x] = sum;
+        part[2 * kSelBlocks + blockIdx.x] = cnt;
+        if (blockIdx.x == 0) *counter = 0ull;  // the stream kernel's work counter
+    }
+}
+
 #ifndef HHUFF_FORCE_DEC  // A/B knob: force a decode variant (kDecS / kDecL / kDecD / kDecT), -1 = by mean length
 #define HHUFF_FORCE_DEC -1
 #endif
@@ -1987,12 +2074,13 @@ static hipError_t alloc_edges(EdgeRec** p, uint32_t n, hipStream_t stream) {
 }
 
 // after a staged kernel launched with deferred edges: write them, release the records (stream order)
-static hipError_t finish_deferred(uint8_t* out, EdgeRec* edges, uint32_t n, hipStream_t stream) {
+static hipError_t finish_deferred(uint8_t* out, EdgeRec* edges, uint32_t n, hipStream_t stream,
+                                  const uint32_t* gate = nullptr) {
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) {
         const uint64_t nrec = edge_recs(n);
         const uint32_t blocks = (uint32_t)min((4 * nrec + 255) / 256, (uint64_t)8192);
-        hipLaunchKernelGGL(edge_fix_kernel, dim3(blocks), dim3(256), 0, stream, out, edges, nrec);
+        hipLaunchKernelGGL(edge_fix_kernel, dim3(blocks), dim3(256), 0, stream, out, edges, nrec, gate);
         e = hipGetLastError();
     }
     const hipError_t f = hipFreeAsync(edges, stream);
@@ -2014,10 +2102,38 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
                          const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
                          uint8_t* status, hipStream_t stream, uint64_t sel_bytes) {
     if (n == 0) return hipSuccess;
-    DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr};
+    DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr, nullptr, nullptr};
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n);
     const int grid = grid_for(v, current_device(), n);
     const bool defer = HHUFF_DEFER_EDGES && (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr;
+    if (v == kDecL && HHUFF_DEC_SELECT) {  // mixed lengths: the device picks staged or stream (see below)
+        uint64_t* sel = nullptr;  // [0, 3 kSelBlocks): partial sums; then the verdict and the work counter
+        hipError_t e = pool_alloc((void**)&sel, (3 * kSelBlocks + 2) * sizeof(uint64_t), stream);
+        if (e != hipSuccess) return e;
+        A.sel = sel;
+        A.gate = reinterpret_cast<uint32_t*>(sel + 3 * kSelBlocks);
+        unsigned long long* ctr = reinterpret_cast<unsigned long long*>(sel + 3 * kSelBlocks + 1);
+        hipLaunchKernelGGL(decode_select_kernel, dim3(kSelBlocks), dim3(64), 0, stream, A, sel, ctr);
+        e = hipGetLastError();
+        if (e == hipSuccess && defer) {
+            e = alloc_edges(&A.edges, n, stream);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(DEC_L, dim3(grid), dim3(384), 0, stream, A);
+                e = finish_deferred(out, A.edges, n, stream, A.gate);
+            }
+        } else if (e == hipSuccess) {
+            hipLaunchKernelGGL(DEC_L, dim3(grid), dim3(384), 0, stream, A);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) {
+            A.edges = nullptr;
+            hipLaunchKernelGGL(DEC_T, dim3(grid_for(kDecT, current_device(), n)), dim3(HHUFF_DTW * 64), 0, stream, A,
+                               ctr);
+            e = hipGetLastError();
+        }
+        const hipError_t f = hipFreeAsync(sel, stream);
+        return e != hipSuccess ? e : f;
+    }
     if (defer) {
         hipError_t e = alloc_edges(&A.edges, n, stream);
         if (e != hipSuccess) return e;

@@ -266,6 +266,57 @@ def test_streaming_decode_long_mixed(torch_cuda, oracle_codec):
     assert compact(g[0], slots, g[1]) == compact(o[0], slots, o[1])
 
 
+def _select_verdict(lens):
+    """host mirror of decode_select_kernel + select_verdict (hhuff_kernels.hip): 1 = stream kernel"""
+    n = len(lens)
+    ntiles = (n + 63) // 64
+    S = min(ntiles, 256)
+    pad = tot = cnt = 0
+    for t in range(S):
+        i0 = (t * ntiles // S) * 64
+        seg = np.minimum(lens[i0:i0 + 64].astype(np.int64), (1 << 29))
+        pad += 64 * int(seg.max())
+        tot += int(seg.sum())
+        cnt += len(seg)
+    return int(184.0 * cnt + 1.15 * tot < 40.0 * cnt + 1.07 * pad)
+
+
+@pytest.mark.parametrize("lengths,verdict", [(("zipf", 8, 512), 1), (("uniform", 110, 130), 0)])
+def test_mixed_length_decode_select(torch_cuda, oracle_codec, lengths, verdict):
+    """mean Huffman length in (40, 128]: the device samples the lengths and runs the staged or the
+    stream kernel (decode_select_kernel); both verdicts, wire layout (deferred edges) + explicit dst"""
+    n = 60000
+    b = synth.make_batch(dict(n=n, lengths=lengths, alphabet="header"), n=n, seed=31, adversarial_frac=0.02)
+    o_out, o_len, _ = oracle_codec.encode_batch(b["data"], b["off"], n, nthreads=8)
+    ok = np.nonzero(o_len != FAIL)[0]
+    huff = [o_out[int(b["off"][i]):int(b["off"][i]) + int(o_len[i])].tobytes() for i in ok]
+    rng = np.random.default_rng(32)
+    for j in rng.choice(len(huff), len(huff) // 50, replace=False):  # a few with bad padding
+        huff[j] = huff[j] + b"\x00"
+    hdata, hoff = synth.pack(huff)
+    m = len(huff)
+    assert 40 < hdata.size // m <= 128
+    assert _select_verdict(np.diff(hoff)) == verdict
+    names = synth.bits_from_bools(rng.random(m) < 0.3)
+    g = gpu_decode(torch_cuda, hdata, hoff, m, is_name_bits=names)
+    o = oracle_codec.decode_batch(hdata, hoff, m, is_name_bits=names, nthreads=8)
+    np.testing.assert_array_equal(g[1], o[1])
+    np.testing.assert_array_equal(g[2], o[2])
+    slots = (hoff[:m].astype(np.uint64) * 8) // 5
+    assert compact(g[0], slots, g[1]) == compact(o[0], slots, o[1])
+    # pairs, reversed order, explicit destinations packed at 2 x len (h2o's buffer rule)
+    idx = np.arange(m)[::-1].copy()
+    starts, lens = hoff[idx].astype(np.uint32), np.diff(hoff)[idx].astype(np.uint32)
+    dst = np.concatenate([[0], np.cumsum(2 * lens.astype(np.uint64))])
+    out_off = dst[:-1].astype(np.uint32)
+    g = gpu_decode(torch_cuda, hdata, starts, m, in_len=lens, out_off=out_off, out_size=int(dst[-1]) + 64)
+    o = oracle_codec.decode_batch(hdata, starts, m, in_len=lens, nthreads=8)
+    np.testing.assert_array_equal(g[1], o[1])
+    np.testing.assert_array_equal(g[2], o[2])
+    sl = (starts.astype(np.uint64) * 8) // 5
+    assert compact(g[0], out_off, g[1]) == compact(o[0], sl, o[1])
+
+
 # ------------------------------------------------------------------------------------------------
 # per-string h2o symbols and the host batch API
 # ------------------------------------------------------------------------------------------------
