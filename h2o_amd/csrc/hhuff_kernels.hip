@@ -57,6 +57,22 @@ __device__ __forceinline__ Tile load_tile(uint64_t base, int lane, uint32_t n, c
     return t;
 }
 
+// The 16 bytes at g when they cross in_size (bytes past it read as 0).  A rolled loop over the < 16 bytes
+// that exist: unrolled, the 16 bounds checks were hoisted as 64-bit lane + b constants that held ~30
+// VGPRs for the whole kernel (and spilled), for a path taken once per launch.
+__device__ __forceinline__ uint4 load16_tail(const uint8_t* __restrict__ in, uint64_t in_size, uint64_t g) {
+    const uint32_t rem = g < in_size ? (uint32_t)min(in_size - g, (uint64_t)16) : 0u;
+    const uint8_t* p = in + g;
+    uint64_t lo = 0, hi = 0;
+#pragma unroll 1
+    for (uint32_t b = 0; b < rem; ++b) {
+        const uint64_t x = p[b];
+        if (b < 8) lo |= x << (8u * b);
+        else hi |= x << (8u * (b - 8u));
+    }
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
 // Stage [a0, a0 + span) of `in` into LDS (16-byte loads; bytes past in_size read as 0).
 __device__ __forceinline__ void stage_span(uint32_t* stage, const uint8_t* __restrict__ in, uint64_t in_size, uint32_t a0,
                                            uint32_t span, int lane) {
@@ -66,10 +82,7 @@ __device__ __forceinline__ void stage_span(uint32_t* stage, const uint8_t* __res
         if (g + 16 <= in_size) {
             v = *reinterpret_cast<const uint4*>(in + g);
         } else {
-            uint32_t w[4] = {0, 0, 0, 0};
-            for (uint32_t b = 0; b < 16; ++b)
-                if (g + b < in_size) w[b >> 2] |= (uint32_t)in[g + b] << (8 * (b & 3));
-            v = make_uint4(w[0], w[1], w[2], w[3]);
+            v = load16_tail(in, in_size, g);
         }
         *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(stage) + k) = v;
     }
@@ -176,12 +189,7 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
             if (k < span) {
                 const uint64_t g = (uint64_t)a0 + k;
                 uint4 x = v[c];
-                if (g + 16 > in_size) {  // the chunk holding the end of the input buffer
-                    uint32_t w[4] = {0, 0, 0, 0};
-                    for (uint32_t b = 0; b < 16; ++b)
-                        if (g + b < in_size) w[b >> 2] |= (uint32_t)in[g + b] << (8 * (b & 3));
-                    x = make_uint4(w[0], w[1], w[2], w[3]);
-                }
+                if (g + 16 > in_size) x = load16_tail(in, in_size, g);  // the chunk holding the input's end
                 if (kSwap) x = make_uint4(bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w));
                 *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(stage) + k) = x;
             }
@@ -650,11 +658,7 @@ __device__ __forceinline__ uint4 load16_bounded(const uint8_t* __restrict__ in, 
         const u32x4a v = *reinterpret_cast<const u32x4a*>(in + a);
         return make_uint4(v.x, v.y, v.z, v.w);
     }
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-#pragma unroll 1
-    for (uint32_t b = 0; b < 16; ++b)
-        if (a + b < in_size) w[b >> 2] |= (uint32_t)in[a + b] << (8u * (b & 3u));
-    return make_uint4(w[0], w[1], w[2], w[3]);
+    return load16_tail(in, in_size, a);
 }
 
 // bytes [lo, hi) of the 16-B LDS chunk `c` to global `g` (16-B aligned): dword stores where whole
