@@ -1917,7 +1917,10 @@ __global__ void literal_fix_kernel(LitArgs A) {
 #define HHUFF_DTOUT 112
 #endif
 #define DEC_T decode_stream_kernel<HHUFF_DTW, HHUFF_DTNW, HHUFF_DTOUT>
-#define ENC_S encode_staged_kernel<16, 3584>
+#ifndef HHUFF_ESW  // waves per block of the short-string encode kernel (c4, ms): 16: 0.83; 12: 0.93;
+#define HHUFF_ESW 16  // 20: does not launch (118 VGPRs allow 4 waves per SIMD)
+#endif
+#define ENC_S encode_staged_kernel<HHUFF_ESW, 3584>
 #define ENC_L encode_staged_kernel<8, 8192>
 #define ENC_D encode_direct_kernel<4>
 #define FLAT_D flatten_direct_kernel<4>
@@ -1948,7 +1951,7 @@ static int variant_threads(int v) {
     switch (v) {
         case kDecS: return HHUFF_DSW * 64;
         case kDecT: return HHUFF_DTW * 64;
-        case kEncS: return 1024;
+        case kEncS: return HHUFF_ESW * 64;
         case kDecL: return 384;
         case kEncL: return 512;
         case kEncC: return 768;
@@ -2208,7 +2211,7 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         if (e != hipSuccess) return e;
     }
     switch (v) {
-        case kEncS: hipLaunchKernelGGL(ENC_S, dim3(grid), dim3(1024), 0, stream, A); break;
+        case kEncS: hipLaunchKernelGGL(ENC_S, dim3(grid), dim3(HHUFF_ESW * 64), 0, stream, A); break;
         case kEncL: hipLaunchKernelGGL(ENC_L, dim3(grid), dim3(512), 0, stream, A); break;
         default: hipLaunchKernelGGL(ENC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }

@@ -92,11 +92,12 @@ def run(names, cfg="c4", rounds=5, steps=10):
                     if i == 2:
                         ev[0].record()
                     if kind == "enc":
-                        L.hhuff_encode_batch(b["data"].data_ptr(), P, off32.data_ptr(), None, n, e_out.data_ptr(),
-                                             None, e_len.data_ptr(), e_st.data_ptr(), s)
+                        rc = L.hhuff_encode_batch(b["data"].data_ptr(), P, off32.data_ptr(), None, n, e_out.data_ptr(),
+                                                  None, e_len.data_ptr(), e_st.data_ptr(), s)
                     else:
-                        L.hhuff_decode_batch(huff.data_ptr(), H, hoff.data_ptr(), None, n_ok, None, d_out.data_ptr(),
-                                             None, d_len.data_ptr(), d_st.data_ptr(), s)
+                        rc = L.hhuff_decode_batch(huff.data_ptr(), H, hoff.data_ptr(), None, n_ok, None,
+                                                  d_out.data_ptr(), None, d_len.data_ptr(), d_st.data_ptr(), s)
+                    assert rc == 0, (nm, kind, rc)  # a launch that failed leaves the last build's outputs
                 ev[1].record()
                 torch.cuda.synchronize()
                 res[nm][kind].append(ev[0].elapsed_time(ev[1]) / steps)
