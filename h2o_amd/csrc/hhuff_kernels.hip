@@ -1118,8 +1118,46 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
 // OR-combined output stage.  Single-lane strings skip pass 1 and fail early as in encode_staged_kernel.
 // Tiles whose span exceeds the stage (strings longer than ~STAGE / 1) fall back to the direct loop.
 // ------------------------------------------------------------------------------------------------
+// Proportional-lane tile size.  A tile of K strings whose span exceeds the stage falls back to the
+// per-lane direct loop, and even a few such tiles set the kernel's tail (c3, Zipf 8..512 B: K = 16
+// overflows 0.2 % of tiles and runs 45 % longer than K = 12, which never does), while uniform lengths
+// want the largest K (fewer tiles; u64: 32 strings per tile 0.079 ms vs 21: 0.099).  So the host plans
+// K0 (bytes per tile / mean, rounded down to 64 / m so that every string gets m lanes) and 64 one-wave
+// blocks sample 4096 positions: for each candidate K <= K0 they count the K-string spans that would
+// not fit.  Every encode_pl block then takes the largest candidate with no overflow in the sample.
+constexpr uint32_t kPlCand[6] = {32u, 21u, 16u, 12u, 10u, 8u};
+constexpr uint32_t kPlBlocks = 64;
+__global__ __launch_bounds__(64) void encode_plan_kernel(EncArgs A, uint32_t K0, uint32_t limit,
+                                                         uint32_t* __restrict__ part) {
+    const uint32_t lane = threadIdx.x;
+    const uint64_t i = ((uint64_t)blockIdx.x * 64 + lane) * A.n / (kPlBlocks * 64);  // < n
+    const uint32_t a = A.in_off[i];
+    uint32_t e[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q)  // independent loads, issued back to back
+        e[q] = kPlCand[q] <= K0 ? A.in_off[min(i + kPlCand[q], (uint64_t)A.n)] : a;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const uint32_t over = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(e[q] - a > limit));
+        if (lane == 0) part[q * kPlBlocks + blockIdx.x] = over;
+    }
+}
+// one whole wave: the largest candidate <= K0 whose sampled spans all fit (else the smallest)
+__device__ __forceinline__ uint32_t plan_tile_strings(const uint32_t* __restrict__ part, uint32_t K0) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t pick = kPlCand[5];
+#pragma unroll
+    for (int q = 5; q >= 0; --q) {
+        uint32_t c = part[q * kPlBlocks + lane];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) c += (uint32_t)__shfl_xor((int)c, d);
+        if (kPlCand[q] <= K0 && c == 0) pick = kPlCand[q];
+    }
+    return pick < K0 ? pick : K0;
+}
+
 template <int WAVES, int STAGE>
-__global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32_t K) {
+__global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32_t K, const uint32_t* __restrict__ kplan) {
     struct __attribute__((aligned(16))) Smem {
         uint2 enc[512];  // 256..511: bytes outside a share
         uint32_t in[WAVES][STAGE / 4];
@@ -1127,9 +1165,15 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
         uint32_t lmap[WAVES][64];
     };
     __shared__ Smem sm;
+    __shared__ uint32_t s_k;
     for (uint32_t k = threadIdx.x; k < 512; k += WAVES * 64)
         sm.enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
+    if (kplan && threadIdx.x < 64) {  // tile size from encode_plan_kernel's samples (K is then its ceiling)
+        const uint32_t k = plan_tile_strings(kplan, K);
+        if (threadIdx.x == 0) s_k = k;
+    }
     __syncthreads();
+    if (kplan) K = s_k;
     const uint2* s_enc = sm.enc;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t* stage = sm.in[wave];
@@ -2047,6 +2091,15 @@ static int pick_decode(uint64_t in_size, uint32_t n) {
 #ifndef HHUFF_ENC_PL  // A/B knobs: proportional-lane encode from this mean string length up (0 = always)
 #define HHUFF_ENC_PL 53
 #endif
+#ifndef HHUFF_ENC_PL_PLAN  // A/B knob: device-sampled tile size (encode_plan_kernel)
+#define HHUFF_ENC_PL_PLAN 1
+#endif
+#ifndef HHUFF_ENC_PL_SNAP  // A/B knob: round K down to 64 / ceil(64 / K)
+#define HHUFF_ENC_PL_SNAP 1
+#endif
+#ifndef HHUFF_ENC_PL_FILL  // mean bytes a proportional-lane tile is planned for (of a 3584-B stage)
+#define HHUFF_ENC_PL_FILL 2560
+#endif
 #ifndef HHUFF_ENC_PL_K  // strings per tile (0 = from the mean length)
 #define HHUFF_ENC_PL_K 0
 #endif
@@ -2194,14 +2247,31 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         // contiguous wire layout: proportional-lane tiles of K strings (about 5/8 of a stage of bytes)
         const uint64_t mean = in_size / n;
         uint32_t K = HHUFF_ENC_PL_K ? (uint32_t)HHUFF_ENC_PL_K
-                                    : (uint32_t)(mean ? (3584u * 5u / 8u) / mean : 64u);
+                                    : (uint32_t)(mean ? (uint64_t)HHUFF_ENC_PL_FILL / mean : 64u);
         K = K < 1 ? 1u : (K > 64 ? 64u : K);
-        const uint64_t tiles = ((uint64_t)n + K - 1) / K;
+        if (HHUFF_ENC_PL_SNAP) K = 64u / ((64u + K - 1u) / K);  // down to 64 / m: m lanes per string, few idle
+        const bool sample = HHUFF_ENC_PL_PLAN && HHUFF_ENC_PL_K == 0 && K > kPlCand[5] && n >= 4096;
+        const uint32_t kmin = sample ? kPlCand[5] : K;
+        const uint64_t tiles = ((uint64_t)n + kmin - 1) / kmin;
         const int g = grid_for(kEncP, current_device(), 0xFFFFFFFFu);
         const uint64_t want = (tiles + 15) / 16;
         const int grid = (int)(want < (uint64_t)g ? (want ? want : 1) : g);
-        hipLaunchKernelGGL(ENC_P, dim3(grid), dim3(1024), 0, stream, A, K);
-        return hipGetLastError();
+        if (!sample) {
+            hipLaunchKernelGGL(ENC_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)nullptr);
+            return hipGetLastError();
+        }
+        uint32_t* part = nullptr;
+        hipError_t e = pool_alloc((void**)&part, 6 * kPlBlocks * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        // a tile fits when its 16-B aligned span does: raw span + 30 <= stage
+        hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, A, K, 3584u - 30u, part);
+        e = hipGetLastError();
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(ENC_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)part);
+            e = hipGetLastError();
+        }
+        const hipError_t f = hipFreeAsync(part, stream);
+        return e != hipSuccess ? e : f;
     }
     const int v = pick_encode(in_size, n);
     const int grid = grid_for(v, current_device(), n);
