@@ -1127,15 +1127,15 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
 // not fit.  Every encode_pl block then takes the largest candidate with no overflow in the sample.
 constexpr uint32_t kPlCand[6] = {32u, 21u, 16u, 12u, 10u, 8u};
 constexpr uint32_t kPlBlocks = 64;
-__global__ __launch_bounds__(64) void encode_plan_kernel(EncArgs A, uint32_t K0, uint32_t limit,
-                                                         uint32_t* __restrict__ part) {
+__global__ __launch_bounds__(64) void encode_plan_kernel(const uint32_t* __restrict__ in_off, uint32_t n, uint32_t K0,
+                                                         uint32_t limit, uint32_t* __restrict__ part) {
     const uint32_t lane = threadIdx.x;
-    const uint64_t i = ((uint64_t)blockIdx.x * 64 + lane) * A.n / (kPlBlocks * 64);  // < n
-    const uint32_t a = A.in_off[i];
+    const uint64_t i = ((uint64_t)blockIdx.x * 64 + lane) * n / (kPlBlocks * 64);  // < n
+    const uint32_t a = in_off[i];
     uint32_t e[6];
 #pragma unroll
     for (int q = 0; q < 6; ++q)  // independent loads, issued back to back
-        e[q] = kPlCand[q] <= K0 ? A.in_off[min(i + kPlCand[q], (uint64_t)A.n)] : a;
+        e[q] = kPlCand[q] <= K0 ? in_off[min(i + kPlCand[q], (uint64_t)n)] : a;
 #pragma unroll
     for (int q = 0; q < 6; ++q) {
         const uint32_t over = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(e[q] - a > limit));
@@ -1649,7 +1649,7 @@ __device__ __forceinline__ uint32_t prefix_int_bytes(uint32_t h0, uint32_t v, ui
 // (qpack.c:1052-1060); raw fallbacks copy their shares after the raw header (qpack.c:1046-1051).
 // ------------------------------------------------------------------------------------------------
 template <int WAVES, int STAGE>
-__global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint32_t K) {
+__global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint32_t K, const uint32_t* __restrict__ kplan) {
     constexpr uint32_t OSTAGE = STAGE + 11u * 64u + 32u;
     struct __attribute__((aligned(16))) Smem {
         uint2 enc[512];
@@ -1658,9 +1658,15 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
         uint32_t lmap[WAVES][64];
     };
     __shared__ Smem sm;
+    __shared__ uint32_t s_k;
     for (uint32_t k = threadIdx.x; k < 512; k += WAVES * 64)
         sm.enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
+    if (kplan && threadIdx.x < 64) {  // tile size from encode_plan_kernel's samples (as encode_pl_kernel)
+        const uint32_t k = plan_tile_strings(kplan, K);
+        if (threadIdx.x == 0) s_k = k;
+    }
     __syncthreads();
+    if (kplan) K = s_k;
     const uint2* s_enc = sm.enc;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t* stage = sm.in[wave];
@@ -2264,7 +2270,7 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         hipError_t e = pool_alloc((void**)&part, 6 * kPlBlocks * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
         // a tile fits when its 16-B aligned span does: raw span + 30 <= stage
-        hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, A, K, 3584u - 30u, part);
+        hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, in_off, n, K, 3584u - 30u, part);
         e = hipGetLastError();
         if (e == hipSuccess) {
             hipLaunchKernelGGL(ENC_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)part);
@@ -2295,14 +2301,30 @@ hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* i
     FlatArgs A{in, in_size, in_off, in_len, n, first_bytes, prefix_bits, raw_bits, out, out_off, out_len};
     if (in_len == nullptr && out_off == nullptr) {  // contiguous layout, implicit slots: proportional lanes
         const uint64_t mean = in_size / n;
-        uint32_t K = (uint32_t)(mean ? (3584u * 5u / 8u) / mean : 64u);
+        uint32_t K = (uint32_t)(mean ? (uint64_t)HHUFF_ENC_PL_FILL / mean : 64u);  // as launch_encode
         K = K < 1 ? 1u : (K > 64 ? 64u : K);
-        const uint64_t tiles = ((uint64_t)n + K - 1) / K;
+        if (HHUFF_ENC_PL_SNAP) K = 64u / ((64u + K - 1u) / K);
+        const bool sample = HHUFF_ENC_PL_PLAN && K > kPlCand[5] && n >= 4096;
+        const uint32_t kmin = sample ? kPlCand[5] : K;
+        const uint64_t tiles = ((uint64_t)n + kmin - 1) / kmin;
         const int g = grid_for(kFlatP, current_device(), 0xFFFFFFFFu);
         const uint64_t want = (tiles + 15) / 16;
         const int grid = (int)(want < (uint64_t)g ? (want ? want : 1) : g);
-        hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K);
-        return hipGetLastError();
+        if (!sample) {
+            hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)nullptr);
+            return hipGetLastError();
+        }
+        uint32_t* part = nullptr;
+        hipError_t e = pool_alloc((void**)&part, 6 * kPlBlocks * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, in_off, n, K, 3584u - 30u, part);
+        e = hipGetLastError();
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)part);
+            e = hipGetLastError();
+        }
+        const hipError_t f = hipFreeAsync(part, stream);
+        return e != hipSuccess ? e : f;
     }
     const int grid = grid_for(kFlatD, current_device(), n);
     hipLaunchKernelGGL(FLAT_D, dim3(grid), dim3(256), 0, stream, A);

@@ -212,6 +212,8 @@ def main():
     from h2o_amd import codec, synth
 
     torch.cuda.set_device(0)
+    if os.environ.get("HHUFF_AB_LIB"):  # A/B: time another build of the library (tools/ab.py build NAME)
+        codec.LIB_PATH = os.environ["HHUFF_AB_LIB"]
     cfgs = sys.argv[1:] or ["c2", "c3", "c5", "lit"]
     for cfg in cfgs:
         if cfg == "lit":
@@ -225,11 +227,15 @@ def main():
             n = int(cfg[6:]) if len(cfg) > 6 else 65536
             print(json.dumps(blocks_line(torch, codec, n)), flush=True)
             continue
-        b = synth.make_batch_torch(cfg, seed=7)
+        if cfg[5:].startswith("u") and cfg[6:].isdigit():  # flat_u<L>: fixed-length strings (A/B only)
+            synth.CONFIGS.setdefault(cfg[5:], dict(n=1 << 20, lengths=("uniform", int(cfg[6:]), int(cfg[6:])),
+                                                   alphabet="header"))
+        flat = cfg.startswith("flat_")  # flat_<config>: flatten_string (prefix 7) over that config's strings
+        b = synth.make_batch_torch(cfg[5:] if flat else cfg, seed=7)
         n, P = b["n"], int(b["total"])
         off32 = b["off"].to(torch.int32)
         line = {"config": cfg, "strings": n, "plain_bytes": P}
-        if cfg in ("c2", "c3"):
+        if cfg in ("c2", "c3") and not flat:
             huff, h_off, n_ok, H, P_ok = packed_huffman(torch, codec, b)
             d_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
             d_len = torch.empty(n_ok, dtype=torch.int32, device="cuda")
