@@ -40,23 +40,6 @@ struct Tile {
     uint32_t lo, hi;  // input span of the tile's non-empty strings
 };
 
-__device__ __forceinline__ Tile load_tile(uint64_t base, int lane, uint32_t n, const uint32_t* __restrict__ in_off,
-                                          const uint32_t* __restrict__ in_len) {
-    Tile t;
-    t.i = (uint32_t)base + lane;
-    t.valid = t.i < n;
-    t.s = 0;
-    t.len = 0;
-    if (t.valid) {
-        t.s = in_off[t.i];
-        t.len = in_len ? in_len[t.i] : in_off[t.i + 1] - t.s;
-    }
-    const bool has = t.valid && t.len != 0;
-    t.lo = wave_min_u32(has ? t.s : 0xFFFFFFFFu);
-    t.hi = wave_max_u32(has ? t.s + t.len : 0u);
-    return t;
-}
-
 // The 16 bytes at g when they cross in_size (bytes past it read as 0).  A rolled loop over the < 16 bytes
 // that exist: unrolled, the 16 bounds checks were hoisted as 64-bit lane + b constants that held ~30
 // VGPRs for the whole kernel (and spilled), for a path taken once per launch.
@@ -92,24 +75,6 @@ __device__ __forceinline__ void stage_span(uint32_t* stage, const uint8_t* __res
 // input span are loaded into registers while the current tile is decoded or encoded from LDS, so the
 // wave never sits on a global-memory round trip between tiles.  Nothing on the LDS path of a tile
 // issues a global load, so no vmcnt wait there can be held up by the prefetch.
-#ifdef HHUFF_NO_SPAN_PREFETCH
-constexpr bool kSpanPrefetch = false;  // A/B switch: load the next span only after the current tile
-#else
-constexpr bool kSpanPrefetch = true;
-#endif
-
-#ifndef HHUFF_DEC_I  // A/B knob: 1 = previous decode step (decode_staged_lane_i, little-endian stage)
-#define HHUFF_DEC_I 0
-#endif
-constexpr bool kDecSwap = !HHUFF_DEC_I;
-
-// Commit the next tile's prefetched span to the input stage as soon as the current tile's steps are
-// done, BEFORE the current tile's output stores: the commit's vmcnt wait then covers only loads issued
-// a whole tile ago (the counter also counts stores, so committing after them waited for their writes).
-#ifndef HHUFF_EARLY_COMMIT  // A/B knob
-#define HHUFF_EARLY_COMMIT 0  // measured neutral (c4: 0.728 vs 0.729 ms decode)
-#endif
-constexpr bool kEarlyCommit = HHUFF_EARLY_COMMIT;
 
 // Phase timing (profile builds only, -DHHUFF_PROFILE): shader cycles per phase summed over waves,
 // read back with hhuff_debug_prof() (tools/ab.py prof).  s_memtime costs a little itself.
@@ -197,12 +162,6 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
     }
 };
 
-#ifndef HHUFF_DEFER_EDGES  // A/B knob: region edges written by edge_fix_kernel after the staged kernels
-#define HHUFF_DEFER_EDGES 1
-#endif
-#ifndef HHUFF_COPY_V2  // A/B knob: 0 = LDS byte reads at the edges; N = N chunks per round, register edges
-#define HHUFF_COPY_V2 0  // measured: register edges 5 % slower (c4 decode 0.7125 -> 0.7485 ms)
-#endif
 // Write LDS bytes [0, ospan) to global [gbase, gbase + ospan) (gbase 16-aligned), keeping only the
 // global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
 // (Measured: batching the LDS reads of all chunks, or taking the edge bytes from the loaded registers,
@@ -210,38 +169,6 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
 template <int NCH>
 __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds, uint32_t ospan,
                                             uint64_t keep_lo, uint64_t keep_hi, int lane) {
-#if HHUFF_COPY_V2
-    // two 1-KiB chunks per round: both LDS reads are issued before the stores, and the two edge chunks
-    // of the region take their bytes from the loaded registers (no LDS round trip per byte)
-    constexpr int CP = HHUFF_COPY_V2;  // chunks per round
-#pragma unroll
-    for (int c0 = 0; c0 < NCH; c0 += CP) {
-        uint4 v[CP];
-#pragma unroll
-        for (int d = 0; d < CP; ++d) {
-            const uint32_t k = (uint32_t)(c0 + d) * 1024u + (uint32_t)lane * 16u;
-            if (c0 + d < NCH && k < ospan) v[d] = *reinterpret_cast<const uint4*>(lds + k);
-        }
-#pragma unroll
-        for (int d = 0; d < CP; ++d) {
-            const uint32_t k = (uint32_t)(c0 + d) * 1024u + (uint32_t)lane * 16u;
-            if (c0 + d >= NCH || k >= ospan) continue;
-            const uint64_t g = gbase + k;
-            if (g >= keep_lo && g + 16 <= keep_hi) {
-                *reinterpret_cast<uint4*>(out + g) = v[d];
-            } else {
-                const int64_t rl = (int64_t)keep_lo - (int64_t)g, rh = (int64_t)keep_hi - (int64_t)g;
-                const uint32_t blo = (uint32_t)min(max(rl, (int64_t)0), (int64_t)16);
-                const uint32_t bhi = (uint32_t)min(max(rh, (int64_t)0), (int64_t)16);
-                const uint32_t m = ((1u << bhi) - 1u) & ~((1u << blo) - 1u);  // bytes [blo, bhi) are ours
-                const uint32_t w[4] = {v[d].x, v[d].y, v[d].z, v[d].w};
-#pragma unroll
-                for (uint32_t b = 0; b < 16; ++b)
-                    if ((m >> b) & 1u) out[g + b] = (uint8_t)(w[b >> 2] >> (8u * (b & 3u)));
-            }
-        }
-    }
-#else
     for (uint32_t k = (uint32_t)lane * 16u; k < ospan; k += 64u * 16u) {
         const uint64_t g = gbase + k;
         if (g >= keep_lo && g + 16 <= keep_hi) {
@@ -251,7 +178,6 @@ __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t 
                 if (g + b >= keep_lo && g + b < keep_hi) out[g + b] = lds[k + b];
         }
     }
-#endif
 }
 
 // Deferred region edges.  Writing the (at most two) 16-byte chunks a tile's output region shares with
@@ -495,7 +421,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     if (cur.fits) pf.issue(A.in, A.in_size, cur.a0(), cur.span(), lane);
     bool have_next = base + stride < A.n;
     if (have_next) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
-    if (cur.fits) pf.template commit<kDecSwap>(stage, A.in, A.in_size, cur.a0(), cur.span(), lane);
+    if (cur.fits) pf.template commit<true>(stage, A.in, A.in_size, cur.a0(), cur.span(), lane);
     Plan nxt;
     uint32_t nxt_name = 0;
     if (have_next) {
@@ -519,26 +445,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
             wave_lds_sync();
             const bool act = t.valid && t.len <= kMaxStrLen;
             const uint32_t rel = t.len ? t.s - cur.a0() : 0u;
-            const uint32_t last = cur.span() ? cur.span() - 4u : 0u;
-#if HHUFF_DEC_I
-            const DecResult r =
-                decode_staged_lane_i(stage, last, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
-#elif HHUFF_DEC_BULK
-            (void)last;
-#ifdef HHUFF_ABL_REPEAT  // ablation: run the step loop twice (same output; times the steps alone)
-            (void)decode_staged_lane_v7(stage, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
-#endif
             const DecResult r = decode_staged_lane_v7(stage, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
-#elif HHUFF_DEC_ACC
-            (void)last;
-            for (uint32_t k = (uint32_t)lane * 16u; k < cur.ospan + 4u; k += 64u * 16u)  // OR target: zeroed
-                *reinterpret_cast<uint4*>(obuf + k) = make_uint4(0u, 0u, 0u, 0u);
-            wave_lds_sync();
-            const DecResult r = decode_staged_lane_v6(stage, rel, t.len, act, obuf, cur.op0, T);
-#else
-            (void)last;
-            const DecResult r = decode_staged_lane_v5(stage, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
-#endif
             PROF_MARK(1);  // steps
             if (t.valid && t.len > kMaxStrLen) {
                 ol = kFailLen;
@@ -563,7 +470,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         uint32_t nn_name = 0;
         bool have_nn = false;
         if (have_next) {
-            if (nxt.fits) pf.template commit<kDecSwap>(stage, A.in, A.in_size, nxt.a0(), nxt.span(), lane);
+            if (nxt.fits) pf.template commit<true>(stage, A.in, A.in_size, nxt.a0(), nxt.span(), lane);
             have_nn = nbase + stride < A.n;
             if (have_nn) {
                 nn = plan(nbase + stride, ti);
@@ -576,11 +483,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         PROF_MARK(3);  // commit + plan
         // ---- the current tile: stores ----
         if (cur.fits) {
-#ifdef HHUFF_ABL_NOCOPY  // ablation: no output copy (timing only)
-            if (region && A.n == 0) {
-#else
             if (region) {
-#endif
                 if (A.edges)
                     region_copy_deferred(A.out, cur.obase(), obuf, cur.ospan, cur.olo(), cur.ohi(), lane,
                                          A.edges + 2 * (base >> 6));
@@ -811,7 +714,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                     accb |= eb;
                     cons += ((eb >> 20) & 15u) & ~slb;
                 }
-                if ((!HHUFF_DEC_LONG2 || longchk) && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
+                if (longchk && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
                     if (sl) {
                         const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
                         const uint32_t ki = T.kinfo[k];
@@ -871,7 +774,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                 }
                 const bool lact = (s1 & (int32_t)e) < 0;
                 uint32_t consl = 0;
-                if ((!HHUFF_DEC_LONG2 || longchk) && __builtin_amdgcn_ballot_w64(lact) != 0) {
+                if (longchk && __builtin_amdgcn_ballot_w64(lact) != 0) {
                     if (lact) {
                         const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
                         const uint32_t ki = T.kinfo[k];
@@ -1028,13 +931,12 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
         Plan nxt;
         if (have_next) {
             nxt = plan(nbase, ti);
-            if (kSpanPrefetch && nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+            if (nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
             if (nbase + stride < A.n) ti = issue_tile(nbase + stride, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
         }
         // ---- the current tile ----
         const Tile& t = cur.t;
         uint32_t ol = kFailLen;
-        bool committed = false;
         PROF_MARK(0);
         if (cur.fits) {
             for (uint32_t k = (uint32_t)lane * 16u; k < cur.ospan + 16u; k += 64u * 16u)
@@ -1043,37 +945,17 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
             const bool act = t.valid && t.len != 0 && t.len <= kMaxStrLen;
             const uint32_t rel = t.len ? t.s - cur.a0 : 0u;
             const uint32_t last = cur.span ? cur.span - 4u : 0u;
-#ifdef HHUFF_ENC_VOTE_LOOP
-            const uint32_t r = encode_staged_lane(stage, last, rel, t.len, act, obuf32, cur.op0, s_enc);
-#elif HHUFF_ENC_V2
-#ifdef HHUFF_ABL_REPEAT
-            (void)encode_chunk_v2(stage, last, rel, t.len, act, lds_addr(obuf32), 8u * cur.op0, s_enc,
-                                  act ? 8 * t.len - 7 : 0xFFFFFFFFu, true);
-#endif
             const uint32_t tb = encode_chunk_v2(stage, last, rel, t.len, act, lds_addr(obuf32), 8u * cur.op0, s_enc,
                                                 act ? 8 * t.len - 7 : 0xFFFFFFFFu, true);
             const uint32_t r = tb == kFailLen ? kFailLen : (tb + 7) >> 3;
             PROF_MARK(1);
             wave_lds_sync();
             stage_bswap(obuf32, (cur.ospan + 15u) & ~15u, lane);
-#else
-            const uint32_t jmax = wave_max_u32(act ? ((rel + t.len - (rel & ~3u) + 3u) >> 2) : 0u);
-            const uint32_t r = encode_staged_lane_u(stage, last, rel, t.len, act, obuf32, cur.op0, s_enc, jmax);
-#endif
             if (act) ol = r;
             wave_lds_sync();
             PROF_MARK(2);
-            if (kEarlyCommit && have_next && nxt.fits) {  // the input stage is free: fill it before our stores
-                if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
-                pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
-                committed = true;
-            }
             PROF_MARK(3);
-#ifdef HHUFF_ABL_NOCOPY
-            if (region && A.n == 0) {
-#else
             if (region) {
-#endif
                 if (A.edges)
                     region_copy_deferred(A.out, cur.a0, obuf, cur.ospan, t.lo, t.hi, lane, A.edges + 2 * (base >> 6));
                 else
@@ -1099,8 +981,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
             PROF_FLUSH(1);
             break;
         }
-        if (nxt.fits && !committed) {
-            if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+        if (nxt.fits) {
             pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
         }
         cur = nxt;
@@ -1126,6 +1007,10 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
 // blocks sample 4096 positions: for each candidate K <= K0 they count the K-string spans that would
 // not fit.  Every encode_pl block then takes the largest candidate with no overflow in the sample.
 constexpr uint32_t kPlCand[6] = {32u, 21u, 16u, 12u, 10u, 8u};
+// input stage bytes per wave of encode_pl_kernel / flatten_pl_kernel: the planner's fit limit derives from it
+// (a tile fits when its 16-B aligned span does: raw span + 30 <= kPlStage).  flatten_pl_kernel's output
+// stage is kPlStage + 11 * 64 + 32 bytes, so a tile whose input fits always fits its framed output too.
+constexpr uint32_t kPlStage = 3584u;
 constexpr uint32_t kPlBlocks = 64;
 __global__ __launch_bounds__(64) void encode_plan_kernel(const uint32_t* __restrict__ in_off, uint32_t n, uint32_t K0,
                                                          uint32_t limit, uint32_t* __restrict__ part) {
@@ -1225,7 +1110,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
         Plan nxt;
         if (have_next) {
             nxt = plan(tn, ns, ne);
-            if (kSpanPrefetch && nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+            if (nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
             if (tn + tstride < ntiles) issue(tn + tstride, ns, ne);
         }
         // ---- the current tile ----
@@ -1296,7 +1181,6 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
         if (own) finish_encode(A, (uint32_t)(cur.i0 + lane), len, ol);
         if (!have_next) break;
         if (nxt.fits) {
-            if (!kSpanPrefetch) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
             pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
         }
         cur = nxt;
@@ -1320,205 +1204,6 @@ __global__ __launch_bounds__(WAVES * 64) void encode_direct_kernel(EncArgs A) {
             ol = encode_core(GlobalSource{A.in, A.in_size}, s, len, sink, s_enc);
         }
         finish_encode(A, (uint32_t)i, len, ol);
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Byte-balanced encode for the implicit contiguous layout (out_off == NULL, in_len == NULL).
-// A tile is K consecutive strings; its input span is staged in LDS and split into 16-byte chunks,
-// one per lane (every lane does the same work whatever the string lengths).  Per chunk round:
-//   A. each lane looks up its 16 bytes' {code, nbits} and sums the bits; a wave exclusive scan gives
-//      every chunk its bit offset G inside the tile's concatenated code stream;
-//   B. the lane that holds a string's first byte records gbase[s] = G at that byte (LDS);
-//   C. each lane emits its codes at bit 8 * start[s] + (G - gbase[s]) of the string's slot in the
-//      zeroed LDS output stage (slot = input offset, h2o's contract), OR-ing whole dwords (ds_or_b32) so
-//      neighbouring lanes and strings never overwrite each other.  Codes that would end past the
-//      string's capacity (8 * len bits) are dropped: that string fails anyway.
-// Finally gbase[s+1] - gbase[s] is each string's code length: Huffman length = ceil(bits / 8) when it is
-// strictly shorter than the string (hpack.c:789-800), else SIZE_MAX; the last byte is padded with ones.
-// ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void chunk_flush(uint32_t* obuf32, uint64_t& acc, uint32_t& fill, uint32_t& dw) {
-    if (fill >= 32) {
-        atomicOr(&obuf32[dw], bswap32((uint32_t)(acc >> 32)));
-        acc <<= 32;
-        fill -= 32;
-        dw += 1;
-    }
-}
-
-template <int WAVES, int STAGE, int KMAX>
-__global__ __launch_bounds__(WAVES * 64) void encode_chunked_kernel(EncArgs A, uint32_t K) {
-    __shared__ __attribute__((aligned(16))) uint2 s_enc[512];  // 256..511: bytes outside any string
-    __shared__ __attribute__((aligned(16))) uint32_t s_in[WAVES][STAGE / 4];
-    __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][STAGE / 4 + 4];
-    __shared__ uint32_t s_start[WAVES][KMAX + 1];  // string starts relative to the span start, + end
-    __shared__ uint32_t s_gbase[WAVES][KMAX + 1];  // tile bit offset at each string start, + total
-    for (uint32_t k = threadIdx.x; k < 512; k += WAVES * 64)
-        s_enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t* stage = s_in[wave];
-    uint32_t* obuf32 = s_out[wave];
-    uint32_t* start = s_start[wave];
-    uint32_t* gbase = s_gbase[wave];
-    const uint64_t ntiles = ((uint64_t)A.n + K - 1) / K;
-    for (uint64_t tile = (uint64_t)blockIdx.x * WAVES + wave; tile < ntiles; tile += (uint64_t)gridDim.x * WAVES) {
-        const uint64_t t0 = tile * K;
-        const uint32_t ns = (uint32_t)min((uint64_t)K, (uint64_t)A.n - t0);
-        const uint32_t lo = A.in_off[t0], hi = A.in_off[t0 + ns];
-        const uint32_t a0 = lo & ~15u;
-        const uint32_t span = ((hi + 15u) & ~15u) - a0;
-        if (span > STAGE) {  // a tile of long strings: one lane per string, straight from global memory
-            for (uint32_t j = lane; j < ns; j += 64) {
-                const uint32_t i = (uint32_t)t0 + j, s = A.in_off[i], len = A.in_off[i + 1] - s;
-                uint32_t ol = kFailLen;
-                if (len <= kMaxStrLen) {
-                    RegSink sink;
-                    sink.init(A.out + s);
-                    ol = encode_core(GlobalSource{A.in, A.in_size}, s, len, sink, s_enc);
-                }
-                finish_encode(A, i, len, ol);
-            }
-            continue;
-        }
-        for (uint32_t j = lane; j <= ns; j += 64) start[j] = A.in_off[t0 + j] - a0;
-        stage_span(stage, A.in, A.in_size, a0, span, lane);
-        for (uint32_t k = (uint32_t)lane * 16u; k < span + 16u; k += 64u * 16u)
-            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(obuf32) + k) = make_uint4(0u, 0u, 0u, 0u);
-        wave_lds_sync();
-        const uint32_t sbeg = start[0], send = start[ns];  // bytes outside [sbeg, send) belong to no string
-        uint32_t carry = 0;
-        for (uint32_t c0 = 0; c0 < span; c0 += 1024u) {
-            const uint32_t p = c0 + 16u * (uint32_t)lane;  // this lane's chunk [p, p + 16)
-            const bool live = p < span;
-            // ---- A: lookups and bit totals per dword ----
-            uint32_t cd[4], nd[4], lng = 0;
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const uint32_t pos = p + 4u * d;
-                const uint32_t w = live ? stage[pos >> 2] : 0u;
-                const int32_t dlo = (int32_t)(sbeg - pos), dhi = (int32_t)(send - pos);
-                const uint32_t nlo = (uint32_t)min(max(dlo, 0), 4), nhi = live ? (uint32_t)min(max(dhi, 0), 4) : 0u;
-                const uint32_t vm = (uint32_t)(0xFFFFFFFFull >> (8 * (4 - nhi))) & (uint32_t)(0xFFFFFFFFull << (8 * nlo));
-                const uint32_t iw = ~vm & 0x01010101u;
-                const uint2 e0 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0400u)];
-                const uint2 e1 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)];
-                const uint2 e2 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)];
-                const uint2 e3 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)];
-                nd[d] = e0.y + e1.y + e2.y + e3.y;
-                cd[d] = (((e0.x << e1.y | e1.x) << e2.y | e2.x) << e3.y) | e3.x;
-                lng |= (max(max(e0.y, e1.y), max(e2.y, e3.y)) > 8 ? 1u : 0u) << d;
-            }
-            const uint32_t tot = nd[0] + nd[1] + nd[2] + nd[3];
-            const uint32_t excl = wave_excl_scan(tot, lane);
-            const uint32_t G0 = carry + excl;
-            carry += __shfl(excl + tot, 63, 64);
-            // ---- B: record gbase for every string that starts in [p, p + 16) ----
-            // first string index with start >= p (binary search over start[0..ns))
-            uint32_t lo_i = 0, hi_i = ns;
-            while (lo_i < hi_i) {
-                const uint32_t mid = (lo_i + hi_i) >> 1;
-                if (start[mid] < p) lo_i = mid + 1;
-                else hi_i = mid;
-            }
-            const uint32_t sfirst = lo_i;
-            if (live) {
-                for (uint32_t j = sfirst; j < ns && start[j] < p + 16u; ++j) {
-                    const uint32_t q = start[j];  // bits of the chunk bytes before q
-                    uint32_t bits = 0;
-                    for (uint32_t b = p; b < q; ++b) {
-                        const uint32_t byte = (stage[b >> 2] >> (8 * (b & 3u))) & 0xFFu;
-                        bits += (b >= sbeg && b < send) ? s_enc[byte].y : 0u;
-                    }
-                    gbase[j] = G0 + bits;
-                }
-            }
-            wave_lds_sync();
-            // ---- C: emit ----
-            if (live) {
-                // the string holding byte p: last s with start[s] <= p and start[s+1] > p
-                int32_t s = (int32_t)sfirst;
-                if (s < (int32_t)ns && start[s] == p) {
-                    while (s + 1 < (int32_t)ns && start[s + 1] == p) ++s;  // skip empty strings at p
-                } else {
-                    s -= 1;
-                }
-                uint32_t G = G0;
-                uint64_t acc = 0;
-                uint32_t fill = 0, dw = 0, rel = 0, capb = 0, nxt = sbeg;
-                bool open = false;
-                auto open_seg = [&](int32_t si) {
-                    const uint32_t st = start[si];
-                    nxt = start[si + 1];
-                    rel = G - gbase[si];
-                    capb = 8u * (nxt - st);
-                    const uint32_t P = 8u * st + rel;
-                    acc = 0;
-                    fill = P & 31u;
-                    dw = P >> 5;
-                    open = true;
-                };
-                auto close_seg = [&]() {
-                    if (open && fill) atomicOr(&obuf32[dw], bswap32((uint32_t)(acc >> 32)));
-                    open = false;
-                };
-                if (s >= 0 && s < (int32_t)ns && p < start[s + 1]) open_seg(s);
-                else nxt = s < 0 ? sbeg : 0xFFFFFFFFu;  // before the first string / past the last
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const uint32_t pos = p + 4u * d;
-                    if (open && pos + 4u <= nxt && !((lng >> d) & 1u)) {  // whole dword in one string, short codes
-                        if (rel + nd[d] <= capb) {
-                            acc |= (uint64_t)cd[d] << ((64u - fill - nd[d]) & 63u);
-                            fill += nd[d];
-                            chunk_flush(obuf32, acc, fill, dw);
-                        }
-                        rel += nd[d];
-                        G += nd[d];
-                    } else {
-                        const uint32_t w = stage[pos >> 2];
-                        for (uint32_t k = 0; k < 4; ++k) {
-                            const uint32_t b = pos + k;
-                            if (b >= send) break;
-                            if (b >= nxt || (!open && b >= sbeg)) {  // a string starts here
-                                close_seg();
-                                int32_t si = s < 0 ? 0 : s + 1;
-                                while (si + 1 < (int32_t)ns && start[si + 1] <= b) ++si;  // skip empty strings
-                                s = si;
-                                open_seg(si);
-                            }
-                            if (!open) continue;
-                            const uint2 e = s_enc[(w >> (8 * k)) & 0xFFu];
-                            if (rel + e.y <= capb) {
-                                acc |= (uint64_t)e.x << ((64u - fill - e.y) & 63u);
-                                fill += e.y;
-                                chunk_flush(obuf32, acc, fill, dw);
-                            }
-                            rel += e.y;
-                            G += e.y;
-                        }
-                    }
-                }
-                close_seg();
-            }
-        }
-        if (lane == 0) gbase[ns] = carry;
-        wave_lds_sync();
-        // ---- per string: length, verdict, padding ----
-        for (uint32_t j = lane; j < ns; j += 64) {
-            const uint32_t T = gbase[j + 1] - gbase[j], len = start[j + 1] - start[j];
-            const bool ok = len != 0 && T + 8u <= 8u * len;  // ceil(T / 8) < len
-            if (ok && (T & 7u)) {  // ones after the last code up to the byte boundary (hpack.c:795-798)
-                const uint32_t P = 8u * start[j] + T;
-                const uint32_t nbit = 8u - (P & 7u);  // 1..7, inside one byte
-                const uint32_t mask = ((1u << nbit) - 1u) << (31u - (P & 31u) - (nbit - 1u));
-                atomicOr(&obuf32[P >> 5], bswap32(mask));
-            }
-            finish_encode(A, (uint32_t)t0 + j, len, ok ? (T + 7u) >> 3 : kFailLen);
-        }
-        wave_lds_sync();
-        region_copy<(STAGE + 1023) / 1024>(A.out, a0, reinterpret_cast<const uint8_t*>(obuf32), span, lo, hi, lane);
-        wave_lds_sync();
     }
 }
 
@@ -1955,31 +1640,22 @@ __global__ void literal_fix_kernel(LitArgs A) {
 //   encode direct:         4 waves/WG                                      [2 KiB]
 // The variant is picked from the mean bytes per string (in_size / n).
 // ------------------------------------------------------------------------------------------------
-#ifndef HHUFF_DSW  // waves per workgroup of the short-string decode (A/B knob)
-#define HHUFF_DSW 16
-#endif
-#define DEC_S decode_staged_kernel<HHUFF_DSW, 3072, 4608>
+// (measured shapes, kept for the record: stream kernel waves / window dwords / output bytes per lane, c3 /
+//  u400 decode ms: 12,12,96: 0.335 / 0.621; 16,8,64: 0.390 / 0.783; 8,16,112: 0.316 / 0.527.  Short-string
+//  encode waves per block, c4 ms: 16: 0.83; 12: 0.93; 20 does not launch at 118 VGPRs.)
+constexpr int kDecSWaves = 16, kDecTWaves = 8, kEncSWaves = 16;
+#define DEC_S decode_staged_kernel<kDecSWaves, 3072, 4608>
 #define DEC_L decode_staged_kernel<6, 8192, 12928>
 #define DEC_D decode_direct_kernel<4>
-#ifndef HHUFF_DTW  // streaming decode shape: waves per block, window dwords, output bytes per lane
-#define HHUFF_DTW 8    // measured (c3 / u400 decode, ms): 12,12,96: 0.335 / 0.621; 16,8,64: 0.390 / 0.783;
-#define HHUFF_DTNW 16  // 8,16,112: 0.316 / 0.527
-#define HHUFF_DTOUT 112
-#endif
-#define DEC_T decode_stream_kernel<HHUFF_DTW, HHUFF_DTNW, HHUFF_DTOUT>
-#ifndef HHUFF_ESW  // waves per block of the short-string encode kernel (c4, ms): 16: 0.83; 12: 0.93;
-#define HHUFF_ESW 16  // 20: does not launch (118 VGPRs allow 4 waves per SIMD)
-#endif
-#define ENC_S encode_staged_kernel<HHUFF_ESW, 3584>
+#define DEC_T decode_stream_kernel<kDecTWaves, 16, 112>
+#define ENC_S encode_staged_kernel<kEncSWaves, 3584>
 #define ENC_L encode_staged_kernel<8, 8192>
 #define ENC_D encode_direct_kernel<4>
 #define FLAT_D flatten_direct_kernel<4>
-#define ENC_P encode_pl_kernel<16, 3584>
-#define FLAT_P flatten_pl_kernel<16, 3584>
-#define ENC_C encode_chunked_kernel<12, 4096, 128>
-#define ENC_CL encode_chunked_kernel<8, 8192, 64>
+#define ENC_P encode_pl_kernel<16, kPlStage>
+#define FLAT_P flatten_pl_kernel<16, kPlStage>
 
-enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncC, kEncCL, kEncP, kFlatP, kDecT, kNumVariants };
+enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncP, kFlatP, kDecT, kNumVariants };
 
 static const void* variant_fn(int v) {
     switch (v) {
@@ -1990,8 +1666,6 @@ static const void* variant_fn(int v) {
         case kEncS: return (const void*)ENC_S;
         case kEncL: return (const void*)ENC_L;
         case kFlatD: return (const void*)FLAT_D;
-        case kEncC: return (const void*)ENC_C;
-        case kEncCL: return (const void*)ENC_CL;
         case kEncP: return (const void*)ENC_P;
         case kFlatP: return (const void*)FLAT_P;
         default: return (const void*)ENC_D;
@@ -1999,13 +1673,11 @@ static const void* variant_fn(int v) {
 }
 static int variant_threads(int v) {
     switch (v) {
-        case kDecS: return HHUFF_DSW * 64;
-        case kDecT: return HHUFF_DTW * 64;
-        case kEncS: return HHUFF_ESW * 64;
+        case kDecS: return kDecSWaves * 64;
+        case kDecT: return kDecTWaves * 64;
+        case kEncS: return kEncSWaves * 64;
         case kDecL: return 384;
         case kEncL: return 512;
-        case kEncC: return 768;
-        case kEncCL: return 512;
         case kEncP:
         case kFlatP: return 1024;
         default: return 256;
@@ -2035,9 +1707,6 @@ static int current_device() {
     return dev;
 }
 
-#ifndef HHUFF_DEC_SELECT  // A/B knob: device-side staged/stream choice for mean lengths in (40, 128]
-#define HHUFF_DEC_SELECT 1
-#endif
 // Mixed lengths (Zipf 8..512 B): a staged tile of 64 strings runs as long as its longest
 // string, while the stream kernel pays a per-string setup but never waits for another lane.  Which is
 // faster depends on the length spread, and the lengths live in device memory: 64 one-wave blocks (on
@@ -2084,31 +1753,14 @@ __global__ __launch_bounds__(64) void decode_select_kernel(DecArgs A, uint64_t* 
     }
 }
 
-#ifndef HHUFF_FORCE_DEC  // A/B knob: force a decode variant (kDecS / kDecL / kDecD / kDecT), -1 = by mean length
-#define HHUFF_FORCE_DEC -1
-#endif
 static int pick_decode(uint64_t in_size, uint32_t n) {
-    if (HHUFF_FORCE_DEC >= 0) return HHUFF_FORCE_DEC;
     const uint64_t mean = n ? in_size / n : 0;  // in_size bounds the bytes the batch can address
     if (mean <= 40) return kDecS;
     if (mean <= 128) return kDecL;
     return kDecT;  // u400: 2.35 ms (kDecL, tiles past the stage go direct) -> 0.53 ms
 }
-#ifndef HHUFF_ENC_PL  // A/B knobs: proportional-lane encode from this mean string length up (0 = always)
-#define HHUFF_ENC_PL 53
-#endif
-#ifndef HHUFF_ENC_PL_PLAN  // A/B knob: device-sampled tile size (encode_plan_kernel)
-#define HHUFF_ENC_PL_PLAN 1
-#endif
-#ifndef HHUFF_ENC_PL_SNAP  // A/B knob: round K down to 64 / ceil(64 / K)
-#define HHUFF_ENC_PL_SNAP 1
-#endif
-#ifndef HHUFF_ENC_PL_FILL  // mean bytes a proportional-lane tile is planned for (of a 3584-B stage)
-#define HHUFF_ENC_PL_FILL 2560
-#endif
-#ifndef HHUFF_ENC_PL_K  // strings per tile (0 = from the mean length)
-#define HHUFF_ENC_PL_K 0
-#endif
+constexpr uint64_t kEncPlMean = 53;   // proportional-lane encode from this mean string length up
+constexpr uint64_t kPlFill = 2560;    // mean bytes a proportional-lane tile is planned for (of kPlStage)
 static uint64_t edge_recs(uint32_t n) { return 2 * (((uint64_t)n + 63) / 64); }
 
 // Edge records come from a library-owned stream-ordered pool that keeps its memory between calls (the
@@ -2155,7 +1807,7 @@ static hipError_t finish_deferred(uint8_t* out, EdgeRec* edges, uint32_t n, hipS
 
 static bool use_pl_encode(uint64_t in_size, uint32_t n) {
     const uint64_t mean = n ? in_size / n : 0;
-    return HHUFF_ENC_PL >= 0 && mean >= (uint64_t)HHUFF_ENC_PL;
+    return mean >= kEncPlMean;
 }
 static int pick_encode(uint64_t in_size, uint32_t n) {
     const uint64_t mean = n ? in_size / n : 0;
@@ -2171,8 +1823,8 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr, nullptr, nullptr};
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n);
     const int grid = grid_for(v, current_device(), n);
-    const bool defer = HHUFF_DEFER_EDGES && (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr;
-    if (v == kDecL && HHUFF_DEC_SELECT) {  // mixed lengths: the device picks staged or stream (see below)
+    const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr;
+    if (v == kDecL) {  // mixed lengths: the device picks staged or stream (see below)
         uint64_t* sel = nullptr;  // [0, 3 kSelBlocks): partial sums; then the verdict and the work counter
         hipError_t e = pool_alloc((void**)&sel, (3 * kSelBlocks + 2) * sizeof(uint64_t), stream);
         if (e != hipSuccess) return e;
@@ -2193,7 +1845,7 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         }
         if (e == hipSuccess) {
             A.edges = nullptr;
-            hipLaunchKernelGGL(DEC_T, dim3(grid_for(kDecT, current_device(), n)), dim3(HHUFF_DTW * 64), 0, stream, A,
+            hipLaunchKernelGGL(DEC_T, dim3(grid_for(kDecT, current_device(), n)), dim3(kDecTWaves * 64), 0, stream, A,
                                ctr);
             e = hipGetLastError();
         }
@@ -2209,7 +1861,7 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         hipError_t e = pool_alloc((void**)&ctr, sizeof(*ctr), stream);
         if (e == hipSuccess) e = hipMemsetAsync(ctr, 0, sizeof(*ctr), stream);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(DEC_T, dim3(grid), dim3(HHUFF_DTW * 64), 0, stream, A, ctr);
+            hipLaunchKernelGGL(DEC_T, dim3(grid), dim3(kDecTWaves * 64), 0, stream, A, ctr);
             e = hipGetLastError();
         }
         if (ctr) {
@@ -2219,7 +1871,7 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         return e;
     }
     switch (v) {
-        case kDecS: hipLaunchKernelGGL(DEC_S, dim3(grid), dim3(HHUFF_DSW * 64), 0, stream, A); break;
+        case kDecS: hipLaunchKernelGGL(DEC_S, dim3(grid), dim3(kDecSWaves * 64), 0, stream, A); break;
         case kDecL: hipLaunchKernelGGL(DEC_L, dim3(grid), dim3(384), 0, stream, A); break;
         default: hipLaunchKernelGGL(DEC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }
@@ -2232,31 +1884,13 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     if (n == 0) return hipSuccess;
     EncArgs A{in, in_size, in_off, in_len, n, out, out_off, out_len, status, nullptr};
     if (sel_bytes) in_size = sel_bytes;  // variant selection only; A keeps the addressable size
-#ifdef HHUFF_ENCODE_CHUNKED
-    if (in_len == nullptr && out_off == nullptr) {  // contiguous implicit layout: byte-balanced chunks
-        const uint64_t mean = in_size / n;
-        const bool big = mean > 96;
-        const uint32_t stage = big ? 8192u : 4096u, kmax = big ? 64u : 128u;
-        const uint64_t k = mean ? (stage * 3u / 5u) / mean : kmax;
-        const uint32_t K = (uint32_t)(k < 1 ? 1 : (k > kmax ? kmax : k));
-        const uint64_t tiles = ((uint64_t)n + K - 1) / K;
-        const int v = big ? kEncCL : kEncC;
-        const int waves = big ? 8 : 12;
-        const int g = grid_for(v, current_device(), 0xFFFFFFFFu);
-        const int grid = (int)((tiles + waves - 1) / waves < (uint64_t)g ? (tiles + waves - 1) / waves : g);
-        if (big) hipLaunchKernelGGL(ENC_CL, dim3(grid), dim3(512), 0, stream, A, K);
-        else hipLaunchKernelGGL(ENC_C, dim3(grid), dim3(768), 0, stream, A, K);
-        return hipGetLastError();
-    }
-#endif
     if (in_len == nullptr && out_off == nullptr && use_pl_encode(in_size, n)) {
         // contiguous wire layout: proportional-lane tiles of K strings (about 5/8 of a stage of bytes)
         const uint64_t mean = in_size / n;
-        uint32_t K = HHUFF_ENC_PL_K ? (uint32_t)HHUFF_ENC_PL_K
-                                    : (uint32_t)(mean ? (uint64_t)HHUFF_ENC_PL_FILL / mean : 64u);
+        uint32_t K = (uint32_t)(mean ? kPlFill / mean : 64u);
         K = K < 1 ? 1u : (K > 64 ? 64u : K);
-        if (HHUFF_ENC_PL_SNAP) K = 64u / ((64u + K - 1u) / K);  // down to 64 / m: m lanes per string, few idle
-        const bool sample = HHUFF_ENC_PL_PLAN && HHUFF_ENC_PL_K == 0 && K > kPlCand[5] && n >= 4096;
+        K = 64u / ((64u + K - 1u) / K);  // down to 64 / m: m lanes per string, few idle
+        const bool sample = K > kPlCand[5] && n >= 4096;
         const uint32_t kmin = sample ? kPlCand[5] : K;
         const uint64_t tiles = ((uint64_t)n + kmin - 1) / kmin;
         const int g = grid_for(kEncP, current_device(), 0xFFFFFFFFu);
@@ -2270,7 +1904,7 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         hipError_t e = pool_alloc((void**)&part, 6 * kPlBlocks * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
         // a tile fits when its 16-B aligned span does: raw span + 30 <= stage
-        hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, in_off, n, K, 3584u - 30u, part);
+        hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, in_off, n, K, kPlStage - 30u, part);
         e = hipGetLastError();
         if (e == hipSuccess) {
             hipLaunchKernelGGL(ENC_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)part);
@@ -2281,13 +1915,13 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     }
     const int v = pick_encode(in_size, n);
     const int grid = grid_for(v, current_device(), n);
-    const bool defer = HHUFF_DEFER_EDGES && v != kEncD && in_len == nullptr && out_off == nullptr;
+    const bool defer = v != kEncD && in_len == nullptr && out_off == nullptr;
     if (defer) {
         hipError_t e = alloc_edges(&A.edges, n, stream);
         if (e != hipSuccess) return e;
     }
     switch (v) {
-        case kEncS: hipLaunchKernelGGL(ENC_S, dim3(grid), dim3(HHUFF_ESW * 64), 0, stream, A); break;
+        case kEncS: hipLaunchKernelGGL(ENC_S, dim3(grid), dim3(kEncSWaves * 64), 0, stream, A); break;
         case kEncL: hipLaunchKernelGGL(ENC_L, dim3(grid), dim3(512), 0, stream, A); break;
         default: hipLaunchKernelGGL(ENC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }
@@ -2301,10 +1935,10 @@ hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* i
     FlatArgs A{in, in_size, in_off, in_len, n, first_bytes, prefix_bits, raw_bits, out, out_off, out_len};
     if (in_len == nullptr && out_off == nullptr) {  // contiguous layout, implicit slots: proportional lanes
         const uint64_t mean = in_size / n;
-        uint32_t K = (uint32_t)(mean ? (uint64_t)HHUFF_ENC_PL_FILL / mean : 64u);  // as launch_encode
+        uint32_t K = (uint32_t)(mean ? kPlFill / mean : 64u);  // as launch_encode
         K = K < 1 ? 1u : (K > 64 ? 64u : K);
-        if (HHUFF_ENC_PL_SNAP) K = 64u / ((64u + K - 1u) / K);
-        const bool sample = HHUFF_ENC_PL_PLAN && K > kPlCand[5] && n >= 4096;
+        K = 64u / ((64u + K - 1u) / K);
+        const bool sample = K > kPlCand[5] && n >= 4096;
         const uint32_t kmin = sample ? kPlCand[5] : K;
         const uint64_t tiles = ((uint64_t)n + kmin - 1) / kmin;
         const int g = grid_for(kFlatP, current_device(), 0xFFFFFFFFu);
@@ -2317,7 +1951,7 @@ hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* i
         uint32_t* part = nullptr;
         hipError_t e = pool_alloc((void**)&part, 6 * kPlBlocks * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, in_off, n, K, 3584u - 30u, part);
+        hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, in_off, n, K, kPlStage - 30u, part);
         e = hipGetLastError();
         if (e == hipSuccess) {
             hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)part);

@@ -639,9 +639,9 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
         int32_t st = q_parse_context(t, max_entries, ctx, A.in, p, end);
         if (st == 0) {
             A.req_insert_count[k] = (uint64_t)ctx.ric;
-            // check_decode_context_blocked (:801-820)
-            const uint64_t nb = A.num_blocked ? A.num_blocked[lo] : 0u;
-            if (!(ctx.ric < t.total())) st = nb >= A.max_blocked ? kDF : HHUFF_QPK_BLOCKED;
+            // check_decode_context_blocked (:801-820); the max_blocked limit is applied per connection in
+            // section order by qpack_blocked_kernel (every parked stream raises num_blocked)
+            if (!(ctx.ric < t.total())) st = HHUFF_QPK_BLOCKED;
         }
         QArena R{A.arena, A.arena_off[k], A.arena_off[k + 1]};
         const uint32_t slot = A.sec_off[k];
@@ -665,6 +665,23 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
     }
 }
 
+// check_decode_context_blocked's slot limit (qpack.c:801-820) across one step's sections of a connection:
+// h2o raises conn->num_qpack_blocked for every stream it parks (lib/http3/server.c:1553), so the blocked
+// sections of a connection, in section order, take the free slots one by one; the first one that finds
+// num_blocked >= max_blocked fails with QPACK_DECOMPRESSION_FAILED.  One lane per connection.
+__global__ __launch_bounds__(256) void qpack_blocked_kernel(QpkArgs A) {
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < A.nconn; c += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t nb = A.num_blocked ? A.num_blocked[c] : 0u;
+        for (uint32_t k = A.conn_first[c]; k < A.conn_first[c + 1]; ++k) {
+            if (A.sstatus[k] != HHUFF_QPK_BLOCKED) continue;
+            if (nb >= A.max_blocked)
+                A.sstatus[k] = kDF;
+            else
+                ++nb;
+        }
+    }
+}
+
 uint64_t qpack_conn_scratch(uint32_t header_table_size) {
     return sizeof(QState) + qpk_ring_bytes(header_table_size) + 16ull * (header_table_size / kEntryOverhead + 1u);
 }
@@ -685,6 +702,9 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || nsec == 0) return e;
     hipLaunchKernelGGL(qpack_sections_kernel, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(qpack_blocked_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
     return hipGetLastError();
 }
 

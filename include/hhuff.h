@@ -177,7 +177,18 @@ int hhuff_hpack_decode_blocks(const uint8_t *in, uint64_t in_size, const uint32_
  *                        field -- against the table as the connection's encoder stream left it
  *        header_table_size  the decoder's SETTINGS_QPACK_MAX_TABLE_CAPACITY (h2o_qpack_create_decoder,
  *                        qpack.c:240); max_blocked its blocked-streams limit; num_blocked[c] (NULL = 0) the
- *                        caller's count of the connection's blocked streams (lib/http3/server.c:1544)
+ *                        caller's count of the connection's blocked streams before this step
+ *                        (lib/http3/server.c:1544).  Blocked sections of one step take the free slots in
+ *                        section order, as h2o raises num_qpack_blocked for every stream it parks
+ *                        (server.c:1553): the first blocked section that finds num_blocked >= max_blocked
+ *                        gets HHUFF_QPK_DECOMPRESSION_FAILED.
+ *      Table semantics: every section of a step is decoded against the table as the step's WHOLE encoder
+ *      stream left it.  h2o decodes a section against the table as it stands when the section arrives;
+ *      the two differ only when the same step's encoder stream evicts an entry an earlier-arriving section
+ *      still references -- which a compliant encoder never does (RFC 9204 2.1.1: an entry that
+ *      unacknowledged sections reference is not evictable).  Against such a peer this call reports
+ *      DECOMPRESSION_FAILED where h2o would have decoded the section; a caller that must match h2o
+ *      byte for byte there splits the step before the evicting instruction.
  *      Per connection: enc_status[c] = 0, HHUFF_QPK_DECOMPRESSION_FAILED (h2o then closes the connection
  *      with H2O_HTTP3_ERROR_QPACK_ENCODER_STREAM) or HHUFF_QPK_SKIPPED (an earlier step failed);
  *      enc_consumed[c] = bytes of complete instructions consumed (the rest waits for more input);

@@ -576,6 +576,12 @@ def qpack_edge_session():
                b"\x00\x00" + q(b"custom-key", 3, 0x20) + q(b"custom-value"),
                b"\x00\x00" + q(b"", 3, 0x20, True) + q(b"v"), b"\x00\x00" + q(b":status", 3, 0x20, True) + q(b"200"),
                b"\x00\x00" + q(b"Upper", 3, 0x20, True) + q(b"v"), b"\x00\x00\x2f\xff\xff\xff\xff\xff\xff\xff\xff\xff\x7f"]),
+        # blocked sections take the free slots in section order (num_blocked = index % 6, max_blocked 2):
+        # connection 12 (num_blocked 0) parks two and fails the third, connection 13 (1) parks one, fails one
+        (b"", []),
+        (b"", []),
+        (b"", [b"\x03\x00\x80", b"\x00\x00\xd1", b"\x03\x00\x80", b"\x04\x00\x80"]),
+        (b"", [b"\x03\x00\x80", b"\x03\x00\x81"]),
     ]
     sec, sec_len, cf, enc = [], [], [0], []
     for e, ss in conns:
@@ -601,7 +607,7 @@ def qpack_set():
     out = {}
     sessions = [(n, QS.make_session(nc, steps=st, seed=sd, header_table_size=h, adversarial_frac=adv), nc, h, mb)
                 for n, sd, nc, st, h, mb, adv in QPACK_SESSIONS]
-    sessions.append(("qedge", qpack_edge_session(), 10, 4096, 2))
+    sessions.append(("qedge", qpack_edge_session(), 14, 4096, 2))
     for name, steps, nconn, hts, mb in sessions:
         sr = O.QpackSession(O.ref(), nconn, hts, mb)
         nbl = (np.arange(nconn) % 6).astype(np.uint32)

@@ -537,7 +537,9 @@ int orc_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, const ui
             enc_status[c] = r;
             t->failed = r != 0;
         }
-        const uint64_t nb = num_blocked ? num_blocked[c] : 0;
+        /* h2o raises conn->num_qpack_blocked for every stream it parks (lib/http3/server.c:1553), so each
+         * blocked section of this step counts against max_blocked for the sections after it */
+        uint64_t nb = num_blocked ? num_blocked[c] : 0;
         for (uint32_t k = conn_first[c]; k < conn_first[c + 1]; ++k) {
             nfields[k] = 0;
             req_insert_count[k] = 0;
@@ -551,8 +553,10 @@ int orc_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, const ui
             if (st == 0) {
                 req_insert_count[k] = (uint64_t)ctx.req_insert_count;
                 /* check_decode_context_blocked (:801-820) */
-                if (!(ctx.req_insert_count < qpk_table_total(t)))
+                if (!(ctx.req_insert_count < qpk_table_total(t))) {
                     st = nb >= s->max_blocked ? ORC_QPK_DECOMPRESSION_FAILED : ORC_QPK_BLOCKED;
+                    nb += st == ORC_QPK_BLOCKED;
+                }
             }
             uint32_t nf = 0, slot = sec_off[k];
             qpk_arena_t A = {arena, arena_off[k], arena_off[k + 1]};

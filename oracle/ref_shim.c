@@ -9,8 +9,10 @@
  * ref_decode_literal below is harness glue: it strings the reference's own public pieces together in
  * the order decode_string (hpack.c:223-261) and decode_header_{name,value}_literal (qpack.c:559-629)
  * call them, minus the memory pool those static functions allocate from.
- * Used here (in the build container) to produce tests/golden/* and to pin the restatement.  It is
- * never needed on the GPU box.
+ * Used in the build container to produce tests/golden/* and to pin the restatement; the built
+ * oracle/_ref/libh2oref.so is git-ignored but travels to the GPU box with the tree (like libhhuff.so),
+ * where bench.py times it as the CPU baseline (cpu_baseline.kind "reference") and the drop-in tests
+ * run h2o's own callers through it.  Built only where /root/reference exists.
  */
 #include "lib/http3/qpack.c"
 
@@ -162,7 +164,7 @@ REF_API int ref_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, 
             enc_status[c] = r;
             s->failed[c] = r != 0;
         }
-        const uint64_t nb = num_blocked ? num_blocked[c] : 0;
+        uint64_t nb = num_blocked ? num_blocked[c] : 0; /* +1 per parked stream (lib/http3/server.c:1553) */
         for (uint32_t k = conn_first[c]; k < conn_first[c + 1]; ++k) {
             nfields[k] = 0;
             req_insert_count[k] = 0;
@@ -178,8 +180,10 @@ REF_API int ref_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, 
             if (st == 0) {
                 req_insert_count[k] = (uint64_t)ctx.req_insert_count;
                 st = check_decode_context_blocked(q, &ctx, nb, &blocked_ref);
-                if (st == 0 && blocked_ref != 0)
+                if (st == 0 && blocked_ref != 0) {
                     st = REF_QPK_BLOCKED;
+                    ++nb;
+                }
             }
             ctx.stats = &stats;
             h2o_mem_pool_t pool;
