@@ -47,6 +47,10 @@ def lib():
         L.hhuff_decode_batch.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]
         L.hhuff_encode_batch.restype = ctypes.c_int
         L.hhuff_encode_batch.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp]
+        L.hhuff_decode_batch_packed.restype = ctypes.c_int
+        L.hhuff_decode_batch_packed.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp, _vp]
+        L.hhuff_encode_batch_packed.restype = ctypes.c_int
+        L.hhuff_encode_batch_packed.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _vp]
         L.hhuff_flatten_batch.restype = ctypes.c_int
         L.hhuff_flatten_batch.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, _vp, ctypes.c_uint, _vp, _vp,
                                           _vp, _vp, _vp]
@@ -87,6 +91,7 @@ def lib():
 
 # symbols include/hhuff.h declares (checked by tests/test_capi_symbols.py)
 EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decode_batch", "hhuff_encode_batch",
+            "hhuff_decode_batch_packed", "hhuff_encode_batch_packed",
             "hhuff_flatten_batch", "hhuff_decode_literals", "hhuff_hpack_decode_blocks", "hhuff_hpack_scratch_size",
             "hhuff_qpack_decode", "hhuff_qpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
@@ -179,6 +184,48 @@ def encode_batch(data, in_off, n, in_len=None, out=None, out_off=None, out_len=N
     _check(lib().hhuff_encode_batch(_dp(data), in_size, _dp(in_off), _dp(in_len), n, _dp(out), _dp(out_off),
                                     _dp(out_len), _dp(status), _stream(stream)), "hhuff_encode_batch")
     return out, out_len, status
+
+
+def decode_batch_packed(data, in_off, n, is_name_bits=None, out=None, out_off=None, out_len=None, status=None,
+                        in_size=None, stream=None):
+    """Batched h2o_hpack_decode_huffman with packed output (include/hhuff.h hhuff_decode_batch_packed):
+    returns (out, out_off [n+1], out_len, status); string i at out[out_off[i] : out_off[i] + out_len[i]]."""
+    import torch
+
+    dev = data.device
+    in_size = data.numel() if in_size is None else in_size
+    if out is None:
+        out = torch.empty(decode_slot_size(in_size), dtype=torch.uint8, device=dev)
+    if out_off is None:
+        out_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    if out_len is None:
+        out_len = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    _check(lib().hhuff_decode_batch_packed(_dp(data), in_size, _dp(in_off), n, _dp(is_name_bits), _dp(out),
+                                           _dp(out_off), _dp(out_len), _dp(status), _stream(stream)),
+           "hhuff_decode_batch_packed")
+    return out, out_off, out_len, status
+
+
+def encode_batch_packed(data, in_off, n, out=None, out_off=None, out_len=None, status=None, in_size=None, stream=None):
+    """Batched h2o_hpack_encode_huffman with packed output (include/hhuff.h hhuff_encode_batch_packed):
+    returns (out, out_off [n+1], out_len, status)."""
+    import torch
+
+    dev = data.device
+    in_size = data.numel() if in_size is None else in_size
+    if out is None:
+        out = torch.empty(in_size + 16, dtype=torch.uint8, device=dev)
+    if out_off is None:
+        out_off = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    if out_len is None:
+        out_len = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    _check(lib().hhuff_encode_batch_packed(_dp(data), in_size, _dp(in_off), n, _dp(out), _dp(out_off), _dp(out_len),
+                                           _dp(status), _stream(stream)), "hhuff_encode_batch_packed")
+    return out, out_off, out_len, status
 
 
 def flatten_batch(data, in_off, n, prefix_bits=7, in_len=None, first_bytes=None, raw_bits=None, out=None, out_off=None,

@@ -123,6 +123,29 @@ HHUFF_API int hhuff_encode_batch(const uint8_t* in, uint64_t in_size, const uint
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "encode launch");
 }
 
+HHUFF_API int hhuff_decode_batch_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+                                        const uint32_t* is_name_bits, uint8_t* out, uint32_t* out_off, uint32_t* out_len,
+                                        uint8_t* status, void* stream) {
+    if (!out_off) return arg_fail("NULL out_off");
+    int rc = check_batch(in, in_off, n, out, out_len);
+    if (rc) return rc;
+    if (n && !status) return arg_fail("NULL status");
+    if ((in_size * 8) / 5 >= 0xFFFFFFFFull) return arg_fail("in_size too large for u32 packed offsets");
+    hipError_t e = hhuff::launch_decode_packed(in, in_size, in_off, n, is_name_bits, out, out_off, out_len, status,
+                                               (hipStream_t)stream);
+    return e == hipSuccess ? HHUFF_OK : hip_fail(e, "packed decode launch");
+}
+
+HHUFF_API int hhuff_encode_batch_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+                                        uint8_t* out, uint32_t* out_off, uint32_t* out_len, uint8_t* status, void* stream) {
+    if (!out_off) return arg_fail("NULL out_off");
+    int rc = check_batch(in, in_off, n, out, out_len);
+    if (rc) return rc;
+    if (in_size >= 0xFFFFFFFFull) return arg_fail("in_size too large for u32 packed offsets");
+    hipError_t e = hhuff::launch_encode_packed(in, in_size, in_off, n, out, out_off, out_len, status, (hipStream_t)stream);
+    return e == hipSuccess ? HHUFF_OK : hip_fail(e, "packed encode launch");
+}
+
 HHUFF_API int hhuff_flatten_batch(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len,
                                   uint32_t n, const uint8_t* first_bytes, unsigned prefix_bits, const uint32_t* raw_bits,
                                   uint8_t* out, const uint32_t* out_off, uint32_t* out_len, void* stream) {

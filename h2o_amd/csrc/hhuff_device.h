@@ -174,6 +174,25 @@ struct RegSink {
     }
 };
 
+// CountSink: counts the bytes and remembers the first and last one, writes nothing (first pass of the
+// packed-output direct path: the lengths fix every string's place before the second pass writes).
+struct CountSink {
+    uint32_t cnt, first, last;
+    __device__ __forceinline__ void init() { cnt = first = last = 0; }
+    __device__ __forceinline__ void put1(uint32_t b) {
+        first = cnt == 0 ? (b & 0xFFu) : first;
+        last = b & 0xFFu;
+        cnt += 1;
+    }
+    __device__ __forceinline__ void put12(uint32_t syms, bool two) {
+        first = cnt == 0 ? (syms & 0xFFu) : first;
+        last = (two ? (syms >> 8) : syms) & 0xFFu;
+        cnt += two ? 2u : 1u;
+    }
+    __device__ __forceinline__ uint32_t count() const { return cnt; }
+    __device__ __forceinline__ void finish() {}
+};
+
 // ---------------------------------------------------------------------------------------------------
 // Huffman bit reader: 64-bit MSB-aligned window; invariant at the top of a step: nb >= 33.
 // ---------------------------------------------------------------------------------------------------
@@ -279,6 +298,47 @@ __device__ __forceinline__ void lds_st8(uint32_t addr, uint32_t v) { *(lds_u8*)(
 __device__ __forceinline__ uint32_t sel_bits(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 __device__ __forceinline__ void lds_or32(uint32_t addr, uint32_t v) {
     __hip_atomic_fetch_or((lds_u32*)(size_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_ld8(uint32_t addr) { return *(const lds_u8*)(size_t)addr; }
+__device__ __forceinline__ uint32_t lds_ld32(uint32_t addr) { return *(const lds_u32*)(size_t)addr; }
+__device__ __forceinline__ void lds_st32(uint32_t addr, uint32_t v) { *(lds_u32*)(size_t)addr = v; }
+
+// Move n bytes from LDS byte address src to LDS byte address dst: one lane's string in a packed-output
+// compaction (the wave's prefix sum of the lengths gives dst).  The destination range must be zero: every
+// destination dword the string touches is OR-ed in (ds_or_b32), bytes outside [dst, dst + n) as zeros, so
+// the dwords a string shares with its neighbours need no byte stores and no ordering between lanes.  The
+// source is read as aligned dwords from 3 bytes before src on (those bytes are masked out) and shifted to
+// the destination's phase with v_alignbyte.  SWAP: the source holds MSB-first words (the encode stage),
+// byte-swapped on the way.
+template <bool SWAP = false>
+__device__ __forceinline__ void lds_move_or(uint32_t src, uint32_t dst, uint32_t n) {
+    if (n == 0) return;
+    const uint32_t ph = dst & 3u;
+    const uint32_t s0 = src - ph;  // source byte of the first destination dword's byte 0
+    const uint32_t q = s0 & ~3u, sh = s0 & 3u;
+    const uint32_t nd = (ph + n + 3u) >> 2;  // destination dwords
+    const uint32_t d4 = dst & ~3u;
+    const uint32_t hi_last = ph + n - 4u * (nd - 1u);  // bytes of the last dword that are ours (1..4)
+    auto rd = [&](uint32_t a) { const uint32_t w = lds_ld32(a); return SWAP ? bswap32(w) : w; };
+    // four destination dwords per round: the five source reads are issued back to back, one wait per round
+    for (uint32_t k = 0; k < nd; k += 4u) {
+        uint32_t w[5];
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j) w[j] = rd(q + 4u * (k + j));
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t kk = k + j;
+            uint32_t m = kk == 0 ? 0xFFFFFFFFu << (8u * ph) : 0xFFFFFFFFu;
+            m &= kk + 1u == nd ? 0xFFFFFFFFu >> (32u - 8u * hi_last) : 0xFFFFFFFFu;
+            if (kk < nd) lds_or32(d4 + 4u * kk, __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh) & m);
+        }
+    }
+}
+
+// Zero LDS bytes [a, b) of a wave's buffer (a, b multiples of 16), 16-B stores by the whole wave.
+__device__ __forceinline__ void lds_zero(uint8_t* base, uint32_t a, uint32_t b, int lane) {
+    for (uint32_t k = a + 16u * (uint32_t)lane; k < b; k += 1024u)
+        *reinterpret_cast<uint4*>(base + k) = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // ---------------------------------------------------------------------------------------------------

@@ -303,6 +303,7 @@ struct DecArgs {
     EdgeRec* edges;  // region layout: 2 records per 64-string tile (deferred edges), or NULL
     uint32_t* gate;        // NULL, or the device-side kernel choice (kGate*), written by the staged kernel
     const uint64_t* sel;   // decode_select_kernel's partial sums [3][kSelBlocks] (with gate)
+    uint32_t* pk_off;      // packed mode (decode_staged_kernel<.., true>): u32[n + 1] output places
 };
 
 __device__ __forceinline__ void load_dec_tables(uint32_t* s_lut, uint32_t* s_kinfo, uint32_t* s_ones, int nthreads) {
@@ -334,15 +335,35 @@ __device__ __forceinline__ void decode_direct(const DecArgs& A, uint32_t s, uint
     }
 }
 
-template <int WAVES, int IN_STAGE, int OUT_STAGE>
+// Packed output (PACKED, contiguous layout): the 64 strings of a tile are written back to back in string
+// order -- the wave's exclusive prefix sum of the decoded lengths places them -- from the tile's bound
+// position G = floor(8 * in_off[first string] / 5) on, so the kernel writes exactly the decoded bytes (the
+// slot layout writes whole floor(8 len / 5) slots).  pk_off[i] = G + place.  Tile runs never overlap: a
+// tile's decoded bytes fit the slot region of its input span.
+//
+// LDS per wave is one buffer of IN + OUT + 256 (+16 slack) bytes whose halves swap roles from tile to tile
+// in packed mode:
+//   even tile: input [0, IN), slot output [IN, IN + OUT), trash [IN + OUT, Z); packed run at [c0, c0 + T),
+//              c0 = G mod 16 (left end);
+//   odd tile:  slot output [0, OUT), trash [OUT, OUT + 256), input [OUT + 256, Z); packed run right-aligned
+//              (the largest c0 <= Z - T with c0 = G mod 16).
+// The compaction moves each lane's string from its slot to its place in two passes: first every byte
+// whose destination lies in the free half (the input / trash area of this tile), then the rest.  Each
+// destination of the second pass holds, as a source, only bytes the first pass has already read (the
+// run starts at least IN bytes away from the slots it is built from), so lanes copying in lock step
+// never overwrite a source another lane still needs.  The next tile's input then goes into the other
+// half, beside the packed run, before the run's 16-B stores are issued (the pipeline order of the slot
+// layout, whose commit also precedes the stores).
+template <int WAVES, int IN_STAGE, int OUT_STAGE, bool PACKED>
 __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
+    constexpr uint32_t Z = IN_STAGE + OUT_STAGE + 256u;  // + 16 slack: the run's last 16-B chunk may read past Z
+    static_assert(OUT_STAGE <= 2 * IN_STAGE + 480 && Z % 16 == 0, "packed compaction needs OUT <= 2 IN");
     // one LDS object, window LUT first: its byte offsets then fit the ds_read address with no base add
     struct __attribute__((aligned(16))) Smem {
         uint32_t lut[1u << HHUFF_LUT_BITS];
         uint32_t kinfo[32];
         uint32_t ones[(HHUFF_ONES_NENT + 3) & ~3];
-        uint32_t in[WAVES][IN_STAGE / 4];
-        uint8_t out[WAVES][OUT_STAGE + 256];  // + a trash dword per lane
+        uint8_t buf[WAVES][Z + 16];
     };
     if (A.gate) {  // mixed-length batch: price both kernels from the sampled tiles (decode_select_kernel)
         __shared__ uint32_t verdict;
@@ -360,14 +381,12 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     uint32_t* s_lut = sm.lut;
     uint32_t* s_kinfo = sm.kinfo;
     uint32_t* s_ones = sm.ones;
-    auto& s_in = sm.in;
-    auto& s_out = sm.out;
     load_dec_tables(s_lut, s_kinfo, s_ones, WAVES * 64);
     __syncthreads();
     const DecTables T{s_lut, s_kinfo, s_ones};
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t* stage = s_in[wave];
-    uint8_t* obuf = s_out[wave];
+    uint8_t* const buf = sm.buf[wave];
+    const uint32_t bufa = lds_addr(buf);
     const bool region = A.in_len == nullptr && A.out_off == nullptr;
     const bool pairs = A.in_len != nullptr;
     const uint64_t stride = (uint64_t)gridDim.x * WAVES * 64;
@@ -379,6 +398,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     struct Plan {
         uint32_t s, len, op0;    // per lane
         uint32_t lo, hi, ospan;  // wave-uniform
+        uint32_t ib, ob;         // byte offsets of the input and slot-output stages in the wave's buffer
         uint64_t dst_g;          // explicit destinations
         bool valid, fits;
         __device__ __forceinline__ uint32_t a0() const { return lo & ~15u; }
@@ -387,7 +407,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         __device__ __forceinline__ uint64_t ohi() const { return dec_slot(hi); }
         __device__ __forceinline__ uint64_t obase() const { return olo() & ~15ull; }
     };
-    auto plan = [&](uint64_t b, const TileIn& ti) {
+    auto plan = [&](uint64_t b, const TileIn& ti, uint32_t par) {
         Plan P;
         const Tile t = finish_tile(b, lane, A.n, ti, pairs);
         P.s = t.s;
@@ -395,6 +415,8 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         P.valid = t.valid;
         P.lo = __builtin_amdgcn_readfirstlane(t.lo);
         P.hi = __builtin_amdgcn_readfirstlane(t.hi);
+        P.ib = par ? OUT_STAGE + 256u : 0u;
+        P.ob = par ? 0u : IN_STAGE;
         P.dst_g = 0;
         if (region) {
             P.ospan = P.hi > P.lo ? (uint32_t)(P.ohi() - P.obase()) : 0u;
@@ -415,17 +437,18 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     // and its stores: the vmcnt counter also counts stores, so a load consumed right after the previous
     // tile's stores would wait for their writes to land.
     SpanPrefetch<(IN_STAGE + 1023) / 1024> pf;
+    uint32_t par = 0;  // layout parity of the current tile (packed mode alternates)
     TileIn ti = issue_tile(base, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
-    Plan cur = plan(base, ti);
+    Plan cur = plan(base, ti, 0);
     uint32_t cur_name = ti.name_word;
     if (cur.fits) pf.issue(A.in, A.in_size, cur.a0(), cur.span(), lane);
     bool have_next = base + stride < A.n;
     if (have_next) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
-    if (cur.fits) pf.template commit<true>(stage, A.in, A.in_size, cur.a0(), cur.span(), lane);
+    if (cur.fits) pf.template commit<true>(reinterpret_cast<uint32_t*>(buf + cur.ib), A.in, A.in_size, cur.a0(), cur.span(), lane);
     Plan nxt;
     uint32_t nxt_name = 0;
     if (have_next) {
-        nxt = plan(base + stride, ti);
+        nxt = plan(base + stride, ti, PACKED ? 1u : 0u);
         nxt_name = ti.name_word;
         if (nxt.fits) pf.issue(A.in, A.in_size, nxt.a0(), nxt.span(), lane);
         if (base + 2 * stride < A.n)
@@ -438,8 +461,12 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         const Plan& t = cur;
         const uint32_t ti_i = (uint32_t)base + (uint32_t)lane;
         const bool is_name = t.valid && A.is_name_bits ? ((cur_name >> (ti_i & 31)) & 1u) : false;
+        uint32_t* stage = reinterpret_cast<uint32_t*>(buf + cur.ib);
+        uint8_t* obuf = buf + cur.ob;
         uint32_t ol = 0;
         uint8_t st = 0;
+        uint64_t G = 0;        // packed: the tile's run start in `out`
+        uint32_t place = 0, T_run = 0, c0 = 0;
         PROF_MARK(0);
         if (cur.fits) {
             wave_lds_sync();
@@ -458,22 +485,83 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
                 ol = kFailLen;
                 st = kStatusFail;
             }
+            if constexpr (PACKED) {
+                // places: wave prefix sum of the kept lengths; then the two-pass compaction (see above)
+                const uint32_t keep = (t.valid && ol != kFailLen) ? ol : 0u;
+                place = wave_excl_scan(keep, lane);
+                T_run = (uint32_t)__builtin_amdgcn_readlane((int)(place + keep), 63);
+                G = dec_slot((uint32_t)__builtin_amdgcn_readfirstlane((int)t.s));
+                const uint32_t g15 = (uint32_t)G & 15u;
+                if (par == 0) {
+                    c0 = g15;
+                } else {
+                    c0 = ((Z - T_run) & ~15u) | g15;
+                    if (c0 > Z - T_run) c0 -= 16u;
+                }
+                const uint32_t D = c0 + place, S = cur.ob + cur.op0;
+                const uint32_t rend = (c0 + T_run + 15u) & ~15u;
+                // bytes [0, cut) of the string go to destinations below `edge`, the rest above it
+                const uint32_t edge = par == 0 ? IN_STAGE : OUT_STAGE;
+                const uint32_t cut = D >= edge ? 0u : min(keep, edge - D);
+                const uint32_t a0 = par == 0 ? 0u : cut, a1 = par == 0 ? cut : keep;  // pass 1: the free half
+                if (par == 0)
+                    lds_zero(buf, 0u, min(rend, IN_STAGE), lane);
+                else
+                    lds_zero(buf, max(c0 & ~15u, OUT_STAGE), rend, lane);
+                wave_lds_sync();
+                lds_move_or(bufa + S + a0, bufa + D + a0, a1 - a0);
+                const uint32_t b0 = par == 0 ? cut : 0u, b1 = par == 0 ? keep : cut;
+                if (__builtin_amdgcn_ballot_w64(b1 > b0) != 0) {  // pass 2: its sources were all read in pass 1
+                    wave_lds_sync();
+                    if (par == 0)
+                        lds_zero(buf, IN_STAGE, rend, lane);
+                    else
+                        lds_zero(buf, c0 & ~15u, OUT_STAGE, lane);
+                    wave_lds_sync();
+                    lds_move_or(bufa + S + b0, bufa + D + b0, b1 - b0);
+                }
+            }
             wave_lds_sync();
             PROF_MARK(2);  // verdicts
-        } else if (t.valid) {
+        } else if (!PACKED && t.valid) {
             const uint64_t d = A.out_off ? cur.dst_g : dec_slot(t.s);
             decode_direct(A, t.s, t.len, is_name, A.out + d, T, ol, st);
             PROF_MARK(6);  // direct path
+        } else if (PACKED) {
+            // a tile larger than the stages: count first (lengths fix the places), then decode into place
+            CountSink cs;
+            cs.init();
+            bool ok = false;
+            if (t.valid && t.len <= kMaxStrLen) {
+                const DecResult r = decode_core(GlobalSource{A.in, A.in_size}, t.s, t.len, cs, T);
+                ok = r.ok;
+                ol = ok ? r.len : kFailLen;
+                st = ok ? soft_bits(is_name, r.len, r.flags, cs.first, cs.last) : kStatusFail;
+            } else if (t.valid) {
+                ol = kFailLen;
+                st = kStatusTooLong;
+            }
+            const uint32_t keep = ok ? ol : 0u;
+            place = wave_excl_scan(keep, lane);
+            G = dec_slot((uint32_t)__builtin_amdgcn_readfirstlane((int)t.s));
+            if (ok && keep) {
+                RegSink sink;
+                sink.init(A.out + G + place);
+                (void)decode_core(GlobalSource{A.in, A.in_size}, t.s, t.len, sink, T);
+                sink.finish();
+            }
+            PROF_MARK(6);
         }
-        // ---- the next tile: commit its span (the input stage is free), plan + prefetch the one after ----
+        // ---- the next tile: commit its span (its input half is free), plan + prefetch the one after ----
         Plan nn;
         uint32_t nn_name = 0;
         bool have_nn = false;
         if (have_next) {
-            if (nxt.fits) pf.template commit<true>(stage, A.in, A.in_size, nxt.a0(), nxt.span(), lane);
+            if (nxt.fits)
+                pf.template commit<true>(reinterpret_cast<uint32_t*>(buf + nxt.ib), A.in, A.in_size, nxt.a0(), nxt.span(), lane);
             have_nn = nbase + stride < A.n;
             if (have_nn) {
-                nn = plan(nbase + stride, ti);
+                nn = plan(nbase + stride, ti, PACKED ? par : 0u);
                 nn_name = ti.name_word;
                 if (nn.fits) pf.issue(A.in, A.in_size, nn.a0(), nn.span(), lane);
                 if (nbase + 2 * stride < A.n)
@@ -483,7 +571,12 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         PROF_MARK(3);  // commit + plan
         // ---- the current tile: stores ----
         if (cur.fits) {
-            if (region) {
+            if (PACKED) {
+                const uint64_t gb = G & ~15ull;
+                region_copy_deferred(A.out, gb, buf + c0 - ((uint32_t)G & 15u),
+                                     (uint32_t)(((G + T_run + 15u) & ~15ull) - gb), G, G + T_run, lane,
+                                     A.edges + 2 * (base >> 6));
+            } else if (region) {
                 if (A.edges)
                     region_copy_deferred(A.out, cur.obase(), obuf, cur.ospan, cur.olo(), cur.ohi(), lane,
                                          A.edges + 2 * (base >> 6));
@@ -500,6 +593,10 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         if (t.valid) {
             A.out_len[ti_i] = ol;
             A.status[ti_i] = st;
+            if (PACKED) {
+                A.pk_off[ti_i] = (uint32_t)(G + place);
+                if (ti_i == A.n - 1) A.pk_off[A.n] = (uint32_t)(G + place + (ol != kFailLen ? ol : 0u));
+            }
         }
         PROF_MARK(4);  // stores
         if (!have_next) {
@@ -512,6 +609,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         nxt_name = nn_name;
         have_next = have_nn;
         base = nbase;
+        if (PACKED) par ^= 1u;
     }
 }
 
@@ -862,6 +960,7 @@ struct EncArgs {
     uint32_t* out_len;
     uint8_t* status;
     EdgeRec* edges;  // region layout, encode_staged_kernel: 2 records per 64-string tile, or NULL
+    uint32_t* pk_off;  // packed mode (encode_staged_kernel<.., true>): u32[n + 1] output places
 };
 
 __device__ __forceinline__ void load_enc_table(uint2* s_enc, int nthreads) {
@@ -873,10 +972,31 @@ __device__ __forceinline__ void finish_encode(const EncArgs& A, uint32_t i, uint
     if (A.status) A.status[i] = ol == kFailLen ? (len > kMaxStrLen ? kStatusTooLong : kStatusFail) : 0;
 }
 
-template <int WAVES, int STAGE>
+__device__ __forceinline__ uint32_t count_code_bits(const GlobalSource& src, uint32_t start, uint32_t len,
+                                                    const uint2* __restrict__ enc) {
+    uint32_t bits = 0;
+    const uint32_t end = start + len;
+    for (uint32_t a = start & ~3u; a < end; a += 4) {
+        const uint32_t w = src.word(a);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t pos = a + k;
+            bits += (pos >= start && pos < end) ? enc[(w >> (8 * k)) & 0xFFu].y : 0u;
+        }
+    }
+    return bits;
+}
+
+// Packed output (PACKED, contiguous layout): as decode_staged_kernel's -- the tile's encoded strings back to
+// back in string order from G = in_off[first string of the tile], failed strings taking no bytes.  The
+// strings are encoded into their slots (the output stage mirrors the input) and then moved to their places
+// in the input stage, which is free once the tile is encoded (the next span is committed after the
+// stores); no two regions overlap, so one pass suffices.
+template <int WAVES, int STAGE, bool PACKED>
 __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
     __shared__ __attribute__((aligned(16))) uint2 s_enc[512];  // 256..511: bytes outside a string
-    __shared__ __attribute__((aligned(16))) uint32_t s_in[WAVES][STAGE / 4];
+    // + 32 B: a packed run starts up to 15 B into the stage and its last 16-B chunk may end 15 B past it
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[WAVES][STAGE / 4 + 8];
     __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][STAGE / 4 + 4];
     for (uint32_t k = threadIdx.x; k < 512; k += WAVES * 64)
         s_enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
@@ -949,13 +1069,36 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
                                                 act ? 8 * t.len - 7 : 0xFFFFFFFFu, true);
             const uint32_t r = tb == kFailLen ? kFailLen : (tb + 7) >> 3;
             PROF_MARK(1);
-            wave_lds_sync();
-            stage_bswap(obuf32, (cur.ospan + 15u) & ~15u, lane);
             if (act) ol = r;
-            wave_lds_sync();
-            PROF_MARK(2);
-            PROF_MARK(3);
-            if (region) {
+            if constexpr (PACKED) {
+                // the run goes to the input stage (free now), byte-swapped on the way (no stage_bswap pass)
+                const uint32_t keep = ol != kFailLen ? ol : 0u;
+                const uint32_t place = wave_excl_scan(keep, lane);
+                const uint32_t T_run = (uint32_t)__builtin_amdgcn_readlane((int)(place + keep), 63);
+                const uint64_t G = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.s);
+                const uint32_t g15 = (uint32_t)G & 15u;
+                lds_zero(reinterpret_cast<uint8_t*>(stage), 0u, (g15 + T_run + 15u) & ~15u, lane);
+                wave_lds_sync();
+                lds_move_or<true>(lds_addr(obuf) + cur.op0, lds_addr(stage) + g15 + place, keep);
+                wave_lds_sync();
+                PROF_MARK(2);
+                PROF_MARK(3);
+                const uint64_t gb = G & ~15ull;
+                region_copy_deferred(A.out, gb, reinterpret_cast<const uint8_t*>(stage),
+                                     (uint32_t)(((G + T_run + 15u) & ~15ull) - gb), G, G + T_run, lane,
+                                     A.edges + 2 * (base >> 6));
+                if (t.valid) {
+                    A.pk_off[t.i] = (uint32_t)(G + place);
+                    if (t.i == A.n - 1) A.pk_off[A.n] = (uint32_t)(G + place + keep);
+                }
+            } else {
+                wave_lds_sync();
+                stage_bswap(obuf32, (cur.ospan + 15u) & ~15u, lane);
+                wave_lds_sync();
+                PROF_MARK(2);
+            }
+            if (PACKED) {
+            } else if (region) {
                 if (A.edges)
                     region_copy_deferred(A.out, cur.a0, obuf, cur.ospan, t.lo, t.hi, lane, A.edges + 2 * (base >> 6));
                 else
@@ -965,6 +1108,26 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
             }
             wave_lds_sync();
             PROF_MARK(4);
+        } else if (PACKED) {
+            // a tile larger than the stage: code lengths first (they fix the places), then encode into place
+            const GlobalSource src{A.in, A.in_size};
+            const bool cand = t.valid && t.len != 0 && t.len <= kMaxStrLen;
+            const uint32_t bits = cand ? count_code_bits(src, t.s, t.len, s_enc) : 0u;
+            const bool ok = cand && bits <= 8u * t.len - 8u;  // ceil(bits / 8) < len (hpack.c:799-800)
+            const uint32_t keep = ok ? (bits + 7u) >> 3 : 0u;
+            if (ok) ol = keep;
+            RegSink sink;
+            const uint32_t place = wave_excl_scan(keep, lane);
+            const uint64_t G = (uint32_t)__builtin_amdgcn_readfirstlane((int)t.s);
+            if (ok) {
+                sink.init(A.out + G + place);
+                (void)encode_core(src, t.s, t.len, sink, s_enc);
+            }
+            if (t.valid) {
+                A.pk_off[t.i] = (uint32_t)(G + place);
+                if (t.i == A.n - 1) A.pk_off[A.n] = (uint32_t)(G + place + keep);
+            }
+            PROF_MARK(6);
         } else if (t.valid && t.len <= kMaxStrLen) {
             RegSink sink;
             sink.init(A.out + (A.out_off ? cur.dst_g : (uint64_t)t.s));
@@ -1248,21 +1411,6 @@ __device__ __forceinline__ void push_prefix_int(RegSink& sink, uint32_t h0, uint
     }
     sink.push((uint32_t)hb, min(hn, 4u));
     if (hn > 4) sink.push((uint32_t)(hb >> 32), hn - 4);
-}
-
-__device__ __forceinline__ uint32_t count_code_bits(const GlobalSource& src, uint32_t start, uint32_t len,
-                                                    const uint2* __restrict__ enc) {
-    uint32_t bits = 0;
-    const uint32_t end = start + len;
-    for (uint32_t a = start & ~3u; a < end; a += 4) {
-        const uint32_t w = src.word(a);
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t pos = a + k;
-            bits += (pos >= start && pos < end) ? enc[(w >> (8 * k)) & 0xFFu].y : 0u;
-        }
-    }
-    return bits;
 }
 
 template <int WAVES>
@@ -1644,23 +1792,32 @@ __global__ void literal_fix_kernel(LitArgs A) {
 //  u400 decode ms: 12,12,96: 0.335 / 0.621; 16,8,64: 0.390 / 0.783; 8,16,112: 0.316 / 0.527.  Short-string
 //  encode waves per block, c4 ms: 16: 0.83; 12: 0.93; 20 does not launch at 118 VGPRs.)
 constexpr int kDecSWaves = 16, kDecTWaves = 8, kEncSWaves = 16;
-#define DEC_S decode_staged_kernel<kDecSWaves, 3072, 4608>
-#define DEC_L decode_staged_kernel<6, 8192, 12928>
+#define DEC_S decode_staged_kernel<kDecSWaves, 3072, 4608, false>
+#define DEC_L decode_staged_kernel<6, 8192, 12928, false>
+#define DEC_SP decode_staged_kernel<kDecSWaves, 3072, 4608, true>
+#define DEC_LP decode_staged_kernel<6, 8192, 12928, true>
 #define DEC_D decode_direct_kernel<4>
 #define DEC_T decode_stream_kernel<kDecTWaves, 16, 112>
-#define ENC_S encode_staged_kernel<kEncSWaves, 3584>
-#define ENC_L encode_staged_kernel<8, 8192>
+#define ENC_S encode_staged_kernel<kEncSWaves, 3584, false>
+#define ENC_L encode_staged_kernel<8, 8192, false>
+#define ENC_SP encode_staged_kernel<kEncSWaves, 3584, true>
+#define ENC_LP encode_staged_kernel<8, 8192, true>
 #define ENC_D encode_direct_kernel<4>
 #define FLAT_D flatten_direct_kernel<4>
 #define ENC_P encode_pl_kernel<16, kPlStage>
 #define FLAT_P flatten_pl_kernel<16, kPlStage>
 
-enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncP, kFlatP, kDecT, kNumVariants };
+enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncP, kFlatP, kDecT, kDecSP, kDecLP, kEncSP, kEncLP,
+               kNumVariants };
 
 static const void* variant_fn(int v) {
     switch (v) {
         case kDecS: return (const void*)DEC_S;
         case kDecL: return (const void*)DEC_L;
+        case kDecSP: return (const void*)DEC_SP;
+        case kDecLP: return (const void*)DEC_LP;
+        case kEncSP: return (const void*)ENC_SP;
+        case kEncLP: return (const void*)ENC_LP;
         case kDecD: return (const void*)DEC_D;
         case kDecT: return (const void*)DEC_T;
         case kEncS: return (const void*)ENC_S;
@@ -1673,11 +1830,15 @@ static const void* variant_fn(int v) {
 }
 static int variant_threads(int v) {
     switch (v) {
-        case kDecS: return kDecSWaves * 64;
+        case kDecS:
+        case kDecSP: return kDecSWaves * 64;
         case kDecT: return kDecTWaves * 64;
-        case kEncS: return kEncSWaves * 64;
-        case kDecL: return 384;
-        case kEncL: return 512;
+        case kEncS:
+        case kEncSP: return kEncSWaves * 64;
+        case kDecL:
+        case kDecLP: return 384;
+        case kEncL:
+        case kEncLP: return 512;
         case kEncP:
         case kFlatP: return 1024;
         default: return 256;
@@ -1820,7 +1981,7 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
                          const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
                          uint8_t* status, hipStream_t stream, uint64_t sel_bytes) {
     if (n == 0) return hipSuccess;
-    DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr, nullptr, nullptr};
+    DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr, nullptr, nullptr, nullptr};
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n);
     const int grid = grid_for(v, current_device(), n);
     const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr;
@@ -1882,7 +2043,7 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
                          uint8_t* out, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, hipStream_t stream,
                          uint64_t sel_bytes) {
     if (n == 0) return hipSuccess;
-    EncArgs A{in, in_size, in_off, in_len, n, out, out_off, out_len, status, nullptr};
+    EncArgs A{in, in_size, in_off, in_len, n, out, out_off, out_len, status, nullptr, nullptr};
     if (sel_bytes) in_size = sel_bytes;  // variant selection only; A keeps the addressable size
     if (in_len == nullptr && out_off == nullptr && use_pl_encode(in_size, n)) {
         // contiguous wire layout: proportional-lane tiles of K strings (about 5/8 of a stage of bytes)
@@ -1926,6 +2087,99 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         default: hipLaunchKernelGGL(ENC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }
     return defer ? finish_deferred(out, A.edges, n, stream) : hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Packed output for the variants without a native packed mode (long strings: stream / direct decode,
+// proportional-lane encode): the kernel writes the slot layout into a stream-ordered scratch buffer,
+// then pack_tiles_kernel moves each 64-string tile's outputs to their places (one wave per tile: wave
+// prefix sum of the kept lengths, then byte copies by all 64 lanes, string after string).  Same places
+// as the native packed kernels; the extra pass costs a read and a write of the output.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pack_tiles_kernel(const uint8_t* __restrict__ tmp, const uint32_t* __restrict__ in_off,
+                                                         uint32_t n, bool dec, const uint32_t* __restrict__ out_len,
+                                                         uint8_t* __restrict__ out, uint32_t* __restrict__ pk_off) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t ntiles = ((uint64_t)n + 63) / 64;
+    for (uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64; t < ntiles;
+         t += (uint64_t)gridDim.x * blockDim.x / 64) {
+        const uint64_t i = t * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t ol = valid ? out_len[i] : 0u;
+        const uint32_t keep = ol != kFailLen ? ol : 0u;
+        const uint32_t place = wave_excl_scan(keep, lane);
+        const uint32_t s = valid ? in_off[i] : 0u;
+        const uint64_t G = dec ? dec_slot(in_off[t * 64]) : (uint64_t)in_off[t * 64];
+        const uint64_t src = dec ? dec_slot(s) : (uint64_t)s;
+        if (valid) {
+            pk_off[i] = (uint32_t)(G + place);
+            if (i == n - 1) pk_off[n] = (uint32_t)(G + place + keep);
+        }
+        for (int j = 0; j < 64; ++j) {
+            const uint32_t kj = (uint32_t)__shfl((int)keep, j, 64);
+            if (kj == 0) continue;
+            const uint64_t sj = ((uint64_t)(uint32_t)__shfl((int)(src >> 32), j, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)src, j, 64);
+            const uint64_t dj = G + (uint32_t)__shfl((int)place, j, 64);
+            for (uint32_t b = (uint32_t)lane; b < kj; b += 64u) out[dj + b] = tmp[sj + b];
+        }
+    }
+}
+
+static hipError_t pack_via_scratch(bool dec, const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+                                   const uint32_t* is_name_bits, uint8_t* out, uint32_t* pk_off, uint32_t* out_len,
+                                   uint8_t* status, hipStream_t stream);
+
+hipError_t launch_decode_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+                                const uint32_t* is_name_bits, uint8_t* out, uint32_t* pk_off, uint32_t* out_len,
+                                uint8_t* status, hipStream_t stream) {
+    if (n == 0) return hipMemsetAsync(pk_off, 0, sizeof(uint32_t), stream);
+    const uint64_t mean = in_size / n;
+    if (mean > 128) return pack_via_scratch(true, in, in_size, in_off, n, is_name_bits, out, pk_off, out_len, status, stream);
+    DecArgs A{in, in_size, in_off, nullptr, n, is_name_bits, out, nullptr, out_len, status, nullptr, nullptr, nullptr, pk_off};
+    const int v = mean <= 40 ? kDecSP : kDecLP;
+    hipError_t e = alloc_edges(&A.edges, n, stream);
+    if (e != hipSuccess) return e;
+    const int grid = grid_for(v, current_device(), n);
+    if (v == kDecSP)
+        hipLaunchKernelGGL(DEC_SP, dim3(grid), dim3(kDecSWaves * 64), 0, stream, A);
+    else
+        hipLaunchKernelGGL(DEC_LP, dim3(grid), dim3(384), 0, stream, A);
+    return finish_deferred(out, A.edges, n, stream);
+}
+
+hipError_t launch_encode_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n, uint8_t* out,
+                                uint32_t* pk_off, uint32_t* out_len, uint8_t* status, hipStream_t stream) {
+    if (n == 0) return hipMemsetAsync(pk_off, 0, sizeof(uint32_t), stream);
+    const uint64_t mean = in_size / n;
+    if (mean > 120) return pack_via_scratch(false, in, in_size, in_off, n, nullptr, out, pk_off, out_len, status, stream);
+    EncArgs A{in, in_size, in_off, nullptr, n, out, nullptr, out_len, status, nullptr, pk_off};
+    const int v = mean <= 52 ? kEncSP : kEncLP;
+    hipError_t e = alloc_edges(&A.edges, n, stream);
+    if (e != hipSuccess) return e;
+    const int grid = grid_for(v, current_device(), n);
+    if (v == kEncSP)
+        hipLaunchKernelGGL(ENC_SP, dim3(grid), dim3(kEncSWaves * 64), 0, stream, A);
+    else
+        hipLaunchKernelGGL(ENC_LP, dim3(grid), dim3(512), 0, stream, A);
+    return finish_deferred(out, A.edges, n, stream);
+}
+
+static hipError_t pack_via_scratch(bool dec, const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+                                   const uint32_t* is_name_bits, uint8_t* out, uint32_t* pk_off, uint32_t* out_len,
+                                   uint8_t* status, hipStream_t stream) {
+    uint8_t* tmp = nullptr;
+    const uint64_t bytes = (dec ? (in_size * 8) / 5 : in_size) + 64;
+    hipError_t e = pool_alloc((void**)&tmp, bytes, stream);
+    if (e != hipSuccess) return e;
+    e = dec ? launch_decode(in, in_size, in_off, nullptr, n, is_name_bits, tmp, nullptr, out_len, status, stream)
+            : launch_encode(in, in_size, in_off, nullptr, n, tmp, nullptr, out_len, status, stream);
+    if (e == hipSuccess) {
+        const uint32_t blocks = (uint32_t)min(((uint64_t)n + 255) / 256, (uint64_t)65535);
+        hipLaunchKernelGGL(pack_tiles_kernel, dim3(blocks), dim3(256), 0, stream, tmp, in_off, n, dec, out_len, out, pk_off);
+        e = hipGetLastError();
+    }
+    const hipError_t f = hipFreeAsync(tmp, stream);
+    return e != hipSuccess ? e : f;
 }
 
 hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,

@@ -10,6 +10,12 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
 hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
                          uint8_t* out, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, hipStream_t stream,
                          uint64_t sel_bytes = 0);
+// Packed output (include/hhuff.h hhuff_{de,en}code_batch_packed): contiguous layout, pk_off u32[n + 1]
+hipError_t launch_decode_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+                                const uint32_t* is_name_bits, uint8_t* out, uint32_t* pk_off, uint32_t* out_len,
+                                uint8_t* status, hipStream_t stream);
+hipError_t launch_encode_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n, uint8_t* out,
+                                uint32_t* pk_off, uint32_t* out_len, uint8_t* status, hipStream_t stream);
 // sel_bytes: bytes the batch's strings span, used only to pick the kernel variant from the mean string
 // length (0 = in_size).  Chunked callers pass `in` shifted back by the chunk base so that absolute
 // offsets address the chunk; in_size is then absolute and sel_bytes carries the chunk's own span.

@@ -82,6 +82,26 @@ int hhuff_decode_batch(const uint8_t *in, uint64_t in_size, const uint32_t *in_o
 int hhuff_encode_batch(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, const uint32_t *in_len, uint32_t n,
                        uint8_t *out, const uint32_t *out_off, uint32_t *out_len, uint8_t *status, void *stream);
 
+/* Packed output (wave-prefix compaction).  Contiguous layout only: string i = in[in_off[i] .. in_off[i+1]).
+ * The strings are cut into tiles of 64 consecutive strings (string i is in tile i / 64).  Within a tile the
+ * outputs are packed back to back in string order -- each wavefront lane owns one string and a wave-wide
+ * prefix sum of the output lengths places them -- and tile t's run starts at its bound position
+ *     decode: floor(8 * in_off[64 t] / 5)        encode: in_off[64 t]
+ * (the first string's slot of the implicit layouts above), so runs of different tiles never overlap and
+ * no byte outside the outputs is written: HBM traffic is exactly the output bytes.  Failed strings
+ * (HHUFF_FAIL_LEN) take no bytes.
+ *   out        decode: floor(8 * in_off[n] / 5) bytes; encode: in_off[n] bytes (16-byte aligned)
+ *   out_off    u32[n + 1], written: string i at out + out_off[i], out_len[i] bytes; out_off[n] = the end of
+ *              the last tile's run.  Inside a tile out_off[i + 1] = out_off[i] + string i's kept length, so
+ *              tile t's run is the one range from out_off[64 t] to the end of its last string.
+ *   out_len, status   as hhuff_decode_batch / hhuff_encode_batch
+ * Device arrays, asynchronous on `stream`; in_size must stay below 2^32 * 5 / 8 (u32 offsets). */
+int hhuff_decode_batch_packed(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, uint32_t n,
+                              const uint32_t *is_name_bits, uint8_t *out, uint32_t *out_off, uint32_t *out_len,
+                              uint8_t *status, void *stream);
+int hhuff_encode_batch_packed(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, uint32_t n, uint8_t *out,
+                              uint32_t *out_off, uint32_t *out_len, uint8_t *status, void *stream);
+
 /* Batched string-literal framing: QPACK flatten_string (lib/http3/qpack.c:1042-1066) and, with
  * first_bytes == NULL and prefix_bits == 7, HPACK h2o_hpack_encode_string (lib/http2/hpack.c:816-837).
  * Per string: Huffman when not flagged in raw_bits (QPACK's dont_compress) and strictly shorter, i.e.

@@ -60,6 +60,13 @@ def main():
     res["enc_packed_dst_ms"] = timed(torch, lambda: codec.encode_batch(b["data"], starts, n, in_len=l32, out=q_out,
                                                                       out_off=q_off32, out_len=e_len, status=e_st,
                                                                       in_size=P))
+    pk_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
+    pk_off = torch.empty(n_ok + 1, dtype=torch.int32, device="cuda")
+    res["dec_packed_ms"] = timed(torch, lambda: codec.decode_batch_packed(huff, h_off, n_ok, out=pk_out, out_off=pk_off,
+                                                                         out_len=d_len, status=d_st, in_size=H))
+    pe_off = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+    res["enc_packed_ms"] = timed(torch, lambda: codec.encode_batch_packed(b["data"], off32, n, out=q_out, out_off=pe_off,
+                                                                         out_len=e_len, status=e_st, in_size=P))
     print(json.dumps({k: round(v, 4) for k, v in res.items()}), flush=True)
     # per-string symbol latency
     s = b"www.example.com" * 3
