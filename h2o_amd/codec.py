@@ -330,7 +330,7 @@ QPK_CONTINUE = 1
 
 
 def qpack_decode(data, enc_off, enc_len, sec_off, conn_first, nsec, header_table_size=4096, max_blocked=100,
-                 num_blocked=None, arena_off=None, in_size=None, stream=None, scratch=None, cont=False):
+                 num_blocked=None, arena_off=None, in_size=None, stream=None, scratch=None, cont=False, arena=None):
     """QPACK decoder step (include/hhuff.h hhuff_qpack_decode) on device tensors: enc_off / enc_len (per
     connection), sec_off / conn_first / num_blocked int32 tensors (u32 bits), arena_off int64; nsec =
     conn_first[-1] as a host int.  Returns a dict of device tensors: arena, name_off, name_len, value_off,
@@ -346,7 +346,9 @@ def qpack_decode(data, enc_off, enc_len, sec_off, conn_first, nsec, header_table
         arena_off = default_arena_off(sec_off, header_table_size)
     nslots = max(1, int(sec_off[-1].item()) & 0xFFFFFFFF)
     i32 = lambda n: torch.empty(max(1, n), dtype=torch.int32, device=dev)  # noqa: E731
-    r = dict(arena=torch.empty(max(1, int(arena_off[-1].item())), dtype=torch.uint8, device=dev),
+    if arena is None:
+        arena = torch.empty(max(1, int(arena_off[-1].item())), dtype=torch.uint8, device=dev)
+    r = dict(arena=arena,
              name_off=i32(nslots), name_len=i32(nslots), value_off=i32(nslots), value_len=i32(nslots),
              fflags=torch.empty(nslots, dtype=torch.uint8, device=dev), nfields=i32(nsec), sstatus=i32(nsec),
              req_insert_count=torch.empty(max(1, nsec), dtype=torch.int64, device=dev), enc_status=i32(nconn),

@@ -314,7 +314,7 @@ __global__ __launch_bounds__(256) void hpack_blocks_kernel(BlkArgs A) {
             uint64_t p = A.blk_off[b];
             const uint64_t end = A.blk_off[b + 1];
             uint64_t cur = A.arena_off[b];
-            const uint64_t aend = A.arena_off[b + 1];
+            const uint64_t aend = min(A.arena_off[b + 1], kArenaLimit);  // field offsets are u32
             const uint32_t slot = A.blk_off[b];
             uint32_t nf = 0;
             int32_t st = 0;

@@ -28,6 +28,7 @@ constexpr uint32_t kFailLen = 0xFFFFFFFFu;
 constexpr uint8_t kStatusFail = 0x80;
 constexpr uint8_t kStatusTooLong = 0xC0;
 constexpr uint32_t kMaxStrLen = (1u << 29) - 1;
+constexpr uint64_t kArenaLimit = 1ull << 32;  // header-block arenas: field offsets are u32
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 

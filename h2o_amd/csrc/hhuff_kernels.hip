@@ -124,6 +124,15 @@ __device__ __forceinline__ Tile finish_tile(uint64_t base, int lane, uint32_t n,
     t.valid = (uint64_t)base + lane < n;
     t.s = in.s;
     t.len = t.valid ? (pairs ? in.len : in.len - in.s) : 0u;
+    if (!pairs) {
+        // contiguous layout: the span runs from the first string's start to the last one's end (empty
+        // strings add no bytes), two lane reads instead of two wave reductions
+        const uint64_t last = min((uint64_t)n - 1u - base, (uint64_t)63);
+        t.lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)in.s);
+        t.hi = (uint32_t)__builtin_amdgcn_readlane((int)in.len, (int)last);
+        if (t.hi == t.lo) t.lo = 0xFFFFFFFFu, t.hi = 0u;  // no bytes: as the reductions would report
+        return t;
+    }
     const bool has = t.valid && t.len != 0;
     t.lo = wave_min_u32(has ? t.s : 0xFFFFFFFFu);
     t.hi = wave_max_u32(has ? t.s + t.len : 0u);
@@ -212,13 +221,16 @@ struct EdgeRec {
     uint4 m;  // {address lo, address hi, lo, hi}: bytes [lo, hi) of the chunk are ours (lo >= hi: none)
 };
 
+// SWAP: the LDS bytes are MSB-first words (the encode stage), byte-swapped in registers on the way out.
+template <bool SWAP = false>
 __device__ __forceinline__ void region_copy_deferred(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds,
                                                      uint32_t ospan, uint64_t keep_lo, uint64_t keep_hi, int lane,
                                                      EdgeRec* __restrict__ rec) {
     const uint32_t kl = ospan ? (ospan - 1u) & ~15u : 0u;  // the last chunk
     for (uint32_t k = (uint32_t)lane * 16u; k < ospan; k += 64u * 16u) {
         const uint64_t g = gbase + k;
-        const uint4 v = *reinterpret_cast<const uint4*>(lds + k);
+        uint4 v = *reinterpret_cast<const uint4*>(lds + k);
+        if (SWAP) v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
         const bool full = g >= keep_lo && g + 16 <= keep_hi;
         if (full) *reinterpret_cast<uint4*>(out + g) = v;
         if (k == 0 || k == kl) {
@@ -1092,15 +1104,18 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
                     if (t.i == A.n - 1) A.pk_off[A.n] = (uint32_t)(G + place + keep);
                 }
             } else {
+                // the input stage is free: commit the next span BEFORE this tile's stores, so the commit's
+                // vmcnt wait covers only loads issued a tile ago, not the stores (vmcnt counts both)
+                if (have_next && nxt.fits) pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
                 wave_lds_sync();
-                stage_bswap(obuf32, (cur.ospan + 15u) & ~15u, lane);
+                if (!(region && A.edges)) stage_bswap(obuf32, (cur.ospan + 15u) & ~15u, lane);
                 wave_lds_sync();
                 PROF_MARK(2);
             }
             if (PACKED) {
             } else if (region) {
-                if (A.edges)
-                    region_copy_deferred(A.out, cur.a0, obuf, cur.ospan, t.lo, t.hi, lane, A.edges + 2 * (base >> 6));
+                if (A.edges)  // the stage's MSB-first words are byte-swapped on the way out
+                    region_copy_deferred<true>(A.out, cur.a0, obuf, cur.ospan, t.lo, t.hi, lane, A.edges + 2 * (base >> 6));
                 else
                     region_copy<(STAGE + 1023) / 1024>(A.out, cur.a0, obuf, cur.ospan, t.lo, t.hi, lane);
             } else if (t.valid && ol != kFailLen) {
@@ -1144,9 +1159,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
             PROF_FLUSH(1);
             break;
         }
-        if (nxt.fits) {
-            pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
-        }
+        if (nxt.fits && (PACKED || !cur.fits)) pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
         cur = nxt;
         base = nbase;
     }

@@ -643,7 +643,7 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
             // section order by qpack_blocked_kernel (every parked stream raises num_blocked)
             if (!(ctx.ric < t.total())) st = HHUFF_QPK_BLOCKED;
         }
-        QArena R{A.arena, A.arena_off[k], A.arena_off[k + 1]};
+        QArena R{A.arena, A.arena_off[k], min(A.arena_off[k + 1], kArenaLimit)};  // field offsets are u32
         const uint32_t slot = A.sec_off[k];
         uint32_t nf = 0;
         while (st == 0 && p != end) {

@@ -281,7 +281,11 @@ def arena_offsets(sec_off, header_table_size):
     """a generous arena slice per section: every field of an L-byte section is either a literal (<= 8/5 of
     its bytes) or a copy of a static (<= 76 bytes) or dynamic (<= table size) entry"""
     L = np.diff(np.asarray(sec_off, dtype=np.uint64))
-    cap = (L * 8) // 5 + L * np.uint64(80) + (L // 2 + 1) * np.uint64(header_table_size) + np.uint64(16)
+    # dynamic entries of the synthetic sessions stay far below 8 KiB: a tighter bound keeps large-table
+    # sessions' arenas under the 2^32 reach of the u32 field offsets (a slice too small is HHUFF_QPK_ARENA on
+    # both sides of a comparison)
+    ent = np.uint64(min(int(header_table_size), 8192))
+    cap = (L * 8) // 5 + L * np.uint64(80) + (L // 2 + 1) * ent + np.uint64(16)
     out = np.zeros(L.size + 1, np.uint64)
     out[1:] = np.cumsum(cap)
     return out

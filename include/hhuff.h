@@ -162,7 +162,8 @@ int hhuff_decode_literals(const uint8_t *in, uint64_t in_size, const uint32_t *l
  *                       capacity (hpack_capacity = hpack_max_capacity, lib/http2/connection.c:1844;
  *                       h2o's default 4096)
  *        arena          decoded names and values; block b writes arena[arena_off[b] .. arena_off[b+1])
- *                       (u64 offsets); every field's name is written, then its value
+ *                       (u64 offsets); every field's name is written, then its value.  Field offsets
+ *                       are u32: arena bytes at or past 2^32 are out of reach (HHUFF_BLK_ARENA there)
  *      Per field f of block b (f in blk_off[b] .. blk_off[b] + nfields[b] - 1: a block of L bytes holds at
  *      most L fields, so field slots reuse the block's byte offsets): name_off/name_len/value_off/
  *      value_len (arena offsets, u32) and fflags = its soft-error bits (HHUFF_SOFT_NAME / _VALUE: the
@@ -215,7 +216,8 @@ int hhuff_hpack_decode_blocks(const uint8_t *in, uint64_t in_size, const uint32_
  *      insert_count[c] as handle_input reports it (the new Insert Count, 0 when nothing was inserted).
  *      Per section k: sstatus[k] = 0, HHUFF_QPK_DECOMPRESSION_FAILED, HHUFF_QPK_BLOCKED (Required Insert
  *      Count not reached and a blocked slot free: h2o parks the stream until more inserts arrive),
- *      HHUFF_QPK_ARENA (a string does not fit arena[arena_off[k] .. arena_off[k+1]): a Huffman literal
+ *      HHUFF_QPK_ARENA (a string does not fit arena[arena_off[k] .. min(arena_off[k+1], 2^32)) -- field
+ *      offsets are u32 --: a Huffman literal
  *      needs floor(8 len / 5) bytes free, a raw one len, an indexed one its size) or HHUFF_QPK_SKIPPED;
  *      req_insert_count[k] (decoded Required Insert Count, for the Section Acknowledgment); nfields[k]
  *      fields in slots sec_off[k] .. + nfields[k] - 1: name_off/name_len/value_off/value_len (arena

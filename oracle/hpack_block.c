@@ -232,7 +232,8 @@ static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
             continue;
         }
         const uint8_t *p = j->in + j->blk_off[b], *end = j->in + j->blk_off[b + 1];
-        orc_arena_t A = {j->arena, j->arena_off[b], j->arena_off[b + 1]};
+        /* field offsets are u32: arena bytes at or past 2^32 are out of reach (include/hhuff.h) */
+        orc_arena_t A = {j->arena, j->arena_off[b], j->arena_off[b + 1] < (1ull << 32) ? j->arena_off[b + 1] : (1ull << 32)};
         uint32_t nf = 0, slot = j->blk_off[b];
         int st = 0;
         while (p != end) {

@@ -559,7 +559,7 @@ int orc_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, const ui
                 }
             }
             uint32_t nf = 0, slot = sec_off[k];
-            qpk_arena_t A = {arena, arena_off[k], arena_off[k + 1]};
+            qpk_arena_t A = {arena, arena_off[k], arena_off[k + 1] < (1ull << 32) ? arena_off[k + 1] : (1ull << 32)};
             while (st == 0 && p != end) {
                 uint32_t no = 0, nl = 0, vo = 0, vl = 0;
                 unsigned soft = 0;

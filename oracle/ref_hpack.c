@@ -42,7 +42,7 @@ REF_API int ref_hpack_decode_blocks(const uint8_t *in, const uint32_t *blk_off, 
             h2o_mem_pool_t pool;
             h2o_mem_init_pool(&pool);
             const uint8_t *src = in + blk_off[b], *end = in + blk_off[b + 1];
-            uint64_t cur = arena_off[b], aend = arena_off[b + 1];
+            uint64_t cur = arena_off[b], aend = arena_off[b + 1] < (1ull << 32) ? arena_off[b + 1] : (1ull << 32);
             uint32_t nf = 0, slot = blk_off[b];
             int st = 0;
             while (src != end) {

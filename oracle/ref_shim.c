@@ -188,7 +188,7 @@ REF_API int ref_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, 
             ctx.stats = &stats;
             h2o_mem_pool_t pool;
             h2o_mem_init_pool(&pool);
-            uint64_t cur = arena_off[k], aend = arena_off[k + 1];
+            uint64_t cur = arena_off[k], aend = arena_off[k + 1] < (1ull << 32) ? arena_off[k + 1] : (1ull << 32);
             uint32_t nf = 0, slot = sec_off[k];
             while (st == 0 && src != end) {
                 h2o_iovec_t *name, value;
