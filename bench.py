@@ -1,19 +1,25 @@
 #!/usr/bin/env python3
 """hhuff benchmark -- BASELINE.json metric "GiB/s device-resident Huffman decode+encode, 16M header strings
-mean 48B" on configuration 4 (16M strings, lengths U[24,72], header alphabet), one MI355X per rank.
+mean 48B" on configuration 4: 16M header strings, lengths U[24,72], header alphabet, batch-sharded across the
+GPUs of one node.
 
-One step = one pass of the hot path over one batch, inputs resident in HBM:
-    encode  all N plain strings         (hhuff_encode_batch, h2o_hpack_encode_huffman per element)
-    decode  the N_ok Huffman strings    (hhuff_decode_batch, h2o_hpack_decode_huffman per element)
-            packed contiguously, i.e. the compressible strings as they would arrive on the wire
-value = sum over ranks of plain bytes P / max over ranks of (t_encode + t_decode)   [GiB/s, 2^30]
-Multi-GPU (torchrun, one process per GPU, RCCL): each rank owns an independent shard of N strings
-(weak scaling); no collective on the data path, only barriers / a max-reduce of the timing.
+The batch (seeded, identical on every rank) is cut byte-balanced with h2o_amd.dist.byte_balanced_bounds; each
+rank keeps its shard resident in its HBM (N = 1: the whole batch on one GPU).  One step = one pass of the hot
+path over the shard, inputs resident in HBM:
+    encode  all the shard's plain strings      (hhuff_encode_batch, h2o_hpack_encode_huffman per element)
+    decode  its compressible strings' Huffman  (hhuff_decode_batch, h2o_hpack_decode_huffman per element),
+            packed back to back as on the wire
+    N > 1:  an RCCL all_gather of every shard's (strings, output bytes) -- the batch split's one exchange,
+            which gives each shard its global output offsets
+value = total plain bytes of the batch / max over ranks of the step time   [GiB/s, 2^30]; strong scaling
+(the batch is fixed, N GPUs share it).
 
-Extra JSON fields: per-direction rates, `roofline` for the dominant kernel (decode; algorithmic bytes
-B_dec = H + P_ok + 9 N_ok + 4 + ceil(N_ok / 8) per launch over its HIP-event duration), and
-`cpu_baseline` (h2o's CPU path -- the reference's hpack.c compiled, or the restatement -- on this host's
-cores, rank 0 only).
+Extra JSON fields: per-direction times and rates; the packed-output mode (hhuff_{de,en}code_batch_packed)
+timed on the same shard; `roofline` for the dominant kernel (algorithmic bytes per launch over its HIP-event
+duration; HBM traffic from rocprofv3 PMC passes run before this process touches the GPU) plus a `secondary`
+ceiling (VALU / LDS issue from the SQ counters); N = 1 only: the other BASELINE configs (c2, c3, c5), the
+per-string symbols' call latency, the H2D/D2H-inclusive rate and `cpu_baseline` (h2o's own CPU path on this
+host's cores).
 """
 import argparse
 import json
@@ -23,9 +29,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy peak ~6300
+N_SIMD, N_CU = 1024, 256
 GIB = float(1 << 30)
+METRIC = "GiB/s device-resident Huffman decode+encode, 16M header strings mean 48B"
 
 
 def parse():
@@ -34,23 +43,40 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4")
-    ap.add_argument("--n", type=int, default=None, help="strings per rank (default: the config's N)")
+    ap.add_argument("--n", type=int, default=None, help="strings in the whole batch (default: the config's N)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=0, help="strings in the CPU-baseline sample (0: the whole batch)")
+    ap.add_argument("--cpu-sample", type=int, default=0, help="strings in the CPU-baseline sample (0: 4M)")
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--only", choices=["encode", "decode"], default=None, help="profile one direction")
-    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes for roofline.traffic")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-host", action="store_true", help="skip the H2D/D2H-inclusive measurement")
+    ap.add_argument("--no-extra", action="store_true", help="skip the other configs and the per-string latency")
+    ap.add_argument("--no-packed", action="store_true", help="skip the packed-output legs")
     return ap.parse_args()
 
 
-def pmc_traffic(args):
-    """HBM bytes per launch of each hhuff kernel from rocprofv3 PMC counters, one counter per pass
-    (MI355X_MICROARCH.md HBM section): FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE
-    reports half the bytes of a wide (16 B/lane) coalesced streaming read, the form of the kernels'
-    input staging, so it is doubled.  Runs this script as a child of rocprofv3 BEFORE this process
-    touches the GPU.  Returns {kernel: bytes} or {} when rocprofv3 is unavailable."""
+def kernel_key(name):
+    if "hhuff::" not in name:
+        return None
+    packed = ", true>" in name
+    if "decode_staged_kernel" in name or "decode_stream_kernel" in name or "decode_direct_kernel" in name:
+        return "decode_packed" if packed else "decode"
+    if "encode_staged_kernel" in name or "encode_pl_kernel" in name or "encode_direct_kernel" in name:
+        return "encode_packed" if packed else "encode"
+    if "edge_fix" in name:
+        return "edge_fix"
+    return None
+
+
+SQ_GROUP = ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_SALU", "SQ_WAVE_CYCLES",
+            "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
+
+
+def pmc_passes(args):
+    """Per-launch PMC counters of each hhuff kernel: one rocprofv3 run per counter group (FETCH_SIZE,
+    WRITE_SIZE, the SQ group, GRBM_GUI_ACTIVE) over this script as a child, BEFORE this process touches the
+    GPU.  Returns {kernel key: {counter: mean per launch}} or {} when rocprofv3 is unavailable."""
     import csv
     import shutil
     import subprocess
@@ -60,71 +86,132 @@ def pmc_traffic(args):
     if not os.path.exists(exe):
         return {}
     child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "2", "--warmup", "1",
-             "--no-cpu-baseline", "--no-traffic", "--no-host", "--config", args.config]
+             "--no-cpu-baseline", "--no-traffic", "--no-host", "--no-extra", "--config", args.config]
     if args.n:
         child += ["--n", str(args.n)]
     vals = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+    for group in (("FETCH_SIZE",), ("WRITE_SIZE",), SQ_GROUP, ("GRBM_GUI_ACTIVE",)):
         d = tempfile.mkdtemp(prefix="hhuff_pmc_")
         try:
-            subprocess.run([exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "pmc", "--"] + child,
-                           check=True, timeout=600, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+            subprocess.run([exe, "--pmc"] + list(group) + ["--output-format", "csv", "-d", d, "-o", "pmc", "--"] + child,
+                           check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
                            env=dict(os.environ, TMPDIR="/tmp"))
             for root, _, files in os.walk(d):
                 for f in files:
                     if f.endswith("counter_collection.csv"):
                         for r in csv.DictReader(open(os.path.join(root, f))):
-                            if "hhuff::" not in r["Kernel_Name"]:
-                                continue
-                            nm = r["Kernel_Name"]
-                            k = "decode" if "decode" in nm else "encode" if "encode" in nm else "edge_fix" if "edge_fix" in nm else None
-                            if k is None:
-                                continue
-                            vals.setdefault((k, r["Counter_Name"]), []).append(float(r["Counter_Value"]))
+                            k = kernel_key(r["Kernel_Name"])
+                            if k is not None:
+                                vals.setdefault(k, {}).setdefault((r["Dispatch_Id"], r["Counter_Name"]), 0.0)
+                                vals[k][(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
         except Exception:
             return {}
         finally:
             shutil.rmtree(d, ignore_errors=True)
     out = {}
-    for k in ("decode", "encode", "edge_fix"):
-        f, w = vals.get((k, "FETCH_SIZE")), vals.get((k, "WRITE_SIZE"))
-        if f and w:
-            out[k] = (2.0 * sum(f) / len(f) + sum(w) / len(w)) * 1024.0
+    for k, per in vals.items():
+        agg = {}
+        for (_, cname), v in per.items():
+            agg.setdefault(cname, []).append(v)
+        # the last two dispatches are the child's timed steps (the first ones build the wire)
+        out[k] = {c: sum(v[-2:]) / len(v[-2:]) for c, v in agg.items()}
     return out
+
+
+def traffic_bytes(c):
+    """HBM bytes per launch (MI355X_MICROARCH.md HBM section): FETCH_SIZE / WRITE_SIZE are KiB; on gfx950
+    FETCH_SIZE reports half the bytes of 16-B/lane streaming reads (the kernels' input staging): doubled"""
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        return (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+    return None
+
+
+def secondary(c):
+    """issue-side ceilings of a kernel from its SQ counters: VALU = SQ_INSTS_VALU x 2 cycles (a wave64 VALU
+    instruction holds a SIMD-32 for 2 cycles) over 1024 SIMDs x the kernel's cycles (GRBM_GUI_ACTIVE / 8: the
+    counter sums the 8 XCDs); LDS ~ (2 cycles per LDS instruction + SQ_LDS_BANK_CONFLICT) over 256 CUs x cycles"""
+    if not all(k in c for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "GRBM_GUI_ACTIVE")):
+        return None
+    cyc = c["GRBM_GUI_ACTIVE"] / 8.0
+    r = {"valu_issue_frac": round(c["SQ_INSTS_VALU"] * 2.0 / (N_SIMD * cyc), 3),
+         "lds_issue_frac": round((2.0 * c["SQ_INSTS_LDS"] + c["SQ_LDS_BANK_CONFLICT"]) / (N_CU * cyc), 3),
+         "lds_conflict_cycles_per_inst": round(c["SQ_LDS_BANK_CONFLICT"] / max(1.0, c["SQ_INSTS_LDS"]), 2)}
+    if "SQ_WAVE_CYCLES" in c and c["SQ_WAVE_CYCLES"] > 0:
+        r["wave_wait_frac"] = round(c.get("SQ_WAIT_ANY", 0.0) / c["SQ_WAVE_CYCLES"], 3)
+        r["wave_issue_stall_frac"] = round(c.get("SQ_WAIT_INST_ANY", 0.0) / c["SQ_WAVE_CYCLES"], 3)
+        r["wave_active_frac"] = round(c.get("SQ_ACTIVE_INST_ANY", 0.0) / c["SQ_WAVE_CYCLES"], 3)
+    return r
+
+
+def timed_events(torch, fns, steps, warmup, world, dist):
+    """warm up, then time `steps` steps of fns (a list of callables, one event pair each) between barriers;
+    returns (wall ms per step, [sorted per-fn ms lists])"""
+    for _ in range(warmup):
+        for f in fns:
+            f()
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in fns]
+          for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for row in ev:
+        for (a, b), f in zip(row, fns):
+            a.record()
+            f()
+            b.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = (time.perf_counter() - t0) * 1e3 / steps
+    per = [sorted(row[k][0].elapsed_time(row[k][1]) for row in ev) for k in range(len(fns))]
+    return wall, per
+
+
+def mean(x):
+    return sum(x) / len(x)
 
 
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    traffic = {}
+    pmc = {}
     if not args.pmc_child and not args.no_traffic and world == 1:
-        traffic = pmc_traffic(args)  # child processes; this process has not touched the GPU yet
-    import numpy as np
+        pmc = pmc_passes(args)  # child processes; this process has not touched the GPU yet
     import torch
     import torch.distributed as dist
 
     from h2o_amd import codec, synth
+    from h2o_amd import dist as hd
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("HHUFF_DIST_BACKEND", "nccl")  # gloo: rehearse N ranks on fewer GPUs
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     codec.lib()
 
-    # ---- synthetic batch, device resident -------------------------------------------------------
-    b = synth.make_batch_torch(args.config, n=args.n, seed=1000 + rank)
-    n = b["n"]
-    P = int(b["total"])
-    off32 = b["off"].to(torch.int32)
-    lens = (b["off"][1:] - b["off"][:-1])
+    # ---- config 4's batch, cut byte-balanced; this rank's shard stays resident -------------------------
+    full = synth.make_batch_torch(args.config, n=args.n, seed=1000)
+    n_all, P_all = full["n"], int(full["total"])
+    bounds = hd.byte_balanced_bounds(full["off"], world).tolist()
+    b = hd.shard(full, bounds[rank], bounds[rank + 1])
+    del full
+    torch.cuda.empty_cache()
+    n, off32 = b["n"], b["off"]
+    P = int(b["data"].numel())
+    lens = (off32[1:].to(torch.int64) - off32[:-1].to(torch.int64))
     enc_out = torch.empty(P + 16, dtype=torch.uint8, device="cuda")
     enc_len = torch.empty(n, dtype=torch.int32, device="cuda")
     enc_st = torch.empty(n, dtype=torch.uint8, device="cuda")
-    codec.encode_batch(b["data"], off32, n, out=enc_out, out_len=enc_len, status=enc_st)
-    # the wire: compressible strings, packed contiguously (second encode with explicit destinations)
+    codec.encode_batch(b["data"], off32, n, out=enc_out, out_len=enc_len, status=enc_st, in_size=P)
+    # the wire: compressible strings packed back to back (packed encode places them; a gather closes the gaps)
     ok = enc_len != -1
     idx = torch.nonzero(ok).squeeze(1)
     n_ok = int(idx.numel())
@@ -133,24 +220,17 @@ def main():
     h_off[1:] = torch.cumsum(hl, 0)
     H = int(h_off[-1].item())
     huff = torch.empty(H + 16, dtype=torch.uint8, device="cuda")
-    tmp_len = torch.empty(n_ok, dtype=torch.int32, device="cuda")
-    codec.encode_batch(b["data"], off32[idx].contiguous(), n_ok, in_len=lens[idx].to(torch.int32).contiguous(),
-                       out=huff, out_off=h_off[:-1].to(torch.int32).contiguous(), out_len=tmp_len, in_size=P)
-    # is_name bits of the kept strings
-    bits = ((b["is_name_bits"].to(torch.int64) & 0xFFFFFFFF).unsqueeze(1) >> torch.arange(32, device="cuda")) & 1
-    names_ok = bits.reshape(-1)[:n][idx]
-    nw = (n_ok + 31) // 32
-    padn = torch.zeros(nw * 32, dtype=torch.int64, device="cuda")
-    padn[:n_ok] = names_ok
-    w = (padn.view(nw, 32) << torch.arange(32, device="cuda")).sum(1)
-    names_bits = torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32).contiguous()
+    rel = torch.arange(H, device="cuda") - torch.repeat_interleave(h_off[:-1], hl)
+    huff[:H] = enc_out[torch.repeat_interleave(off32[:-1].to(torch.int64)[idx], hl) + rel]
+    del rel
+    names_ok = hd.bits_to_bool(b["is_name_bits"], n)[idx]
+    names_bits = hd.bool_to_bits(names_ok)
     h_off32 = h_off.to(torch.int32).contiguous()
-    P_ok = int(hl.numel() and lens[idx].sum().item())
+    P_ok = int(lens[idx].sum().item()) if n_ok else 0
     dec_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
     dec_len = torch.empty(n_ok, dtype=torch.int32, device="cuda")
     dec_st = torch.empty(n_ok, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
-    del tmp_len
 
     def run_encode():
         codec.encode_batch(b["data"], off32, n, out=enc_out, out_len=enc_len, status=enc_st, in_size=P)
@@ -159,159 +239,197 @@ def main():
         codec.decode_batch(huff, h_off32, n_ok, is_name_bits=names_bits, out=dec_out, out_len=dec_len, status=dec_st,
                            in_size=H)
 
+    def run_exchange():  # the batch split's all_gather of (strings, output bytes) -- device-resident sums
+        hd.exchange_sizes(n_ok, torch.clamp(dec_len, min=0).to(torch.int64).sum())
+
     # correctness spot check before timing: decoded lengths equal the plain lengths of the kept strings
     run_decode()
     torch.cuda.synchronize()
     assert bool((dec_len == lens[idx].to(torch.int32)).all()), "decode does not invert encode"
 
-    # ---- timed region ----------------------------------------------------------------------------
     do_enc = args.only in (None, "encode")
     do_dec = args.only in (None, "decode")
-    for _ in range(args.warmup):
-        if do_enc:
-            run_encode()
-        if do_dec:
-            run_decode()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-           torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    fns = ([run_encode] if do_enc else []) + ([run_decode] if do_dec else []) + ([run_exchange] if world > 1 else [])
+    ms_step, per = timed_events(torch, fns, args.steps, args.warmup, world, dist)
+    t_enc = mean(per[0]) if do_enc else 0.0
+    t_dec = mean(per[1 if do_enc else 0]) if do_dec else 0.0
+
+    # ---- packed-output mode on the same shard (hhuff_{de,en}code_batch_packed) ----------------------------
+    packed = None
+    if not args.no_packed and args.only is None:
+        pe_out = torch.empty(P + 16, dtype=torch.uint8, device="cuda")
+        pe_off = torch.empty(n + 1, dtype=torch.int32, device="cuda")
+        pd_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
+        pd_off = torch.empty(n_ok + 1, dtype=torch.int32, device="cuda")
+
+        def run_encode_packed():
+            codec.encode_batch_packed(b["data"], off32, n, out=pe_out, out_off=pe_off, out_len=enc_len, status=enc_st,
+                                      in_size=P)
+
+        def run_decode_packed():
+            codec.decode_batch_packed(huff, h_off32, n_ok, is_name_bits=names_bits, out=pd_out, out_off=pd_off,
+                                      out_len=dec_len, status=dec_st, in_size=H)
+
+        run_decode_packed()
+        torch.cuda.synchronize()
+        assert bool((dec_len == lens[idx].to(torch.int32)).all()), "packed decode does not invert encode"
+        pk_ms, pk = timed_events(torch, [run_encode_packed, run_decode_packed], args.steps, args.warmup, world, dist)
+        packed = {"encode_ms": round(mean(pk[0]), 4), "decode_ms": round(mean(pk[1]), 4), "ms_per_step": round(pk_ms, 4),
+                  "value": round(P / GIB / ((mean(pk[0]) + mean(pk[1])) * 1e-3), 3)}
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for e0, e1, e2 in ev:
-        e0.record()
-        if do_enc:
-            run_encode()
-        e1.record()
-        if do_dec:
-            run_decode()
-        e2.record()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t_wall = time.perf_counter() - t0
-    t_enc = sorted(a.elapsed_time(b_) for a, b_, _ in ev)
-    t_dec = sorted(b_.elapsed_time(c) for _, b_, c in ev)
-    t_enc_avg = sum(t_enc) / len(t_enc)
-    t_dec_avg = sum(t_dec) / len(t_dec)
-    ms_step = t_wall * 1e3 / args.steps
-    if world > 1:
-        t = torch.tensor([ms_step], device="cuda", dtype=torch.float64)
+        t = torch.tensor([ms_step], device="cuda" if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms_step = float(t.item())
-        tot = torch.tensor([P, P_ok, n, n_ok], device="cuda", dtype=torch.float64)
-        dist.all_reduce(tot)
-        P_all, P_ok_all, n_all, n_ok_all = (float(x) for x in tot.tolist())
-    else:
-        P_all, P_ok_all, n_all, n_ok_all = float(P), float(P_ok), float(n), float(n_ok)
 
     if rank == 0:
         B_dec = H + P_ok + 9 * n_ok + 4 + (n_ok + 7) // 8
-        B_enc = P + int(hl.sum().item()) + 9 * n + 4
-        dec_gbps = B_dec / (t_dec_avg * 1e-3) / 1e9
-        enc_gbps = B_enc / (t_enc_avg * 1e-3) / 1e9
-        dominant = "decode" if t_dec_avg >= t_enc_avg or args.only == "decode" else "encode"
-        if args.only == "encode":
-            dominant = "encode"
-        ach = dec_gbps if dominant == "decode" else enc_gbps
-        value = P_all / GIB / (ms_step * 1e-3)
+        E = int(hl.sum().item())
+        B_enc = P + E + 9 * n + 4
+        gb = lambda B, t: B / (t * 1e-3) / 1e9  # noqa: E731
+        dominant = "encode" if (t_enc >= t_dec and do_enc) or not do_dec else "decode"
+        B_dom, t_dom = (B_enc, t_enc) if dominant == "encode" else (B_dec, t_dec)
+        ach = gb(B_dom, t_dom)
+        roof = {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBPS, 4),
+                "traffic": round(traffic_bytes(pmc[dominant])) if dominant in pmc and traffic_bytes(pmc[dominant]) else None,
+                "algorithmic_bytes": B_dom,
+                "bytes_per_unit": "decode: H + P + 9 N + 4 + ceil(N/8); encode: P + E + 9 N + 4 (SURVEY 8d)"}
+        sec = secondary(pmc.get(dominant, {}))
+        if sec:
+            roof["secondary"] = sec
         line = {
-            "metric": "GiB/s device-resident Huffman decode+encode, 16M header strings mean 48B",
-            "value": round(value, 3),
+            "metric": METRIC,
+            "value": round(P_all / GIB / (ms_step * 1e-3), 3),
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded, header alphabet P~2^-nbits, 1% adversarial)",
-            "config": {"workload": "%s: %d header strings/GPU, lengths %s, encode all + decode the compressible"
-                                   % (args.config, n, synth.CONFIGS[args.config]["lengths"]),
-                       "strings_per_gpu": n, "global_strings": int(n_all), "plain_bytes_per_gpu": P,
-                       "huffman_bytes_per_gpu": H, "parallelism": "shard%d" % world},
-            "encode_ms": round(t_enc_avg, 4),
-            "decode_ms": round(t_dec_avg, 4),
-            "encode_gibps": round(P / GIB / (t_enc_avg * 1e-3), 3) if do_enc else None,
-            "decode_gibps": round(P_ok / GIB / (t_dec_avg * 1e-3), 3) if do_dec else None,
-            "roofline": {"bound": "hbm", "kernel": dominant, "achieved": round(ach, 2), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
-                         "traffic": round(traffic[dominant]) if dominant in traffic else None,
-                         "algorithmic_bytes": B_dec if dominant == "decode" else B_enc},
-            "traffic_bytes_per_launch": {k: round(v) for k, v in traffic.items()} or None,
+            "config": {"workload": "%s: %d header strings, lengths %s, byte-balanced over %d GPU(s); encode all + "
+                                   "decode the compressible" % (args.config, n_all, synth.CONFIGS[args.config]["lengths"],
+                                                                world),
+                       "global_strings": n_all, "global_plain_bytes": P_all, "strings_rank0": n,
+                       "plain_bytes_rank0": P, "huffman_bytes_rank0": H, "parallelism": "shard%d" % world},
+            "encode_ms": round(t_enc, 4),
+            "decode_ms": round(t_dec, 4),
+            "encode_gibps": round(P / GIB / (t_enc * 1e-3), 3) if do_enc else None,
+            "decode_gibps": round(P_ok / GIB / (t_dec * 1e-3), 3) if do_dec else None,
+            "roofline": roof,
+            "traffic_bytes_per_launch": {k: round(traffic_bytes(v)) for k, v in pmc.items() if traffic_bytes(v)} or None,
         }
-        if not args.no_host and not args.pmc_child:
-            line["host_inclusive"] = host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, P_ok, torch)
-        if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(b, args, np)
+        if world > 1:
+            line["exchange_ms"] = round(mean(per[-1]), 4)
+        if packed is not None:
+            B_dec_pk = B_dec + 4 * (n_ok + 1)  # + out_off[n + 1]
+            B_enc_pk = B_enc + 4 * (n + 1)
+            tr = {k: traffic_bytes(pmc[k]) for k in ("encode_packed", "decode_packed") if k in pmc}
+            packed["roofline"] = {
+                k: {"achieved": round(gb(B, packed[k.split("_")[0] + "_ms"]), 2),
+                    "frac": round(gb(B, packed[k.split("_")[0] + "_ms"]) / HBM_PEAK_GBPS, 4),
+                    "algorithmic_bytes": B, "traffic": round(tr[k]) if tr.get(k) else None,
+                    "traffic_over_algorithmic": round(tr[k] / B, 4) if tr.get(k) else None}
+                for k, B in (("encode_packed", B_enc_pk), ("decode_packed", B_dec_pk))}
+            line["packed"] = packed
+        if world == 1 and not args.pmc_child:
+            if not args.no_extra:
+                line["configs"] = other_configs(torch, codec, synth)
+                line["per_string_latency_us"] = per_string_latency(codec)
+            if not args.no_host:
+                line["host_inclusive"] = host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch)
+            if not args.no_cpu_baseline:
+                line["cpu_baseline"] = cpu_baseline(b, args)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, P_ok, torch, reps=3):
-    """The same step with the strings starting and ending in pinned host memory: H2D of the inputs,
-    encode + decode, D2H of the outputs, all on one stream (PCIe-bound; recorded in DESIGN.md, never
-    `value`)."""
+def other_configs(torch, codec, synth):
+    """BASELINE configs 2, 3, 5 (device-resident, HIP-event medians; tools/bench_configs.py)"""
+    import bench_configs as BC
+
+    res = {}
+    for cfg in ("c2", "c3", "c5"):
+        b = synth.make_batch_torch(cfg, seed=7)
+        n, P = b["n"], int(b["total"])
+        off32 = b["off"].to(torch.int32)
+        r = {"strings": n, "plain_bytes": P}
+        if cfg in ("c2", "c3"):
+            huff, h_off, n_ok, H, P_ok = BC.packed_huffman(torch, codec, b)
+            d_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
+            d_len = torch.empty(n_ok, dtype=torch.int32, device="cuda")
+            d_st = torch.empty(n_ok, dtype=torch.uint8, device="cuda")
+            t_dec = BC.timed(torch, lambda: codec.decode_batch(huff, h_off, n_ok, out=d_out, out_len=d_len, status=d_st,
+                                                               in_size=H))
+            r.update(decode_ms=round(t_dec, 4), decode_gibps=round(P_ok / GIB / (t_dec * 1e-3), 2))
+            if cfg == "c3":
+                e_out = torch.empty(P + 16, dtype=torch.uint8, device="cuda")
+                e_len = torch.empty(n, dtype=torch.int32, device="cuda")
+                t_enc = BC.timed(torch, lambda: codec.encode_batch(b["data"], off32, n, out=e_out, out_len=e_len,
+                                                                   in_size=P))
+                r.update(encode_ms=round(t_enc, 4), encode_gibps=round(P / GIB / (t_enc * 1e-3), 2),
+                         round_trip_gibps=round(P / GIB / ((t_enc + t_dec) * 1e-3), 2))
+        else:  # QPACK values, flatten_string(prefix 7) framing (encode-only)
+            f_out = torch.empty(P + 11 * n + 16, dtype=torch.uint8, device="cuda")
+            f_len = torch.empty(n, dtype=torch.int32, device="cuda")
+            t = BC.timed(torch, lambda: codec.flatten_batch(b["data"], off32, n, 7, out=f_out, out_len=f_len, in_size=P))
+            r.update(flatten_ms=round(t, 4), flatten_gibps=round(P / GIB / (t * 1e-3), 2))
+        res[cfg] = r
+        del b
+        torch.cuda.empty_cache()
+    return res
+
+
+def per_string_latency(codec, calls=2000):
+    """h2o's per-string symbols (a synchronous batch of one on the GPU): median / p99 microseconds per call"""
+    s = (b"accept-encoding: gzip, deflate, br, zstd" * 2)[:48]
+    h = codec.encode_huffman(s)
+    out = {}
+    for name, fn in (("h2o_hpack_encode_huffman", lambda: codec.encode_huffman(s)),
+                     ("h2o_hpack_decode_huffman", lambda: codec.decode_huffman(h, False))):
+        for _ in range(50):
+            fn()
+        t = []
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            fn()
+            t.append(time.perf_counter() - t0)
+        t.sort()
+        out[name] = {"median": round(t[len(t) // 2] * 1e6, 2), "p99": round(t[int(len(t) * 0.99)] * 1e6, 2)}
+    out["string_bytes"] = len(s)
+    return out
+
+
+def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, reps=3):
+    """The same step with the strings starting and ending in host memory: the library's pipelined host path
+    (hhuff_*_batch_host_pipelined: chunks overlap host staging, H2D, kernels and D2H on three streams) with
+    pinned and with pageable caller buffers (PCIe-bound; recorded in DESIGN.md, never `value`)."""
+    import numpy as np
+
     from h2o_amd import codec
 
     def pin(t):
         return t.cpu().pin_memory()
 
     h_plain, h_off, h_huff, h_hoff, h_names = pin(b["data"]), pin(off32), pin(huff[:H]), pin(h_off32), pin(names_bits)
-    d_plain, d_off = torch.empty(P + 16, dtype=torch.uint8, device="cuda"), torch.empty_like(off32)
-    d_huff, d_hoff, d_names = torch.empty(H + 16, dtype=torch.uint8, device="cuda"), torch.empty_like(h_off32), \
-        torch.empty_like(names_bits)
-    e_out = torch.empty(P + 16, dtype=torch.uint8, device="cuda")
-    e_len, e_st = torch.empty(n, dtype=torch.int32, device="cuda"), torch.empty(n, dtype=torch.uint8, device="cuda")
-    d_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
-    d_len, d_st = torch.empty(n_ok, dtype=torch.int32, device="cuda"), torch.empty(n_ok, dtype=torch.uint8, device="cuda")
-    o_enc, o_elen, o_est = torch.empty(P, dtype=torch.uint8).pin_memory(), torch.empty(n, dtype=torch.int32).pin_memory(), \
-        torch.empty(n, dtype=torch.uint8).pin_memory()
-    o_dec, o_dlen, o_dst = torch.empty(d_out.numel(), dtype=torch.uint8).pin_memory(), \
-        torch.empty(n_ok, dtype=torch.int32).pin_memory(), torch.empty(n_ok, dtype=torch.uint8).pin_memory()
-    times = []
-    for _ in range(reps + 1):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        d_plain[:P].copy_(h_plain, non_blocking=True)
-        d_off.copy_(h_off, non_blocking=True)
-        d_huff[:H].copy_(h_huff, non_blocking=True)
-        d_hoff.copy_(h_hoff, non_blocking=True)
-        d_names.copy_(h_names, non_blocking=True)
-        codec.encode_batch(d_plain, d_off, n, out=e_out, out_len=e_len, status=e_st, in_size=P)
-        codec.decode_batch(d_huff, d_hoff, n_ok, is_name_bits=d_names, out=d_out, out_len=d_len, status=d_st,
-                           in_size=H)
-        o_enc.copy_(e_out[:P], non_blocking=True)
-        o_elen.copy_(e_len, non_blocking=True)
-        o_est.copy_(e_st, non_blocking=True)
-        o_dec.copy_(d_out, non_blocking=True)
-        o_dlen.copy_(d_len, non_blocking=True)
-        o_dst.copy_(d_st, non_blocking=True)
-        torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
-    t_serial = min(times[1:])
-    # the library's pipelined host path (hhuff_*_batch_host_pipelined): chunks overlap host staging,
-    # H2D, kernels and D2H on three streams; caller buffers pinned, then pageable
-    np_ = __import__("numpy")
     res = {}
     for kind in ("pinned", "pageable"):
         def hbuf(count, dt):
             if kind == "pinned":
                 return torch.empty(count, dtype=dt).pin_memory().numpy()
-            return np_.empty(count, {torch.uint8: np_.uint8, torch.int32: np_.int32}[dt])
+            return np.empty(count, {torch.uint8: np.uint8, torch.int32: np.int32}[dt])
 
-        if kind == "pinned":
-            src_p, src_h = h_plain.numpy(), h_huff.numpy()
-        else:
-            src_p, src_h = h_plain.numpy().copy(), h_huff.numpy().copy()
+        src_p, src_h = (h_plain.numpy(), h_huff.numpy()) if kind == "pinned" else (h_plain.numpy().copy(),
+                                                                                   h_huff.numpy().copy())
         out_e, out_d = hbuf(P + 16, torch.uint8), hbuf(codec.decode_slot_size(H), torch.uint8)
-        el, es = hbuf(n, torch.int32).view(np_.uint32), hbuf(n, torch.uint8)
-        dl, ds = hbuf(n_ok, torch.int32).view(np_.uint32), hbuf(n_ok, torch.uint8)
-        off_np, hoff_np = h_off.numpy().view(np_.uint32), h_hoff.numpy().view(np_.uint32)
-        names_np = h_names.numpy().view(np_.uint32)
+        el, es = hbuf(n, torch.int32).view(np.uint32), hbuf(n, torch.uint8)
+        dl, ds = hbuf(n_ok, torch.int32).view(np.uint32), hbuf(n_ok, torch.uint8)
+        off_np, hoff_np = h_off.numpy().view(np.uint32), h_hoff.numpy().view(np.uint32)
+        names_np = h_names.numpy().view(np.uint32)
         if kind == "pageable":
             off_np, hoff_np, names_np = off_np.copy(), hoff_np.copy(), names_np.copy()
         ts = []
@@ -324,54 +442,57 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, P_ok, tor
         res[kind] = min(ts[1:])
     t = res["pinned"]
     return {"value": round(P / GIB / t, 3), "unit": "GiB/s", "ms_per_step": round(t * 1e3, 3),
-            "pageable_value": round(P / GIB / res["pageable"], 3), "pageable_ms_per_step": round(res["pageable"] * 1e3, 3),
-            "serial_value": round(P / GIB / t_serial, 3), "serial_ms_per_step": round(t_serial * 1e3, 3),
-            "note": "strings start and end in host memory; value: hhuff_{encode,decode}_batch_host_pipelined with "
-                    "pinned caller buffers (64 MiB chunks, 3 streams); pageable_*: same with pageable buffers; "
-                    "serial_*: pinned H2D + kernels + D2H on one stream; best of %d" % reps}
+            "pageable_value": round(P / GIB / res["pageable"], 3),
+            "pageable_ms_per_step": round(res["pageable"] * 1e3, 3),
+            "note": "strings start and end in host memory; hhuff_{encode,decode}_batch_host_pipelined, 64 MiB chunks, "
+                    "3 streams; pinned / pageable caller buffers; best of %d" % reps}
 
 
-def cpu_baseline(b, args, np):
-    """h2o's own CPU path on this host's cores, timed like one step (encode all strings, then decode the
-    compressible ones).  kind "reference": oracle/_ref/libh2oref.so, the reference's lib/http2/hpack.c
-    compiled where it lies (it travels with the tree); kind "port": the clean-room restatement when the
-    reference build is absent.  Multi-threaded over a bounded sample of rank 0's batch (default: all
-    of it, ~10-30 s of CPU work), contiguous per-thread ranges; plus a single-thread rate on a smaller
-    sample."""
+def cpu_baseline(b, args):
+    """h2o's own CPU path on this host's cores, timed like one step (encode the sample's strings, then decode
+    the compressible ones).  kind "reference": oracle/_ref/libh2oref.so -- the reference's lib/http2/hpack.c
+    compiled where it lies by oracle/Makefile in the build container; the built .so travels to the GPU box
+    with the tree.  kind "port": the clean-room restatement, when that build is absent.  Contiguous
+    per-thread ranges over a bounded sample of rank 0's shard; median of 5; plus one thread on 256K strings."""
+    import numpy as np
+
     from oracle import oracle as O
 
     kind = "reference" if O.ref_available() else "port"
-    codec = O.ref() if kind == "reference" else O.oracle()
-    m = min(args.cpu_sample, b["n"]) if args.cpu_sample else b["n"]
-    off = b["off"][:m + 1].cpu().numpy().astype(np.uint32)
+    cdc = O.ref() if kind == "reference" else O.oracle()
+    m = min(args.cpu_sample or (1 << 22), b["n"])
+    off = b["off"][:m + 1].cpu().numpy().view(np.uint32).astype(np.uint32)
     data = b["data"][:int(off[-1])].cpu().numpy()
     names = b["is_name_bits"][:(m + 31) // 32].cpu().numpy().view(np.uint32)
-    threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)  # the box's CPU share per GPU (16 on the GPU pool)
+    threads = args.cpu_threads or (min(affinity, share) if share > 0 else affinity)
 
     def rate(mm, nthreads, reps):
         o = off[:mm + 1]
         d = data[:int(o[-1])]
-        enc, el, _ = codec.encode_batch(d, o, mm, nthreads=nthreads)  # also produces the decode input
+        enc, el, _ = cdc.encode_batch(d, o, mm, nthreads=nthreads)  # also produces the decode input
         hl = np.where(el != O.FAIL, el, 0).astype(np.uint32)
         starts = o[:-1].copy()
-        best = None
+        ts = []
         for _ in range(reps):
             t0 = time.perf_counter()
-            codec.encode_batch(d, o, mm, nthreads=nthreads)
-            codec.decode_batch(enc, starts, mm, in_len=hl, is_name_bits=names, nthreads=nthreads)
-            t = time.perf_counter() - t0
-            best = t if best is None else min(best, t)
-        return float(o[-1]) / GIB / best, float(o[-1])
+            cdc.encode_batch(d, o, mm, nthreads=nthreads)
+            cdc.decode_batch(enc, starts, mm, in_len=hl, is_name_bits=names, nthreads=nthreads)
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return float(o[-1]) / GIB / ts[len(ts) // 2], float(o[-1])
 
-    v, P = rate(m, threads, 3)
+    v, Ps = rate(m, threads, 5)
     m1 = min(m, 1 << 18)
-    v1, P1 = rate(m1, 1, 3)
-    return {"value": round(v, 4), "unit": "GiB/s", "cores": threads, "kind": kind,
-            "sample": "%d strings (%.1f MB) of rank 0's batch, encode + decode, best of 3, %d threads "
-                      "(%s)" % (m, P / 1e6, threads, "oracle/_ref: lib/http2/hpack.c compiled" if kind == "reference"
-                                else "clean-room restatement"),
+    v1, P1 = rate(m1, 1, 5)
+    return {"value": round(v, 4), "unit": "GiB/s", "cores": threads, "affinity_cpus": affinity, "kind": kind,
+            "sample": "%d strings (%.1f MB) of rank 0's shard, encode + decode, median of 5, %d threads of %d in the "
+                      "affinity mask (%s)" % (m, Ps / 1e6, threads, affinity,
+                                              "oracle/_ref: the reference's lib/http2/hpack.c, compiled" if kind ==
+                                              "reference" else "clean-room restatement"),
             "single_thread_value": round(v1, 4),
-            "single_thread_sample": "%d strings (%.1f MB), 1 thread" % (m1, P1 / 1e6)}
+            "single_thread_sample": "%d strings (%.1f MB), 1 thread, median of 5" % (m1, P1 / 1e6)}
 
 
 if __name__ == "__main__":

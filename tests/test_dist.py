@@ -1,11 +1,14 @@
-"""Multi-rank sharding on CPU (gloo, world_size 2 and 3): scatter a batch from rank 0 in byte-balanced
-shards, decode every shard (the CPU oracle stands in for the per-rank HIP codec here), gather on rank 0,
-and require byte-for-byte the single-process result."""
+"""Multi-rank sharding (h2o_amd/dist.py) on CPU tensors over gloo, world sizes 2 and 3: scatter a batch from
+rank 0 in byte-balanced shards, run the per-rank codec, all_gather the shard sizes, gather on rank 0, and
+require byte-for-byte the single-process result.  The per-rank codec keeps the contract of
+hhuff_decode_batch_packed (out, out_off, out_len, status); with no GPU here the CPU restatement computes it
+(on a GPU node dist.py runs the same code on CUDA tensors over RCCL: bench.py --gpus N)."""
 import os
 import socket
 
 import numpy as np
 import pytest
+import torch
 import torch.multiprocessing as mp
 
 from h2o_amd import dist as hd
@@ -18,16 +21,25 @@ def _free_port():
 
 
 def _oracle_decode(shard):
+    """hhuff_decode_batch_packed's contract on CPU tensors, computed by the restatement (slot places)"""
     from oracle import oracle as O
 
-    o = O.oracle()
     n = shard["n"]
-    out, out_len, status = o.decode_batch(shard["data"], shard["off"], n, is_name_bits=shard["is_name_bits"])
-    out_off = (shard["off"][:n].astype(np.uint64) * 8) // 5
-    return out, out_off, out_len, status
+    data = shard["data"].numpy()
+    off = shard["off"].numpy().view(np.uint32)
+    names = shard["is_name_bits"].numpy().view(np.uint32)
+    out, out_len, status = O.oracle().decode_batch(data, off, n, is_name_bits=names)
+    out_off = ((off.astype(np.uint64) * 8) // 5).astype(np.int64)
+    return (torch.from_numpy(out), torch.from_numpy(out_off), torch.from_numpy(out_len.astype(np.int64)),
+            torch.from_numpy(status))
 
 
-def _worker(rank, world, port, q):
+def _tensors(b):
+    return dict(data=torch.from_numpy(b["data"]), off=torch.from_numpy(b["off"].view(np.int32)),
+                is_name_bits=torch.from_numpy(b["is_name_bits"].view(np.int32)), n=b["n"])
+
+
+def _worker(rank, world, port, q, with_names):
     import torch.distributed as dist
 
     from h2o_amd import synth
@@ -36,16 +48,25 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        batch = synth.make_batch("c2", n=5000, seed=31, adversarial_frac=0.05) if rank == 0 else None
+        batch = None
+        if rank == 0:
+            batch = _tensors(synth.make_batch("c2", n=5000, seed=31, adversarial_frac=0.05))
+            if not with_names:
+                batch["is_name_bits"] = None
         res = hd.decode_sharded(batch, _oracle_decode, root=0)
+        # the size exchange alone: every rank learns its shard's global string index and output offset
+        local = torch.tensor([rank + 1, 10 * (rank + 1)])
+        sizes, first, obase = hd.exchange_sizes(local[0], local[1])
+        exp = sum(r + 1 for r in range(rank)), sum(10 * (r + 1) for r in range(rank))
+        assert (int(first), int(obase)) == exp and sizes.shape == (world, 2)
         if rank == 0:
             q.put(tuple(np.asarray(x).tobytes() for x in res))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_scatter_decode_gather_matches_single_process(world):
+@pytest.mark.parametrize("world,with_names", [(2, True), (3, True), (2, False)])
+def test_scatter_decode_gather_matches_single_process(world, with_names):
     from h2o_amd import synth
     from oracle import oracle as O
 
@@ -53,38 +74,45 @@ def test_scatter_decode_gather_matches_single_process(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, with_names)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    batch = synth.make_batch("c2", n=5000, seed=31, adversarial_frac=0.05)
-    full = {"data": batch["data"], "off": batch["off"], "is_name_bits": batch["is_name_bits"], "n": batch["n"]}
-    ref = hd.compact_results(*_oracle_decode(full))
-    assert got == tuple(np.asarray(x).tobytes() for x in ref)
+    full = _tensors(synth.make_batch("c2", n=5000, seed=31, adversarial_frac=0.05))
+    if not with_names:
+        full["is_name_bits"] = torch.zeros_like(full["is_name_bits"])
+    out, out_off, out_len, status = _oracle_decode(full)
+    ol, data = hd.compact_results(out, out_off, out_len)
+    assert got == tuple(np.asarray(x).tobytes() for x in (ol, status, data))
 
 
 def test_byte_balanced_bounds():
-    off = np.cumsum(np.r_[0, np.full(1000, 48)])
+    off = torch.cumsum(torch.tensor([0] + [48] * 1000), 0)
     for world in (1, 2, 4, 8):
         b = hd.byte_balanced_bounds(off, world)
-        assert b[0] == 0 and b[-1] == 1000 and (np.diff(b) >= 0).all()
+        assert int(b[0]) == 0 and int(b[-1]) == 1000 and bool((b[1:] >= b[:-1]).all())
         sizes = off[b[1:]] - off[b[:-1]]
-        assert sizes.max() - sizes.min() <= 48
-    # skewed lengths: one huge string
-    off = np.cumsum(np.r_[0, [10] * 50, [100000], [10] * 50])
+        assert int(sizes.max() - sizes.min()) <= 48
+    off = torch.cumsum(torch.tensor([0] + [10] * 50 + [100000] + [10] * 50), 0)  # one huge string
     b = hd.byte_balanced_bounds(off, 4)
-    assert b[0] == 0 and b[-1] == 101 and (np.diff(b) >= 0).all()
+    assert int(b[0]) == 0 and int(b[-1]) == 101 and bool((b[1:] >= b[:-1]).all())
+    # u32 offsets carried in int32 (bit 31 set) are read as unsigned
+    big = torch.tensor([0, 3 << 30, (3 << 30) + 10], dtype=torch.int64)
+    assert hd.byte_balanced_bounds(big.to(torch.int32), 2).tolist() == hd.byte_balanced_bounds(big, 2).tolist()
 
 
 def test_shard_rebases_offsets_and_names():
     from h2o_amd import synth
 
-    batch = synth.make_batch("c2", n=300, seed=5)
-    s = hd.shard(batch, 100, 250)
-    assert s["off"][0] == 0 and s["n"] == 150
-    assert bytes(s["data"]) == bytes(batch["data"][batch["off"][100]:batch["off"][250]])
-    names = hd._bits_to_bool(batch["is_name_bits"], 300)[100:250]
-    assert (hd._bits_to_bool(s["is_name_bits"], 150) == names).all()
+    b = synth.make_batch("c2", n=300, seed=5)
+    t = _tensors(b)
+    s = hd.shard(t, 100, 250)
+    assert int(s["off"][0]) == 0 and s["n"] == 150
+    assert bytes(s["data"].numpy()) == bytes(b["data"][b["off"][100]:b["off"][250]])
+    names = hd.bits_to_bool(t["is_name_bits"], 300)[100:250]
+    assert bool((hd.bits_to_bool(s["is_name_bits"], 150) == names).all())
+    t["is_name_bits"] = None  # an encode batch: no name bits -> zero bits, no KeyError
+    assert int(hd.shard(t, 10, 50)["is_name_bits"].abs().sum()) == 0
