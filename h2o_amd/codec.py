@@ -37,6 +37,11 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise HhuffError("libhhuff.so not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        # torch first: its ROCm wheel ships its own libamdhip64.so, and libhhuff.so's dependency must
+        # resolve to that already-loaded runtime -- one HIP runtime per process (loaded the other way round,
+        # two runtimes end up sharing the device and the per-string path fails)
+        import torch  # noqa: F401
+
         L = ctypes.CDLL(LIB_PATH)
         L.h2o_hpack_decode_huffman.restype = ctypes.c_size_t
         L.h2o_hpack_decode_huffman.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint), ctypes.c_char_p,

@@ -37,12 +37,15 @@ int arg_fail(const char* what) {
     } while (0)
 
 // Per-thread device context: a stream on the chosen device plus growable device / pinned buffers.
+// bind() never changes the calling thread's current device for good: the per-string symbols run on the
+// thread's current device (h2o's worker threads may have set one), the host batch calls on their `device`
+// argument with the caller's current device restored on return (DeviceGuard).
 struct Ctx {
     int dev = -1;
     hipStream_t stream = nullptr;
     uint8_t* d = nullptr;
     size_t dcap = 0;
-    uint8_t* h = nullptr;
+    uint8_t* h = nullptr;  // pinned, device-visible (the per-string kernel reads and writes it in place)
     size_t hcap = 0;
     ~Ctx() {
         // thread exit: release what this thread allocated (ignore errors at process teardown)
@@ -50,16 +53,21 @@ struct Ctx {
         if (h) (void)hipHostFree(h);
         if (stream) (void)hipStreamDestroy(stream);
     }
+    // make `device` (-1: the thread's current device) this context's device; the caller's current device is
+    // the one left current (the stream of a device can be used with another device current)
     int bind(int device) {
-        if (device < 0) HIP_TRY(hipGetDevice(&device), "hipGetDevice");
+        int cur = 0;
+        HIP_TRY(hipGetDevice(&cur), "hipGetDevice");
+        if (device < 0) device = cur;
         if (dev != device) {
             if (d) (void)hipFree(d), d = nullptr, dcap = 0;
+            if (h) (void)hipHostFree(h), h = nullptr, hcap = 0;
             if (stream) (void)hipStreamDestroy(stream), stream = nullptr;
-            HIP_TRY(hipSetDevice(device), "hipSetDevice");
-            HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking), "hipStreamCreate");
+            if (device != cur) HIP_TRY(hipSetDevice(device), "hipSetDevice");
+            const hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+            if (device != cur) (void)hipSetDevice(cur);
+            if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
             dev = device;
-        } else {
-            HIP_TRY(hipSetDevice(device), "hipSetDevice");
         }
         return HHUFF_OK;
     }
@@ -73,21 +81,31 @@ struct Ctx {
         if (hneed > hcap) {
             if (h) (void)hipHostFree(h), h = nullptr, hcap = 0;
             size_t cap = hneed < (1u << 16) ? (1u << 16) : hneed + hneed / 4;
-            HIP_TRY(hipHostMalloc(&h, cap, hipHostMallocDefault), "hipHostMalloc");
+            // coherent (fine-grained): the per-string kernel reads and writes it in place across PCIe
+            HIP_TRY(hipHostMalloc(&h, cap, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
             hcap = cap;
         }
         return HHUFF_OK;
     }
 };
 
+// Makes `device` current for the scope of a host batch call, restoring the caller's device on exit.
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (device >= 0 && device != prev) err = hipSetDevice(device);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
 thread_local Ctx t_ctx;
 
 inline size_t up16(size_t x) { return (x + 15) & ~(size_t)15; }
-
-[[noreturn]] void die(const char* fn) {
-    fprintf(stderr, "hhuff: %s failed: %s\n", fn, t_err);
-    abort();
-}
 
 int check_batch(const uint8_t* in, const uint32_t* in_off, uint32_t n, const uint8_t* out, const uint32_t* out_len) {
     if (n == 0) return HHUFF_OK;
@@ -229,23 +247,45 @@ HHUFF_API int hhuff_qpack_decode(const uint8_t* in, uint64_t in_size, const uint
 }
 
 // ---------------------------------------------------------------------------------------------------
-// (1) h2o per-string symbols: a batch of one on the thread's stream, synchronously
-// device/pinned layout: [meta 32 B: u32 in_off[2], out_len, is_name word, u8 status][input][output]
+// (1) h2o per-string symbols: one string per launch on the thread's stream, synchronously.
+// Strings up to kOneMax bytes go through one_string_kernel on a pinned, device-visible buffer
+// [u32 len, is_name, result, status][input][output] (no copies: one launch, one synchronisation); longer
+// ones through the batch kernels with device copies.  A HIP failure (no GPU, a lost device) never aborts
+// the caller: decode returns SIZE_MAX -- h2o's decode_string then reports H2O_HTTP2_ERROR_COMPRESSION for
+// that literal (hpack.c:241-242) and the connection closes --, encode returns SIZE_MAX -- every caller then
+// emits the string raw (hpack.c:836, qpack.c:1046-1051), which is a correct encoding; the reason is in
+// hhuff_last_error_string().
 // ---------------------------------------------------------------------------------------------------
 namespace {
 constexpr size_t kMeta = 32;
-}
 
-HHUFF_API size_t h2o_hpack_decode_huffman(char* dst, unsigned* soft_errors, const uint8_t* src, size_t len, int is_name,
-                                          const char** err_desc) {
-    (void)err_desc;  // never written, as in the reference (hpack.c:142-144 is unreachable)
+size_t per_string(bool encode, uint8_t* dst, const uint8_t* src, size_t len, int is_name, unsigned* soft_errors) {
     Ctx& c = t_ctx;
     if (len > 0x1FFFFFFFu) {
         snprintf(t_err, sizeof(t_err), "string of %zu bytes exceeds the per-string limit", len);
-        die("h2o_hpack_decode_huffman");
+        return SIZE_MAX;
     }
-    const size_t in_cap = up16(len ? len : 1), out_cap = up16(len * 8 / 5 + 4);
-    if (c.bind(-1) || c.reserve(kMeta + in_cap + out_cap, kMeta + in_cap + out_cap)) die("h2o_hpack_decode_huffman");
+    if (c.bind(-1)) return SIZE_MAX;
+    const size_t in_cap = up16(len ? len : 1);
+    if (len <= hhuff::kOneMax) {
+        const size_t out_cap = up16(len * 8 / 5 + 4);
+        if (c.reserve(0, 16 + in_cap + out_cap)) return SIZE_MAX;
+        uint32_t* meta = reinterpret_cast<uint32_t*>(c.h);
+        meta[0] = (uint32_t)len;
+        meta[1] = is_name ? 1u : 0u;
+        memcpy(c.h + 16, src, len);
+        hipError_t e = hhuff::launch_one(c.h, (uint32_t)len, (uint32_t)in_cap, is_name != 0, encode, c.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+        if (e != hipSuccess) return hip_fail(e, encode ? "encode (one string)" : "decode (one string)"), SIZE_MAX;
+        const uint32_t r = __atomic_load_n(&meta[2], __ATOMIC_ACQUIRE);
+        if (r == HHUFF_FAIL_LEN) return SIZE_MAX;
+        memcpy(dst, c.h + 16 + in_cap, r);
+        if (!encode) *soft_errors |= meta[3] & 3u;
+        return r;
+    }
+    // long strings: the batch kernels on a batch of one, device copies
+    const size_t out_cap = up16(len * 8 / 5 + 4);
+    if (c.reserve(kMeta + in_cap + out_cap, kMeta + in_cap + out_cap)) return SIZE_MAX;
     uint32_t* meta = reinterpret_cast<uint32_t*>(c.h);
     meta[0] = 0;
     meta[1] = (uint32_t)len;
@@ -255,53 +295,32 @@ HHUFF_API size_t h2o_hpack_decode_huffman(char* dst, unsigned* soft_errors, cons
     uint32_t* d_meta = reinterpret_cast<uint32_t*>(c.d);
     uint8_t* d_in = c.d + kMeta;
     uint8_t* d_out = c.d + kMeta + in_cap;
-    hipError_t e = hipMemcpyAsync(c.d, c.h, kMeta + len, hipMemcpyHostToDevice, c.stream);
-    if (e != hipSuccess) hip_fail(e, "H2D"), die("h2o_hpack_decode_huffman");
-    e = hhuff::launch_decode(d_in, len, d_meta, nullptr, 1, d_meta + 3, d_out, nullptr, d_meta + 2,
-                             reinterpret_cast<uint8_t*>(d_meta + 4), c.stream);
-    if (e != hipSuccess) hip_fail(e, "decode launch"), die("h2o_hpack_decode_huffman");
     uint8_t* h_out = c.h + kMeta + in_cap;
-    e = hipMemcpyAsync(c.h, c.d, kMeta, hipMemcpyDeviceToHost, c.stream);
+    hipError_t e = hipMemcpyAsync(c.d, c.h, kMeta + len, hipMemcpyHostToDevice, c.stream);
+    if (e == hipSuccess)
+        e = encode ? hhuff::launch_encode(d_in, len, d_meta, nullptr, 1, d_out, nullptr, d_meta + 2, nullptr, c.stream)
+                   : hhuff::launch_decode(d_in, len, d_meta, nullptr, 1, d_meta + 3, d_out, nullptr, d_meta + 2,
+                                          reinterpret_cast<uint8_t*>(d_meta + 4), c.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(c.h, c.d, kMeta, hipMemcpyDeviceToHost, c.stream);
     if (e == hipSuccess) e = hipMemcpyAsync(h_out, d_out, out_cap, hipMemcpyDeviceToHost, c.stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
-    if (e != hipSuccess) hip_fail(e, "D2H"), die("h2o_hpack_decode_huffman");
+    if (e != hipSuccess) return hip_fail(e, encode ? "encode (long string)" : "decode (long string)"), SIZE_MAX;
     const uint32_t r = meta[2];
     if (r == HHUFF_FAIL_LEN) return SIZE_MAX;
     memcpy(dst, h_out, r);
-    *soft_errors |= *reinterpret_cast<const uint8_t*>(meta + 4);
+    if (!encode) *soft_errors |= *reinterpret_cast<const uint8_t*>(meta + 4);
     return r;
+}
+}  // namespace
+
+HHUFF_API size_t h2o_hpack_decode_huffman(char* dst, unsigned* soft_errors, const uint8_t* src, size_t len, int is_name,
+                                          const char** err_desc) {
+    (void)err_desc;  // never written, as in the reference (hpack.c:142-144 is unreachable)
+    return per_string(false, reinterpret_cast<uint8_t*>(dst), src, len, is_name, soft_errors);
 }
 
 HHUFF_API size_t h2o_hpack_encode_huffman(uint8_t* dst, const uint8_t* src, size_t len) {
-    Ctx& c = t_ctx;
-    if (len > 0x1FFFFFFFu) {
-        snprintf(t_err, sizeof(t_err), "string of %zu bytes exceeds the per-string limit", len);
-        die("h2o_hpack_encode_huffman");
-    }
-    const size_t in_cap = up16(len ? len : 1), out_cap = up16(len + 4);
-    if (c.bind(-1) || c.reserve(kMeta + in_cap + out_cap, kMeta + in_cap + out_cap)) die("h2o_hpack_encode_huffman");
-    uint32_t* meta = reinterpret_cast<uint32_t*>(c.h);
-    meta[0] = 0;
-    meta[1] = (uint32_t)len;
-    meta[2] = 0;
-    meta[3] = 0;
-    memcpy(c.h + kMeta, src, len);
-    uint8_t* d_in = c.d + kMeta;
-    uint8_t* d_out = c.d + kMeta + in_cap;
-    uint32_t* d_meta = reinterpret_cast<uint32_t*>(c.d);
-    hipError_t e = hipMemcpyAsync(c.d, c.h, kMeta + len, hipMemcpyHostToDevice, c.stream);
-    if (e != hipSuccess) hip_fail(e, "H2D"), die("h2o_hpack_encode_huffman");
-    e = hhuff::launch_encode(d_in, len, d_meta, nullptr, 1, d_out, nullptr, d_meta + 2, nullptr, c.stream);
-    if (e != hipSuccess) hip_fail(e, "encode launch"), die("h2o_hpack_encode_huffman");
-    uint8_t* h_out = c.h + kMeta + in_cap;
-    e = hipMemcpyAsync(c.h, c.d, kMeta, hipMemcpyDeviceToHost, c.stream);
-    if (e == hipSuccess && len) e = hipMemcpyAsync(h_out, d_out, len, hipMemcpyDeviceToHost, c.stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
-    if (e != hipSuccess) hip_fail(e, "D2H"), die("h2o_hpack_encode_huffman");
-    uint32_t r = meta[2];
-    if (r == HHUFF_FAIL_LEN) return SIZE_MAX;
-    memcpy(dst, h_out, r);
-    return r;
+    return per_string(true, dst, src, len, 0, nullptr);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -334,6 +353,8 @@ int host_batch(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t*
     if (!in || !in_off || !out || !out_len || (decode && !status)) return arg_fail("NULL array");
     if (!in_len && !out_off && in_size >= 2 * kDefaultChunk && in_off[n] <= in_size)  // large contiguous batch
         return pipelined(decode, in, in_size, in_off, n, is_name_bits, out, out_size, out_len, status, device, 0);
+    DeviceGuard guard(device);
+    if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
     Ctx& c = t_ctx;
     int rc = c.bind(device);
     if (rc) return rc;
@@ -462,6 +483,8 @@ int pipelined(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* 
               const uint32_t* is_name_bits, uint8_t* out, uint64_t out_size, uint32_t* out_len, uint8_t* status,
               int device, uint64_t chunk_bytes) {
     if (chunk_bytes == 0) chunk_bytes = kDefaultChunk;
+    DeviceGuard guard(device);
+    if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
     Ctx& c = t_ctx;
     int rc = c.bind(device);
     if (rc) return rc;
@@ -614,6 +637,7 @@ HHUFF_API int hhuff_debug_prof(unsigned long long* out16, int reset) {
 HHUFF_API const char* hhuff_version(void) { return "hhuff 0.1.0 (gfx950)"; }
 HHUFF_API const char* hhuff_last_error_string(void) { return t_err; }
 HHUFF_API int hhuff_grid_size(int device, int which) {
-    if (hipSetDevice(device) != hipSuccess) return -1;
+    DeviceGuard guard(device);
+    if (guard.err != hipSuccess) return -1;
     return hhuff::grid_size(device, which);
 }

@@ -2103,6 +2103,62 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
 }
 
 // ------------------------------------------------------------------------------------------------
+// One string per launch: the h2o per-string symbols (h2o_hpack_{de,en}code_huffman).  The string sits in
+// pinned, device-visible host memory, [meta 16 B][input][output]: one launch reads it across PCIe (the
+// block's 16-B loads in one round trip) into LDS, lane 0 runs the codec from LDS into an LDS output buffer,
+// and the wave writes the result and the meta words back -- no copies, one launch, one synchronisation.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void one_string_kernel(uint8_t* __restrict__ h, uint32_t len, uint32_t in_cap,
+                                                         uint32_t is_name, uint32_t encode) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
+    __shared__ uint32_t s_kinfo[32];
+    __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[kOneMax / 4 + 4];
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[(kOneMax * 8) / 5 + 64];
+    uint2* s_enc = reinterpret_cast<uint2*>(s_lut);  // encode: the table takes the LUT's place
+    if (encode) {
+        for (uint32_t k = threadIdx.x; k < 256; k += 256) s_enc[k] = make_uint2(g_enc_code[k], g_enc_nbits[k]);
+    } else {
+        load_dec_tables(s_lut, s_kinfo, s_ones, 256);
+    }
+    for (uint32_t k = 16u * threadIdx.x; k < len; k += 16u * 256u)
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_in) + k) = *reinterpret_cast<const uint4*>(h + 16 + k);
+    __syncthreads();
+    __shared__ uint32_t s_res[2];
+    if (threadIdx.x == 0) {
+        const LdsSource src{s_in, len ? ((len + 3u) & ~3u) - 4u : 0u};
+        LdsSink sink{s_out, 0u, 0u, (kOneMax * 8) / 5 + 60};
+        uint32_t ol, st = 0;
+        if (encode) {
+            ol = encode_core(src, 0u, len, sink, s_enc);
+            st = ol == kFailLen ? kStatusFail : 0u;
+        } else {
+            const DecResult r = decode_core(src, 0u, len, sink, DecTables{s_lut, s_kinfo, s_ones});
+            ol = r.ok ? r.len : kFailLen;
+            st = r.ok ? soft_bits(is_name != 0, r.len, r.flags, r.len ? s_out[0] : 0u, r.len ? s_out[r.len - 1] : 0u)
+                      : kStatusFail;
+        }
+        s_res[0] = ol;
+        s_res[1] = st;
+    }
+    __syncthreads();
+    const uint32_t ol = s_res[0];
+    const uint32_t n = ol == kFailLen ? 0u : ol;
+    for (uint32_t k = 4u * threadIdx.x; k < n; k += 4u * 256u)
+        *reinterpret_cast<uint32_t*>(h + 16 + in_cap + k) = *reinterpret_cast<const uint32_t*>(s_out + k);
+    if (threadIdx.x == 0) {
+        reinterpret_cast<uint32_t*>(h)[2] = ol;
+        reinterpret_cast<uint32_t*>(h)[3] = s_res[1];
+    }
+}
+
+hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, bool encode, hipStream_t stream) {
+    hipLaunchKernelGGL(one_string_kernel, dim3(1), dim3(256), 0, stream, h, len, in_cap, is_name ? 1u : 0u,
+                       encode ? 1u : 0u);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
 // Packed output for the variants without a native packed mode (long strings: stream / direct decode,
 // proportional-lane encode): the kernel writes the slot layout into a stream-ordered scratch buffer,
 // then pack_tiles_kernel moves each 64-string tile's outputs to their places (one wave per tile: wave

@@ -10,6 +10,10 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
 hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
                          uint8_t* out, const uint32_t* out_off, uint32_t* out_len, uint8_t* status, hipStream_t stream,
                          uint64_t sel_bytes = 0);
+// One string per launch (the per-string h2o symbols): h = device-visible pinned host buffer
+// [u32 len, is_name, result len, status][input, in_cap bytes (16-aligned)][output]; len <= kOneMax
+constexpr uint32_t kOneMax = 8192;
+hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, bool encode, hipStream_t stream);
 // Packed output (include/hhuff.h hhuff_{de,en}code_batch_packed): contiguous layout, pk_off u32[n + 1]
 hipError_t launch_decode_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
                                 const uint32_t* is_name_bits, uint8_t* out, uint32_t* pk_off, uint32_t* out_len,

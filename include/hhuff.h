@@ -6,9 +6,12 @@
  * NULL for the legacy default stream).
  *
  * 1. Per-string symbols with h2o's exact signatures and semantics.  A maintainer links libhhuff in
- *    place of the definitions in lib/http2/hpack.c.  Each call runs the HIP
- *    kernels on a batch of one string, synchronously, on a per-thread stream of the current device.
- *    Launch latency (~10-20 us) makes this the compatibility path; throughput comes from the batch API.
+ *    place of the definitions in lib/http2/hpack.c.  Each call runs one HIP launch
+ *    on the string, synchronously, on a per-thread stream of the calling thread's current device (which
+ *    the call leaves as it was).  About 20 us per call on MI355X (bench.py per_string_latency_us) makes
+ *    this the compatibility path; throughput comes from the batch API.  A HIP failure never aborts: the
+ *    call returns SIZE_MAX (decode: h2o reports the literal as a COMPRESSION error; encode: h2o sends the
+ *    string raw, a correct encoding) and hhuff_last_error_string() says why.
  * 2. Batch entry points on device-resident arrays (the hot path) and on host arrays (pinned staging,
  *    H2D/D2H included).  Element i of a batch has exactly the per-string semantics of (1).
  *

@@ -22,7 +22,7 @@ def test_library_exports_every_declared_symbol():
     from h2o_amd import build, codec
 
     build.build(verbose=False)
-    lib = ctypes.CDLL(codec.LIB_PATH)
+    lib = codec.lib()
     for name in declared_functions():
         assert hasattr(lib, name), name
     assert set(codec.EXPORTED) == set(declared_functions())
@@ -33,3 +33,58 @@ def test_library_is_gfx950_code_object():
 
     blob = open(codec.LIB_PATH, "rb").read()
     assert b"gfx950" in blob
+
+
+CAPI_CHECK = os.path.join(ROOT, "build", "capi_check")
+
+
+def build_capi_check():
+    """tests/capi_check.c: a C translation unit against include/hhuff.h, linked with libhhuff.so"""
+    import subprocess
+
+    from h2o_amd import build
+
+    build.build(verbose=False)
+    os.makedirs(os.path.dirname(CAPI_CHECK), exist_ok=True)
+    src = os.path.join(ROOT, "tests", "capi_check.c")
+    if not os.path.exists(CAPI_CHECK) or os.path.getmtime(CAPI_CHECK) < max(os.path.getmtime(src),
+                                                                            os.path.getmtime(build.LIB)):
+        subprocess.run(["gcc", "-std=c11", "-O1", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                        "-I" + os.path.join(ROOT, "include"), "-I/opt/rocm/include", src, "-o", CAPI_CHECK,
+                        "-L" + os.path.dirname(build.LIB), "-lhhuff", "-L/opt/rocm/lib", "-lamdhip64", "-lpthread",
+                        "-Wl,-rpath," + os.path.dirname(build.LIB) + ":/opt/rocm/lib"], check=True)
+    return CAPI_CHECK
+
+
+def test_c_translation_unit_builds_and_links():
+    """include/hhuff.h is plain C and every symbol the check program uses resolves in libhhuff.so"""
+    assert os.path.exists(build_capi_check())
+
+
+def test_per_string_symbols_fail_soft_without_a_gpu():
+    """no GPU (this container): h2o_hpack_{de,en}code_huffman return SIZE_MAX with a reason, never abort --
+    decode then becomes h2o's COMPRESSION error for that literal, encode its raw fallback"""
+    import subprocess
+
+    import torch
+
+    if torch.cuda.is_available():
+        import pytest
+
+        pytest.skip("a GPU is present (the GPU test runs the full check)")
+    r = subprocess.run([build_capi_check(), "nogpu"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "err=" in r.stdout and "decode=%d" % (2 ** 64 - 1) in r.stdout
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_c_translation_unit_on_the_gpu():
+    """per-string symbols from 8 concurrent threads, a NULL-stream batch, the host API on device 0"""
+    import subprocess
+
+    r = subprocess.run([build_capi_check()], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "capi_check: ok" in r.stdout
