@@ -89,6 +89,7 @@ def lib():
         L.hhuff_version.restype = ctypes.c_char_p
         L.hhuff_last_error_string.restype = ctypes.c_char_p
         L.hhuff_grid_size.restype = ctypes.c_int
+        L.hhuff_per_string_calls.restype = ctypes.c_uint64
         L.hhuff_grid_size.argtypes = [ctypes.c_int, ctypes.c_int]
         _lib = L
     return _lib
@@ -100,7 +101,7 @@ EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decod
             "hhuff_flatten_batch", "hhuff_decode_literals", "hhuff_hpack_decode_blocks", "hhuff_hpack_scratch_size",
             "hhuff_qpack_decode", "hhuff_qpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
-            "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string",
+            "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string", "hhuff_per_string_calls",
             "hhuff_grid_size")
 
 

@@ -258,8 +258,10 @@ HHUFF_API int hhuff_qpack_decode(const uint8_t* in, uint64_t in_size, const uint
 // ---------------------------------------------------------------------------------------------------
 namespace {
 constexpr size_t kMeta = 32;
+uint64_t g_per_string_calls = 0;  // process-wide, atomic adds (hhuff_per_string_calls)
 
 size_t per_string(bool encode, uint8_t* dst, const uint8_t* src, size_t len, int is_name, unsigned* soft_errors) {
+    __atomic_fetch_add(&g_per_string_calls, 1, __ATOMIC_RELAXED);
     Ctx& c = t_ctx;
     if (len > 0x1FFFFFFFu) {
         snprintf(t_err, sizeof(t_err), "string of %zu bytes exceeds the per-string limit", len);
@@ -322,6 +324,8 @@ HHUFF_API size_t h2o_hpack_decode_huffman(char* dst, unsigned* soft_errors, cons
 HHUFF_API size_t h2o_hpack_encode_huffman(uint8_t* dst, const uint8_t* src, size_t len) {
     return per_string(true, dst, src, len, 0, nullptr);
 }
+
+HHUFF_API uint64_t hhuff_per_string_calls(void) { return __atomic_load_n(&g_per_string_calls, __ATOMIC_RELAXED); }
 
 // ---------------------------------------------------------------------------------------------------
 // (3) host batch API: copy in, run, copy out (synchronous)

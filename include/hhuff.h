@@ -63,6 +63,11 @@ size_t h2o_hpack_decode_huffman(char *dst, unsigned *soft_errors, const uint8_t 
  * `dst` must hold `len` bytes; its contents are unspecified on SIZE_MAX. */
 size_t h2o_hpack_encode_huffman(uint8_t *dst, const uint8_t *src, size_t len);
 
+/* Number of calls the two symbols above have taken in this process (both, any outcome).  An integration
+ * check: after linking h2o against this library, a non-zero count after decoding a Huffman literal shows
+ * h2o's callers (decode_string, h2o_hpack_encode_string, QPACK's flatten_string ...) bound here. */
+uint64_t hhuff_per_string_calls(void);
+
 /* ---------------------------------------------------------------------------------------------
  * (2) batch API, device-resident arrays (hot path).  Asynchronous on `stream`.
  * ------------------------------------------------------------------------------------------- */

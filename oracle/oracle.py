@@ -285,3 +285,17 @@ def ref() -> _Codec:
     if _ref is None:
         _ref = _Codec(os.path.join(HERE, "_ref", "libh2oref.so"), "ref")
     return _ref
+
+
+CALLERS_PATH = os.path.join(HERE, "_ref", "libh2ocallers.so")
+
+
+def callers_available() -> bool:
+    return os.path.exists(CALLERS_PATH)
+
+
+def callers() -> _Codec:
+    """h2o's own callers (hpack.c / qpack.c built with default visibility): their calls to
+    h2o_hpack_{de,en}code_huffman go through the PLT and bind to the first definition in the global scope --
+    libhhuff.so when it was loaded RTLD_GLOBAL before this library (tests/dropin_replay.py)."""
+    return _Codec(CALLERS_PATH, "ref")
