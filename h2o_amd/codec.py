@@ -80,6 +80,10 @@ def lib():
         L.hhuff_hpack_decode_blocks.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp,
                                                 _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64,
                                                 ctypes.c_uint, _vp]
+        L.hhuff_hpack_parse_requests.restype = ctypes.c_int
+        L.hhuff_hpack_parse_requests.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp,
+                                                 _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64,
+                                                 ctypes.c_uint, _vp]
         L.hhuff_qpack_scratch_size.restype = ctypes.c_uint64
         L.hhuff_qpack_scratch_size.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         L.hhuff_qpack_decode.restype = ctypes.c_int
@@ -99,6 +103,7 @@ def lib():
 EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decode_batch", "hhuff_encode_batch",
             "hhuff_decode_batch_packed", "hhuff_encode_batch_packed",
             "hhuff_flatten_batch", "hhuff_decode_literals", "hhuff_hpack_decode_blocks", "hhuff_hpack_scratch_size",
+            "hhuff_hpack_parse_requests",
             "hhuff_qpack_decode", "hhuff_qpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string", "hhuff_per_string_calls",
@@ -297,11 +302,19 @@ def default_arena_off(blk_off, table_size=4096):
 BLK_CONTINUE = 1
 
 
+# include/hhuff.h hhuff_request_t: 12 u32 words per block
+REQUEST_FIELDS = ("content_length", "method", "scheme", "authority", "path", "protocol", "expect", "exists_map",
+                  "nheaders", "err", "scheme_kind")
+FIELD_HEADER = 0x4
+
+
 def hpack_decode_blocks(data, blk_off, conn_first, table_size=4096, arena_off=None, in_size=None, stream=None,
-                        scratch=None, cont=False):
+                        scratch=None, cont=False, requests=False):
     """HPACK header blocks (include/hhuff.h hhuff_hpack_decode_blocks) on device tensors: blk_off / conn_first
     int32 tensors (u32 bits), arena_off int64.  Returns a dict of device tensors: arena, name_off, name_len,
-    value_off, value_len, fflags (per field slot), nfields, bstatus (per block)."""
+    value_off, value_len, fflags (per field slot), nfields, bstatus (per block).  requests=True runs
+    hhuff_hpack_parse_requests (h2o_hpack_parse_request per block) and adds req: int32 [nblk, 12], the
+    hhuff_request_t words (REQUEST_FIELDS; content_length is words 0-1)."""
     import torch
 
     dev = data.device
@@ -322,12 +335,15 @@ def hpack_decode_blocks(data, blk_off, conn_first, table_size=4096, arena_off=No
     ss = int(lib().hhuff_hpack_scratch_size(nconn, table_size))
     if scratch is None:  # pass the previous call's r["scratch"] back with cont=True to carry the tables over
         scratch = torch.empty(max(16, ss), dtype=torch.uint8, device=dev)
-    _check(lib().hhuff_hpack_decode_blocks(_dp(data), in_size, _dp(blk_off), _dp(conn_first), nconn, table_size,
-                                           _dp(r["arena"]), _dp(arena_off), _dp(r["name_off"]), _dp(r["name_len"]),
-                                           _dp(r["value_off"]), _dp(r["value_len"]), _dp(r["fflags"]), _dp(r["nfields"]),
-                                           _dp(r["bstatus"]), _dp(scratch), scratch.numel(),
-                                           BLK_CONTINUE if cont else 0, _stream(stream)),
-           "hhuff_hpack_decode_blocks")
+    args = [_dp(data), in_size, _dp(blk_off), _dp(conn_first), nconn, table_size, _dp(r["arena"]), _dp(arena_off),
+            _dp(r["name_off"]), _dp(r["name_len"]), _dp(r["value_off"]), _dp(r["value_len"]), _dp(r["fflags"]),
+            _dp(r["nfields"]), _dp(r["bstatus"])]
+    tail = [_dp(scratch), scratch.numel(), BLK_CONTINUE if cont else 0, _stream(stream)]
+    if requests:
+        r["req"] = torch.empty((max(1, nblk), 12), dtype=torch.int32, device=dev)
+        _check(lib().hhuff_hpack_parse_requests(*args, _dp(r["req"]), *tail), "hhuff_hpack_parse_requests")
+    else:
+        _check(lib().hhuff_hpack_decode_blocks(*args, *tail), "hhuff_hpack_decode_blocks")
     r["scratch"] = scratch  # keep alive until the stream has run the launch
     return r
 

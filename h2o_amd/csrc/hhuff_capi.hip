@@ -198,22 +198,44 @@ HHUFF_API uint64_t hhuff_hpack_scratch_size(uint32_t nconn, uint32_t table_size)
     return (uint64_t)nconn * hhuff::hpack_conn_scratch(table_size);
 }
 
-HHUFF_API int hhuff_hpack_decode_blocks(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off,
-                                        const uint32_t* conn_first, uint32_t nconn, uint32_t table_size, uint8_t* arena,
-                                        const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len,
-                                        uint32_t* value_off, uint32_t* value_len, uint8_t* fflags, uint32_t* nfields,
-                                        int32_t* bstatus, void* scratch, uint64_t scratch_size, unsigned flags,
-                                        void* stream) {
+namespace {
+int hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off, const uint32_t* conn_first, uint32_t nconn,
+                 uint32_t table_size, uint8_t* arena, const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len,
+                 uint32_t* value_off, uint32_t* value_len, uint8_t* fflags, uint32_t* nfields, int32_t* bstatus,
+                 hhuff_request_t* req, void* scratch, uint64_t scratch_size, unsigned flags, void* stream) {
     if (nconn == 0) return HHUFF_OK;
     if (!in || !blk_off || !conn_first || !arena || !arena_off || !name_off || !name_len || !value_off || !value_len ||
         !fflags || !nfields || !bstatus || !scratch)
         return arg_fail("NULL array");
     if (scratch_size < hhuff_hpack_scratch_size(nconn, table_size)) return arg_fail("scratch smaller than hhuff_hpack_scratch_size");
     if (((uintptr_t)scratch & 15u) != 0) return arg_fail("scratch must be 16-byte aligned");
+    if (((uintptr_t)req & 7u) != 0) return arg_fail("req must be 8-byte aligned");
     hipError_t e = hhuff::launch_hpack_blocks(in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off,
-                                              name_len, value_off, value_len, fflags, nfields, bstatus,
+                                              name_len, value_off, value_len, fflags, nfields, bstatus, req,
                                               (uint8_t*)scratch, flags, (hipStream_t)stream);
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "hpack block launch");
+}
+}  // namespace
+
+HHUFF_API int hhuff_hpack_decode_blocks(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off,
+                                        const uint32_t* conn_first, uint32_t nconn, uint32_t table_size, uint8_t* arena,
+                                        const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len,
+                                        uint32_t* value_off, uint32_t* value_len, uint8_t* fflags, uint32_t* nfields,
+                                        int32_t* bstatus, void* scratch, uint64_t scratch_size, unsigned flags,
+                                        void* stream) {
+    return hpack_blocks(in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len,
+                        value_off, value_len, fflags, nfields, bstatus, nullptr, scratch, scratch_size, flags, stream);
+}
+
+HHUFF_API int hhuff_hpack_parse_requests(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off,
+                                         const uint32_t* conn_first, uint32_t nconn, uint32_t table_size, uint8_t* arena,
+                                         const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len,
+                                         uint32_t* value_off, uint32_t* value_len, uint8_t* fflags, uint32_t* nfields,
+                                         int32_t* bstatus, hhuff_request_t* req, void* scratch, uint64_t scratch_size,
+                                         unsigned flags, void* stream) {
+    if (nconn != 0 && !req) return arg_fail("NULL array");
+    return hpack_blocks(in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len,
+                        value_off, value_len, fflags, nfields, bstatus, req, scratch, scratch_size, flags, stream);
 }
 
 HHUFF_API uint64_t hhuff_qpack_scratch_size(uint32_t nconn, uint32_t header_table_size) {
@@ -636,6 +658,12 @@ hipError_t read_prof(unsigned long long* out16, bool reset);
 }
 HHUFF_API int hhuff_debug_prof(unsigned long long* out16, int reset) {
     return hhuff::read_prof(out16, reset != 0) == hipSuccess ? 0 : -1;
+}
+namespace hhuff {
+hipError_t read_bprof(unsigned long long* out8, bool reset);
+}
+HHUFF_API int hhuff_debug_prof_blocks(unsigned long long* out8, int reset) {
+    return hhuff::read_bprof(out8, reset != 0) == hipSuccess ? 0 : -1;
 }
 #endif
 HHUFF_API const char* hhuff_version(void) { return "hhuff 0.1.0 (gfx950)"; }

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "hhuff.h"
+
 namespace hhuff {
 hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
                          const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
@@ -36,8 +38,8 @@ uint64_t hpack_conn_scratch(uint32_t table_size);
 hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off, const uint32_t* conn_first,
                                uint32_t nconn, uint32_t table_size, uint8_t* arena, const uint64_t* arena_off,
                                uint32_t* name_off, uint32_t* name_len, uint32_t* value_off, uint32_t* value_len,
-                               uint8_t* fflags, uint32_t* nfields, int32_t* bstatus, uint8_t* scratch, uint32_t flags,
-                               hipStream_t stream);
+                               uint8_t* fflags, uint32_t* nfields, int32_t* bstatus, hhuff_request_t* req,
+                               uint8_t* scratch, uint32_t flags, hipStream_t stream);
 // QPACK decoder (f4): see include/hhuff.h hhuff_qpack_decode; scratch = nconn x
 // qpack_conn_scratch(header_table_size) bytes of device memory
 uint64_t qpack_conn_scratch(uint32_t header_table_size);

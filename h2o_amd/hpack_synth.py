@@ -129,6 +129,59 @@ def _request(rng, V, host):
     return f
 
 
+def _request_rules(rng, f):
+    """one of h2o_hpack_parse_request's cases (hpack.c:502-637) applied to a request's field list"""
+    kind = int(rng.integers(17))
+    reg = [(b"x-h%d" % i, b"v%d" % i) for i in range(int(rng.integers(1, 4)))]
+    if kind == 0:  # duplicate pseudo-header
+        k = int(rng.integers(4))
+        f.insert(k + 1, f[k])
+    elif kind == 1:  # pseudo-header after a regular field
+        f.append([(b":path", b"/late"), (b":method", b"GET"), (b":authority", b"x.example")][int(rng.integers(3))])
+    elif kind == 2:  # empty :path
+        f[3] = (b":path", b"")
+    elif kind == 3:  # unknown / response pseudo-headers
+        f.insert(int(rng.integers(4)), [(b":status", b"200"), (b":foo", b"bar"), (b":", b"x")][int(rng.integers(3))])
+    elif kind == 4:  # :protocol once (extended CONNECT) or twice
+        f.insert(1, (b":protocol", b"websocket"))
+        if rng.random() < 0.5:
+            f.insert(2, (b":protocol", b"websocket"))
+    elif kind == 5:  # content-length, valid or not (h2o_strtosize)
+        v = [b"0", b"123", b"9999999999999999999", b"10000000000000000000", b"", b"12a", b"-1", b" 5", b"1" * 20,
+             b"007"][int(rng.integers(10))]
+        f.append((b"content-length", v))
+        if rng.random() < 0.2:
+            f.append((b"content-length", b"42"))
+    elif kind == 6:  # connection-specific fields
+        f.append(([(b"connection", b"keep-alive"), (b"transfer-encoding", b"chunked"), (b"upgrade", b"h2c"),
+                   (b"http2-settings", b"AAMAAABkAAQAAP__")][int(rng.integers(4))]))
+    elif kind == 7:  # te
+        f.append((b"te", [b"trailers", b"Trailers", b"TRAILERS", b"gzip", b"trailers, gzip"][int(rng.integers(5))]))
+    elif kind == 8:  # host, with or without :authority
+        if rng.random() < 0.5:
+            del f[2]
+        f.append((b"host", b"h.example"))
+    elif kind == 9:  # expect, once or twice
+        f.append((b"expect", b"100-continue"))
+        if rng.random() < 0.4:
+            f.append((b"expect", b"other"))
+    elif kind == 10:  # datagram-flow-id (dropped for HTTP/2), cache-digest (listed)
+        f.append([(b"datagram-flow-id", b"4"), (b"cache-digest", b"AfdA; complete")][int(rng.integers(2))])
+    elif kind == 11:  # past H2O_MAX_HEADERS (100): the rest is dropped, the block ends soft
+        f += [(b"x-n%d" % (i % 7), b"%d" % i) for i in range(int(rng.integers(95, 130)))]
+    elif kind == 12:  # past H2O_HPACK_MAX_HEADERS_HARD_LIMIT (1000)
+        f += [(b"accept-encoding", b"gzip, deflate")] * int(rng.integers(990, 1010))
+    elif kind == 13:  # :scheme variants
+        f[1] = (b":scheme", [b"http", b"masque", b"ftp", b"HTTPS", b""][int(rng.integers(5))])
+    elif kind == 14:  # fields h2o lists even though other servers treat them as hop-by-hop
+        f.append([(b"keep-alive", b"timeout=5"), (b"proxy-connection", b"keep-alive")][int(rng.integers(2))])
+    elif kind == 15:  # regular fields between pseudo-headers, a CONNECT without :path
+        f.insert(2, reg[0])
+    else:  # only pseudo-headers / only regular fields
+        f = f[:4] if rng.random() < 0.5 else f[4:]
+    return f
+
+
 def encode_block(rng, table, fields, max_cap, size_update=None):
     out = bytearray()
     if size_update is not None:
@@ -181,8 +234,9 @@ def _mutate(rng, blocks, max_cap):
     blocks[b] = bytes(blk)
 
 
-def make_connections(nconn, blocks_per_conn=(1, 8), seed=0, table_size=4096, adversarial_frac=0.05):
-    """-> dict(data u8[], blk_off u32[nb+1], conn_first u32[nconn+1], table_size)"""
+def make_connections(nconn, blocks_per_conn=(1, 8), seed=0, table_size=4096, adversarial_frac=0.05, request_frac=0.0):
+    """-> dict(data u8[], blk_off u32[nb+1], conn_first u32[nconn+1], table_size); request_frac of the requests
+    exercise one of h2o_hpack_parse_request's rules (_request_rules)"""
     rng = np.random.default_rng(seed)
     V = _vocab(rng)
     hosts = V[0]
@@ -196,7 +250,10 @@ def make_connections(nconn, blocks_per_conn=(1, 8), seed=0, table_size=4096, adv
             su = None
             if rng.random() < 0.05:
                 su = int(rng.integers(0, table_size + 1))
-            cb.append(encode_block(rng, table, _request(rng, V, host), table_size, su))
+            f = _request(rng, V, host)
+            if request_frac and rng.random() < request_frac:
+                f = _request_rules(rng, f)
+            cb.append(encode_block(rng, table, f, table_size, su))
         if rng.random() < adversarial_frac:
             _mutate(rng, cb, table_size)
         blocks += cb

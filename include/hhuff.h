@@ -195,6 +195,49 @@ int hhuff_hpack_decode_blocks(const uint8_t *in, uint64_t in_size, const uint32_
                               uint8_t *fflags, uint32_t *nfields, int32_t *bstatus, void *scratch, uint64_t scratch_size,
                               unsigned flags, void *stream);
 
+/* (2c') HTTP/2 request header blocks: the same pass with h2o_hpack_parse_request's own rules applied to each
+ *      field as it is decoded (lib/http2/hpack.c:502-637), called as h2o's HTTP/2 server calls it
+ *      (lib/http2/connection.c:626-629: every out-pointer given, cache digests loaded, no datagram flow id):
+ *        - more than H2O_HPACK_MAX_HEADERS_HARD_LIMIT (1000) fields -> COMPRESSION (:528-532)
+ *        - pseudo-headers (:533-586): only before the first regular field; :authority, :method, :path,
+ *          :scheme at most once, :path not empty, :protocol at most once; any other ':' name -> PROTOCOL
+ *        - content-length must parse (h2o_strtosize) -> else PROTOCOL (:591-597); expect, host (fills a
+ *          missing authority) and datagram-flow-id are taken out of the list; te other than "trailers"
+ *          (case-insensitive) and connection / http2-settings / transfer-encoding / upgrade -> PROTOCOL
+ *          (:587-619)
+ *        - the first H2O_MAX_HEADERS (100) remaining fields go to the request's header list; beyond that
+ *          they are dropped and the block ends with H2O_HTTP2_ERROR_INVALID_HEADER_CHAR (:620-637)
+ *      Outputs as hhuff_hpack_decode_blocks plus, per block, req[b]; per field, fflags gains
+ *      HHUFF_FIELD_HEADER when h2o_add_header took the field.  bstatus[b] is h2o_hpack_parse_request's
+ *      return value: 0, -254 (H2O_HTTP2_ERROR_INVALID_HEADER_CHAR: a soft error, the connection lives on),
+ *      -1 / -9 (connection errors: later blocks of the connection are HHUFF_BLK_SKIPPED), or the
+ *      HHUFF_BLK_* codes.  The field that triggered an error is counted in nfields (it was decoded and,
+ *      for incremental indexing, entered the table).  The cache-digest field goes to the header list (h2o
+ *      also feeds it to h2o_cache_digests_load_header; that side effect is the caller's). */
+#define HHUFF_FIELD_HEADER 0x4u /* fflags: the field is in h2o's h2o_headers_t (h2o_add_header) */
+#define HHUFF_HERR_NONE 0u               /* *err_desc == NULL */
+#define HHUFF_HERR_SOFT_NAME 1u          /* h2o_hpack_soft_err_found_invalid_char_in_header_name */
+#define HHUFF_HERR_SOFT_VALUE 2u         /* h2o_hpack_soft_err_found_invalid_char_in_header_value */
+#define HHUFF_HERR_HEADERS_TOO_LONG 3u   /* h2o_hpack_err_headers_too_long */
+#define HHUFF_HERR_INVALID_PSEUDO 4u     /* h2o_hpack_err_invalid_pseudo_header */
+#define HHUFF_HERR_CONTENT_LENGTH 5u     /* h2o_hpack_err_invalid_content_length_header */
+#define HHUFF_HERR_CONNECTION_SPECIFIC 6u /* h2o_hpack_err_unexpected_connection_specific_header */
+#define HHUFF_HERR_UPPER_CASE_NAME 7u    /* h2o_hpack_err_found_upper_case_in_header_name */
+typedef struct hhuff_request {
+    uint64_t content_length; /* h2o's *content_length: SIZE_MAX (all ones) without a content-length field */
+    int32_t method, scheme, authority, path, protocol, expect; /* the field (0-based within the block) whose
+                                value h2o stored in *method ... *expect, or -1; authority may be a host field */
+    uint32_t exists_map;  /* *pseudo_header_exists_map: H2O_HPACK_PARSE_HEADERS_*_EXISTS (hpack.h:81-85) */
+    uint32_t nheaders;    /* fields added to the header list */
+    uint32_t err;         /* HHUFF_HERR_*: what *err_desc points at when the call returns */
+    uint32_t scheme_kind; /* *scheme: 0 unset, 1 H2O_URL_SCHEME_HTTP, 2 _HTTPS, 3 _MASQUE */
+} hhuff_request_t;        /* 48 bytes */
+int hhuff_hpack_parse_requests(const uint8_t *in, uint64_t in_size, const uint32_t *blk_off, const uint32_t *conn_first,
+                               uint32_t nconn, uint32_t table_size, uint8_t *arena, const uint64_t *arena_off,
+                               uint32_t *name_off, uint32_t *name_len, uint32_t *value_off, uint32_t *value_len,
+                               uint8_t *fflags, uint32_t *nfields, int32_t *bstatus, hhuff_request_t *req,
+                               void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
+
 /* (2d) QPACK decoder (QPACK half): h2o's QPACK decoder (lib/http3/qpack.c) for many
  *      connections at once.  One call is one step of every connection c:
  *        encoder stream  in[enc_off[c] .. + enc_len[c]): h2o_qpack_decoder_handle_input (qpack.c:420-485,

@@ -495,7 +495,7 @@ def soft_code(bits):
     return np.where(bits & 1, 1, np.where(bits & 2, 2, 0)).astype(np.uint8)
 
 
-def blocks_set(conns, table_size):
+def blocks_set(conns, table_size, requests=False):
     from h2o_amd import hpack_synth as HS
 
     b = HS.pack_connections(conns, table_size)
@@ -510,9 +510,28 @@ def blocks_set(conns, table_size):
             soft.append(r["fflags"][f])
     nd, no = pack(names)
     vd, vo = pack(values)
-    return dict(data=b["data"], blk_off=b["blk_off"], conn_first=b["conn_first"],
-                table_size=np.asarray([table_size], np.uint32), nfields=r["nfields"][:nb], bstatus=r["bstatus"][:nb],
-                fld_name=nd, fld_name_off=no, fld_value=vd, fld_value_off=vo, fld_soft=np.asarray(soft, np.uint8))
+    out = dict(data=b["data"], blk_off=b["blk_off"], conn_first=b["conn_first"],
+               table_size=np.asarray([table_size], np.uint32), nfields=r["nfields"][:nb], bstatus=r["bstatus"][:nb],
+               fld_name=nd, fld_name_off=no, fld_value=vd, fld_value_off=vo, fld_soft=np.asarray(soft, np.uint8))
+    if requests:
+        # h2o_hpack_parse_request over the same blocks (ref_hpack_parse_requests): its verdicts, the request
+        # record of every block and each decoded field's flags (soft bits | HHUFF_FIELD_HEADER).  Its fields
+        # are a prefix of the decode-only fields of the same block (the same decoder, stopped earlier), which
+        # is checked here so the fixture need not repeat them.
+        q = O.ref().hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], table_size, requests=True)
+        fl = []
+        for bi in range(nb):
+            s0, k = int(b["blk_off"][bi]), int(q["nfields"][bi])
+            assert k <= int(r["nfields"][bi]) or int(r["bstatus"][bi]) != 0
+            for f in range(s0, s0 + k):
+                assert q["arena"][q["name_off"][f]:q["name_off"][f] + q["name_len"][f]].tobytes() == \
+                    r["arena"][r["name_off"][f]:r["name_off"][f] + r["name_len"][f]].tobytes()
+                assert q["arena"][q["value_off"][f]:q["value_off"][f] + q["value_len"][f]].tobytes() == \
+                    r["arena"][r["value_off"][f]:r["value_off"][f] + r["value_len"][f]].tobytes()
+                fl.append(q["fflags"][f])
+        out.update(rq_nfields=q["nfields"][:nb], rq_bstatus=q["bstatus"][:nb],
+                   rq_req=q["req"][:nb].view(np.uint32).reshape(nb, 12), rq_fflags=np.asarray(fl, np.uint8))
+    return out
 
 
 def blocks_sets():
@@ -532,7 +551,10 @@ def blocks_sets():
     s256_conns = [[s256["data"][s256["blk_off"][k]:s256["blk_off"][k + 1]].tobytes()
                    for k in range(s256["conn_first"][c], s256["conn_first"][c + 1])]
                   for c in range(len(s256["conn_first"]) - 1)]
-    out = {"blocks": blocks_set(UNIT_REQUESTS + static_sweep + corpus + syn_conns, 4096),
+    rq = HS.make_connections(1500, seed=23, adversarial_frac=0.05, request_frac=0.12)
+    rq_conns = [[rq["data"][rq["blk_off"][k]:rq["blk_off"][k + 1]].tobytes()
+                 for k in range(rq["conn_first"][c], rq["conn_first"][c + 1])] for c in range(len(rq["conn_first"]) - 1)]
+    out = {"blocks": blocks_set(UNIT_REQUESTS + static_sweep + corpus + syn_conns + rq_conns, 4096, requests=True),
            "blocks_256": blocks_set(UNIT_RESPONSES_256 + s256_conns, 256)}
     for k, v in out.items():
         print("%-12s connections %5d  blocks %6d  fields %7d  errors %d" % (

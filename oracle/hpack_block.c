@@ -9,6 +9,7 @@
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
+#include <strings.h>
 
 #include "huff_oracle.h"
 #include "huff_tables.h"
@@ -210,6 +211,153 @@ static int orc_block_field(orc_table_t *t, const uint8_t **src, const uint8_t *e
     return soft ? ORC_ERR_INVALID_CHAR : 0;
 }
 
+/* ---- h2o_hpack_parse_request (hpack.c:502-637) as h2o's HTTP/2 server calls it (connection.c:626-629) ----
+ * The request record is include/hhuff.h hhuff_request_t, 12 u32 words: [0..1] content_length, [2..7]
+ * method, scheme, authority, path, protocol, expect (field index or -1), [8] exists map, [9] nheaders,
+ * [10] err (HHUFF_HERR_*), [11] scheme kind. */
+enum {
+    RQ_REGULAR, RQ_AUTHORITY, RQ_METHOD, RQ_PATH, RQ_PROTOCOL, RQ_SCHEME, RQ_CONTENT_LENGTH, RQ_EXPECT, RQ_HOST, RQ_TE,
+    RQ_CACHE_DIGEST, RQ_DATAGRAM_FLOW_ID, RQ_REJECT
+};
+/* the tokens parse_request tells apart: the pseudo-header tokens and the is_hpack_special ones
+ * (lib/common/token_table.h, 5th flag) */
+static const struct {
+    const char *name;
+    int kind;
+} rq_tokens[] = {{":authority", RQ_AUTHORITY}, {":method", RQ_METHOD}, {":path", RQ_PATH}, {":protocol", RQ_PROTOCOL},
+                 {":scheme", RQ_SCHEME}, {"cache-digest", RQ_CACHE_DIGEST}, {"connection", RQ_REJECT},
+                 {"content-length", RQ_CONTENT_LENGTH}, {"datagram-flow-id", RQ_DATAGRAM_FLOW_ID},
+                 {"expect", RQ_EXPECT}, {"host", RQ_HOST}, {"http2-settings", RQ_REJECT}, {"te", RQ_TE},
+                 {"transfer-encoding", RQ_REJECT}, {"upgrade", RQ_REJECT}};
+
+static int rq_kind(const uint8_t *s, uint32_t n)
+{
+    for (size_t i = 0; i < sizeof(rq_tokens) / sizeof(rq_tokens[0]); ++i)
+        if (strlen(rq_tokens[i].name) == n && memcmp(rq_tokens[i].name, s, n) == 0)
+            return rq_tokens[i].kind;
+    return RQ_REGULAR;
+}
+
+/* h2o_strtosize (lib/common/string.c:86-113) */
+static uint64_t rq_strtosize(const uint8_t *s, uint32_t n)
+{
+    uint64_t v = 0, m = 1;
+    if (n == 0)
+        return UINT64_MAX;
+    for (uint32_t i = n; i-- > 0;) {
+        if (s[i] < '0' || s[i] > '9')
+            return UINT64_MAX;
+        v += (uint64_t)(s[i] - '0') * m;
+        if (i == 0)
+            break;
+        m *= 10;
+        if (m == 10000000000000000000ull)
+            return UINT64_MAX;
+    }
+    return v;
+}
+
+typedef struct {
+    uint64_t content_length;
+    int32_t slot[6]; /* method, scheme, authority, path, protocol, expect */
+    uint32_t map, nheaders, err, scheme_kind, ndecoded;
+    int pseudo_ok;
+} orc_req_t;
+
+static void rq_init(orc_req_t *r)
+{
+    memset(r, 0, sizeof(*r));
+    r->content_length = UINT64_MAX;
+    for (int i = 0; i < 6; ++i)
+        r->slot[i] = -1;
+    r->pseudo_ok = 1;
+}
+
+static void rq_store(uint32_t *w, const orc_req_t *r)
+{
+    memcpy(w, &r->content_length, 8);
+    memcpy(w + 2, r->slot, 24);
+    w[8] = r->map, w[9] = r->nheaders, w[10] = r->err, w[11] = r->scheme_kind;
+}
+
+/* field k decoded with soft bits `soft`: 0, or the hard error; *header = h2o_add_header took it */
+static int rq_field(orc_req_t *r, const uint8_t *name, uint32_t nl, const uint8_t *value, uint32_t vl, unsigned soft,
+                    int32_t k, int *header)
+{
+    enum { M = 0, S = 1, A = 2, P = 3, PR = 4, E = 5 };
+    *header = 0;
+    if (soft && r->err == 0)
+        r->err = (soft & ORC_SOFT_NAME) ? 1 : 2;
+    if (++r->ndecoded > 1000) { /* H2O_HPACK_MAX_HEADERS_HARD_LIMIT */
+        r->err = 3;
+        return ORC_ERR_COMPRESSION;
+    }
+    int kind = rq_kind(name, nl);
+    if (nl > 0 && name[0] == ':') {
+        if (!r->pseudo_ok) {
+            r->err = 4;
+            return ORC_ERR_PROTOCOL;
+        }
+        int which, bit;
+        switch (kind) {
+        case RQ_AUTHORITY: which = A, bit = 8; break;
+        case RQ_METHOD: which = M, bit = 1; break;
+        case RQ_PATH: which = P, bit = 4; break;
+        case RQ_SCHEME: which = S, bit = 2; break;
+        case RQ_PROTOCOL:
+            if (r->slot[PR] >= 0)
+                return ORC_ERR_PROTOCOL; /* no err_desc */
+            r->slot[PR] = k, r->map |= 16;
+            return 0;
+        default:
+            return ORC_ERR_PROTOCOL; /* unknown pseudo-header: no err_desc */
+        }
+        if (r->slot[which] >= 0 || (which == P && vl == 0)) {
+            r->err = 4;
+            return ORC_ERR_PROTOCOL;
+        }
+        r->slot[which] = k, r->map |= (uint32_t)bit;
+        if (which == S)
+            r->scheme_kind = (vl == 5 && memcmp(value, "https", 5) == 0) ? 2 : (vl == 6 && memcmp(value, "masque", 6) == 0) ? 3 : 1;
+        return 0;
+    }
+    r->pseudo_ok = 0;
+    switch (kind) {
+    case RQ_CONTENT_LENGTH:
+        if ((r->content_length = rq_strtosize(value, vl)) == UINT64_MAX) {
+            r->err = 5;
+            return ORC_ERR_PROTOCOL;
+        }
+        return 0;
+    case RQ_EXPECT:
+        r->slot[E] = k;
+        return 0;
+    case RQ_HOST:
+        if (r->slot[A] < 0)
+            r->slot[A] = k;
+        return 0;
+    case RQ_DATAGRAM_FLOW_ID:
+        return 0;
+    case RQ_TE:
+        if (vl == 8 && strncasecmp((const char *)value, "trailers", 8) == 0)
+            break;
+        r->err = 6;
+        return ORC_ERR_PROTOCOL;
+    case RQ_REJECT:
+        r->err = 6;
+        return ORC_ERR_PROTOCOL;
+    default:
+        break;
+    }
+    if (r->nheaders < 100) { /* H2O_MAX_HEADERS */
+        ++r->nheaders;
+        *header = 1;
+    } else if (r->err == 0) {
+        r->err = 3;
+    }
+    return 0;
+}
+
 typedef struct {
     const uint8_t *in;
     const uint32_t *blk_off, *conn_first;
@@ -219,6 +367,7 @@ typedef struct {
     uint32_t *name_off, *name_len, *value_off, *value_len, *nfields;
     uint8_t *fflags;
     int32_t *bstatus;
+    uint32_t *req; /* request mode: 12 words per block, else NULL */
 } orc_blk_job_t;
 
 static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
@@ -226,9 +375,13 @@ static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
     orc_table_t t = {NULL, 0, 0, 0, j->table_size, j->table_size};
     int failed = 0;
     for (uint32_t b = j->conn_first[c]; b < j->conn_first[c + 1]; ++b) {
+        orc_req_t rq;
+        rq_init(&rq);
         j->nfields[b] = 0;
         if (failed) {
             j->bstatus[b] = ORC_BLK_SKIPPED;
+            if (j->req)
+                rq_store(j->req + 12 * (size_t)b, &rq);
             continue;
         }
         const uint8_t *p = j->in + j->blk_off[b], *end = j->in + j->blk_off[b + 1];
@@ -242,18 +395,31 @@ static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
             int rc = orc_block_field(&t, &p, end, &A, &no, &nl, &vo, &vl, &soft);
             if (rc != 0 && rc != ORC_ERR_INVALID_CHAR) {
                 st = rc;
+                rq.err = rc == ORC_ERR_PROTOCOL ? 7 : 0; /* *err_desc = decode_err (hpack.c:523-525) */
                 break;
             }
+            int header = 0, rr = 0;
+            if (j->req)
+                rr = rq_field(&rq, j->arena + no, nl, j->arena + vo, vl, soft, (int32_t)nf, &header);
             j->name_off[slot + nf] = no;
             j->name_len[slot + nf] = nl;
             j->value_off[slot + nf] = vo;
             j->value_len[slot + nf] = vl;
-            j->fflags[slot + nf] = (uint8_t)soft;
+            j->fflags[slot + nf] = (uint8_t)(soft | (header ? 4u : 0u));
             ++nf;
+            if (rr != 0) {
+                st = rr;
+                break;
+            }
+        }
+        if (j->req) {
+            if (st == 0 && rq.err != 0)
+                st = ORC_ERR_INVALID_CHAR; /* hpack.c:636-637 */
+            rq_store(j->req + 12 * (size_t)b, &rq);
         }
         j->nfields[b] = nf;
         j->bstatus[b] = st;
-        failed = st != 0;
+        failed = st != 0 && st != ORC_ERR_INVALID_CHAR;
     }
     tbl_free(&t);
 }
@@ -266,10 +432,10 @@ static void *orc_blk_worker(void *arg)
     return NULL;
 }
 
-int orc_hpack_decode_blocks(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
+static int orc_hpack_blocks(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
                             uint32_t table_size, uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off,
                             uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,
-                            uint32_t *nfields, int32_t *bstatus, int nthreads)
+                            uint32_t *nfields, int32_t *bstatus, uint32_t *req, int nthreads)
 {
     if (nthreads < 1)
         nthreads = 1;
@@ -287,7 +453,7 @@ int orc_hpack_decode_blocks(const uint8_t *in, const uint32_t *blk_off, const ui
         j->in = in, j->blk_off = blk_off, j->conn_first = conn_first, j->table_size = table_size;
         j->arena = arena, j->arena_off = arena_off, j->name_off = name_off, j->name_len = name_len;
         j->value_off = value_off, j->value_len = value_len, j->fflags = fflags, j->nfields = nfields;
-        j->bstatus = bstatus;
+        j->bstatus = bstatus, j->req = req;
         j->c_begin = (uint32_t)(((uint64_t)nconn * k) / nthreads);
         j->c_end = (uint32_t)(((uint64_t)nconn * (k + 1)) / nthreads);
     }
@@ -299,4 +465,22 @@ int orc_hpack_decode_blocks(const uint8_t *in, const uint32_t *blk_off, const ui
     free(jobs);
     free(th);
     return 0;
+}
+
+int orc_hpack_decode_blocks(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
+                            uint32_t table_size, uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off,
+                            uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,
+                            uint32_t *nfields, int32_t *bstatus, int nthreads)
+{
+    return orc_hpack_blocks(in, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len, value_off,
+                            value_len, fflags, nfields, bstatus, NULL, nthreads);
+}
+
+int orc_hpack_parse_requests(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
+                             uint32_t table_size, uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off,
+                             uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,
+                             uint32_t *nfields, int32_t *bstatus, uint32_t *req, int nthreads)
+{
+    return orc_hpack_blocks(in, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len, value_off,
+                            value_len, fflags, nfields, bstatus, req, nthreads);
 }

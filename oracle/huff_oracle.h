@@ -66,3 +66,9 @@ int orc_hpack_decode_blocks(const uint8_t *in, const uint32_t *blk_off, const ui
                             uint32_t table_size, uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off,
                             uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,
                             uint32_t *nfields, int32_t *bstatus, int nthreads);
+/* the same with h2o_hpack_parse_request's rules (hpack.c:502-637); req: 12 u32 words per block
+ * (include/hhuff.h hhuff_request_t) */
+int orc_hpack_parse_requests(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
+                             uint32_t table_size, uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off,
+                             uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,
+                             uint32_t *nfields, int32_t *bstatus, uint32_t *req, int nthreads);

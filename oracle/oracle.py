@@ -16,6 +16,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 FAIL = 0xFFFFFFFF
 STATUS_FAIL = 0x80
 
+# include/hhuff.h hhuff_request_t (48 bytes)
+REQ_DTYPE = np.dtype([("content_length", "<u8"), ("method", "<i4"), ("scheme", "<i4"), ("authority", "<i4"),
+                      ("path", "<i4"), ("protocol", "<i4"), ("expect", "<i4"), ("exists_map", "<u4"),
+                      ("nheaders", "<u4"), ("err", "<u4"), ("scheme_kind", "<u4")])
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 
@@ -69,6 +73,10 @@ class _Codec:
         f.restype = ctypes.c_int
         f.argtypes = [_u8p, _u32p, _u32p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.POINTER(ctypes.c_uint64),
                       _u32p, _u32p, _u32p, _u32p, _u8p, _u32p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int]
+        f = getattr(L, P + "_hpack_parse_requests")
+        f.restype = ctypes.c_int
+        f.argtypes = [_u8p, _u32p, _u32p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.POINTER(ctypes.c_uint64),
+                      _u32p, _u32p, _u32p, _u32p, _u8p, _u32p, ctypes.POINTER(ctypes.c_int32), _u32p, ctypes.c_int]
         f = getattr(L, P + "_literals_batch")
         f.restype = ctypes.c_int
         f.argtypes = [_u8p, _u32p, _u32p, ctypes.c_uint32, ctypes.c_uint, ctypes.c_uint, _u32p, _u8p, _u32p, _u32p,
@@ -176,9 +184,11 @@ class _Codec:
         return out, out_len, pay_off, consumed, status
 
 
-    def hpack_decode_blocks(self, data, blk_off, conn_first, table_size=4096, arena_off=None, nthreads=1):
+    def hpack_decode_blocks(self, data, blk_off, conn_first, table_size=4096, arena_off=None, nthreads=1,
+                            requests=False):
         """HPACK header blocks (include/hhuff.h hhuff_hpack_decode_blocks contract) -> dict of arrays:
-        arena, name_off, name_len, value_off, value_len, fflags (per field slot), nfields, bstatus (per block)"""
+        arena, name_off, name_len, value_off, value_len, fflags (per field slot), nfields, bstatus (per block);
+        requests=True: hhuff_hpack_parse_requests (h2o_hpack_parse_request per block), plus req (REQ_DTYPE)"""
         data = np.ascontiguousarray(data, dtype=np.uint8)
         blk_off = np.ascontiguousarray(blk_off, dtype=np.uint32)
         conn_first = np.ascontiguousarray(conn_first, dtype=np.uint32)
@@ -192,12 +202,17 @@ class _Codec:
                  value_off=np.zeros(nslots, np.uint32), value_len=np.zeros(nslots, np.uint32),
                  fflags=np.zeros(nslots, np.uint8), nfields=np.zeros(max(1, nb), np.uint32),
                  bstatus=np.zeros(max(1, nb), np.int32))
-        rc = getattr(self.lib, self.prefix + "_hpack_decode_blocks")(
-            _ptr(data, _u8p), _ptr(blk_off, _u32p), _ptr(conn_first, _u32p), conn_first.size - 1, table_size,
-            _ptr(r["arena"], _u8p), arena_off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
-            _ptr(r["name_off"], _u32p), _ptr(r["name_len"], _u32p), _ptr(r["value_off"], _u32p),
-            _ptr(r["value_len"], _u32p), _ptr(r["fflags"], _u8p), _ptr(r["nfields"], _u32p),
-            r["bstatus"].ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), nthreads)
+        args = [_ptr(data, _u8p), _ptr(blk_off, _u32p), _ptr(conn_first, _u32p), conn_first.size - 1, table_size,
+                _ptr(r["arena"], _u8p), arena_off.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                _ptr(r["name_off"], _u32p), _ptr(r["name_len"], _u32p), _ptr(r["value_off"], _u32p),
+                _ptr(r["value_len"], _u32p), _ptr(r["fflags"], _u8p), _ptr(r["nfields"], _u32p),
+                r["bstatus"].ctypes.data_as(ctypes.POINTER(ctypes.c_int32))]
+        if requests:
+            words = np.zeros((max(1, nb), 12), np.uint32)
+            rc = getattr(self.lib, self.prefix + "_hpack_parse_requests")(*args, _ptr(words, _u32p), nthreads)
+            r["req"] = words.view(REQ_DTYPE).reshape(-1)
+        else:
+            rc = getattr(self.lib, self.prefix + "_hpack_decode_blocks")(*args, nthreads)
         assert rc == 0
         return r
 

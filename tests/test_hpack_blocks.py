@@ -59,6 +59,85 @@ def test_restatement_matches_reference_fixtures(oracle_codec, name):
     check_against_golden(res, g)
 
 
+# ---- h2o_hpack_parse_request (hhuff_hpack_parse_requests) ----
+W_SLOTS = slice(2, 8)  # method, scheme, authority, path, protocol, expect: field indices within the block
+W_EXPECT = 7
+
+
+def req_words(res, nblk):
+    return np.ascontiguousarray(res["req"][:nblk]).view(np.uint32).reshape(nblk, 12)
+
+
+def check_requests_against_golden(res, g):
+    """verdicts, request records and field flags of h2o_hpack_parse_request (blocks.npz rq_*); the fields
+    themselves are a prefix of the decode-only fixture fields of the same block"""
+    nblk = len(g["blk_off"]) - 1
+    np.testing.assert_array_equal(np.asarray(res["nfields"][:nblk], np.uint32), g["rq_nfields"])
+    np.testing.assert_array_equal(np.asarray(res["bstatus"][:nblk], np.int32), g["rq_bstatus"])
+    got, exp = req_words(res, nblk), g["rq_req"]
+    # everything but `expect` word for word; expect (the last one wins in h2o) by the bytes it points at
+    keep = np.ones(12, bool)
+    keep[W_EXPECT] = False
+    np.testing.assert_array_equal(got[:, keep], exp[:, keep])
+    en, ev, _ = expected_fields(g)
+    first = np.concatenate([[0], np.cumsum(g["nfields"])])
+    a = res["arena"]
+    flags = []
+    for b in range(nblk):
+        s0, k = int(g["blk_off"][b]), int(g["rq_nfields"][b])
+        for f in range(k):
+            gi = int(first[b]) + f
+            no, nl, vo, vl = (int(res[x][s0 + f]) for x in ("name_off", "name_len", "value_off", "value_len"))
+            assert a[no:no + nl].tobytes() == en[gi] and a[vo:vo + vl].tobytes() == ev[gi], (b, f)
+            flags.append(int(res["fflags"][s0 + f]))
+        ge, ee = int(got[b, W_EXPECT].view(np.int32)), int(exp[b, W_EXPECT].view(np.int32))
+        assert (ge < 0) == (ee < 0), b
+        if ge >= 0:
+            assert ev[int(first[b]) + ge] == ev[int(first[b]) + ee], b
+    fl = np.asarray(flags, np.uint8)
+    np.testing.assert_array_equal(fl & 4, g["rq_fflags"] & 4)  # HHUFF_FIELD_HEADER
+    np.testing.assert_array_equal(soft_code(fl & 3), soft_code(g["rq_fflags"] & 3))
+
+
+def test_restatement_matches_reference_request_verdicts(oracle_codec):
+    g = load_golden("blocks")
+    res = oracle_codec.hpack_decode_blocks(g["data"], g["blk_off"], g["conn_first"], int(g["table_size"][0]),
+                                           nthreads=8, requests=True)
+    check_requests_against_golden(res, g)
+
+
+def test_request_fixtures_cover_the_rules():
+    g = load_golden("blocks")
+    w = g["rq_req"]
+    st = set(int(x) for x in g["rq_bstatus"])
+    assert {0, -254, -1, -9, -301} <= st
+    assert set(range(8)) <= set(int(x) for x in w[:, 10])  # every HHUFF_HERR_* (err_desc) value
+    assert {0, 1, 2, 3} <= set(int(x) for x in w[:, 11])  # scheme unset / http / https / masque
+    cl = w[:, 0].astype(np.uint64) | (w[:, 1].astype(np.uint64) << np.uint64(32))
+    assert (cl != np.uint64(2 ** 64 - 1)).sum() > 10 and (cl == np.uint64(9999999999999999999)).any()
+    assert (w[:, 9] == 100).any() and (w[:, 8] & 16).any()  # header-list limit reached; :protocol seen
+    assert (w[:, W_EXPECT].view(np.int32) >= 0).any() and (g["rq_fflags"] & 4).any()
+    assert (g["rq_nfields"] > 1000).any()
+
+
+def test_restatement_matches_compiled_reference_on_fresh_requests():
+    from oracle import oracle as O
+
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    for seed, ts in ((35, 4096), (36, 256), (37, 0)):
+        b = HS.make_connections(800, seed=seed, table_size=ts, adversarial_frac=0.1, request_frac=0.3)
+        ro = O.oracle().hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], ts, requests=True)
+        rr = O.ref().hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], ts, requests=True)
+        nblk = len(b["blk_off"]) - 1
+        np.testing.assert_array_equal(ro["nfields"][:nblk], rr["nfields"][:nblk])
+        np.testing.assert_array_equal(ro["bstatus"][:nblk], rr["bstatus"][:nblk])
+        np.testing.assert_array_equal(req_words(ro, nblk), req_words(rr, nblk))
+        for b_ in range(nblk):
+            s0, k = int(b["blk_off"][b_]), int(ro["nfields"][b_])
+            np.testing.assert_array_equal(ro["fflags"][s0:s0 + k] & 4, rr["fflags"][s0:s0 + k] & 4)
+
+
 def test_fixtures_cover_the_paths():
     g = load_golden("blocks")
     st = set(int(x) for x in g["bstatus"])
@@ -101,14 +180,14 @@ def torch_cuda():
     return torch
 
 
-def gpu_blocks(torch, data, blk_off, conn_first, table_size, arena_off=None):
+def gpu_blocks(torch, data, blk_off, conn_first, table_size, arena_off=None, requests=False):
     from h2o_amd import codec
 
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
     d = dev(data if data.size else np.zeros(1, np.uint8))
     ao = None if arena_off is None else dev(np.asarray(arena_off, np.uint64).view(np.int64))
     r = codec.hpack_decode_blocks(d, dev(blk_off.view(np.int32)), dev(conn_first.view(np.int32)), table_size,
-                                  arena_off=ao, in_size=int(data.size))
+                                  arena_off=ao, in_size=int(data.size), requests=requests)
     torch.cuda.synchronize()
     out = {}
     for k, v in r.items():
@@ -235,3 +314,26 @@ def test_gpu_tables_carry_over_between_calls(torch_cuda, oracle_codec):
             exp.setdefault(c, []).extend(zip(want[0][i:i + n], want[1][i:i + n]))
             i += n
     assert per_conn(st, got) == exp
+
+
+@pytest.mark.gpu
+def test_gpu_request_verdicts_match_reference_fixtures(torch_cuda):
+    g = load_golden("blocks")
+    res = gpu_blocks(torch_cuda, g["data"], g["blk_off"], g["conn_first"], int(g["table_size"][0]), requests=True)
+    check_requests_against_golden(res, g)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,table_size", [(45, 4096), (46, 256), (47, 0)])
+def test_gpu_request_verdicts_match_restatement(torch_cuda, oracle_codec, seed, table_size):
+    b = HS.make_connections(3000, seed=seed, table_size=table_size, adversarial_frac=0.1, request_frac=0.3)
+    ro = oracle_codec.hpack_decode_blocks(b["data"], b["blk_off"], b["conn_first"], table_size, nthreads=8,
+                                          requests=True)
+    rg = gpu_blocks(torch_cuda, b["data"], b["blk_off"], b["conn_first"], table_size, requests=True)
+    nblk = len(b["blk_off"]) - 1
+    np.testing.assert_array_equal(rg["nfields"][:nblk], ro["nfields"][:nblk])
+    np.testing.assert_array_equal(rg["bstatus"][:nblk], ro["bstatus"][:nblk])
+    np.testing.assert_array_equal(req_words(rg, nblk), req_words(ro, nblk))
+    for b_ in range(nblk):
+        s0, k = int(b["blk_off"][b_]), int(ro["nfields"][b_])
+        np.testing.assert_array_equal(rg["fflags"][s0:s0 + k], ro["fflags"][s0:s0 + k])
