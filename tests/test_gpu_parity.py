@@ -120,6 +120,45 @@ def test_random_batches_vs_oracle(torch_cuda, oracle_codec, cfg, n, seed):
     assert compact(gd[0], slots, gd[1]) == compact(od[0], slots, od[1])
 
 
+def _gather(buf, starts, lens):
+    """the bytes of every successful slot, concatenated (vectorised compact())"""
+    ok = lens != FAIL
+    st, ln = np.asarray(starts, np.int64)[ok], np.asarray(lens, np.int64)[ok]
+    idx = np.repeat(st - np.concatenate([[0], np.cumsum(ln)[:-1]]), ln) + np.arange(int(ln.sum()), dtype=np.int64)
+    return np.asarray(buf)[idx]
+
+
+@pytest.mark.parametrize("cfg", ["c2", "c3", "c5"])
+def test_full_size_vs_oracle(torch_cuda, oracle_codec, cfg):
+    """SURVEY 8d configs at their full sizes (1M / 1M / 512K strings) against the restatement, through the
+    bench's own layouts: encode to slots = in_off, then decode of the Huffman strings packed back to back
+    (region layout, deferred tile edges; for c3 the mixed-length kernel choice runs on the whole batch)."""
+    b = synth.make_batch(cfg, seed=11)
+    n = b["n"]
+    o_out, o_len, o_st = oracle_codec.encode_batch(b["data"], b["off"], n, nthreads=16)
+    g_out, g_len, g_st = gpu_encode(torch_cuda, b["data"], b["off"], n)
+    np.testing.assert_array_equal(g_len, o_len)
+    np.testing.assert_array_equal(g_st, o_st)
+    np.testing.assert_array_equal(_gather(g_out, b["off"][:n], g_len), _gather(o_out, b["off"][:n], o_len))
+    ok = o_len != FAIL
+    hl = o_len[ok].astype(np.int64)
+    h_off = np.zeros(hl.size + 1, np.int64)
+    h_off[1:] = np.cumsum(hl)
+    huff = _gather(o_out, b["off"][:n], o_len)
+    names = np.unpackbits(b["is_name_bits"].view(np.uint8), bitorder="little")[:n].astype(bool)[ok]
+    nb = np.packbits(names, bitorder="little")
+    nb = np.concatenate([nb, np.zeros((-nb.size) % 4, np.uint8)]).view(np.uint32)
+    m = int(hl.size)
+    h32 = h_off.astype(np.uint32)
+    od = oracle_codec.decode_batch(huff, h32, m, is_name_bits=nb, nthreads=16)
+    gd = gpu_decode(torch_cuda, huff, h32, m, is_name_bits=nb)
+    np.testing.assert_array_equal(gd[1], od[1])
+    np.testing.assert_array_equal(gd[2], od[2])
+    slots = (h_off[:m] * 8) // 5
+    np.testing.assert_array_equal(_gather(gd[0], slots, gd[1]), _gather(od[0], slots, od[1]))
+    assert int((gd[1] != FAIL).sum()) == m  # every encoder output decodes
+
+
 def test_explicit_out_off_unaligned_and_long_strings(torch_cuda, oracle_codec):
     """explicit destinations at odd byte offsets, strings longer than the LDS stage (global path),
     empty strings, strings starting at every alignment"""
