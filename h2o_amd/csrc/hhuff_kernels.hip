@@ -718,6 +718,8 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
     constexpr int32_t kFinal = 32 * (NW - 2);      // a string ending at or before this bit ends in the window
 
     // per-lane string state
+    uint4 pfv[NW / 4];       // the prefetched next window (its input address: pfa)
+    uint64_t pfa = ~0ull;
     bool busy = false, head = false, is_name = false;
     uint32_t i = 0, s = 0, len = 0, P = 0, ocnt = 0, flags = 0, first = 0, lastb = 0, fail = 0;
     uint64_t dst = 0;
@@ -768,19 +770,31 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
         }
 
         // ---- 2. the lane's window: NW dwords from its current byte (dword-aligned) ----
+        // A round that does not finish its string stops with its next byte at wb + 4 (NW - 3) (bulk steps
+        // run to bit 32 (NW - 2) - 30 and overshoot by < 32), so that window was prefetched into registers
+        // at the start of the round before: its loads had the whole round to land.
         const uint64_t cur = (uint64_t)s + (P >> 3);
         const uint64_t wb = cur & ~3ull;
+        const uint64_t rem = (uint64_t)len * 8u - P;  // string bits left
         if (busy) {
+            if (wb != pfa) {
+#pragma unroll
+                for (int j = 0; j < NW / 4; ++j) pfv[j] = load16_bounded(A.in, A.in_size, wb + 16u * j);
+            }
 #pragma unroll
             for (int j = 0; j < NW / 4; ++j) {
-                const uint4 x = load16_bounded(A.in, A.in_size, wb + 16u * j);
-                win[4 * j + 0] = bswap32(x.x);
-                win[4 * j + 1] = bswap32(x.y);
-                win[4 * j + 2] = bswap32(x.z);
-                win[4 * j + 3] = bswap32(x.w);
+                win[4 * j + 0] = bswap32(pfv[j].x);
+                win[4 * j + 1] = bswap32(pfv[j].y);
+                win[4 * j + 2] = bswap32(pfv[j].z);
+                win[4 * j + 3] = bswap32(pfv[j].w);
+            }
+            // the string goes on past this window: fetch the next one now
+            pfa = rem + 8u * (uint32_t)(cur - wb) + (P & 7u) > 32u * (NW - 2) ? wb + 4u * (NW - 3) : ~0ull;
+            if (pfa != ~0ull) {
+#pragma unroll
+                for (int j = 0; j < NW / 4; ++j) pfv[j] = load16_bounded(A.in, A.in_size, pfa + 16u * j);
             }
         }
-        const uint64_t rem = (uint64_t)len * 8u - P;  // string bits left
         int32_t pm = busy ? (int32_t)(8u * (uint32_t)(cur - wb) + (P & 7u)) - 1 : -1;
         const int32_t pm0 = pm;
         const int32_t end = busy ? (int32_t)min((uint64_t)(pm + 1) + rem, (uint64_t)0x40000000u) : 0;
