@@ -349,7 +349,8 @@ def main():
 
 
 def other_configs(torch, codec, synth):
-    """BASELINE configs 2, 3, 5 (device-resident, HIP-event medians; tools/bench_configs.py)"""
+    """BASELINE configs 2, 3, 5 (device-resident, HIP-event medians; tools/bench_configs.py): encode to slots,
+    decode of the compressible strings' Huffman packed back to back, and for c5 the flatten_string framing"""
     import bench_configs as BC
 
     res = {}
@@ -358,22 +359,20 @@ def other_configs(torch, codec, synth):
         n, P = b["n"], int(b["total"])
         off32 = b["off"].to(torch.int32)
         r = {"strings": n, "plain_bytes": P}
-        if cfg in ("c2", "c3"):
-            huff, h_off, n_ok, H, P_ok = BC.packed_huffman(torch, codec, b)
-            d_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
-            d_len = torch.empty(n_ok, dtype=torch.int32, device="cuda")
-            d_st = torch.empty(n_ok, dtype=torch.uint8, device="cuda")
-            t_dec = BC.timed(torch, lambda: codec.decode_batch(huff, h_off, n_ok, out=d_out, out_len=d_len, status=d_st,
-                                                               in_size=H))
-            r.update(decode_ms=round(t_dec, 4), decode_gibps=round(P_ok / GIB / (t_dec * 1e-3), 2))
-            if cfg == "c3":
-                e_out = torch.empty(P + 16, dtype=torch.uint8, device="cuda")
-                e_len = torch.empty(n, dtype=torch.int32, device="cuda")
-                t_enc = BC.timed(torch, lambda: codec.encode_batch(b["data"], off32, n, out=e_out, out_len=e_len,
-                                                                   in_size=P))
-                r.update(encode_ms=round(t_enc, 4), encode_gibps=round(P / GIB / (t_enc * 1e-3), 2),
-                         round_trip_gibps=round(P / GIB / ((t_enc + t_dec) * 1e-3), 2))
-        else:  # QPACK values, flatten_string(prefix 7) framing (encode-only)
+        huff, h_off, n_ok, H, P_ok = BC.packed_huffman(torch, codec, b)
+        d_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
+        d_len = torch.empty(n_ok, dtype=torch.int32, device="cuda")
+        d_st = torch.empty(n_ok, dtype=torch.uint8, device="cuda")
+        t_dec = BC.timed(torch, lambda: codec.decode_batch(huff, h_off, n_ok, out=d_out, out_len=d_len, status=d_st,
+                                                           in_size=H))
+        e_out = torch.empty(P + 16, dtype=torch.uint8, device="cuda")
+        e_len = torch.empty(n, dtype=torch.int32, device="cuda")
+        t_enc = BC.timed(torch, lambda: codec.encode_batch(b["data"], off32, n, out=e_out, out_len=e_len, in_size=P))
+        r.update(decode_ms=round(t_dec, 4), decode_gibps=round(P_ok / GIB / (t_dec * 1e-3), 2),
+                 encode_ms=round(t_enc, 4), encode_gibps=round(P / GIB / (t_enc * 1e-3), 2),
+                 round_trip_gibps=round(P / GIB / ((t_enc + t_dec) * 1e-3), 2))
+        del huff, h_off, d_out, e_out
+        if cfg == "c5":  # QPACK values: flatten_string(prefix 7) framing, the config's own operation
             f_out = torch.empty(P + 11 * n + 16, dtype=torch.uint8, device="cuda")
             f_len = torch.empty(n, dtype=torch.int32, device="cuda")
             t = BC.timed(torch, lambda: codec.flatten_batch(b["data"], off32, n, 7, out=f_out, out_len=f_len, in_size=P))

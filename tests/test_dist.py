@@ -34,15 +34,31 @@ def _oracle_decode(shard):
             torch.from_numpy(status))
 
 
+def _gpu_decode(shard):
+    """the library's hhuff_decode_batch_packed on this rank's GPU; results back on the CPU for gloo"""
+    from h2o_amd import codec
+
+    n = shard["n"]
+    d = shard["data"].cuda()
+    out, out_off, out_len, status = codec.decode_batch_packed(d, shard["off"].cuda(), n,
+                                                              is_name_bits=shard["is_name_bits"].cuda(),
+                                                              in_size=int(d.numel()))
+    torch.cuda.synchronize()
+    return out.cpu(), out_off[:n].cpu(), out_len[:n].cpu(), status[:n].cpu()
+
+
 def _tensors(b):
     return dict(data=torch.from_numpy(b["data"]), off=torch.from_numpy(b["off"].view(np.int32)),
                 is_name_bits=torch.from_numpy(b["is_name_bits"].view(np.int32)), n=b["n"])
 
 
-def _worker(rank, world, port, q, with_names):
+def _worker(rank, world, port, q, with_names, gpu=False):
     import torch.distributed as dist
 
     from h2o_amd import synth
+
+    if gpu:
+        torch.cuda.set_device(rank % torch.cuda.device_count())
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -53,7 +69,7 @@ def _worker(rank, world, port, q, with_names):
             batch = _tensors(synth.make_batch("c2", n=5000, seed=31, adversarial_frac=0.05))
             if not with_names:
                 batch["is_name_bits"] = None
-        res = hd.decode_sharded(batch, _oracle_decode, root=0)
+        res = hd.decode_sharded(batch, _gpu_decode if gpu else _oracle_decode, root=0, device="cpu")
         # the size exchange alone: every rank learns its shard's global string index and output offset
         local = torch.tensor([rank + 1, 10 * (rank + 1)])
         sizes, first, obase = hd.exchange_sizes(local[0], local[1])
@@ -116,3 +132,26 @@ def test_shard_rebases_offsets_and_names():
     assert bool((hd.bits_to_bool(s["is_name_bits"], 150) == names).all())
     t["is_name_bits"] = None  # an encode batch: no name bits -> zero bits, no KeyError
     assert int(hd.shard(t, 10, 50)["is_name_bits"].abs().sum()) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_decode_on_the_gpu(world):
+    """the same scatter / per-rank decode / gather with the per-rank codec being libhhuff.so's
+    hhuff_decode_batch_packed on the GPU (every rank on cuda:0 of a one-GPU box), collectives over gloo"""
+    from h2o_amd import synth
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, True, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = _tensors(synth.make_batch("c2", n=5000, seed=31, adversarial_frac=0.05))
+    out, out_off, out_len, status = _oracle_decode(full)
+    ol, data = hd.compact_results(out, out_off, out_len)
+    assert got == tuple(np.asarray(x).tobytes() for x in (ol, status, data))
