@@ -1,17 +1,21 @@
 // HPACK header blocks on the GPU: h2o_hpack_decode_header (lib/http2/hpack.c:319-435)
 // applied field after field over each block, the way h2o_hpack_parse_request loops over a block
 // (hpack.c:513-527), with one dynamic table per connection (header_table_add :277-317, eviction
-// :263-275, size updates :352-366).
+// :263-275, size updates :352-366), and optionally h2o_hpack_parse_request's own rules (:502-637).
 //
-// Decomposition: a header block cannot be split -- every field may change the connection's dynamic
-// table, which the next field may read -- so the parallel axis is the connection: one lane per
-// connection walks its blocks in order (h2o serves thousands of connections per node; a batch is one
-// event-loop tick's worth of them).  The dynamic table lives in per-connection scratch in HBM: a byte
-// ring of table_size bytes (live entries never exceed it: each entry costs its bytes + 32 of the
-// capacity) and an entry ring of table_size / 32 + 1 {byte offset, name length, value length, soft
-// bits} records, newest first as in h2o.  Huffman literals decode with the same decode_core as the
-// string kernels (window LUT in LDS, per workgroup); raw literals validate with the reference's rules.
-// Every decoded name and value is written to the caller's arena; indexed fields copy the table entry.
+// A header block cannot be split -- every field may change the dynamic table the next one reads -- so the
+// table work is sequential per connection.  What is not sequential is moved out of that walk:
+//   1. literal pre-pass (blk_mark_kernel .. blk_list_kernel): a block's representation is readable without
+//      its table (index values and literal lengths are explicit), so one lane per block finds every string
+//      literal, and the literal kernels (launch_literals_dev) decode them all, balanced across connections;
+//   2. the walk (hpack_walk_kernel, one lane per connection) does only the bookkeeping: representation,
+//      table lookups and inserts, arena offsets, verdicts.  A field's name and value are *references* to
+//      where their bytes already are -- a decoded literal, the static table, the connection's ring, or
+//      (literals decoded in place) the arena -- and a table entry is such a pair of references;
+//   3. the copy pass (blk_copy_kernel, one thread per 32 field slots) moves every field's bytes into the
+//      arena, and the table pass (blk_table_kernel, one wave per connection) writes each connection's live
+//      entries into its other ring, so the next call (HHUFF_BLK_CONTINUE) finds them there.
+// The walk stores little and waits on few loads; the byte traffic runs in the parallel passes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -36,22 +40,9 @@ constexpr int32_t kBlkArena = HHUFF_BLK_ARENA;
 constexpr int32_t kBlkSkipped = HHUFF_BLK_SKIPPED;
 constexpr uint32_t kEntryOverhead = 32;  // HEADER_TABLE_ENTRY_SIZE_OFFSET (hpack.c:30)
 constexpr int64_t kIntIncomplete = -255, kIntBad = -9;
+constexpr uint32_t kLitHuffmanV = 4, kLitUpperV = 5;  // HHUFF_LIT_HUFFMAN / _UPPERCASE verdicts
+constexpr uint32_t kClsUnknown = 0xFFFFu;  // a table entry's name class not computed yet
 }  // namespace
-
-// Phase timing (profile builds only, -DHHUFF_PROFILE; tools/prof_blocks.py): per lane, the shader cycles
-// between the begin and end marks of each phase while the lane was in it, summed over lanes.
-#ifdef HHUFF_PROFILE
-__device__ unsigned long long g_bprof[8];
-struct BProf {
-    uint64_t a[8];
-};
-#define BP_T() __builtin_readcyclecounter()
-#define BP_ADD(bp, k, t0) ((bp).a[k] += BP_T() - (t0))
-#else
-struct BProf {};
-#define BP_T() 0ull
-#define BP_ADD(bp, k, t0) ((void)(t0))
-#endif
 
 struct BlkArgs {
     const uint8_t* in;
@@ -69,13 +60,56 @@ struct BlkArgs {
     uint64_t conn_scratch;  // bytes of scratch per connection
     uint32_t flags;         // HHUFF_BLK_CONTINUE: start from the tables the previous call left in scratch
     hhuff_request_t* req;   // request mode (hhuff_hpack_parse_requests): h2o_hpack_parse_request per block
+    // pre-decoded literals: bit p of lit_bits marks a string literal starting at input byte p, word_pre[w]
+    // counts the marks before word w, and literal r (in position order) has the results of the literal
+    // kernels: lit_len, lit_pay, lit_cons, lit_st, bytes at lit_out + floor(8 lit_pay[r] / 5).  NULL
+    // lit_bits: every literal is decoded in place.
+    const uint32_t* lit_bits;
+    const uint32_t* word_pre;
+    const uint32_t* lit_len;
+    const uint32_t* lit_pay;
+    const uint32_t* lit_cons;
+    const uint8_t* lit_st;
+    const uint8_t* lit_out;
+    // per field slot: the byte sources of its name and value (read by the copy pass)
+    uint64_t* fsrc_n;
+    uint64_t* fsrc_v;
 };
 
-// per-connection scratch: [TableState 32 B][byte ring, table_size rounded to 16][entry ring]
+// Byte sources: kind in the top three bits, offset below.  All stay valid until the call's passes have run.
+constexpr uint64_t kSrcLit = 0;              // lit_out offset (a pre-decoded Huffman literal)
+constexpr uint64_t kSrcStatic = 1ull << 61;  // static-table bytes (RFC 7541 Appendix A)
+constexpr uint64_t kSrcScr = 2ull << 61;     // scratch offset (a connection's ring: bytes of earlier calls)
+constexpr uint64_t kSrcArena = 3ull << 61;   // arena offset (a literal decoded in place)
+constexpr uint64_t kSrcIn = 4ull << 61;      // input offset (a raw literal's payload, where it lies)
+constexpr uint64_t kSrcOff = (1ull << 61) - 1;
+
+__device__ __forceinline__ const uint8_t* src_ptr(const BlkArgs& A, uint64_t s) {
+    const uint64_t o = s & kSrcOff;
+    switch (s >> 61) {
+        case 0: return A.lit_out + o;
+        case 1: return b_static_bytes + o;
+        case 2: return A.scratch + o;
+        case 3: return A.arena + o;
+        default: return A.in + o;
+    }
+}
+
+// per-connection scratch: [TableState 32 B][Entry x E][ring 0][ring 1] (rings: table_size rounded to 16)
 struct TableState {
-    uint32_t start, num, whead, failed;
+    uint32_t start, num, ring, failed;  // ring: which ring holds the entries' bytes between calls
     uint64_t size, cap;
 };
+struct Entry {  // one dynamic-table entry: references to its name and value bytes
+    uint64_t nsrc, vsrc;
+    uint32_t nl, vl;
+    uint16_t soft, cls;  // soft-error bits (hpack.c:419-421), name class for the request rules
+    uint32_t pad;
+};
+static_assert(sizeof(TableState) == 32 && sizeof(Entry) == 32, "scratch records");
+
+__device__ __host__ __forceinline__ uint32_t tbl_entries(uint32_t table_size) { return table_size / kEntryOverhead + 1; }
+__device__ __host__ __forceinline__ uint64_t tbl_ring(uint32_t table_size) { return ((uint64_t)table_size + 15u) & ~15ull; }
 
 constexpr uint32_t kBlkThreads = 256;
 
@@ -113,7 +147,6 @@ __device__ int64_t blk_decode_int(const Win& in, uint64_t& p, uint64_t end, uint
     if (v > 0x7FFFFFFFFFFFFFFFull) return kIntBad;
     return (int64_t)v;
 }
-
 // Byte copies in batches of 16: the 16 loads issue back to back and one wait covers them, instead of a
 // load-to-store round trip per byte (a lane's strings sit at unrelated addresses, so nothing coalesces).
 template <typename Src, typename Dst>
@@ -129,225 +162,64 @@ __device__ __forceinline__ void copy16(Src src, Dst dst, uint32_t n) {
     }
 }
 
-struct DynTable {  // one connection's dynamic table (newest entry = dynamic index 62)
-    uint8_t* ring;   // R bytes
-    uint4* ent;      // E records {byte offset, name length, value length, soft bits}
-    uint32_t R, E, start, num, whead;
-    uint64_t size, cap, maxcap;
-    __device__ __forceinline__ uint4 get(uint32_t k) const {
-        uint32_t i = start + k;
-        return ent[i >= E ? i - E : i];
+// The wave copies 64 byte segments at once (lane i holds segment i: src, dst, len; len 0 = none) in 16-byte
+// pieces spread over all lanes, so a long segment does not serialise one lane: every 64 pieces cost one
+// round trip.  Piece t belongs to the last lane k whose piece prefix excl[k] <= t (binary search by lanes).
+__device__ void wave_copy64(const uint8_t* src, uint8_t* dst, uint32_t len, int lane) {
+    const uint32_t chunks = (len + 15u) >> 4;
+    const uint32_t excl = wave_excl_scan(chunks, lane);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(excl + chunks), 63);
+    for (uint32_t t0 = 0; t0 < total; t0 += 64) {
+        const uint32_t t = t0 + (uint32_t)lane;
+        int k = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const uint32_t e = (uint32_t)__shfl((int)excl, k + step);
+            k += e <= t ? step : 0;
+        }
+        const uint32_t c = t - (uint32_t)__shfl((int)excl, k);
+        const uint8_t* s = (const uint8_t*)__shfl((long long)(uintptr_t)src, k);
+        uint8_t* d = (uint8_t*)__shfl((long long)(uintptr_t)dst, k);
+        const uint32_t n = (uint32_t)__shfl((int)len, k);
+        if (t < total) {
+            const uint32_t a = 16u * c, m = min(16u, n - a);
+            uint8_t v[16];
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j)
+                if (j < m) v[j] = s[a + j];
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j)
+                if (j < m) d[a + j] = v[j];
+        }
     }
+}
+
+struct DynTable {  // one connection's dynamic table (newest entry = dynamic index 62)
+    Entry* ent;
+    uint32_t E, start, num;
+    uint64_t size, cap, maxcap;
+    __device__ __forceinline__ uint32_t slot(uint32_t k) const {
+        const uint32_t i = start + k;
+        return i >= E ? i - E : i;
+    }
+    __device__ __forceinline__ Entry get(uint32_t k) const { return ent[slot(k)]; }
     __device__ __forceinline__ void evict_one() {
         --num;
-        const uint4 e = get(num);
-        size -= (uint64_t)e.y + e.z + kEntryOverhead;
+        const uint2 l = *reinterpret_cast<const uint2*>(&ent[slot(num)].nl);
+        size -= (uint64_t)l.x + l.y + kEntryOverhead;
     }
-    __device__ __forceinline__ uint32_t wrap(uint32_t a) const { return a >= R ? a - R : a; }  // a < 2R
-    __device__ __forceinline__ void put(const uint8_t* src, uint32_t n) {
-        uint8_t* rg = ring;
-        const uint32_t h = whead, RR = R;
-        copy16([&](uint32_t i) { return src[i]; },
-               [&](uint32_t i, uint8_t v) { rg[h + i >= RR ? h + i - RR : h + i] = v; }, n);
-        whead = wrap(whead + n);
-    }
-    __device__ __forceinline__ void copy_out(uint32_t off, uint32_t n, uint8_t* dst) const {
-        const uint8_t* rg = ring;
-        const uint32_t RR = R;
-        copy16([&](uint32_t i) { return rg[off + i >= RR ? off + i - RR : off + i]; },
-               [&](uint32_t i, uint8_t v) { dst[i] = v; }, n);
-    }
-    __device__ void add(const uint8_t* name, uint32_t nlen, const uint8_t* value, uint32_t vlen, uint32_t soft) {
-        const uint64_t add = (uint64_t)nlen + vlen + kEntryOverhead;
+    __device__ void add(const Entry& e) {
+        const uint64_t add = (uint64_t)e.nl + e.vl + kEntryOverhead;
         while (num != 0 && size + add > cap) evict_one();
         if (num == 0 && add > cap) return;  // does not fit an empty table: not added (hpack.c:285-289)
-        const uint32_t b0 = whead;
-        put(name, nlen);
-        put(value, vlen);
         start = start == 0 ? E - 1 : start - 1;
-        ent[start] = make_uint4(b0, nlen, vlen, soft);
+        ent[start] = e;
         size += add;
         ++num;
     }
 };
 
 enum : int { kStrOk = 0, kStrFail = 1, kStrUpper = 2, kStrArena = 3 };
-
-// decode_string (hpack.c:223-261) at in[p] into arena[cur..aend)
-__device__ int blk_string(const BlkArgs& A, const Win& W, uint64_t& p, uint64_t end, bool is_name, uint32_t& soft,
-                          uint64_t& cur, uint64_t aend, uint32_t& off, uint32_t& len, const DecTables& T) {
-    if (p >= end) return kStrFail;
-    const bool huff = (W.byte(p) & 0x80u) != 0;
-    const int64_t n = blk_decode_int(W, p, end, 7);
-    if (n < 0 || (uint64_t)n > end - p) return kStrFail;
-    if (huff) {
-        if (cur + ((uint64_t)n * 8u) / 5u > aend) return kStrArena;
-        if ((uint64_t)n > kMaxStrLen) return kStrFail;
-        RegSink sink;
-        sink.init(A.arena + cur);
-        // decode with first / last byte tracking (soft bits need them, hpack.c:136-152)
-        struct SinkFL {
-            RegSink s;
-            uint32_t first, last;
-            __device__ __forceinline__ void put1(uint32_t b) {
-                first = s.cnt == 0 ? (b & 0xFFu) : first;
-                last = b & 0xFFu;
-                s.put1(b);
-            }
-            __device__ __forceinline__ void put12(uint32_t syms, bool two) {
-                first = s.cnt == 0 ? (syms & 0xFFu) : first;
-                last = (two ? (syms >> 8) : syms) & 0xFFu;
-                s.put12(syms, two);
-            }
-            __device__ __forceinline__ uint32_t count() const { return s.count(); }
-        } fl{sink, 0u, 0u};
-        const DecResult r = decode_core(WinSource{&W}, (uint32_t)p, (uint32_t)n, fl, T);
-        if (!r.ok) return kStrFail;
-        fl.s.finish();
-        soft |= soft_bits(is_name, r.len, r.flags, fl.first, fl.last);
-        len = r.len;
-    } else {
-        const uint8_t* src = A.in + p;
-        if (cur + (uint64_t)n > aend) {  // the validators' verdicts come first (an upper-case name is PROTOCOL)
-            if (is_name && (n == 0 || src[0] != ':')) {
-                for (int64_t i = 0; i < n; ++i) {
-                    const uint32_t c = src[i];
-                    if (c - 'A' < 26u) return kStrUpper;
-                }
-            }
-            return kStrArena;
-        }
-        // one pass: 16 bytes in, validated (h2o_hpack_validate_header_name / _value, hpack.c:163-221), out
-        const bool check_name = is_name && (n == 0 || src[0] != ':');
-        bool bad = is_name ? (n == 0 && check_name) : false, upper = false;
-        uint8_t* dst = A.arena + cur;
-        const uint32_t nn = (uint32_t)n;
-        copy16([&](uint32_t i) { return src[i]; },
-               [&](uint32_t i, uint8_t v) {
-                   const uint32_t c = v;
-                   if (is_name) {
-                       if (check_name && ((b_name_invalid[c >> 5] >> (c & 31)) & 1u)) {
-                           if (c - 'A' < 26u)
-                               upper = true;
-                           else
-                               bad = true;
-                       }
-                   } else {
-                       bad |= ((b_value_invalid[c >> 5] >> (c & 31)) & 1u) != 0;
-                   }
-                   dst[i] = v;
-               },
-               nn);
-        if (upper) return kStrUpper;
-        if (!is_name && n != 0) {  // whole-value rule (hpack.c:110-115): no surrounding whitespace
-            const uint32_t a = src[0], z = src[n - 1];
-            bad |= a == ' ' || a == '\t' || z == ' ' || z == '\t';
-        }
-        if (bad) soft |= is_name ? 0x1u : 0x2u;
-        len = (uint32_t)n;
-    }
-    off = (uint32_t)cur;
-    cur += len;
-    p += (uint64_t)n;
-    return kStrOk;
-}
-
-// one field (h2o_hpack_decode_header): 0 / kErrInvalidChar = a field was produced
-__device__ int32_t blk_field(const BlkArgs& A, const Win& W, DynTable& t, uint64_t& p, uint64_t end, uint64_t& cur, uint64_t aend,
-                             uint32_t& noff, uint32_t& nlen, uint32_t& voff, uint32_t& vlen, uint32_t& soft_out,
-                             const DecTables& T, const uint8_t* SB, const uint16_t* SE, BProf& bp) {
-    uint64_t t0 = BP_T();
-    int64_t index = 0;
-    bool value_indexed = false, do_index = false;
-    for (;;) {
-        if (p >= end) return kErrCompression;
-        const uint32_t b = W.byte(p);
-        if (b >= 128) {  // indexed header field
-            if ((index = blk_decode_int(W, p, end, 7)) <= 0) return kErrCompression;
-            value_indexed = true;
-        } else if (b >= 64) {  // literal with incremental indexing
-            if (b == 64)
-                ++p;
-            else if ((index = blk_decode_int(W, p, end, 6)) <= 0)
-                return kErrCompression;
-            do_index = true;
-        } else if (b < 32) {  // literal without indexing / never indexed
-            if ((b & 0xFu) == 0)
-                ++p;
-            else if ((index = blk_decode_int(W, p, end, 4)) <= 0)
-                return kErrCompression;
-        } else {  // dynamic table size update
-            const int64_t c = blk_decode_int(W, p, end, 5);
-            if (c < 0 || (uint64_t)c > t.maxcap) return kErrCompression;
-            t.cap = (uint64_t)c;
-            while (t.num != 0 && t.size > t.cap) t.evict_one();
-            continue;
-        }
-        break;
-    }
-    uint32_t soft = 0;
-    BP_ADD(bp, 0, t0);
-    t0 = BP_T();
-    if (index > 0) {
-        if (index <= 61) {
-            const uint32_t k = 4u * (uint32_t)(index - 1);
-            const uint32_t no = SE[k], nl = SE[k + 1];
-            if (cur + nl > aend) return kBlkArena;
-            uint8_t* dn = A.arena + cur;
-            copy16([&](uint32_t i) { return SB[no + i]; }, [&](uint32_t i, uint8_t v) { dn[i] = v; }, nl);
-            noff = (uint32_t)cur;
-            nlen = nl;
-            cur += nl;
-            if (value_indexed) {
-                const uint32_t vo = SE[k + 2], vl = SE[k + 3];
-                if (cur + vl > aend) return kBlkArena;
-                uint8_t* dv = A.arena + cur;
-                copy16([&](uint32_t i) { return SB[vo + i]; }, [&](uint32_t i, uint8_t v) { dv[i] = v; }, vl);
-                voff = (uint32_t)cur;
-                vlen = vl;
-                cur += vl;
-            }
-        } else if ((uint64_t)(index - 62) < t.num) {
-            const uint4 e = t.get((uint32_t)(index - 62));
-            soft = e.w;
-            if (cur + e.y > aend) return kBlkArena;
-            t.copy_out(e.x, e.y, A.arena + cur);
-            noff = (uint32_t)cur;
-            nlen = e.y;
-            cur += e.y;
-            if (value_indexed) {
-                if (cur + e.z > aend) return kBlkArena;
-                uint32_t vo = e.x + e.y;
-                if (vo >= t.R) vo -= t.R;
-                t.copy_out(vo, e.z, A.arena + cur);
-                voff = (uint32_t)cur;
-                vlen = e.z;
-                cur += e.z;
-            }
-        } else {
-            return kErrCompression;
-        }
-        BP_ADD(bp, index <= 61 ? 1 : 2, t0);
-    } else {
-        const int r = blk_string(A, W, p, end, true, soft, cur, aend, noff, nlen, T);
-        if (r == kStrArena) return kBlkArena;
-        if (r != kStrOk) return r == kStrUpper ? kErrProtocol : kErrCompression;
-        BP_ADD(bp, 3, t0);
-    }
-    t0 = BP_T();
-    if (!value_indexed) {
-        soft &= ~0x2u;
-        const int r = blk_string(A, W, p, end, false, soft, cur, aend, voff, vlen, T);
-        if (r == kStrArena) return kBlkArena;
-        if (r != kStrOk) return kErrCompression;
-        BP_ADD(bp, 4, t0);
-    }
-    t0 = BP_T();
-    if (do_index) t.add(A.arena + noff, nlen, A.arena + voff, vlen, soft);
-    BP_ADD(bp, 5, t0);
-    soft_out = soft;
-    return soft ? kErrInvalidChar : 0;
-}
 
 // ---------------------------------------------------------------------------------------------------
 // h2o_hpack_parse_request's rules (hpack.c:502-637), applied to each field right after it is decoded.
@@ -435,16 +307,15 @@ constexpr uint32_t kMaxHeaders = 100;       // H2O_MAX_HEADERS (include/h2o/head
 
 // one decoded field k of the block (hpack.c:515-635); returns 0 or the hard error; sets *header when
 // h2o_add_header takes the field
-__device__ int32_t req_field(ReqState& r, const uint8_t* name, uint32_t nl, const uint8_t* value, uint32_t vl,
-                             uint32_t soft, int32_t k, bool& header) {
+__device__ int32_t req_field(ReqState& r, uint32_t cls, const uint8_t* value, uint32_t vl, uint32_t soft, int32_t k,
+                             bool& header) {
     header = false;
     if (soft != 0 && r.err == HHUFF_HERR_NONE) r.err = (soft & 1u) ? HHUFF_HERR_SOFT_NAME : HHUFF_HERR_SOFT_VALUE;
     if (++r.ndecoded > kMaxHeadersHard) {
         r.err = HHUFF_HERR_HEADERS_TOO_LONG;
         return kErrCompression;
     }
-    const uint32_t cls = req_name_class(name, nl);
-    if (nl != 0 && name[0] == ':') {
+    if (cls >= kNAuthority && cls <= kNPseudoOther) {  // a pseudo-header name (first byte a colon)
         if (!r.pseudo_ok) {
             r.err = HHUFF_HERR_INVALID_PSEUDO;
             return kErrProtocol;
@@ -542,53 +413,253 @@ __device__ __forceinline__ void req_store(hhuff_request_t* out, const ReqState& 
     out->scheme_kind = r.scheme_kind;
 }
 
+// decode_string (hpack.c:223-261) at position p: the string's arena place [off, off + len) and the source of
+// its bytes (a pre-decoded literal; or, decoded in place, the arena itself)
+__device__ int blk_string(const BlkArgs& A, const Win& W, uint64_t& p, uint64_t end, bool is_name, uint32_t& soft,
+                          uint64_t& cur, uint64_t aend, uint32_t& off, uint32_t& len, uint64_t& src, const DecTables& T) {
+    if (p >= end) return kStrFail;
+    if (A.lit_bits) {  // decoded already (hhuff_decode_literals over every literal the parse pass found)
+        const uint32_t w = A.lit_bits[p >> 5], m = 1u << (p & 31);
+        const uint32_t r = A.word_pre[p >> 5] + (uint32_t)__builtin_popcount(w & (m - 1u));
+        const uint32_t st = (w & m) ? A.lit_st[r] : 0xFFu;
+        const uint32_t verdict = (st >> 2) & 7u;
+        if ((w & m) && (verdict == 0 || verdict == kLitHuffmanV || verdict == kLitUpperV)) {
+            const uint32_t ln = A.lit_len[r];
+            const bool huff = (W.byte(p) & 0x80u) != 0;
+            uint64_t q = p;
+            const uint64_t n = (uint64_t)blk_decode_int(W, q, end, 7);  // fits: the parse pass checked it
+            // decode_string's order: Huffman -- arena room, then the decoder's verdict; raw -- the name
+            // validator's verdict, then arena room
+            if (huff) {
+                if (cur + (n * 8u) / 5u > aend) return kStrArena;
+                if (verdict != 0) return kStrFail;
+            } else {
+                if (verdict == kLitUpperV) return kStrUpper;
+                if (cur + n > aend) return kStrArena;
+            }
+            src = huff ? kSrcLit | ((q * 8u) / 5u) : kSrcIn | q;  // raw payloads are not copied by the pre-pass
+            soft |= st & 3u;
+            len = ln;
+            off = (uint32_t)cur;
+            cur += ln;
+            p = q + n;
+            return kStrOk;
+        }
+        // unmarked, or another verdict (a payload past the library's length limit): decode in place below
+    }
+    const bool huff = (W.byte(p) & 0x80u) != 0;
+    const int64_t n = blk_decode_int(W, p, end, 7);
+    if (n < 0 || (uint64_t)n > end - p) return kStrFail;
+    if (huff) {
+        if (cur + ((uint64_t)n * 8u) / 5u > aend) return kStrArena;
+        if ((uint64_t)n > kMaxStrLen) return kStrFail;
+        RegSink sink;
+        sink.init(A.arena + cur);
+        // decode with first / last byte tracking (soft bits need them, hpack.c:136-152)
+        struct SinkFL {
+            RegSink s;
+            uint32_t first, last;
+            __device__ __forceinline__ void put1(uint32_t b) {
+                first = s.cnt == 0 ? (b & 0xFFu) : first;
+                last = b & 0xFFu;
+                s.put1(b);
+            }
+            __device__ __forceinline__ void put12(uint32_t syms, bool two) {
+                first = s.cnt == 0 ? (syms & 0xFFu) : first;
+                last = (two ? (syms >> 8) : syms) & 0xFFu;
+                s.put12(syms, two);
+            }
+            __device__ __forceinline__ uint32_t count() const { return s.count(); }
+        } fl{sink, 0u, 0u};
+        const DecResult r = decode_core(WinSource{&W}, (uint32_t)p, (uint32_t)n, fl, T);
+        if (!r.ok) return kStrFail;
+        fl.s.finish();
+        soft |= soft_bits(is_name, r.len, r.flags, fl.first, fl.last);
+        len = r.len;
+    } else {
+        const uint8_t* rsrc = A.in + p;
+        if (cur + (uint64_t)n > aend) {  // the validators' verdicts come first (an upper-case name is PROTOCOL)
+            if (is_name && (n == 0 || rsrc[0] != ':')) {
+                for (int64_t i = 0; i < n; ++i) {
+                    const uint32_t c = rsrc[i];
+                    if (c - 'A' < 26u) return kStrUpper;
+                }
+            }
+            return kStrArena;
+        }
+        // one pass: 16 bytes in, validated (h2o_hpack_validate_header_name / _value, hpack.c:163-221), out
+        const bool check_name = is_name && (n == 0 || rsrc[0] != ':');
+        bool bad = is_name ? (n == 0 && check_name) : false, upper = false;
+        uint8_t* dst = A.arena + cur;
+        const uint32_t nn = (uint32_t)n;
+        copy16([&](uint32_t i) { return rsrc[i]; },
+               [&](uint32_t i, uint8_t v) {
+                   const uint32_t c = v;
+                   if (is_name) {
+                       if (check_name && ((b_name_invalid[c >> 5] >> (c & 31)) & 1u)) {
+                           if (c - 'A' < 26u)
+                               upper = true;
+                           else
+                               bad = true;
+                       }
+                   } else {
+                       bad |= ((b_value_invalid[c >> 5] >> (c & 31)) & 1u) != 0;
+                   }
+                   dst[i] = v;
+               },
+               nn);
+        if (upper) return kStrUpper;
+        if (!is_name && n != 0) {  // whole-value rule (hpack.c:110-115): no surrounding whitespace
+            const uint32_t a = rsrc[0], z = rsrc[n - 1];
+            bad |= a == ' ' || a == '\t' || z == ' ' || z == '\t';
+        }
+        if (bad) soft |= is_name ? 0x1u : 0x2u;
+        len = (uint32_t)n;
+    }
+    off = (uint32_t)cur;
+    src = kSrcArena | cur;
+    cur += len;
+    p += (uint64_t)n;
+    return kStrOk;
+}
+
+
+// one field (h2o_hpack_decode_header, hpack.c:319-435): 0 / kErrInvalidChar = a field was produced.  F gets
+// its arena places and byte sources; no bytes move here.
+struct FieldDesc {
+    uint32_t noff, nl, voff, vl, soft, cls;
+    uint64_t nsrc, vsrc;
+};
+
+__device__ int32_t blk_field(const BlkArgs& A, const Win& W, DynTable& t, uint64_t& p, uint64_t end, uint64_t& cur,
+                             uint64_t aend, FieldDesc& F, const DecTables& T, const uint16_t* SE, const uint16_t* scls,
+                             bool want_cls) {
+    int64_t index = 0;
+    bool value_indexed = false, do_index = false;
+    for (;;) {
+        if (p >= end) return kErrCompression;
+        const uint32_t b = W.byte(p);
+        if (b >= 128) {  // indexed header field
+            if ((index = blk_decode_int(W, p, end, 7)) <= 0) return kErrCompression;
+            value_indexed = true;
+        } else if (b >= 64) {  // literal with incremental indexing
+            if (b == 64)
+                ++p;
+            else if ((index = blk_decode_int(W, p, end, 6)) <= 0)
+                return kErrCompression;
+            do_index = true;
+        } else if (b < 32) {  // literal without indexing / never indexed
+            if ((b & 0xFu) == 0)
+                ++p;
+            else if ((index = blk_decode_int(W, p, end, 4)) <= 0)
+                return kErrCompression;
+        } else {  // dynamic table size update
+            const int64_t c = blk_decode_int(W, p, end, 5);
+            if (c < 0 || (uint64_t)c > t.maxcap) return kErrCompression;
+            t.cap = (uint64_t)c;
+            while (t.num != 0 && t.size > t.cap) t.evict_one();
+            continue;
+        }
+        break;
+    }
+    uint32_t soft = 0, cls = kClsUnknown;
+    if (index > 0) {
+        if (index <= 61) {
+            const uint32_t k = 4u * (uint32_t)(index - 1);
+            const uint32_t no = SE[k], nl = SE[k + 1];
+            if (cur + nl > aend) return kBlkArena;
+            F.nsrc = kSrcStatic | no;
+            F.nl = nl;
+            F.noff = (uint32_t)cur;
+            cur += nl;
+            cls = scls[index - 1];
+            if (value_indexed) {
+                const uint32_t vo = SE[k + 2], vl = SE[k + 3];
+                if (cur + vl > aend) return kBlkArena;
+                F.vsrc = kSrcStatic | vo;
+                F.vl = vl;
+                F.voff = (uint32_t)cur;
+                cur += vl;
+            }
+        } else if ((uint64_t)(index - 62) < t.num) {
+            const Entry e = t.get((uint32_t)(index - 62));
+            soft = e.soft;
+            if (cur + e.nl > aend) return kBlkArena;
+            F.nsrc = e.nsrc;
+            F.nl = e.nl;
+            F.noff = (uint32_t)cur;
+            cur += e.nl;
+            cls = e.cls;
+            if (value_indexed) {
+                if (cur + e.vl > aend) return kBlkArena;
+                F.vsrc = e.vsrc;
+                F.vl = e.vl;
+                F.voff = (uint32_t)cur;
+                cur += e.vl;
+            }
+        } else {
+            return kErrCompression;
+        }
+    } else {
+        const int r = blk_string(A, W, p, end, true, soft, cur, aend, F.noff, F.nl, F.nsrc, T);
+        if (r == kStrArena) return kBlkArena;
+        if (r != kStrOk) return r == kStrUpper ? kErrProtocol : kErrCompression;
+    }
+    if (!value_indexed) {
+        soft &= ~0x2u;
+        const int r = blk_string(A, W, p, end, false, soft, cur, aend, F.voff, F.vl, F.vsrc, T);
+        if (r == kStrArena) return kBlkArena;
+        if (r != kStrOk) return kErrCompression;
+    }
+    if (want_cls && cls == kClsUnknown) cls = req_name_class(src_ptr(A, F.nsrc), F.nl);
+    if (do_index) t.add(Entry{F.nsrc, F.vsrc, F.nl, F.vl, (uint16_t)soft, (uint16_t)cls, 0u});
+    F.soft = soft;
+    F.cls = cls;
+    return soft ? kErrInvalidChar : 0;
+}
+
 template <bool REQ>
-__global__ __launch_bounds__(kBlkThreads) void hpack_blocks_kernel(BlkArgs A) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
+__global__ __launch_bounds__(kBlkThreads) void hpack_walk_kernel(BlkArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];  // literals decoded in place
     __shared__ uint32_t s_kinfo[32];
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
-    __shared__ uint8_t s_static[HHUFF_STATIC_NBYTES];  // the static table (RFC 7541 Appendix A) for indexed copies
     __shared__ uint16_t s_sent[61 * 4];
-    for (uint32_t k = threadIdx.x; k < HHUFF_STATIC_NBYTES; k += blockDim.x) s_static[k] = b_static_bytes[k];
+    __shared__ uint16_t s_scls[61];  // the static names' classes for the request rules
     for (uint32_t k = threadIdx.x; k < 61 * 4; k += blockDim.x) s_sent[k] = b_static_ent[k];
     for (uint32_t k = threadIdx.x; k < (1u << HHUFF_LUT_BITS) / 4; k += blockDim.x)
         reinterpret_cast<uint4*>(s_lut)[k] = reinterpret_cast<const uint4*>(b_dec_lut)[k];
     for (uint32_t k = threadIdx.x; k < HHUFF_ONES_NENT; k += blockDim.x) s_ones[k] = b_ones[k];
     if (threadIdx.x < 31) s_kinfo[threadIdx.x] = b_kinfo[threadIdx.x];
+    if (threadIdx.x < 61)
+        s_scls[threadIdx.x] = (uint16_t)req_name_class(b_static_bytes + b_static_ent[4 * threadIdx.x],
+                                                       b_static_ent[4 * threadIdx.x + 1]);
     __syncthreads();
     DecTables T;  // assigned, not brace-initialised: a constant aggregate of LDS addresses cannot be a static initializer
     T.lut = s_lut;
     T.kinfo = s_kinfo;
     T.ones = s_ones;
-    const uint32_t R = A.table_size, E = A.table_size / kEntryOverhead + 1;
+    const uint32_t E = tbl_entries(A.table_size);
+    const Win W{A.in, A.in_size};
     for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < A.nconn; c += (uint64_t)gridDim.x * blockDim.x) {
         uint8_t* scr = A.scratch + c * A.conn_scratch;
         TableState* ts = reinterpret_cast<TableState*>(scr);
-        uint8_t* ring = scr + sizeof(TableState);
-        DynTable t{ring, reinterpret_cast<uint4*>(ring + ((R + 15u) & ~15u)), R, E, 0u, 0u, 0u, 0u, A.table_size,
-                   A.table_size};
-        const Win W{A.in, A.in_size};
-        BProf bp{};
-        bool failed = false;
-        if (A.flags & HHUFF_BLK_CONTINUE) {
-            const TableState s0 = *ts;
-            t.start = s0.start;
-            t.num = s0.num;
-            t.whead = s0.whead;
-            t.size = s0.size;
-            t.cap = s0.cap;
-            failed = s0.failed != 0;
-        }
+        DynTable t{reinterpret_cast<Entry*>(scr + sizeof(TableState)), E, 0u, 0u, 0ull, A.table_size, A.table_size};
+        TableState s0{0u, 0u, 0u, 0u, 0ull, A.table_size};
+        if (A.flags & HHUFF_BLK_CONTINUE) s0 = *ts;
+        t.start = s0.start;
+        t.num = s0.num;
+        t.size = s0.size;
+        t.cap = s0.cap;
+        bool failed = s0.failed != 0;
         for (uint32_t b = A.conn_first[c]; b < A.conn_first[c + 1]; ++b) {
-            A.nfields[b] = 0;
             ReqState rq;
             if (REQ) rq.reset();
             if (failed) {
+                A.nfields[b] = 0;
                 A.bstatus[b] = kBlkSkipped;
                 if (REQ) req_store(A.req + b, rq);
                 continue;
             }
-            const uint64_t tb = BP_T();
             uint64_t p = A.blk_off[b];
             const uint64_t end = A.blk_off[b + 1];
             uint64_t cur = A.arena_off[b];
@@ -597,8 +668,8 @@ __global__ __launch_bounds__(kBlkThreads) void hpack_blocks_kernel(BlkArgs A) {
             uint32_t nf = 0;
             int32_t st = 0;
             while (p != end) {
-                uint32_t no = 0, nl = 0, vo = 0, vl = 0, soft = 0;
-                const int32_t rc = blk_field(A, W, t, p, end, cur, aend, no, nl, vo, vl, soft, T, s_static, s_sent, bp);
+                FieldDesc F{0u, 0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
+                const int32_t rc = blk_field(A, W, t, p, end, cur, aend, F, T, s_sent, s_scls, REQ);
                 if (rc != 0 && rc != kErrInvalidChar) {
                     st = rc;
                     // h2o_hpack_parse_request: *err_desc = decode_err (:523-525) -- only the upper-case name
@@ -608,14 +679,15 @@ __global__ __launch_bounds__(kBlkThreads) void hpack_blocks_kernel(BlkArgs A) {
                 }
                 bool header = false;
                 int32_t rr = 0;
-                const uint64_t tr = BP_T();
-                if (REQ) rr = req_field(rq, A.arena + no, nl, A.arena + vo, vl, soft, (int32_t)nf, header);
-                BP_ADD(bp, 6, tr);
-                A.name_off[slot + nf] = no;
-                A.name_len[slot + nf] = nl;
-                A.value_off[slot + nf] = vo;
-                A.value_len[slot + nf] = vl;
-                A.fflags[slot + nf] = (uint8_t)(soft | (header ? HHUFF_FIELD_HEADER : 0u));
+                if (REQ) rr = req_field(rq, F.cls, src_ptr(A, F.vsrc), F.vl, F.soft, (int32_t)nf, header);
+                const uint32_t f = slot + nf;
+                A.name_off[f] = F.noff;
+                A.name_len[f] = F.nl;
+                A.value_off[f] = F.voff;
+                A.value_len[f] = F.vl;
+                A.fflags[f] = (uint8_t)(F.soft | (header ? HHUFF_FIELD_HEADER : 0u));
+                A.fsrc_n[f] = F.nsrc;
+                A.fsrc_v[f] = F.vsrc;
                 ++nf;
                 if (rr != 0) {
                     st = rr;
@@ -629,29 +701,216 @@ __global__ __launch_bounds__(kBlkThreads) void hpack_blocks_kernel(BlkArgs A) {
             A.nfields[b] = nf;
             A.bstatus[b] = st;
             failed = st != 0 && st != kErrInvalidChar;
-            BP_ADD(bp, 7, tb);
         }
-#ifdef HHUFF_PROFILE
-        for (int k = 0; k < 8; ++k) atomicAdd(&g_bprof[k], (unsigned long long)bp.a[k]);
-#endif
-        *ts = TableState{t.start, t.num, t.whead, failed ? 1u : 0u, t.size, t.cap};
+        *ts = TableState{t.start, t.num, s0.ring, failed ? 1u : 0u, t.size, t.cap};
     }
 }
 
-#ifdef HHUFF_PROFILE
-hipError_t read_bprof(unsigned long long* out8, bool reset) {
-    hipError_t e = hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_bprof), sizeof(g_bprof));
-    if (e == hipSuccess && reset) {
-        unsigned long long z[8] = {};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(g_bprof), z, sizeof(z));
+// Copy pass: one wave per block (grid-stride), 32 fields (64 name / value segments) per round through
+// wave_copy64 (literals decoded in place already sit in the arena).
+__global__ __launch_bounds__(256) void blk_copy_kernel(BlkArgs A) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nblk = A.conn_first[A.nconn];
+    const uint32_t nw = gridDim.x * 4u;
+    for (uint32_t b = blockIdx.x * 4u + (threadIdx.x >> 6); b < nblk; b += nw) {
+        const uint32_t s0 = A.blk_off[b], nf = A.nfields[b];
+        for (uint32_t g = 0; g < nf; g += 32) {
+            const uint32_t fi = g + ((uint32_t)lane >> 1), f = s0 + fi;
+            const bool val = lane & 1;
+            uint32_t len = 0, off = 0;
+            uint64_t src = 0;
+            if (fi < nf) {
+                len = val ? A.value_len[f] : A.name_len[f];
+                off = val ? A.value_off[f] : A.name_off[f];
+                src = val ? A.fsrc_v[f] : A.fsrc_n[f];
+                if (src == (kSrcArena | off)) len = 0;
+            }
+            wave_copy64(src_ptr(A, src), A.arena + off, len, lane);
+        }
     }
-    return e;
 }
-#endif
 
+// Table pass: one wave per connection writes its live entries' bytes, newest first, into the ring the
+// entries do not use now, and points the entries there: the next call (HHUFF_BLK_CONTINUE) reads only
+// scratch.  Live bytes never exceed table_size (each entry costs its bytes + 32 of the capacity).
+__global__ __launch_bounds__(256) void blk_table_kernel(BlkArgs A) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (c >= A.nconn) return;
+    const uint32_t E = tbl_entries(A.table_size);
+    const uint64_t base = c * A.conn_scratch;
+    TableState* ts = reinterpret_cast<TableState*>(A.scratch + base);
+    Entry* ent = reinterpret_cast<Entry*>(A.scratch + base + sizeof(TableState));
+    const TableState s = *ts;
+    const uint32_t nring = s.ring ^ 1u;
+    const uint64_t rbase = base + sizeof(TableState) + (uint64_t)E * sizeof(Entry) + nring * tbl_ring(A.table_size);
+    uint32_t carry = 0;
+    for (uint32_t k0 = 0; k0 < s.num; k0 += 64) {
+        const uint32_t k = k0 + (uint32_t)lane;
+        const bool live = k < s.num;
+        uint32_t i = s.start + k;
+        i = i >= E ? i - E : i;
+        Entry e{};
+        if (live) e = ent[i];
+        const uint32_t sz = live ? e.nl + e.vl : 0u;
+        const uint32_t dst = carry + wave_excl_scan(sz, lane);
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)(dst - carry + sz), 63);
+        uint8_t* d = A.scratch + rbase + dst;
+        wave_copy64(src_ptr(A, e.nsrc), d, live ? e.nl : 0u, lane);
+        wave_copy64(src_ptr(A, e.vsrc), d + e.nl, live ? e.vl : 0u, lane);
+        if (live) {
+            ent[i].nsrc = kSrcScr | (rbase + dst);
+            ent[i].vsrc = kSrcScr | (rbase + dst + e.nl);
+        }
+    }
+    if (lane == 0) ts->ring = nring;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Literal pre-pass.  The representation of a block is readable without its connection's table: index
+// values and literal lengths are explicit (hpack.c:336-366, 223-236), so one lane per block can find every
+// string literal a decoder of that block could reach.  Those are decoded together by the literal kernels
+// (balanced across all connections, launch_literals_dev), and the per-connection walk then copies results
+// instead of running a Huffman decoder per lane -- one lane per connection otherwise steps through 64
+// connections' literals in lock step, each field costing the wave its slowest lane's literal.  The walk
+// marks may include literals past a table-dependent error (an index beyond the table): decoded, unused.
+// ---------------------------------------------------------------------------------------------------
+constexpr uint32_t kMarkThreads = 256, kChunkWords = 1024;  // list pass: 1024 bitmap words per block
+
+// literal at p (H flag + 7-bit-prefix length, then the payload) inside [p, end): mark it, step over it
+__device__ __forceinline__ bool mark_literal(const Win& W, uint64_t& p, uint64_t end, bool is_name,
+                                             uint32_t* __restrict__ lit_bits, uint32_t* __restrict__ name_bits) {
+    if (p >= end) return false;
+    uint64_t q = p;
+    const int64_t n = blk_decode_int(W, q, end, 7);
+    if (n < 0 || (uint64_t)n > end - q) return false;
+    atomicOr(lit_bits + (p >> 5), 1u << (p & 31));
+    if (is_name) atomicOr(name_bits + (p >> 5), 1u << (p & 31));
+    p = q + (uint64_t)n;
+    return true;
+}
+
+__global__ __launch_bounds__(kMarkThreads) void blk_mark_kernel(const uint8_t* __restrict__ in, uint64_t in_size,
+                                                               const uint32_t* __restrict__ blk_off,
+                                                               const uint32_t* __restrict__ conn_first, uint32_t nconn,
+                                                               uint32_t* __restrict__ lit_bits,
+                                                               uint32_t* __restrict__ name_bits) {
+    const uint32_t nblk = conn_first[nconn];
+    const Win W{in, in_size};
+    for (uint32_t b = blockIdx.x * kMarkThreads + threadIdx.x; b < nblk; b += gridDim.x * kMarkThreads) {
+        uint64_t p = blk_off[b];
+        const uint64_t end = blk_off[b + 1];
+        while (p < end) {  // the representation switch of blk_field / h2o_hpack_decode_header
+            const uint32_t c = W.byte(p);
+            bool name_lit = false;
+            if (c >= 128) {
+                if (blk_decode_int(W, p, end, 7) <= 0) break;
+                continue;  // indexed: no literal
+            } else if (c >= 64) {
+                if (c == 64) {
+                    ++p;
+                    name_lit = true;
+                } else if (blk_decode_int(W, p, end, 6) <= 0) {
+                    break;
+                }
+            } else if (c < 32) {
+                if ((c & 0xFu) == 0) {
+                    ++p;
+                    name_lit = true;
+                } else if (blk_decode_int(W, p, end, 4) <= 0) {
+                    break;
+                }
+            } else {
+                if (blk_decode_int(W, p, end, 5) < 0) break;
+                continue;  // table size update
+            }
+            if (name_lit && !mark_literal(W, p, end, true, lit_bits, name_bits)) break;
+            if (!mark_literal(W, p, end, false, lit_bits, name_bits)) break;
+        }
+    }
+}
+
+// block-wide exclusive scan of one value per thread (kMarkThreads threads); *total = the block's sum
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane == 63) sh[wave] = incl;
+    __syncthreads();
+    uint32_t base = 0, sum = 0;
+    for (int k = 0; k < (int)(kMarkThreads / 64); ++k) {
+        base += k < wave ? sh[k] : 0u;
+        sum += sh[k];
+    }
+    __syncthreads();
+    *total = sum;
+    return base + incl - v;
+}
+
+// marks per chunk of kChunkWords bitmap words
+__global__ __launch_bounds__(kMarkThreads) void blk_count_kernel(const uint32_t* __restrict__ lit_bits, uint64_t nwords,
+                                                                uint32_t* __restrict__ chunk_sum) {
+    __shared__ uint32_t sh[kMarkThreads / 64];
+    const uint64_t w0 = (uint64_t)blockIdx.x * kChunkWords + threadIdx.x * (kChunkWords / kMarkThreads);
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kChunkWords / kMarkThreads; ++k)
+        c += w0 + k < nwords ? (uint32_t)__builtin_popcount(lit_bits[w0 + k]) : 0u;
+    uint32_t total;
+    (void)block_excl_scan(c, sh, &total);
+    if (threadIdx.x == 0) chunk_sum[blockIdx.x] = total;
+}
+
+// exclusive scan of the chunk sums in place (one block); *n_lit = the number of literals
+__global__ __launch_bounds__(kMarkThreads) void blk_chunk_scan_kernel(uint32_t* __restrict__ chunk_sum, uint32_t nchunks,
+                                                                     uint32_t* __restrict__ n_lit) {
+    __shared__ uint32_t sh[kMarkThreads / 64];
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < nchunks; c0 += kMarkThreads) {
+        const uint32_t i = c0 + threadIdx.x;
+        const uint32_t v = i < nchunks ? chunk_sum[i] : 0u;
+        uint32_t total;
+        const uint32_t ex = block_excl_scan(v, sh, &total);
+        if (i < nchunks) chunk_sum[i] = carry + ex;
+        carry += total;
+    }
+    if (threadIdx.x == 0) *n_lit = carry;
+}
+
+// per bitmap word: the marks before it (word_pre), and the literal list in position order: lit_off[r],
+// and bit r of lnames for the names
+__global__ __launch_bounds__(kMarkThreads) void blk_list_kernel(const uint32_t* __restrict__ lit_bits,
+                                                               const uint32_t* __restrict__ name_bits, uint64_t nwords,
+                                                               const uint32_t* __restrict__ chunk_pre,
+                                                               uint32_t* __restrict__ word_pre,
+                                                               uint32_t* __restrict__ lit_off, uint32_t* __restrict__ lnames) {
+    __shared__ uint32_t sh[kMarkThreads / 64];
+    constexpr uint32_t K = kChunkWords / kMarkThreads;
+    const uint64_t w0 = (uint64_t)blockIdx.x * kChunkWords + threadIdx.x * K;
+    uint32_t bits[K], c = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < K; ++k) {
+        bits[k] = w0 + k < nwords ? lit_bits[w0 + k] : 0u;
+        c += (uint32_t)__builtin_popcount(bits[k]);
+    }
+    uint32_t total;
+    uint32_t r = chunk_pre[blockIdx.x] + block_excl_scan(c, sh, &total);
+#pragma unroll
+    for (uint32_t k = 0; k < K; ++k) {
+        if (w0 + k >= nwords) break;
+        word_pre[w0 + k] = r;
+        uint32_t m = bits[k];
+        const uint32_t nm = m ? name_bits[w0 + k] : 0u;
+        while (m) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            lit_off[r] = (uint32_t)(32u * (w0 + k) + bit);
+            if ((nm >> bit) & 1u) atomicOr(lnames + (r >> 5), 1u << (r & 31));
+            ++r;
+        }
+    }
+}
 uint64_t hpack_conn_scratch(uint32_t table_size) {
-    const uint64_t R = ((uint64_t)table_size + 15u) & ~15ull;
-    return sizeof(TableState) + R + 16ull * (table_size / kEntryOverhead + 1u);
+    return sizeof(TableState) + (uint64_t)tbl_entries(table_size) * sizeof(Entry) + 2 * tbl_ring(table_size);
 }
 
 hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off, const uint32_t* conn_first,
@@ -661,13 +920,83 @@ hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32
                                uint8_t* scratch, uint32_t flags, hipStream_t stream) {
     if (nconn == 0) return hipSuccess;
     BlkArgs A{in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len, value_off,
-              value_len, fflags, nfields, bstatus, scratch, hpack_conn_scratch(table_size), flags, req};
-    const uint32_t blocks = min((nconn + kBlkThreads - 1u) / kBlkThreads, 65535u);
-    if (req)
-        hipLaunchKernelGGL(hpack_blocks_kernel<true>, dim3(blocks), dim3(kBlkThreads), 0, stream, A);
-    else
-        hipLaunchKernelGGL(hpack_blocks_kernel<false>, dim3(blocks), dim3(kBlkThreads), 0, stream, A);
-    return hipGetLastError();
+              value_len, fflags, nfields, bstatus, scratch, hpack_conn_scratch(table_size), flags, req,
+              nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    // workspace (the library's stream-ordered pool): field sources for every slot (block byte);
+    // with the literal pre-pass (inputs below 4 GiB: u32 positions) its bitmaps, word prefixes, chunk sums,
+    // the literal list and results, and the decoded bytes
+    const uint64_t nslots = in_size;
+    const bool prepass = in_size > 0 && in_size < (1ull << 32);
+    const uint64_t nwords = (in_size + 31) / 32, nchunks = (nwords + kChunkWords - 1) / kChunkWords;
+    const uint64_t n_max = (2 * in_size) / 3 + 2;  // a field with two literals takes >= 3 bytes
+    auto up = [](uint64_t x) { return (x + 255) & ~255ull; };
+    uint64_t o = 0;
+    const uint64_t o_lit = o;
+    if (prepass) o += up(4 * nwords);
+    const uint64_t o_name = o;
+    if (prepass) o += up(4 * nwords);
+    const uint64_t o_lnames = o;
+    if (prepass) o += up(4 * ((n_max + 31) / 32));
+    const uint64_t zero_end = o;  // [0, zero_end) starts zeroed
+    const uint64_t o_fsn = o;
+    o += up(8 * nslots + 8);
+    const uint64_t o_fsv = o;
+    o += up(8 * nslots + 8);
+    const uint64_t o_pre = o, o_chunk = o_pre + (prepass ? up(4 * nwords) : 0);
+    const uint64_t o_list = o_chunk + (prepass ? up(4 * nchunks + 4) : 0);
+    const uint64_t o_len = o_list + (prepass ? up(4 * n_max) : 0);
+    const uint64_t o_pay = o_len + (prepass ? up(4 * n_max) : 0);
+    const uint64_t o_cons = o_pay + (prepass ? up(4 * n_max) : 0);
+    const uint64_t o_st = o_cons + (prepass ? up(4 * n_max) : 0);
+    const uint64_t o_ws = o_st + (prepass ? up(n_max) : 0);
+    const uint64_t o_out = o_ws + (prepass ? up(literals_dev_ws((uint32_t)n_max, in_size)) : 0);
+    o = o_out + (prepass ? up((8 * in_size) / 5 + 64) : 0);
+    uint8_t* work = nullptr;
+    hipError_t e = work_alloc((void**)&work, o, stream);
+    if (e != hipSuccess) return e;
+    A.fsrc_n = reinterpret_cast<uint64_t*>(work + o_fsn);
+    A.fsrc_v = reinterpret_cast<uint64_t*>(work + o_fsv);
+    e = hipMemsetAsync(work, 0, zero_end, stream);
+    if (e == hipSuccess && prepass) {
+        uint32_t* lit_bits = reinterpret_cast<uint32_t*>(work + o_lit);
+        uint32_t* name_bits = reinterpret_cast<uint32_t*>(work + o_name);
+        uint32_t* lnames = reinterpret_cast<uint32_t*>(work + o_lnames);
+        uint32_t* word_pre = reinterpret_cast<uint32_t*>(work + o_pre);
+        uint32_t* chunk = reinterpret_cast<uint32_t*>(work + o_chunk);
+        uint32_t* n_lit = chunk + nchunks;
+        uint32_t* list = reinterpret_cast<uint32_t*>(work + o_list);
+        hipLaunchKernelGGL(blk_mark_kernel, dim3(2048), dim3(kMarkThreads), 0, stream, in, in_size, blk_off, conn_first,
+                           nconn, lit_bits, name_bits);
+        hipLaunchKernelGGL(blk_count_kernel, dim3((uint32_t)nchunks), dim3(kMarkThreads), 0, stream, lit_bits, nwords,
+                           chunk);
+        hipLaunchKernelGGL(blk_chunk_scan_kernel, dim3(1), dim3(kMarkThreads), 0, stream, chunk, (uint32_t)nchunks, n_lit);
+        hipLaunchKernelGGL(blk_list_kernel, dim3((uint32_t)nchunks), dim3(kMarkThreads), 0, stream, lit_bits, name_bits,
+                           nwords, chunk, word_pre, list, lnames);
+        e = hipGetLastError();
+        if (e == hipSuccess)
+            e = launch_literals_dev(in, in_size, list, (uint32_t)n_max, n_lit, 7u, kLitNoRawCopy, lnames, work + o_out,
+                                    reinterpret_cast<uint32_t*>(work + o_len), reinterpret_cast<uint32_t*>(work + o_pay),
+                                    reinterpret_cast<uint32_t*>(work + o_cons), work + o_st, work + o_ws, stream);
+        A.lit_bits = lit_bits;
+        A.word_pre = word_pre;
+        A.lit_len = reinterpret_cast<const uint32_t*>(work + o_len);
+        A.lit_pay = reinterpret_cast<const uint32_t*>(work + o_pay);
+        A.lit_cons = reinterpret_cast<const uint32_t*>(work + o_cons);
+        A.lit_st = work + o_st;
+        A.lit_out = work + o_out;
+    }
+    if (e == hipSuccess) {
+        const uint32_t blocks = min((nconn + kBlkThreads - 1u) / kBlkThreads, 65535u);
+        if (req)
+            hipLaunchKernelGGL(hpack_walk_kernel<true>, dim3(blocks), dim3(kBlkThreads), 0, stream, A);
+        else
+            hipLaunchKernelGGL(hpack_walk_kernel<false>, dim3(blocks), dim3(kBlkThreads), 0, stream, A);
+        hipLaunchKernelGGL(blk_copy_kernel, dim3(4096), dim3(256), 0, stream, A);
+        hipLaunchKernelGGL(blk_table_kernel, dim3((uint32_t)(((uint64_t)nconn + 3) / 4)), dim3(256), 0, stream, A);
+        e = hipGetLastError();
+    }
+    const hipError_t f = hipFreeAsync(work, stream);
+    return e != hipSuccess ? e : f;
 }
 
 }  // namespace hhuff

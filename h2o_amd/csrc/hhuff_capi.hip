@@ -187,7 +187,7 @@ HHUFF_API int hhuff_decode_literals(const uint8_t* in, uint64_t in_size, const u
     hipStream_t s = (hipStream_t)stream;
     void* ws = nullptr;  // Huffman payload lengths + per-literal verdict bytes, stream-ordered scratch
     HIP_TRY(hipMallocAsync(&ws, (size_t)n * 5, s), "hipMallocAsync");
-    hipError_t e = hhuff::launch_literals(in, in_size, lit_off, lit_end, n, prefix_bits, flags, is_name_bits, out, out_len,
+    hipError_t e = hhuff::launch_literals(in, in_size, lit_off, lit_end, n, prefix_bits, flags & HHUFF_LIT_QPACK, is_name_bits, out, out_len,
                                           pay_off, consumed, status, (uint32_t*)ws, s);
     hipError_t f = hipFreeAsync(ws, s);
     if (e != hipSuccess) return hip_fail(e, "literal launch");
@@ -658,12 +658,6 @@ hipError_t read_prof(unsigned long long* out16, bool reset);
 }
 HHUFF_API int hhuff_debug_prof(unsigned long long* out16, int reset) {
     return hhuff::read_prof(out16, reset != 0) == hipSuccess ? 0 : -1;
-}
-namespace hhuff {
-hipError_t read_bprof(unsigned long long* out8, bool reset);
-}
-HHUFF_API int hhuff_debug_prof_blocks(unsigned long long* out8, int reset) {
-    return hhuff::read_bprof(out8, reset != 0) == hipSuccess ? 0 : -1;
 }
 #endif
 HHUFF_API const char* hhuff_version(void) { return "hhuff 0.1.0 (gfx950)"; }

@@ -316,6 +316,7 @@ struct DecArgs {
     uint32_t* gate;        // NULL, or the device-side kernel choice (kGate*), written by the staged kernel
     const uint64_t* sel;   // decode_select_kernel's partial sums [3][kSelBlocks] (with gate)
     uint32_t* pk_off;      // packed mode (decode_staged_kernel<.., true>): u32[n + 1] output places
+    const uint32_t* n_dev;  // stream kernel: NULL, or the string count in device memory (n an upper bound)
 };
 
 __device__ __forceinline__ void load_dec_tables(uint32_t* s_lut, uint32_t* s_kinfo, uint32_t* s_ones, int nthreads) {
@@ -726,6 +727,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
     // wave batch
     uint64_t bnext = 0, bend = 0;
     bool qdone = false;
+    const uint64_t nwork = A.n_dev ? (uint64_t)*A.n_dev : (uint64_t)A.n;
 
     for (;;) {
         // ---- 1. idle lanes take strings ----
@@ -738,12 +740,12 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                 if (lane == 0) b = atomicAdd(counter, 64ull);
                 b = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
-                if (b >= A.n) {
+                if (b >= nwork) {
                     qdone = true;
                     break;
                 }
                 bnext = b;
-                bend = min(b + 64u, (uint64_t)A.n);
+                bend = min(b + 64u, nwork);
             }
             const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
@@ -1671,14 +1673,19 @@ struct LitArgs {
     uint8_t* status;
     uint32_t* huff_len;  // workspace: Huffman payload length (0 for raw literals and errors)
     uint8_t* code;       // workspace: verdict | H flag << 3 | soft bits << 4
+    const uint32_t* n_dev;  // NULL, or the literal count in device memory (n is then an upper bound)
+    uint32_t* long_list;    // NULL, or: raw payloads longer than kLongRaw are validated by literal_long_kernel
+    uint32_t* long_count;
 };
+
+constexpr uint32_t kLongRaw = 512;  // raw payload bytes above which one wave validates the literal
 
 enum : uint32_t { kLitIncomplete = 1, kLitBadInt = 2, kLitTruncated = 3, kLitHuffman = 4, kLitUpper = 5, kLitTooLong = 6 };
 
 // header of literal i -> verdict (0 = ok); hdr = header bytes, len = payload bytes, huff = H flag
 __device__ __forceinline__ uint32_t lit_header(const LitArgs& A, uint32_t i, bool& huff, uint32_t& hdr, uint32_t& len) {
     const uint64_t off = A.lit_off[i];
-    const uint64_t end = min((uint64_t)A.lit_end[i], A.in_size);
+    const uint64_t end = A.lit_end ? min((uint64_t)A.lit_end[i], A.in_size) : A.in_size;
     huff = false;
     hdr = 0;
     len = 0;
@@ -1731,43 +1738,55 @@ __device__ __forceinline__ bool pseudo_token(const uint8_t* s, uint32_t len) {  
 // Pass 1: headers; raw payloads are validated and copied here (they skip the Huffman kernel, which
 // sees length 0 for them).  code[i] = verdict | H flag << 3 | soft bits << 4 for the fix-up.
 __global__ void literal_parse_kernel(LitArgs A) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t n = A.n_dev ? (uint64_t)*A.n_dev : (uint64_t)A.n;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         bool huff;
         uint32_t hdr, len;
         uint32_t v = lit_header(A, (uint32_t)i, huff, hdr, len);
         uint32_t soft = 0;
-        if (v == 0 && !huff) {
+        if (v == 0 && !huff && A.long_list && len > kLongRaw) {  // one lane would walk it alone: defer
+            A.long_list[atomicAdd(A.long_count, 1u)] = (uint32_t)i;
+        } else if (v == 0 && !huff) {
             const bool is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) != 0 : false;
             const uint64_t s0 = (uint64_t)A.lit_off[i] + hdr;
             const uint8_t* src = A.in + s0;
             const bool skip = is_name && ((A.flags & 1u) ? pseudo_token(src, len) : (len != 0 && src[0] == ':'));
             const uint32_t* inval = is_name ? g_name_invalid : g_value_invalid;
             uint8_t* dst = A.out + (s0 * 8u) / 5u;
-            // 16-byte aligned loads, no early exit: the loads of a long raw literal stay in flight together
+            // 16-byte aligned loads, four per round and no early exit: the loads of a long raw literal stay
+            // in flight together (and the blocks pipeline, kLitNoRawCopy, stores nothing in between)
+            const bool copy = !(A.flags & kLitNoRawCopy);
             bool anybad = false, softbad = false, upper = false;
             const uint64_t a0 = s0 & ~15ull, e0 = s0 + len;
-            for (uint64_t a = a0; a < e0; a += 16) {
-                uint4 w4;
-                if (a + 16 <= A.in_size) {
-                    w4 = *reinterpret_cast<const uint4*>(A.in + a);
-                } else {
-                    uint32_t w[4] = {0, 0, 0, 0};
-                    for (uint32_t k = 0; k < 16; ++k)
-                        if (a + k < A.in_size) w[k >> 2] |= (uint32_t)A.in[a + k] << (8 * (k & 3));
-                    w4 = make_uint4(w[0], w[1], w[2], w[3]);
-                }
-                const uint32_t wv[4] = {w4.x, w4.y, w4.z, w4.w};
+            for (uint64_t ar = a0; ar < e0; ar += 64) {
+                uint4 w4[4];
 #pragma unroll
-                for (uint32_t k = 0; k < 16; ++k) {
-                    const uint64_t pos = a + k;
-                    if (pos < s0 || pos >= e0) continue;
-                    const uint32_t c = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
-                    const bool bad = ((inval[c >> 5] >> (c & 31)) & 1u) != 0;
-                    const bool up = bad && (c - 'A' < 26u);
-                    anybad |= bad;
-                    softbad |= bad && !up && !upper;  // names: only what precedes the first upper-case letter
-                    upper |= up;
-                    dst[pos - s0] = (uint8_t)c;
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint64_t a = ar + 16u * q;
+                    if (a + 16 <= A.in_size) {
+                        w4[q] = *reinterpret_cast<const uint4*>(A.in + a);
+                    } else {
+                        uint32_t w[4] = {0, 0, 0, 0};
+                        for (uint32_t k = 0; k < 16; ++k)
+                            if (a + k < A.in_size) w[k >> 2] |= (uint32_t)A.in[a + k] << (8 * (k & 3));
+                        w4[q] = make_uint4(w[0], w[1], w[2], w[3]);
+                    }
+                }
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t wv[4] = {w4[q].x, w4[q].y, w4[q].z, w4[q].w};
+#pragma unroll
+                    for (uint32_t k = 0; k < 16; ++k) {
+                        const uint64_t pos = ar + 16u * q + k;
+                        if (pos < s0 || pos >= e0) continue;
+                        const uint32_t c = (wv[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+                        const bool bad = ((inval[c >> 5] >> (c & 31)) & 1u) != 0;
+                        const bool up = bad && (c - 'A' < 26u);
+                        anybad |= bad;
+                        softbad |= bad && !up && !upper;  // names: only what precedes the first upper-case letter
+                        upper |= up;
+                        if (copy) dst[pos - s0] = (uint8_t)c;
+                    }
                 }
             }
             if (is_name) {
@@ -1787,9 +1806,69 @@ __global__ void literal_parse_kernel(LitArgs A) {
     }
 }
 
+// Long raw payloads (deferred by literal_parse_kernel): one wave per literal, 16 bytes per lane per round.  The
+// name rule needs the first upper-case letter's position (h2o_hpack_validate_header_name stops there, soft
+// errors count only before it), so lanes keep the first position of each kind and the wave takes minima.
+__global__ __launch_bounds__(256) void literal_long_kernel(LitArgs A) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nl = *A.long_count;
+    const bool copy = !(A.flags & kLitNoRawCopy);
+    for (uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6); w < nl; w += gridDim.x * 4u) {
+        const uint32_t i = A.long_list[w];
+        bool huff;
+        uint32_t hdr, len;
+        (void)lit_header(A, i, huff, hdr, len);  // verdict 0, raw: checked by the parse kernel
+        const bool is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) != 0 : false;
+        const uint64_t s0 = (uint64_t)A.lit_off[i] + hdr, e0 = s0 + len;
+        const uint8_t* src = A.in + s0;
+        const bool skip = is_name && ((A.flags & 1u) ? pseudo_token(src, len) : (len != 0 && src[0] == ':'));
+        const uint32_t* inval = is_name ? g_name_invalid : g_value_invalid;
+        uint8_t* dst = A.out + (s0 * 8u) / 5u;
+        uint32_t first_up = 0xFFFFFFFFu, first_soft = 0xFFFFFFFFu, anybad = 0;
+        for (uint64_t a = s0 + 16u * (uint32_t)lane; a < e0; a += 1024) {
+            uint8_t v[16];
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) v[k] = a + k < e0 ? A.in[a + k] : 0u;
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) {
+                if (a + k >= e0) break;
+                const uint32_t c = v[k];
+                const bool bad = ((inval[c >> 5] >> (c & 31)) & 1u) != 0;
+                const bool up = bad && (c - 'A' < 26u);
+                const uint32_t pos = (uint32_t)(a + k - s0);
+                anybad |= bad ? 1u : 0u;
+                if (up) first_up = min(first_up, pos);
+                if (bad && !up) first_soft = min(first_soft, pos);
+                if (copy) dst[pos] = (uint8_t)c;
+            }
+        }
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            first_up = min(first_up, (uint32_t)__shfl_xor((int)first_up, d));
+            first_soft = min(first_soft, (uint32_t)__shfl_xor((int)first_soft, d));
+            anybad |= (uint32_t)__shfl_xor((int)anybad, d);
+        }
+        if (lane == 0) {
+            uint32_t v = 0, soft = 0;
+            if (is_name) {
+                if (!skip) {  // h2o_hpack_validate_header_name: empty -> soft; upper case -> hard error
+                    soft = first_soft < first_up ? 0x1u : 0u;
+                    if (first_up != 0xFFFFFFFFu) v = kLitUpper;
+                }
+            } else {  // h2o_hpack_validate_header_value, with the whitespace rule (hpack.c:110-115)
+                const bool ws = src[0] == ' ' || src[0] == '\t' || src[len - 1] == ' ' || src[len - 1] == '\t';
+                soft = (anybad || ws) ? 0x2u : 0u;
+            }
+            A.consumed[i] = v == 0 ? hdr + len : 0u;
+            A.code[i] = (uint8_t)(v | (soft << 4));
+        }
+    }
+}
+
 // Pass 3: fold the header / raw verdicts into out_len and status (the Huffman kernel ran in between).
 __global__ void literal_fix_kernel(LitArgs A) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t n = A.n_dev ? (uint64_t)*A.n_dev : (uint64_t)A.n;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t c = A.code[i];
         const uint32_t v = c & 7u, soft = c >> 4;
         if (v) {
@@ -2008,7 +2087,7 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
                          const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
                          uint8_t* status, hipStream_t stream, uint64_t sel_bytes) {
     if (n == 0) return hipSuccess;
-    DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr, nullptr, nullptr, nullptr};
+    DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr, nullptr, nullptr, nullptr, nullptr};
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n);
     const int grid = grid_for(v, current_device(), n);
     const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr;
@@ -2218,7 +2297,7 @@ hipError_t launch_decode_packed(const uint8_t* in, uint64_t in_size, const uint3
     if (n == 0) return hipMemsetAsync(pk_off, 0, sizeof(uint32_t), stream);
     const uint64_t mean = in_size / n;
     if (mean > 128) return pack_via_scratch(true, in, in_size, in_off, n, is_name_bits, out, pk_off, out_len, status, stream);
-    DecArgs A{in, in_size, in_off, nullptr, n, is_name_bits, out, nullptr, out_len, status, nullptr, nullptr, nullptr, pk_off};
+    DecArgs A{in, in_size, in_off, nullptr, n, is_name_bits, out, nullptr, out_len, status, nullptr, nullptr, nullptr, pk_off, nullptr};
     const int v = mean <= 40 ? kDecSP : kDecLP;
     hipError_t e = alloc_edges(&A.edges, n, stream);
     if (e != hipSuccess) return e;
@@ -2308,7 +2387,7 @@ hipError_t launch_literals(const uint8_t* in, uint64_t in_size, const uint32_t* 
                            hipStream_t stream) {
     if (n == 0) return hipSuccess;
     LitArgs A{in, in_size, lit_off, lit_end, n, prefix_bits, flags, is_name_bits, out, out_len, pay_off, consumed, status,
-              huff_len, reinterpret_cast<uint8_t*>(huff_len + n)};
+              huff_len, reinterpret_cast<uint8_t*>(huff_len + n), nullptr, nullptr, nullptr};
     const uint32_t blocks = min((n + 255u) / 256u, 4096u);
     hipLaunchKernelGGL(literal_parse_kernel, dim3(blocks), dim3(256), 0, stream, A);
     hipError_t e = hipGetLastError();
@@ -2318,6 +2397,42 @@ hipError_t launch_literals(const uint8_t* in, uint64_t in_size, const uint32_t* 
     hipLaunchKernelGGL(literal_fix_kernel, dim3(blocks), dim3(256), 0, stream, A);
     return hipGetLastError();
 }
+
+// Literals whose count is only known on the device (the header-block pipeline, hhuff_blocks.hip): n_max
+// bounds the arrays, *n_dev is the count.  Huffman payloads go through the stream kernel, which takes its
+// strings from a work counter and so needs no host-side count.  ws: 5 n_max bytes + 16.
+hipError_t launch_literals_dev(const uint8_t* in, uint64_t in_size, const uint32_t* lit_off, uint32_t n_max,
+                               const uint32_t* n_dev, uint32_t prefix_bits, uint32_t flags, const uint32_t* is_name_bits,
+                               uint8_t* out, uint32_t* out_len, uint32_t* pay_off, uint32_t* consumed, uint8_t* status,
+                               uint8_t* ws, hipStream_t stream) {
+    if (n_max == 0) return hipSuccess;
+    // ws: huff_len u32[n_max], code u8[n_max], then (8-aligned) the stream counter u64, the long-literal
+    // count u32 (+ pad) and list u32[in_size / kLongRaw + 1]
+    uint32_t* huff_len = reinterpret_cast<uint32_t*>(ws);
+    uint8_t* tail = ws + 5ull * n_max + ((8 - (5ull * n_max) % 8) % 8);
+    unsigned long long* ctr = reinterpret_cast<unsigned long long*>(tail);
+    uint32_t* long_count = reinterpret_cast<uint32_t*>(tail + 8);
+    uint32_t* long_list = reinterpret_cast<uint32_t*>(tail + 16);
+    LitArgs A{in, in_size, lit_off, nullptr, n_max, prefix_bits, flags, is_name_bits, out, out_len, pay_off, consumed,
+              status, huff_len, reinterpret_cast<uint8_t*>(huff_len + n_max), n_dev, long_list, long_count};
+    const int dev = current_device();
+    const uint32_t blocks = min((n_max + 255u) / 256u, 8192u);
+    hipError_t e = hipMemsetAsync(tail, 0, 16, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(literal_parse_kernel, dim3(blocks), dim3(256), 0, stream, A);
+    hipLaunchKernelGGL(literal_long_kernel, dim3(1024), dim3(256), 0, stream, A);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    DecArgs D{in, in_size, pay_off, huff_len, n_max, is_name_bits, out, nullptr, out_len, status, nullptr, nullptr, nullptr,
+              nullptr, n_dev};
+    hipLaunchKernelGGL(DEC_T, dim3(grid_for(kDecT, dev, n_max)), dim3(kDecTWaves * 64), 0, stream, D, ctr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(literal_fix_kernel, dim3(blocks), dim3(256), 0, stream, A);
+    return hipGetLastError();
+}
+
+uint64_t literals_dev_ws(uint32_t n_max, uint64_t in_size) { return 5ull * n_max + 8 + 16 + 4 * (in_size / kLongRaw + 1); }
+
+hipError_t work_alloc(void** p, uint64_t bytes, hipStream_t stream) { return pool_alloc(p, bytes, stream); }
 
 int grid_size(int device, int which) { return grid_for(which == 0 ? kDecS : kEncS, device, 0xFFFFFFFFu); }
 

@@ -32,6 +32,17 @@ hipError_t launch_literals(const uint8_t* in, uint64_t in_size, const uint32_t* 
                            uint32_t prefix_bits, uint32_t flags, const uint32_t* is_name_bits, uint8_t* out,
                            uint32_t* out_len, uint32_t* pay_off, uint32_t* consumed, uint8_t* status, uint32_t* huff_len,
                            hipStream_t stream);
+// literals whose count lives in device memory (*n_dev <= n_max); ws: literals_dev_ws bytes.  flags: the
+// HHUFF_LIT_* flags, plus kLitNoRawCopy: raw payloads are validated but not copied to out
+constexpr uint32_t kLitNoRawCopy = 0x100u;
+hipError_t launch_literals_dev(const uint8_t* in, uint64_t in_size, const uint32_t* lit_off, uint32_t n_max,
+                               const uint32_t* n_dev, uint32_t prefix_bits, uint32_t flags, const uint32_t* is_name_bits,
+                               uint8_t* out, uint32_t* out_len, uint32_t* pay_off, uint32_t* consumed, uint8_t* status,
+                               uint8_t* ws, hipStream_t stream);
+uint64_t literals_dev_ws(uint32_t n_max, uint64_t in_size);
+// stream-ordered device memory from the library's pool (free with hipFreeAsync on the same stream)
+hipError_t work_alloc(void** p, uint64_t bytes, hipStream_t stream);
+
 // HPACK header blocks (f4): see include/hhuff.h hhuff_hpack_decode_blocks; scratch = nconn x
 // hpack_conn_scratch(table_size) bytes of device memory
 uint64_t hpack_conn_scratch(uint32_t table_size);

@@ -182,7 +182,9 @@ int hhuff_decode_literals(const uint8_t *in, uint64_t in_size, const uint32_t *l
  *      earlier block of the connection failed: h2o drops the connection).  Fields before the error stand.
  *      Device arrays; scratch = device memory of hhuff_hpack_scratch_size(nconn, table_size) bytes (the
  *      dynamic tables, 16-byte aligned), kept by the caller between calls for HHUFF_BLK_CONTINUE;
- *      asynchronous on `stream`. */
+ *      asynchronous on `stream`.  The call also takes a stream-ordered workspace of about 16 bytes per input
+ *      byte from the library's device memory pool (the literal pre-pass and the field sources; released
+ *      on the stream, kept by the pool for the next call). */
 #define HHUFF_BLK_CONTINUE 1u /* flags: the tables (and failed state) the previous call left in scratch
                                  carry over -- connection c of this call is connection c of that one; without
                                  it every connection starts with an empty table */

@@ -29,7 +29,8 @@ def main():
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
     d, bo, cf = dev(b["data"]), dev(b["blk_off"].view(np.int32)), dev(b["conn_first"].view(np.int32))
     L = np.diff(b["blk_off"].astype(np.int64))
-    ao = dev(np.concatenate([[0], np.cumsum(16 * L + 1024)]).astype(np.int64))
+    fa, fb = (int(x) for x in os.environ.get("HHUFF_AB_ARENA", "16,1024").split(","))  # arena bytes per block: fa L + fb
+    ao = dev(np.concatenate([[0], np.cumsum(fa * L + fb)]).astype(np.int64))
     nblk = len(L)
     nslots = int(b["blk_off"][-1])
     out = {k: torch.empty(nslots, dtype=torch.int32, device="cuda") for k in ("no", "nl", "vo", "vl")}
