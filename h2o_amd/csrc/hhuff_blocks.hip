@@ -147,21 +147,6 @@ __device__ int64_t blk_decode_int(const Win& in, uint64_t& p, uint64_t end, uint
     if (v > 0x7FFFFFFFFFFFFFFFull) return kIntBad;
     return (int64_t)v;
 }
-// Byte copies in batches of 16: the 16 loads issue back to back and one wait covers them, instead of a
-// load-to-store round trip per byte (a lane's strings sit at unrelated addresses, so nothing coalesces).
-template <typename Src, typename Dst>
-__device__ __forceinline__ void copy16(Src src, Dst dst, uint32_t n) {
-    for (uint32_t i = 0; i < n; i += 16) {
-        uint8_t t[16];
-#pragma unroll
-        for (uint32_t k = 0; k < 16; ++k)
-            if (i + k < n) t[k] = src(i + k);
-#pragma unroll
-        for (uint32_t k = 0; k < 16; ++k)
-            if (i + k < n) dst(i + k, t[k]);
-    }
-}
-
 // The wave copies 64 byte segments at once (lane i holds segment i: src, dst, len; len 0 = none) in 16-byte
 // pieces spread over all lanes, so a long segment does not serialise one lane: every 64 pieces cost one
 // round trip.  Piece t belongs to the last lane k whose piece prefix excl[k] <= t (binary search by lanes).
@@ -882,7 +867,9 @@ __global__ __launch_bounds__(kMarkThreads) void blk_list_kernel(const uint32_t* 
                                                                const uint32_t* __restrict__ name_bits, uint64_t nwords,
                                                                const uint32_t* __restrict__ chunk_pre,
                                                                uint32_t* __restrict__ word_pre,
-                                                               uint32_t* __restrict__ lit_off, uint32_t* __restrict__ lnames) {
+                                                               uint32_t* __restrict__ lit_off, uint32_t* __restrict__ lnames,
+                                                               const uint32_t* __restrict__ pfx_bits, uint32_t pfx_alt,
+                                                               uint8_t* __restrict__ prefix_of) {
     __shared__ uint32_t sh[kMarkThreads / 64];
     constexpr uint32_t K = kChunkWords / kMarkThreads;
     const uint64_t w0 = (uint64_t)blockIdx.x * kChunkWords + threadIdx.x * K;
@@ -900,15 +887,31 @@ __global__ __launch_bounds__(kMarkThreads) void blk_list_kernel(const uint32_t* 
         word_pre[w0 + k] = r;
         uint32_t m = bits[k];
         const uint32_t nm = m ? name_bits[w0 + k] : 0u;
+        const uint32_t pm = m && prefix_of ? pfx_bits[w0 + k] : 0u;
         while (m) {
             const uint32_t bit = (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
             lit_off[r] = (uint32_t)(32u * (w0 + k) + bit);
             if ((nm >> bit) & 1u) atomicOr(lnames + (r >> 5), 1u << (r & 31));
+            if (prefix_of) prefix_of[r] = (uint8_t)(((pm >> bit) & 1u) ? pfx_alt : 7u);
             ++r;
         }
     }
 }
+uint64_t literal_list_chunks(uint64_t nwords) { return (nwords + kChunkWords - 1) / kChunkWords; }
+
+hipError_t launch_literal_list(const uint32_t* lit_bits, const uint32_t* name_bits, const uint32_t* pfx_bits, uint32_t pfx_alt,
+                               uint64_t nwords, uint32_t* chunk, uint32_t* word_pre, uint32_t* list, uint32_t* lnames,
+                               uint8_t* prefix_of, hipStream_t stream) {
+    const uint64_t nchunks = literal_list_chunks(nwords);
+    hipLaunchKernelGGL(blk_count_kernel, dim3((uint32_t)nchunks), dim3(kMarkThreads), 0, stream, lit_bits, nwords, chunk);
+    hipLaunchKernelGGL(blk_chunk_scan_kernel, dim3(1), dim3(kMarkThreads), 0, stream, chunk, (uint32_t)nchunks,
+                       chunk + nchunks);
+    hipLaunchKernelGGL(blk_list_kernel, dim3((uint32_t)nchunks), dim3(kMarkThreads), 0, stream, lit_bits, name_bits, nwords,
+                       chunk, word_pre, list, lnames, pfx_bits, pfx_alt, prefix_of);
+    return hipGetLastError();
+}
+
 uint64_t hpack_conn_scratch(uint32_t table_size) {
     return sizeof(TableState) + (uint64_t)tbl_entries(table_size) * sizeof(Entry) + 2 * tbl_ring(table_size);
 }
@@ -967,12 +970,9 @@ hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32
         uint32_t* list = reinterpret_cast<uint32_t*>(work + o_list);
         hipLaunchKernelGGL(blk_mark_kernel, dim3(2048), dim3(kMarkThreads), 0, stream, in, in_size, blk_off, conn_first,
                            nconn, lit_bits, name_bits);
-        hipLaunchKernelGGL(blk_count_kernel, dim3((uint32_t)nchunks), dim3(kMarkThreads), 0, stream, lit_bits, nwords,
-                           chunk);
-        hipLaunchKernelGGL(blk_chunk_scan_kernel, dim3(1), dim3(kMarkThreads), 0, stream, chunk, (uint32_t)nchunks, n_lit);
-        hipLaunchKernelGGL(blk_list_kernel, dim3((uint32_t)nchunks), dim3(kMarkThreads), 0, stream, lit_bits, name_bits,
-                           nwords, chunk, word_pre, list, lnames);
         e = hipGetLastError();
+        if (e == hipSuccess)
+            e = launch_literal_list(lit_bits, name_bits, nullptr, 7u, nwords, chunk, word_pre, list, lnames, nullptr, stream);
         if (e == hipSuccess)
             e = launch_literals_dev(in, in_size, list, (uint32_t)n_max, n_lit, 7u, kLitNoRawCopy, lnames, work + o_out,
                                     reinterpret_cast<uint32_t*>(work + o_len), reinterpret_cast<uint32_t*>(work + o_pay),

@@ -336,6 +336,21 @@ __device__ __forceinline__ void lds_move_or(uint32_t src, uint32_t dst, uint32_t
     }
 }
 
+// Byte copies in batches of 16: the 16 loads issue back to back and one wait covers them, instead of a
+// load-to-store round trip per byte (a lane's strings sit at unrelated addresses, so nothing coalesces).
+template <typename Src, typename Dst>
+__device__ __forceinline__ void copy16(Src src, Dst dst, uint32_t n) {
+    for (uint32_t i = 0; i < n; i += 16) {
+        uint8_t t[16];
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k)
+            if (i + k < n) t[k] = src(i + k);
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k)
+            if (i + k < n) dst(i + k, t[k]);
+    }
+}
+
 // Zero LDS bytes [a, b) of a wave's buffer (a, b multiples of 16), 16-B stores by the whole wave.
 __device__ __forceinline__ void lds_zero(uint8_t* base, uint32_t a, uint32_t b, int lane) {
     for (uint32_t k = a + 16u * (uint32_t)lane; k < b; k += 1024u)

@@ -1676,6 +1676,7 @@ struct LitArgs {
     const uint32_t* n_dev;  // NULL, or the literal count in device memory (n is then an upper bound)
     uint32_t* long_list;    // NULL, or: raw payloads longer than kLongRaw are validated by literal_long_kernel
     uint32_t* long_count;
+    const uint8_t* prefix_of;  // NULL, or each literal's own prefix_bits
 };
 
 constexpr uint32_t kLongRaw = 512;  // raw payload bytes above which one wave validates the literal
@@ -1690,7 +1691,7 @@ __device__ __forceinline__ uint32_t lit_header(const LitArgs& A, uint32_t i, boo
     hdr = 0;
     len = 0;
     if (off >= end) return kLitIncomplete;
-    const uint32_t p = A.prefix_bits;
+    const uint32_t p = A.prefix_of ? A.prefix_of[i] : A.prefix_bits;
     const uint32_t b0 = A.in[off];
     huff = ((b0 >> p) & 1u) != 0;
     const uint64_t pmax = (1u << p) - 1u;
@@ -2387,7 +2388,7 @@ hipError_t launch_literals(const uint8_t* in, uint64_t in_size, const uint32_t* 
                            hipStream_t stream) {
     if (n == 0) return hipSuccess;
     LitArgs A{in, in_size, lit_off, lit_end, n, prefix_bits, flags, is_name_bits, out, out_len, pay_off, consumed, status,
-              huff_len, reinterpret_cast<uint8_t*>(huff_len + n), nullptr, nullptr, nullptr};
+              huff_len, reinterpret_cast<uint8_t*>(huff_len + n), nullptr, nullptr, nullptr, nullptr};
     const uint32_t blocks = min((n + 255u) / 256u, 4096u);
     hipLaunchKernelGGL(literal_parse_kernel, dim3(blocks), dim3(256), 0, stream, A);
     hipError_t e = hipGetLastError();
@@ -2404,7 +2405,7 @@ hipError_t launch_literals(const uint8_t* in, uint64_t in_size, const uint32_t* 
 hipError_t launch_literals_dev(const uint8_t* in, uint64_t in_size, const uint32_t* lit_off, uint32_t n_max,
                                const uint32_t* n_dev, uint32_t prefix_bits, uint32_t flags, const uint32_t* is_name_bits,
                                uint8_t* out, uint32_t* out_len, uint32_t* pay_off, uint32_t* consumed, uint8_t* status,
-                               uint8_t* ws, hipStream_t stream) {
+                               uint8_t* ws, hipStream_t stream, const uint8_t* prefix_of) {
     if (n_max == 0) return hipSuccess;
     // ws: huff_len u32[n_max], code u8[n_max], then (8-aligned) the stream counter u64, the long-literal
     // count u32 (+ pad) and list u32[in_size / kLongRaw + 1]
@@ -2414,7 +2415,7 @@ hipError_t launch_literals_dev(const uint8_t* in, uint64_t in_size, const uint32
     uint32_t* long_count = reinterpret_cast<uint32_t*>(tail + 8);
     uint32_t* long_list = reinterpret_cast<uint32_t*>(tail + 16);
     LitArgs A{in, in_size, lit_off, nullptr, n_max, prefix_bits, flags, is_name_bits, out, out_len, pay_off, consumed,
-              status, huff_len, reinterpret_cast<uint8_t*>(huff_len + n_max), n_dev, long_list, long_count};
+              status, huff_len, reinterpret_cast<uint8_t*>(huff_len + n_max), n_dev, long_list, long_count, prefix_of};
     const int dev = current_device();
     const uint32_t blocks = min((n_max + 255u) / 256u, 8192u);
     hipError_t e = hipMemsetAsync(tail, 0, 16, stream);

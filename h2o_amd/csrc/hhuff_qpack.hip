@@ -68,6 +68,15 @@ struct QpkArgs {
     uint8_t* scratch;
     uint64_t conn_scratch;
     uint32_t flags;
+    // pre-decoded encoder-stream literals (launch_qpack's pre-pass): bit p of lit_bits marks a literal whose
+    // header starts at input byte p; word_pre[w] counts the marks before word w; literal r has the literal
+    // kernels' results lit_len / lit_st, its bytes at lit_out + floor(8 payload / 5) (Huffman) or in the
+    // input (raw).  NULL lit_bits: every literal is decoded in place.
+    const uint32_t* lit_bits;
+    const uint32_t* word_pre;
+    const uint32_t* lit_len;
+    const uint8_t* lit_st;
+    const uint8_t* lit_out;
 };
 
 // per-connection scratch: [QState 64 B][byte ring RB = max(2T, 16) rounded to 16][entry ring E x 16 B]
@@ -235,24 +244,39 @@ struct QTable {  // one connection's table, as the kernels see it
     }
 };
 
+// the pre-decoded literal whose header is at input byte p, or -1: not marked, or a verdict other than
+// success (the in-place path then reproduces the reference's exact failure)
+__device__ __forceinline__ int64_t q_pre(const QpkArgs& A, uint64_t p) {
+    if (!A.lit_bits) return -1;
+    const uint32_t w = A.lit_bits[p >> 5], m = 1u << (p & 31);
+    if (!(w & m)) return -1;
+    const uint32_t r = A.word_pre[p >> 5] + (uint32_t)__builtin_popcount(w & (m - 1u));
+    return ((A.lit_st[r] >> 2) & 7u) == 0 ? (int64_t)r : -1;
+}
+
 // writes n bytes get(0..n-1) at ring[pos...], at most `room` of them
 template <class Get>
 __device__ void ring_put(QTable& t, uint32_t pos, Get get, uint64_t n, uint32_t room) {
-    const uint64_t m = n < room ? n : room;
-    for (uint64_t i = 0; i < m; ++i) {
-        t.ring[pos] = (uint8_t)get(i);
-        pos = pos + 1 == t.RB ? 0u : pos + 1;
-    }
+    const uint32_t m = (uint32_t)(n < room ? n : room), RB = t.RB;
+    uint8_t* ring = t.ring;
+    copy16([&](uint32_t i) { return (uint8_t)get(i); },
+           [&](uint32_t i, uint8_t v) { ring[pos + i >= RB ? pos + i - RB : pos + i] = v; }, m);
 }
 
 // the value half of an insert (decode_value_and_insert :273-287) once the name sits at ring[w0, +nlen)
+// (pre: the value's pre-decoded literal, or -1)
 __device__ int32_t q_value_and_insert(QTable& t, const QpkArgs& A, uint32_t w0, uint64_t nlen, uint32_t soft,
-                                      bool vhuff, uint64_t vp, uint64_t vlen, const DecTables& T) {
+                                      bool vhuff, uint64_t vp, uint64_t vlen, int64_t pre, const DecTables& T) {
     const uint32_t cap = A.T;
     const uint32_t room = nlen < cap ? cap - (uint32_t)nlen : 0u;
     const uint32_t vpos = (uint32_t)(((uint64_t)w0 + (nlen < cap ? nlen : cap)) % t.RB);
     uint64_t r;
-    if (vhuff) {
+    if (pre >= 0) {
+        r = A.lit_len[pre];
+        soft |= A.lit_st[pre] & 3u;
+        const uint8_t* src = vhuff ? A.lit_out + (vp * 8u) / 5u : A.in + vp;
+        ring_put(t, vpos, [&](uint64_t i) { return (uint32_t)src[i]; }, r, room);
+    } else if (vhuff) {
         if (vlen > kMaxStrLen) return kDF;
         RingSinkFL sk{t.ring, t.RB, vpos, 0u, room, 0u, 0u};
         const DecResult d = decode_core(GlobalSource{A.in, A.in_size}, (uint32_t)vp, (uint32_t)vlen, sk, T);
@@ -287,6 +311,7 @@ __device__ int32_t q_handle_input(QTable& t, const QpkArgs& A, uint64_t p, uint6
                 const bool name_is_static = (b & 0x40u) != 0;
                 if ((ret = q_int(name_index, in, p, end, 6)) != 0) goto Exit;
                 if (p == end) goto Exit;
+                const int64_t vpre = q_pre(A, p);
                 const bool vhuff = (in[p] & 0x80u) != 0;
                 if ((ret = q_int(value_len, in, p, end, 7)) != 0) goto Exit;
                 if (!((uint64_t)value_len <= end - p)) goto Exit;
@@ -298,7 +323,7 @@ __device__ int32_t q_handle_input(QTable& t, const QpkArgs& A, uint64_t p, uint6
                         const uint32_t k = 4u * (uint32_t)name_index;
                         const uint32_t no = q_static_ent[k], nl = q_static_ent[k + 1];
                         ring_put(t, w0, [&](uint64_t i) { return (uint32_t)q_static_bytes[no + i]; }, nl, A.T);
-                        ret = q_value_and_insert(t, A, w0, nl, 0u, vhuff, p, (uint64_t)value_len, T);
+                        ret = q_value_and_insert(t, A, w0, nl, 0u, vhuff, p, (uint64_t)value_len, vpre, T);
                     }
                 } else {  // dynamic (:335-348): token names carry no name bit, literal names keep theirs
                     const int64_t base_index = t.total() - 1;
@@ -307,7 +332,7 @@ __device__ int32_t q_handle_input(QTable& t, const QpkArgs& A, uint64_t p, uint6
                         ret = kDF;
                     } else {
                         ring_put(t, w0, [&](uint64_t i) { return t.at(e.x + (uint32_t)i); }, e.y, A.T);
-                        ret = q_value_and_insert(t, A, w0, e.y, e.w & 0x1u, vhuff, p, (uint64_t)value_len, T);
+                        ret = q_value_and_insert(t, A, w0, e.y, e.w & 0x1u, vhuff, p, (uint64_t)value_len, vpre, T);
                     }
                 }
                 p += (uint64_t)value_len;
@@ -316,10 +341,12 @@ __device__ int32_t q_handle_input(QTable& t, const QpkArgs& A, uint64_t p, uint6
             case 3: {  // insert without name reference (:446-462, :352-393)
                 int64_t name_len, value_len;
                 const bool nhuff = (b & 0x20u) != 0;
+                const int64_t npre = q_pre(A, p);
                 if ((ret = q_int(name_len, in, p, end, 5)) != 0) goto Exit;
                 if (!((uint64_t)name_len < end - p)) goto Exit;
                 const uint64_t qn = p;
                 p += (uint64_t)name_len;
+                const int64_t vpre = q_pre(A, p);
                 const bool vhuff = (in[p] & 0x80u) != 0;
                 if ((ret = q_int(value_len, in, p, end, 7)) != 0) goto Exit;
                 if (!((uint64_t)value_len <= end - p)) goto Exit;
@@ -327,7 +354,12 @@ __device__ int32_t q_handle_input(QTable& t, const QpkArgs& A, uint64_t p, uint6
                 const uint32_t w0 = t.s.whead;
                 uint64_t nl = 0;
                 bool ok = true;
-                if (nhuff) {
+                if (npre >= 0) {  // decoded and validated by the pre-pass
+                    nl = A.lit_len[npre];
+                    soft = A.lit_st[npre] & 3u;
+                    const uint8_t* src = nhuff ? A.lit_out + (qn * 8u) / 5u : in + qn;
+                    ring_put(t, w0, [&](uint64_t i) { return (uint32_t)src[i]; }, nl, A.T);
+                } else if (nhuff) {
                     if ((uint64_t)name_len > kMaxStrLen) {
                         ok = false;
                     } else {
@@ -350,7 +382,7 @@ __device__ int32_t q_handle_input(QTable& t, const QpkArgs& A, uint64_t p, uint6
                     // a name h2o_lookup_token knows goes in as a token header with soft bits 0 (:383-384)
                     if (soft && nl <= A.T && q_pseudo_token([&](uint64_t i) { return t.at(w0 + (uint32_t)i); }, nl))
                         soft = 0;
-                    ret = q_value_and_insert(t, A, w0, nl, soft, vhuff, p, (uint64_t)value_len, T);
+                    ret = q_value_and_insert(t, A, w0, nl, soft, vhuff, p, (uint64_t)value_len, vpre, T);
                 }
                 p += (uint64_t)value_len;
             } break;
@@ -408,7 +440,10 @@ __global__ __launch_bounds__(256) void qpack_encoder_kernel(QpkArgs A) {
     __shared__ uint32_t s_kinfo[32];
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
     load_dec_tables(s_lut, s_kinfo, s_ones);
-    const DecTables T{s_lut, s_kinfo, s_ones};
+    DecTables T;  // assigned, not brace-initialised (see hhuff_blocks.hip)
+    T.lut = s_lut;
+    T.kinfo = s_kinfo;
+    T.ones = s_ones;
     for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < A.nconn; c += (uint64_t)gridDim.x * blockDim.x) {
         QState* ps = reinterpret_cast<QState*>(A.scratch + c * A.conn_scratch);
         if (!(A.flags & HHUFF_QPK_CONTINUE)) {  // h2o_qpack_create_decoder (:240-252)
@@ -492,7 +527,8 @@ struct QArena {
 
 __device__ __forceinline__ int32_t q_copy_static(QArena& R, uint32_t so, uint32_t n, uint32_t& off) {
     if (R.cur + n > R.end) return HHUFF_QPK_ARENA;
-    for (uint32_t i = 0; i < n; ++i) R.a[R.cur + i] = q_static_bytes[so + i];
+    uint8_t* d = R.a + R.cur;
+    copy16([&](uint32_t i) { return q_static_bytes[so + i]; }, [&](uint32_t i, uint8_t v) { d[i] = v; }, n);
     off = (uint32_t)R.cur;
     R.cur += n;
     return 0;
@@ -501,10 +537,11 @@ __device__ __forceinline__ int32_t q_copy_static(QArena& R, uint32_t so, uint32_
 __device__ __forceinline__ int32_t q_copy_ring(QArena& R, const QTable& t, uint32_t ro, uint32_t n, uint32_t& off) {
     if (R.cur + n > R.end) return HHUFF_QPK_ARENA;
     if (ro >= t.RB) ro -= t.RB;
-    for (uint32_t i = 0; i < n; ++i) {
-        R.a[R.cur + i] = t.ring[ro];
-        ro = ro + 1 == t.RB ? 0u : ro + 1;
-    }
+    uint8_t* d = R.a + R.cur;
+    const uint8_t* ring = t.ring;
+    const uint32_t RB = t.RB;
+    copy16([&](uint32_t i) { return ring[ro + i >= RB ? ro + i - RB : ro + i]; }, [&](uint32_t i, uint8_t v) { d[i] = v; },
+           n);
     off = (uint32_t)R.cur;
     R.cur += n;
     return 0;
@@ -539,7 +576,8 @@ __device__ int32_t q_literal(const QpkArgs& A, QArena& R, uint32_t& soft, uint64
             q_valid_value(get, (uint64_t)n, soft);
         }
         if (R.cur + (uint64_t)n > R.end) return HHUFF_QPK_ARENA;
-        for (int64_t i = 0; i < n; ++i) R.a[R.cur + i] = src[i];
+        uint8_t* d = R.a + R.cur;
+        copy16([&](uint32_t i) { return src[i]; }, [&](uint32_t i, uint8_t v) { d[i] = v; }, (uint32_t)n);
         len = (uint32_t)n;
     }
     off = (uint32_t)R.cur;
@@ -614,7 +652,10 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
     __shared__ uint32_t s_kinfo[32];
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
     load_dec_tables(s_lut, s_kinfo, s_ones);
-    const DecTables T{s_lut, s_kinfo, s_ones};
+    DecTables T;  // assigned, not brace-initialised (see hhuff_blocks.hip)
+    T.lut = s_lut;
+    T.kinfo = s_kinfo;
+    T.ones = s_ones;
     const uint32_t max_entries = A.T / kEntryOverhead;
     for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < A.nsec; k += (uint64_t)gridDim.x * blockDim.x) {
         // the section's connection: the last c with conn_first[c] <= k
@@ -682,6 +723,52 @@ __global__ __launch_bounds__(256) void qpack_blocked_kernel(QpkArgs A) {
     }
 }
 
+// ---- encoder-stream literal pre-pass ----
+// An encoder stream's instructions are readable without the table (name indexes and literal lengths are
+// explicit, qpack.c:420-474), so one lane per connection finds every literal the walk could reach and the
+// literal kernels decode them all together, balanced across connections; the walk (qpack_encoder_kernel)
+// then copies bytes instead of running a Huffman decoder per lane.  Marks past a table-dependent error (an
+// index the table does not hold) are decoded and unused.
+
+// the literal with `prefix`-bit length at p inside [p, end): mark it, step over it
+__device__ __forceinline__ bool q_mark_literal(const uint8_t* in, uint64_t& p, uint64_t end, uint32_t prefix,
+                                               uint32_t* __restrict__ lit_bits, uint32_t* __restrict__ name_bits) {
+    uint64_t q = p;
+    const int64_t n = q_hpack_int(in, q, end, prefix);
+    if (n < 0 || (uint64_t)n > end - q) return false;
+    atomicOr(lit_bits + (p >> 5), 1u << (p & 31));
+    if (prefix == 5) atomicOr(name_bits + (p >> 5), 1u << (p & 31));
+    p = q + (uint64_t)n;
+    return true;
+}
+
+__global__ __launch_bounds__(256) void qpack_mark_kernel(const uint8_t* __restrict__ in,
+                                                        const uint32_t* __restrict__ enc_off,
+                                                        const uint32_t* __restrict__ enc_len, uint32_t nconn,
+                                                        uint32_t* __restrict__ lit_bits, uint32_t* __restrict__ name_bits) {
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nconn; c += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t p = enc_off[c];
+        const uint64_t end = p + enc_len[c];
+        bool go = true;
+        while (go && p < end) {  // the instruction switch of q_handle_input
+            const uint32_t b = in[p];
+            switch (b >> 5) {
+                default:  // insert with name reference: index, then the value
+                    go = q_hpack_int(in, p, end, 6) >= 0 && p < end &&
+                         q_mark_literal(in, p, end, 7, lit_bits, name_bits);
+                    break;
+                case 2:
+                case 3:  // insert with a literal name: the name (5-bit prefix), then the value
+                    go = q_mark_literal(in, p, end, 5, lit_bits, name_bits) && p < end &&
+                         q_mark_literal(in, p, end, 7, lit_bits, name_bits);
+                    break;
+                case 0:
+                case 1: go = q_hpack_int(in, p, end, 5) >= 0; break;  // duplicate, set capacity
+            }
+        }
+    }
+}
+
 uint64_t qpack_conn_scratch(uint32_t header_table_size) {
     return sizeof(QState) + qpk_ring_bytes(header_table_size) + 16ull * (header_table_size / kEntryOverhead + 1u);
 }
@@ -697,9 +784,58 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
     QpkArgs A{in, in_size, enc_off, enc_len, sec_off, conn_first, num_blocked, nconn, nsec, header_table_size,
               max_blocked, arena, arena_off, name_off, name_len, value_off, value_len, fflags, nfields, sstatus,
               req_insert_count, enc_status, enc_consumed, insert_count, scratch, qpack_conn_scratch(header_table_size),
-              flags};
-    hipLaunchKernelGGL(qpack_encoder_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
-    hipError_t e = hipGetLastError();
+              flags, nullptr, nullptr, nullptr, nullptr, nullptr};
+    // literal pre-pass workspace (inputs below 4 GiB: u32 positions): bitmaps, word prefixes, chunk sums, the
+    // literal list with each literal's prefix, the literal kernels' results, the decoded bytes
+    const bool prepass = in_size > 0 && in_size < (1ull << 32);
+    const uint64_t nwords = (in_size + 31) / 32, nchunks = literal_list_chunks(nwords);
+    const uint64_t n_max = in_size + 2;  // every literal header takes a byte
+    auto up = [](uint64_t x) { return (x + 255) & ~255ull; };
+    const uint64_t o_lit = 0, o_name = o_lit + up(4 * nwords), o_lnames = o_name + up(4 * nwords);
+    const uint64_t zero_end = o_lnames + up(4 * ((n_max + 31) / 32));  // [0, zero_end) starts zeroed
+    const uint64_t o_pre = zero_end, o_chunk = o_pre + up(4 * nwords), o_list = o_chunk + up(4 * nchunks + 4);
+    const uint64_t o_pfx = o_list + up(4 * n_max), o_len = o_pfx + up(n_max), o_pay = o_len + up(4 * n_max);
+    const uint64_t o_cons = o_pay + up(4 * n_max), o_st = o_cons + up(4 * n_max), o_ws = o_st + up(n_max);
+    const uint64_t o_out = o_ws + up(literals_dev_ws((uint32_t)n_max, in_size));
+    const uint64_t wbytes = o_out + up((8 * in_size) / 5 + 64);
+    uint8_t* work = nullptr;
+    hipError_t e = hipSuccess;
+    if (prepass) {
+        e = work_alloc((void**)&work, wbytes, stream);
+        if (e == hipSuccess) e = hipMemsetAsync(work, 0, zero_end, stream);
+        uint32_t* lit_bits = reinterpret_cast<uint32_t*>(work + o_lit);
+        uint32_t* name_bits = reinterpret_cast<uint32_t*>(work + o_name);
+        uint32_t* chunk = reinterpret_cast<uint32_t*>(work + o_chunk);
+        uint32_t* list = reinterpret_cast<uint32_t*>(work + o_list);
+        uint32_t* word_pre = reinterpret_cast<uint32_t*>(work + o_pre);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(qpack_mark_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, in,
+                               enc_off, enc_len, nconn, lit_bits, name_bits);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess)  // names are exactly the 5-bit-prefix literals
+            e = launch_literal_list(lit_bits, name_bits, name_bits, 5u, nwords, chunk, word_pre, list,
+                                    reinterpret_cast<uint32_t*>(work + o_lnames), work + o_pfx, stream);
+        if (e == hipSuccess)
+            e = launch_literals_dev(in, in_size, list, (uint32_t)n_max, chunk + nchunks, 7u,
+                                    HHUFF_LIT_QPACK | kLitNoRawCopy, reinterpret_cast<uint32_t*>(work + o_lnames),
+                                    work + o_out, reinterpret_cast<uint32_t*>(work + o_len),
+                                    reinterpret_cast<uint32_t*>(work + o_pay), reinterpret_cast<uint32_t*>(work + o_cons),
+                                    work + o_st, work + o_ws, stream, work + o_pfx);
+        A.lit_bits = lit_bits;
+        A.word_pre = word_pre;
+        A.lit_len = reinterpret_cast<const uint32_t*>(work + o_len);
+        A.lit_st = work + o_st;
+        A.lit_out = work + o_out;
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(qpack_encoder_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
+        e = hipGetLastError();
+    }
+    if (work) {
+        const hipError_t f = hipFreeAsync(work, stream);
+        if (e == hipSuccess) e = f;
+    }
     if (e != hipSuccess || nsec == 0) return e;
     hipLaunchKernelGGL(qpack_sections_kernel, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
     e = hipGetLastError();
