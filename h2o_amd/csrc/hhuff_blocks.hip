@@ -147,38 +147,6 @@ __device__ int64_t blk_decode_int(const Win& in, uint64_t& p, uint64_t end, uint
     if (v > 0x7FFFFFFFFFFFFFFFull) return kIntBad;
     return (int64_t)v;
 }
-// The wave copies 64 byte segments at once (lane i holds segment i: src, dst, len; len 0 = none) in 16-byte
-// pieces spread over all lanes, so a long segment does not serialise one lane: every 64 pieces cost one
-// round trip.  Piece t belongs to the last lane k whose piece prefix excl[k] <= t (binary search by lanes).
-__device__ void wave_copy64(const uint8_t* src, uint8_t* dst, uint32_t len, int lane) {
-    const uint32_t chunks = (len + 15u) >> 4;
-    const uint32_t excl = wave_excl_scan(chunks, lane);
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(excl + chunks), 63);
-    for (uint32_t t0 = 0; t0 < total; t0 += 64) {
-        const uint32_t t = t0 + (uint32_t)lane;
-        int k = 0;
-#pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-            const uint32_t e = (uint32_t)__shfl((int)excl, k + step);
-            k += e <= t ? step : 0;
-        }
-        const uint32_t c = t - (uint32_t)__shfl((int)excl, k);
-        const uint8_t* s = (const uint8_t*)__shfl((long long)(uintptr_t)src, k);
-        uint8_t* d = (uint8_t*)__shfl((long long)(uintptr_t)dst, k);
-        const uint32_t n = (uint32_t)__shfl((int)len, k);
-        if (t < total) {
-            const uint32_t a = 16u * c, m = min(16u, n - a);
-            uint8_t v[16];
-#pragma unroll
-            for (uint32_t j = 0; j < 16; ++j)
-                if (j < m) v[j] = s[a + j];
-#pragma unroll
-            for (uint32_t j = 0; j < 16; ++j)
-                if (j < m) d[a + j] = v[j];
-        }
-    }
-}
-
 struct DynTable {  // one connection's dynamic table (newest entry = dynamic index 62)
     Entry* ent;
     uint32_t E, start, num;
@@ -869,7 +837,7 @@ __global__ __launch_bounds__(kMarkThreads) void blk_list_kernel(const uint32_t* 
                                                                uint32_t* __restrict__ word_pre,
                                                                uint32_t* __restrict__ lit_off, uint32_t* __restrict__ lnames,
                                                                const uint32_t* __restrict__ pfx_bits, uint32_t pfx_alt,
-                                                               uint8_t* __restrict__ prefix_of) {
+                                                               uint32_t pfx_name, uint8_t* __restrict__ prefix_of) {
     __shared__ uint32_t sh[kMarkThreads / 64];
     constexpr uint32_t K = kChunkWords / kMarkThreads;
     const uint64_t w0 = (uint64_t)blockIdx.x * kChunkWords + threadIdx.x * K;
@@ -893,7 +861,7 @@ __global__ __launch_bounds__(kMarkThreads) void blk_list_kernel(const uint32_t* 
             m &= m - 1u;
             lit_off[r] = (uint32_t)(32u * (w0 + k) + bit);
             if ((nm >> bit) & 1u) atomicOr(lnames + (r >> 5), 1u << (r & 31));
-            if (prefix_of) prefix_of[r] = (uint8_t)(((pm >> bit) & 1u) ? pfx_alt : 7u);
+            if (prefix_of) prefix_of[r] = (uint8_t)(((pm >> bit) & 1u) ? pfx_alt : ((nm >> bit) & 1u) ? pfx_name : 7u);
             ++r;
         }
     }
@@ -901,14 +869,14 @@ __global__ __launch_bounds__(kMarkThreads) void blk_list_kernel(const uint32_t* 
 uint64_t literal_list_chunks(uint64_t nwords) { return (nwords + kChunkWords - 1) / kChunkWords; }
 
 hipError_t launch_literal_list(const uint32_t* lit_bits, const uint32_t* name_bits, const uint32_t* pfx_bits, uint32_t pfx_alt,
-                               uint64_t nwords, uint32_t* chunk, uint32_t* word_pre, uint32_t* list, uint32_t* lnames,
+                               uint32_t pfx_name, uint64_t nwords, uint32_t* chunk, uint32_t* word_pre, uint32_t* list, uint32_t* lnames,
                                uint8_t* prefix_of, hipStream_t stream) {
     const uint64_t nchunks = literal_list_chunks(nwords);
     hipLaunchKernelGGL(blk_count_kernel, dim3((uint32_t)nchunks), dim3(kMarkThreads), 0, stream, lit_bits, nwords, chunk);
     hipLaunchKernelGGL(blk_chunk_scan_kernel, dim3(1), dim3(kMarkThreads), 0, stream, chunk, (uint32_t)nchunks,
                        chunk + nchunks);
     hipLaunchKernelGGL(blk_list_kernel, dim3((uint32_t)nchunks), dim3(kMarkThreads), 0, stream, lit_bits, name_bits, nwords,
-                       chunk, word_pre, list, lnames, pfx_bits, pfx_alt, prefix_of);
+                       chunk, word_pre, list, lnames, pfx_bits, pfx_alt, pfx_name, prefix_of);
     return hipGetLastError();
 }
 
@@ -972,7 +940,7 @@ hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32
                            nconn, lit_bits, name_bits);
         e = hipGetLastError();
         if (e == hipSuccess)
-            e = launch_literal_list(lit_bits, name_bits, nullptr, 7u, nwords, chunk, word_pre, list, lnames, nullptr, stream);
+            e = launch_literal_list(lit_bits, name_bits, nullptr, 7u, 7u, nwords, chunk, word_pre, list, lnames, nullptr, stream);
         if (e == hipSuccess)
             e = launch_literals_dev(in, in_size, list, (uint32_t)n_max, n_lit, 7u, kLitNoRawCopy, lnames, work + o_out,
                                     reinterpret_cast<uint32_t*>(work + o_len), reinterpret_cast<uint32_t*>(work + o_pay),

@@ -351,6 +351,38 @@ __device__ __forceinline__ void copy16(Src src, Dst dst, uint32_t n) {
     }
 }
 
+// The wave copies 64 byte segments at once (lane i holds segment i: src, dst, len; len 0 = none) in 16-byte
+// pieces spread over all lanes, so a long segment does not serialise one lane: every 64 pieces cost one
+// round trip.  Piece t belongs to the last lane k whose piece prefix excl[k] <= t (binary search by lanes).
+__device__ void wave_copy64(const uint8_t* src, uint8_t* dst, uint32_t len, int lane) {
+    const uint32_t chunks = (len + 15u) >> 4;
+    const uint32_t excl = wave_excl_scan(chunks, lane);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(excl + chunks), 63);
+    for (uint32_t t0 = 0; t0 < total; t0 += 64) {
+        const uint32_t t = t0 + (uint32_t)lane;
+        int k = 0;
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const uint32_t e = (uint32_t)__shfl((int)excl, k + step);
+            k += e <= t ? step : 0;
+        }
+        const uint32_t c = t - (uint32_t)__shfl((int)excl, k);
+        const uint8_t* s = (const uint8_t*)__shfl((long long)(uintptr_t)src, k);
+        uint8_t* d = (uint8_t*)__shfl((long long)(uintptr_t)dst, k);
+        const uint32_t n = (uint32_t)__shfl((int)len, k);
+        if (t < total) {
+            const uint32_t a = 16u * c, m = min(16u, n - a);
+            uint8_t v[16];
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j)
+                if (j < m) v[j] = s[a + j];
+#pragma unroll
+            for (uint32_t j = 0; j < 16; ++j)
+                if (j < m) d[a + j] = v[j];
+        }
+    }
+}
+
 // Zero LDS bytes [a, b) of a wave's buffer (a, b multiples of 16), 16-B stores by the whole wave.
 __device__ __forceinline__ void lds_zero(uint8_t* base, uint32_t a, uint32_t b, int lane) {
     for (uint32_t k = a + 16u * (uint32_t)lane; k < b; k += 1024u)

@@ -42,11 +42,11 @@ hipError_t launch_literals_dev(const uint8_t* in, uint64_t in_size, const uint32
 uint64_t literals_dev_ws(uint32_t n_max, uint64_t in_size);
 // The literal list of marked input bytes (hhuff_blocks.hip): bit p of lit_bits marks a literal at byte p.
 // Writes word_pre (marks before each bitmap word), list (positions in order), lnames (bit r set when the
-// literal's name_bits bit is), prefix_of[r] = pfx_bits bit ? pfx_alt : 7 (when prefix_of is given) and
-// *n_lit = chunk[nchunks]; chunk: u32[literal_list_chunks(nwords) + 1] of workspace.
+// literal's name_bits bit is), prefix_of[r] (when given) = pfx_alt if its pfx_bits bit is set, else pfx_name for
+// a name, else 7, and *n_lit = chunk[nchunks]; chunk: u32[literal_list_chunks(nwords) + 1] of workspace.
 uint64_t literal_list_chunks(uint64_t nwords);
 hipError_t launch_literal_list(const uint32_t* lit_bits, const uint32_t* name_bits, const uint32_t* pfx_bits, uint32_t pfx_alt,
-                               uint64_t nwords, uint32_t* chunk, uint32_t* word_pre, uint32_t* list, uint32_t* lnames,
+                               uint32_t pfx_name, uint64_t nwords, uint32_t* chunk, uint32_t* word_pre, uint32_t* list, uint32_t* lnames,
                                uint8_t* prefix_of, hipStream_t stream);
 // stream-ordered device memory from the library's pool (free with hipFreeAsync on the same stream)
 hipError_t work_alloc(void** p, uint64_t bytes, hipStream_t stream);

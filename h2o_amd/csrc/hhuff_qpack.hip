@@ -76,7 +76,12 @@ struct QpkArgs {
     const uint32_t* word_pre;
     const uint32_t* lit_len;
     const uint8_t* lit_st;
+    const uint8_t* lit_pfx;  // the prefix literal r was decoded with
     const uint8_t* lit_out;
+    // deferred section copies (with the pre-pass): per field slot, the address of its name's / value's
+    // bytes (0: already in the arena); qpack_copy_kernel moves them.  NULL: the sections kernel copies.
+    uint64_t* fsrc_n;
+    uint64_t* fsrc_v;
 };
 
 // per-connection scratch: [QState 64 B][byte ring RB = max(2T, 16) rounded to 16][entry ring E x 16 B]
@@ -244,14 +249,17 @@ struct QTable {  // one connection's table, as the kernels see it
     }
 };
 
-// the pre-decoded literal whose header is at input byte p, or -1: not marked, or a verdict other than
-// success (the in-place path then reproduces the reference's exact failure)
-__device__ __forceinline__ int64_t q_pre(const QpkArgs& A, uint64_t p) {
+// pre-pass literal marks (qpack_mark_kernel): names are the 5-bit-prefix literals (encoder stream) and the
+// 3-bit-prefix ones (sections, also in p3_bits); everything else is a value (7-bit prefix)
+// the pre-decoded literal whose header is at input byte p, or -1: not marked, decoded with another prefix
+// (input regions that overlap), or a verdict other than success (the in-place path then reproduces the
+// reference's exact failure)
+__device__ __forceinline__ int64_t q_pre(const QpkArgs& A, uint64_t p, uint32_t prefix) {
     if (!A.lit_bits) return -1;
     const uint32_t w = A.lit_bits[p >> 5], m = 1u << (p & 31);
     if (!(w & m)) return -1;
     const uint32_t r = A.word_pre[p >> 5] + (uint32_t)__builtin_popcount(w & (m - 1u));
-    return ((A.lit_st[r] >> 2) & 7u) == 0 ? (int64_t)r : -1;
+    return ((A.lit_st[r] >> 2) & 7u) == 0 && A.lit_pfx[r] == prefix ? (int64_t)r : -1;
 }
 
 // writes n bytes get(0..n-1) at ring[pos...], at most `room` of them
@@ -311,7 +319,7 @@ __device__ int32_t q_handle_input(QTable& t, const QpkArgs& A, uint64_t p, uint6
                 const bool name_is_static = (b & 0x40u) != 0;
                 if ((ret = q_int(name_index, in, p, end, 6)) != 0) goto Exit;
                 if (p == end) goto Exit;
-                const int64_t vpre = q_pre(A, p);
+                const int64_t vpre = q_pre(A, p, 7);
                 const bool vhuff = (in[p] & 0x80u) != 0;
                 if ((ret = q_int(value_len, in, p, end, 7)) != 0) goto Exit;
                 if (!((uint64_t)value_len <= end - p)) goto Exit;
@@ -341,12 +349,12 @@ __device__ int32_t q_handle_input(QTable& t, const QpkArgs& A, uint64_t p, uint6
             case 3: {  // insert without name reference (:446-462, :352-393)
                 int64_t name_len, value_len;
                 const bool nhuff = (b & 0x20u) != 0;
-                const int64_t npre = q_pre(A, p);
+                const int64_t npre = q_pre(A, p, 5);
                 if ((ret = q_int(name_len, in, p, end, 5)) != 0) goto Exit;
                 if (!((uint64_t)name_len < end - p)) goto Exit;
                 const uint64_t qn = p;
                 p += (uint64_t)name_len;
-                const int64_t vpre = q_pre(A, p);
+                const int64_t vpre = q_pre(A, p, 7);
                 const bool vhuff = (in[p] & 0x80u) != 0;
                 if ((ret = q_int(value_len, in, p, end, 7)) != 0) goto Exit;
                 if (!((uint64_t)value_len <= end - p)) goto Exit;
@@ -525,38 +533,68 @@ struct QArena {
     uint64_t cur, end;
 };
 
-__device__ __forceinline__ int32_t q_copy_static(QArena& R, uint32_t so, uint32_t n, uint32_t& off) {
+// a field string's bytes go to arena[off, off + n): recorded for qpack_copy_kernel (fs = their address), or
+// copied now (no deferred copies)
+__device__ __forceinline__ void q_put(const QpkArgs& A, const uint8_t* src, uint32_t off, uint32_t n, uint64_t& fs) {
+    if (A.fsrc_n) {
+        fs = (uint64_t)(uintptr_t)src;
+        return;
+    }
+    uint8_t* d = A.arena + off;
+    copy16([&](uint32_t i) { return src[i]; }, [&](uint32_t i, uint8_t v) { d[i] = v; }, n);
+    fs = 0;
+}
+
+__device__ __forceinline__ int32_t q_copy_static(const QpkArgs& A, QArena& R, uint32_t so, uint32_t n, uint32_t& off,
+                                                 uint64_t& fs) {
     if (R.cur + n > R.end) return HHUFF_QPK_ARENA;
-    uint8_t* d = R.a + R.cur;
-    copy16([&](uint32_t i) { return q_static_bytes[so + i]; }, [&](uint32_t i, uint8_t v) { d[i] = v; }, n);
     off = (uint32_t)R.cur;
+    q_put(A, q_static_bytes + so, off, n, fs);
     R.cur += n;
     return 0;
 }
 
-__device__ __forceinline__ int32_t q_copy_ring(QArena& R, const QTable& t, uint32_t ro, uint32_t n, uint32_t& off) {
+__device__ __forceinline__ int32_t q_copy_ring(const QpkArgs& A, QArena& R, const QTable& t, uint32_t ro, uint32_t n,
+                                               uint32_t& off, uint64_t& fs) {
     if (R.cur + n > R.end) return HHUFF_QPK_ARENA;
     if (ro >= t.RB) ro -= t.RB;
-    uint8_t* d = R.a + R.cur;
-    const uint8_t* ring = t.ring;
-    const uint32_t RB = t.RB;
-    copy16([&](uint32_t i) { return ring[ro + i >= RB ? ro + i - RB : ro + i]; }, [&](uint32_t i, uint8_t v) { d[i] = v; },
-           n);
     off = (uint32_t)R.cur;
     R.cur += n;
+    const uint32_t RB = t.RB;
+    if (ro + n <= RB) {
+        q_put(A, t.ring + ro, off, n, fs);
+        return 0;
+    }
+    uint8_t* d = A.arena + off;  // wraps around the ring end: copied here
+    const uint8_t* ring = t.ring;
+    copy16([&](uint32_t i) { return ring[ro + i >= RB ? ro + i - RB : ro + i]; }, [&](uint32_t i, uint8_t v) { d[i] = v; },
+           n);
+    fs = 0;
     return 0;
 }
 
 // decode_header_value_literal (qpack.c:603-629) / decode_header_name_literal (:559-601, prefix 3)
 __device__ int32_t q_literal(const QpkArgs& A, QArena& R, uint32_t& soft, uint64_t& p, uint64_t end, bool is_name,
-                             uint32_t& off, uint32_t& len, const DecTables& T) {
+                             uint32_t& off, uint32_t& len, uint64_t& fs, const DecTables& T) {
     const uint8_t* in = A.in;
     if (!is_name && !(p < end)) return kDF;
     const uint32_t prefix = is_name ? 3u : 7u;
     const bool huff = ((in[p] >> prefix) & 1u) != 0;
+    const int64_t pre = q_pre(A, p, prefix);
     int64_t n;
     if (q_int(n, in, p, end, prefix) != 0) return kDF;
     if ((int64_t)(end - p) < n) return kDF;
+    fs = 0;
+    if (pre >= 0) {  // decoded and validated by the pre-pass; the reference's order of checks holds
+        if (R.cur + (huff ? ((uint64_t)n * 8u) / 5u : (uint64_t)n) > R.end) return HHUFF_QPK_ARENA;
+        len = A.lit_len[pre];
+        soft |= A.lit_st[pre] & 3u;
+        off = (uint32_t)R.cur;
+        q_put(A, huff ? A.lit_out + (p * 8u) / 5u : in + p, off, len, fs);
+        R.cur += len;
+        p += (uint64_t)n;
+        return 0;
+    }
     if (huff) {
         if (R.cur + ((uint64_t)n * 8u) / 5u > R.end) return HHUFF_QPK_ARENA;
         if ((uint64_t)n > kMaxStrLen) return kDF;
@@ -589,7 +627,7 @@ __device__ int32_t q_literal(const QpkArgs& A, QArena& R, uint32_t& soft, uint64
 // decode_header (qpack.c:652-752): 0 / kErrInvalidChar = a field was produced
 __device__ int32_t q_field(const QpkArgs& A, const QTable& t, const QCtx& ctx, uint64_t& p, uint64_t end, QArena& R,
                            uint32_t& noff, uint32_t& nlen, uint32_t& voff, uint32_t& vlen, uint32_t& soft_out,
-                           const DecTables& T) {
+                           uint64_t& fn, uint64_t& fv, const DecTables& T) {
     const uint8_t* in = A.in;
     uint32_t soft = 0;
     int32_t r;
@@ -604,9 +642,9 @@ __device__ int32_t q_field(const QpkArgs& A, const QTable& t, const QCtx& ctx, u
             if (q_int(si, in, p, end, 6) != 0 || (uint64_t)si >= kQStaticCount) return kDF;
             const uint32_t k = 4u * (uint32_t)si;
             nlen = q_static_ent[k + 1];
-            if ((r = q_copy_static(R, q_static_ent[k], nlen, noff)) != 0) return r;
+            if ((r = q_copy_static(A, R, q_static_ent[k], nlen, noff, fn)) != 0) return r;
             vlen = q_static_ent[k + 3];
-            if ((r = q_copy_static(R, q_static_ent[k + 2], vlen, voff)) != 0) return r;
+            if ((r = q_copy_static(A, R, q_static_ent[k + 2], vlen, voff, fv)) != 0) return r;
         } break;
         case 8:
         case 9:
@@ -614,8 +652,8 @@ __device__ int32_t q_field(const QpkArgs& A, const QTable& t, const QCtx& ctx, u
         case 11:  // indexed field line, dynamic (:670-682)
         case 1:   // indexed field line, post-base (:713-722)
             if (!q_dyn(t, ctx, in, p, end, kind == 1 ? 4u : 6u, kind == 1, e)) return kDF;
-            if ((r = q_copy_ring(R, t, e.x, e.y, noff)) != 0) return r;
-            if ((r = q_copy_ring(R, t, e.x + e.y, e.z, voff)) != 0) return r;
+            if ((r = q_copy_ring(A, R, t, e.x, e.y, noff, fn)) != 0) return r;
+            if ((r = q_copy_ring(A, R, t, e.x + e.y, e.z, voff, fv)) != 0) return r;
             nlen = e.y;
             vlen = e.z;
             soft = e.w;
@@ -626,21 +664,21 @@ __device__ int32_t q_field(const QpkArgs& A, const QTable& t, const QCtx& ctx, u
             if (q_int(si, in, p, end, 4) != 0 || (uint64_t)si >= kQStaticCount) return kDF;
             const uint32_t k = 4u * (uint32_t)si;
             nlen = q_static_ent[k + 1];
-            if ((r = q_copy_static(R, q_static_ent[k], nlen, noff)) != 0) return r;
-            if ((r = q_literal(A, R, soft, p, end, false, voff, vlen, T)) != 0) return r;
+            if ((r = q_copy_static(A, R, q_static_ent[k], nlen, noff, fn)) != 0) return r;
+            if ((r = q_literal(A, R, soft, p, end, false, voff, vlen, fv, T)) != 0) return r;
         } break;
         case 4:
         case 6:  // literal field line, dynamic name reference (:693-704)
         case 0:  // literal field line, post-base name reference (:723-733)
             if (!q_dyn(t, ctx, in, p, end, kind == 0 ? 3u : 4u, kind == 0, e)) return kDF;
-            if ((r = q_copy_ring(R, t, e.x, e.y, noff)) != 0) return r;
+            if ((r = q_copy_ring(A, R, t, e.x, e.y, noff, fn)) != 0) return r;
             nlen = e.y;
             soft = e.w & 0x1u;
-            if ((r = q_literal(A, R, soft, p, end, false, voff, vlen, T)) != 0) return r;
+            if ((r = q_literal(A, R, soft, p, end, false, voff, vlen, fv, T)) != 0) return r;
             break;
         default:  // 2, 3: literal field line with a literal name (:705-712)
-            if ((r = q_literal(A, R, soft, p, end, true, noff, nlen, T)) != 0) return r;
-            if ((r = q_literal(A, R, soft, p, end, false, voff, vlen, T)) != 0) return r;
+            if ((r = q_literal(A, R, soft, p, end, true, noff, nlen, fn, T)) != 0) return r;
+            if ((r = q_literal(A, R, soft, p, end, false, voff, vlen, fv, T)) != 0) return r;
             break;
     }
     soft_out = soft;
@@ -689,10 +727,15 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
         uint32_t nf = 0;
         while (st == 0 && p != end) {
             uint32_t no = 0, nl = 0, vo = 0, vl = 0, soft = 0;
-            const int32_t rc = q_field(A, t, ctx, p, end, R, no, nl, vo, vl, soft, T);
+            uint64_t fn = 0, fv = 0;
+            const int32_t rc = q_field(A, t, ctx, p, end, R, no, nl, vo, vl, soft, fn, fv, T);
             if (rc != 0 && rc != kErrInvalidChar) {
                 st = rc;
                 break;
+            }
+            if (A.fsrc_n) {
+                A.fsrc_n[slot + nf] = fn;
+                A.fsrc_v[slot + nf] = fv;
             }
             A.name_off[slot + nf] = no;
             A.name_len[slot + nf] = nl;
@@ -703,6 +746,28 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
         }
         A.nfields[k] = nf;
         A.sstatus[k] = st;
+    }
+}
+
+// Copy pass (with the pre-pass): one wave per section, 32 fields (64 name / value segments) per round
+// through wave_copy64.  A failed section's fields up to the failure are copied too, as the in-lane path does.
+__global__ __launch_bounds__(256) void qpack_copy_kernel(QpkArgs A) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nw = gridDim.x * 4u;
+    for (uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6); k < A.nsec; k += nw) {
+        const uint32_t s0 = A.sec_off[k], nf = A.nfields[k];
+        for (uint32_t g = 0; g < nf; g += 32) {
+            const uint32_t fi = g + ((uint32_t)lane >> 1), f = s0 + fi;
+            const bool val = lane & 1;
+            uint32_t len = 0, off = 0;
+            uint64_t src = 0;
+            if (fi < nf) {
+                src = val ? A.fsrc_v[f] : A.fsrc_n[f];
+                len = src ? (val ? A.value_len[f] : A.name_len[f]) : 0u;
+                off = val ? A.value_off[f] : A.name_off[f];
+            }
+            wave_copy64(reinterpret_cast<const uint8_t*>(src), A.arena + off, len, lane);
+        }
     }
 }
 
@@ -730,37 +795,61 @@ __global__ __launch_bounds__(256) void qpack_blocked_kernel(QpkArgs A) {
 // then copies bytes instead of running a Huffman decoder per lane.  Marks past a table-dependent error (an
 // index the table does not hold) are decoded and unused.
 
+struct QMarks {
+    uint32_t *lit, *name, *p3;
+};
+
 // the literal with `prefix`-bit length at p inside [p, end): mark it, step over it
 __device__ __forceinline__ bool q_mark_literal(const uint8_t* in, uint64_t& p, uint64_t end, uint32_t prefix,
-                                               uint32_t* __restrict__ lit_bits, uint32_t* __restrict__ name_bits) {
+                                               const QMarks& M) {
+    if (p >= end) return false;
     uint64_t q = p;
     const int64_t n = q_hpack_int(in, q, end, prefix);
     if (n < 0 || (uint64_t)n > end - q) return false;
-    atomicOr(lit_bits + (p >> 5), 1u << (p & 31));
-    if (prefix == 5) atomicOr(name_bits + (p >> 5), 1u << (p & 31));
+    const uint32_t w = (uint32_t)(p >> 5), m = 1u << (p & 31);
+    atomicOr(M.lit + w, m);
+    if (prefix != 7) atomicOr(M.name + w, m);
+    if (prefix == 3) atomicOr(M.p3 + w, m);
     p = q + (uint64_t)n;
     return true;
 }
 
-__global__ __launch_bounds__(256) void qpack_mark_kernel(const uint8_t* __restrict__ in,
-                                                        const uint32_t* __restrict__ enc_off,
-                                                        const uint32_t* __restrict__ enc_len, uint32_t nconn,
-                                                        uint32_t* __restrict__ lit_bits, uint32_t* __restrict__ name_bits) {
-    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nconn; c += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t p = enc_off[c];
-        const uint64_t end = p + enc_len[c];
+// one lane per encoder stream (items [0, nconn)) or field section (the rest)
+__global__ __launch_bounds__(256) void qpack_mark_kernel(QpkArgs A, QMarks M) {
+    const uint8_t* in = A.in;
+    const uint64_t nitems = (uint64_t)A.nconn + A.nsec;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nitems; c += (uint64_t)gridDim.x * blockDim.x) {
+        if (c >= A.nconn) {  // a section: the decode context, then the representation switch of q_field
+            const uint64_t k = c - A.nconn;
+            uint64_t p = A.sec_off[k];
+            const uint64_t end = A.sec_off[k + 1];
+            bool go = q_hpack_int(in, p, end, 8) >= 0 && p < end && q_hpack_int(in, p, end, 7) >= 0;
+            while (go && p < end) {
+                const uint32_t kind = in[p] >> 4;
+                if (kind >= 8) {  // indexed, static or dynamic
+                    go = q_hpack_int(in, p, end, 6) >= 0;
+                } else if (kind == 1) {  // indexed, post-base
+                    go = q_hpack_int(in, p, end, 4) >= 0;
+                } else if (kind == 2 || kind == 3) {  // literal name, then the value
+                    go = q_mark_literal(in, p, end, 3, M) && q_mark_literal(in, p, end, 7, M);
+                } else {  // name reference (static / dynamic 4 bits, post-base 3), then the value
+                    go = q_hpack_int(in, p, end, kind == 0 ? 3 : 4) >= 0 && q_mark_literal(in, p, end, 7, M);
+                }
+            }
+            continue;
+        }
+        uint64_t p = A.enc_off[c];
+        const uint64_t end = p + A.enc_len[c];
         bool go = true;
         while (go && p < end) {  // the instruction switch of q_handle_input
             const uint32_t b = in[p];
             switch (b >> 5) {
                 default:  // insert with name reference: index, then the value
-                    go = q_hpack_int(in, p, end, 6) >= 0 && p < end &&
-                         q_mark_literal(in, p, end, 7, lit_bits, name_bits);
+                    go = q_hpack_int(in, p, end, 6) >= 0 && q_mark_literal(in, p, end, 7, M);
                     break;
                 case 2:
                 case 3:  // insert with a literal name: the name (5-bit prefix), then the value
-                    go = q_mark_literal(in, p, end, 5, lit_bits, name_bits) && p < end &&
-                         q_mark_literal(in, p, end, 7, lit_bits, name_bits);
+                    go = q_mark_literal(in, p, end, 5, M) && q_mark_literal(in, p, end, 7, M);
                     break;
                 case 0:
                 case 1: go = q_hpack_int(in, p, end, 5) >= 0; break;  // duplicate, set capacity
@@ -784,20 +873,22 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
     QpkArgs A{in, in_size, enc_off, enc_len, sec_off, conn_first, num_blocked, nconn, nsec, header_table_size,
               max_blocked, arena, arena_off, name_off, name_len, value_off, value_len, fflags, nfields, sstatus,
               req_insert_count, enc_status, enc_consumed, insert_count, scratch, qpack_conn_scratch(header_table_size),
-              flags, nullptr, nullptr, nullptr, nullptr, nullptr};
+              flags, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // literal pre-pass workspace (inputs below 4 GiB: u32 positions): bitmaps, word prefixes, chunk sums, the
     // literal list with each literal's prefix, the literal kernels' results, the decoded bytes
     const bool prepass = in_size > 0 && in_size < (1ull << 32);
     const uint64_t nwords = (in_size + 31) / 32, nchunks = literal_list_chunks(nwords);
     const uint64_t n_max = in_size + 2;  // every literal header takes a byte
     auto up = [](uint64_t x) { return (x + 255) & ~255ull; };
-    const uint64_t o_lit = 0, o_name = o_lit + up(4 * nwords), o_lnames = o_name + up(4 * nwords);
+    const uint64_t o_lit = 0, o_name = o_lit + up(4 * nwords), o_p3 = o_name + up(4 * nwords);
+    const uint64_t o_lnames = o_p3 + up(4 * nwords);
     const uint64_t zero_end = o_lnames + up(4 * ((n_max + 31) / 32));  // [0, zero_end) starts zeroed
     const uint64_t o_pre = zero_end, o_chunk = o_pre + up(4 * nwords), o_list = o_chunk + up(4 * nchunks + 4);
     const uint64_t o_pfx = o_list + up(4 * n_max), o_len = o_pfx + up(n_max), o_pay = o_len + up(4 * n_max);
     const uint64_t o_cons = o_pay + up(4 * n_max), o_st = o_cons + up(4 * n_max), o_ws = o_st + up(n_max);
     const uint64_t o_out = o_ws + up(literals_dev_ws((uint32_t)n_max, in_size));
-    const uint64_t wbytes = o_out + up((8 * in_size) / 5 + 64);
+    const uint64_t o_fsn = o_out + up((8 * in_size) / 5 + 64), o_fsv = o_fsn + up(8 * in_size + 8);
+    const uint64_t wbytes = o_fsv + up(8 * in_size + 8);  // field slots: one per input byte
     uint8_t* work = nullptr;
     hipError_t e = hipSuccess;
     if (prepass) {
@@ -808,13 +899,15 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
         uint32_t* chunk = reinterpret_cast<uint32_t*>(work + o_chunk);
         uint32_t* list = reinterpret_cast<uint32_t*>(work + o_list);
         uint32_t* word_pre = reinterpret_cast<uint32_t*>(work + o_pre);
+        uint32_t* p3_bits = reinterpret_cast<uint32_t*>(work + o_p3);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(qpack_mark_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, in,
-                               enc_off, enc_len, nconn, lit_bits, name_bits);
+            const uint64_t items = (uint64_t)nconn + nsec;
+            hipLaunchKernelGGL(qpack_mark_kernel, dim3((uint32_t)std::min<uint64_t>((items + 255) / 256, 65535)), dim3(256),
+                               0, stream, A, QMarks{lit_bits, name_bits, p3_bits});
             e = hipGetLastError();
         }
-        if (e == hipSuccess)  // names are exactly the 5-bit-prefix literals
-            e = launch_literal_list(lit_bits, name_bits, name_bits, 5u, nwords, chunk, word_pre, list,
+        if (e == hipSuccess)  // prefixes: section names 3, encoder-stream names 5, values 7
+            e = launch_literal_list(lit_bits, name_bits, p3_bits, 3u, 5u, nwords, chunk, word_pre, list,
                                     reinterpret_cast<uint32_t*>(work + o_lnames), work + o_pfx, stream);
         if (e == hipSuccess)
             e = launch_literals_dev(in, in_size, list, (uint32_t)n_max, chunk + nchunks, 7u,
@@ -826,22 +919,26 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
         A.word_pre = word_pre;
         A.lit_len = reinterpret_cast<const uint32_t*>(work + o_len);
         A.lit_st = work + o_st;
+        A.lit_pfx = work + o_pfx;
         A.lit_out = work + o_out;
+        A.fsrc_n = reinterpret_cast<uint64_t*>(work + o_fsn);
+        A.fsrc_v = reinterpret_cast<uint64_t*>(work + o_fsv);
     }
     if (e == hipSuccess) {
         hipLaunchKernelGGL(qpack_encoder_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess && nsec != 0) {
+        hipLaunchKernelGGL(qpack_sections_kernel, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
+        if (A.fsrc_n) hipLaunchKernelGGL(qpack_copy_kernel, dim3(4096), dim3(256), 0, stream, A);
+        hipLaunchKernelGGL(qpack_blocked_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
         e = hipGetLastError();
     }
     if (work) {
         const hipError_t f = hipFreeAsync(work, stream);
         if (e == hipSuccess) e = f;
     }
-    if (e != hipSuccess || nsec == 0) return e;
-    hipLaunchKernelGGL(qpack_sections_kernel, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(qpack_blocked_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
-    return hipGetLastError();
+    return e;
 }
 
 }  // namespace hhuff
