@@ -258,6 +258,7 @@ HHUFF_API int hhuff_qpack_decode(const uint8_t* in, uint64_t in_size, const uint
                  !sstatus || !req_insert_count))
         return arg_fail("NULL array");
     if (header_table_size > (1u << 30)) return arg_fail("header_table_size above 2^30");
+    if (in_size >= (1ull << 32)) return arg_fail("in_size must be below 2^32 (u32 offsets)");
     if (scratch_size < hhuff_qpack_scratch_size(nconn, header_table_size))
         return arg_fail("scratch smaller than hhuff_qpack_scratch_size");
     if (((uintptr_t)scratch & 15u) != 0) return arg_fail("scratch must be 16-byte aligned");

@@ -9,18 +9,22 @@
 //                   :559-629)
 //
 // Decomposition.  Unlike HPACK, a QPACK field section never changes the dynamic table: only the encoder
-// stream does.  So a step runs in two launches on the stream:
-//   qpack_encoder_kernel   one lane per connection applies its encoder-stream bytes, in order;
-//   qpack_sections_kernel  one lane per field SECTION (many per connection) decodes it against the table
-//                          the first launch left -- the wide, parallel part.
-// The table lives in per-connection scratch in HBM: a byte ring of 2 x header_table_size bytes and an
-// entry ring of header_table_size / 32 + 1 records {byte offset, name length, value length, soft bits},
-// oldest first, absolute index = base_offset + position as in h2o (base_offset starts at 1, :143).
-// Live entries hold at most max_size <= header_table_size bytes, so the free part of the byte ring is
-// always >= header_table_size bytes: a new entry is written (Huffman-decoded straight into the ring,
-// or copied from the static table, the input or a live entry -- its own name source included) before
-// the eviction it causes is booked, without ever touching a live byte.  Writes stop at
-// header_table_size bytes; anything longer fails the reference's size check anyway (:278-281).
+// stream does.  A step runs as passes on the stream:
+//   literal pre-pass       qpack_mark_kernel (one lane per encoder stream or section) marks every string
+//                          literal -- instructions and field lines are readable without the table -- and
+//                          the literal kernels decode them all, balanced across connections;
+//   qpack_encoder_kernel   one lane per connection applies its encoder-stream instructions in order, on
+//                          integers only: an entry is a pair of REFERENCES to where its name and value bytes
+//                          are (a pre-decoded literal, the input, the static table, or an entry's ring);
+//   qpack_table_kernel     one wave per connection whose table changed writes the live entries' bytes back
+//                          to back into its other ring and points the entries there;
+//   qpack_sections_kernel  one lane per field SECTION (many per connection) decodes it against that table,
+//                          recording each field string's source; qpack_copy_kernel (one wave per section)
+//                          moves the bytes into the arena.
+// The table lives in per-connection scratch in HBM: an entry ring of header_table_size / 32 + 1 records
+// {name source, value source, lengths, soft bits}, oldest first, absolute index = base_offset + position as
+// in h2o (base_offset starts at 1, :143), and two byte rings of header_table_size bytes (live entries hold
+// at most max_size <= header_table_size bytes).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -84,19 +88,43 @@ struct QpkArgs {
     uint64_t* fsrc_v;
 };
 
-// per-connection scratch: [QState 64 B][byte ring RB = max(2T, 16) rounded to 16][entry ring E x 16 B]
+// Byte sources of table entries and field strings: kind in the top 3 bits, offset below.  Every source stays
+// valid until the call's last pass has run; between calls the entries' sources are all kQScr (their
+// connection's ring in scratch), so a caller may keep scratch anywhere (offsets, not addresses).
+constexpr uint64_t kQLit = 0;              // lit_out offset (a literal the pre-pass decoded, or decoded in place)
+constexpr uint64_t kQStatic = 1ull << 61;  // static-table bytes
+constexpr uint64_t kQScr = 2ull << 61;     // scratch offset (a ring: bytes an earlier call's table pass wrote)
+constexpr uint64_t kQIn = 3ull << 61;      // input offset (a raw literal)
+constexpr uint64_t kQOff = (1ull << 61) - 1;
+
+__device__ __forceinline__ const uint8_t* q_src(const QpkArgs& A, uint64_t s) {
+    const uint64_t o = s & kQOff;
+    switch (s >> 61) {
+        case 0: return A.lit_out + o;
+        case 1: return q_static_bytes + o;
+        case 2: return A.scratch + o;
+        default: return A.in + o;
+    }
+}
+
+// per-connection scratch: [QState 64 B][entry ring E x 32 B][ring 0][ring 1] (rings: T rounded up to 16 B).
+// Live entries hold at most max_size <= T bytes, so the table pass (qpack_table_kernel) writes them back to
+// back into the ring they do not use now, reading their sources from the other one.
 struct QState {
     int64_t base_offset;
     uint64_t total_inserts, num_bytes, max_size;
-    uint32_t start, num, whead, failed;
-    uint32_t pad[4];
+    uint32_t start, num, ring, failed;  // ring: which ring holds the entries' bytes between calls
+    uint32_t dirty, pad[3];             // dirty: entries inserted by this call (the table pass rewrites)
 };
 static_assert(sizeof(QState) == 64, "QState layout");
+struct QEntry {  // one dynamic-table entry: references to its name and value bytes
+    uint64_t nsrc, vsrc;
+    uint32_t nl, vl, soft, pad;
+};
+static_assert(sizeof(QEntry) == 32, "QEntry layout");
 
-__host__ __device__ __forceinline__ uint32_t qpk_ring_bytes(uint32_t T) {
-    const uint32_t r = 2u * T < 16u ? 16u : 2u * T;
-    return (r + 15u) & ~15u;
-}
+__host__ __device__ __forceinline__ uint32_t qpk_ring_bytes(uint32_t T) { return ((T < 16u ? 16u : T) + 15u) & ~15u; }
+__host__ __device__ __forceinline__ uint32_t qpk_entries(uint32_t T) { return T / kEntryOverhead + 1u; }
 
 // h2o_hpack_decode_int (lib/http2/hpack.c:52-83) at in[p], bounded by end
 __device__ int64_t q_hpack_int(const uint8_t* __restrict__ in, uint64_t& p, uint64_t end, uint32_t prefix_bits) {
@@ -188,64 +216,39 @@ struct ArenaSinkFL {
     __device__ __forceinline__ uint32_t count() const { return s.count(); }
 };
 
-// byte-ring sink: writes the first `cap` bytes at ring[pos...] (wrapping), counts them all
-struct RingSinkFL {
-    uint8_t* ring;
-    uint32_t RB, pos, cnt, cap, first, last;
-    __device__ __forceinline__ void put1(uint32_t b) {
-        b &= 0xFFu;
-        first = cnt == 0 ? b : first;
-        last = b;
-        if (cnt < cap) {
-            ring[pos] = (uint8_t)b;
-            pos = pos + 1 == RB ? 0u : pos + 1;
-        }
-        ++cnt;
-    }
-    __device__ __forceinline__ void put12(uint32_t syms, bool two) {
-        put1(syms);
-        if (two) put1(syms >> 8);
-    }
-    __device__ __forceinline__ uint32_t count() const { return cnt; }
-};
-
 struct QTable {  // one connection's table, as the kernels see it
-    uint8_t* ring;
-    uint4* ent;  // {byte offset, name length, value length, soft bits}
-    uint32_t RB, E;
+    QEntry* ent;
+    uint32_t E;
     QState s;
-    __device__ __forceinline__ uint4 get(uint32_t k) const {  // k-th oldest live entry
-        uint32_t i = s.start + k;
-        return ent[i >= E ? i - E : i];
+    __device__ __forceinline__ uint32_t slot(uint32_t k) const {
+        const uint32_t i = s.start + k;
+        return i >= E ? i - E : i;
     }
+    __device__ __forceinline__ QEntry get(uint32_t k) const { return ent[slot(k)]; }  // k-th oldest live entry
     __device__ __forceinline__ int64_t total() const { return s.base_offset + (int64_t)s.num; }  // :321-324
-    __device__ __forceinline__ bool resolve_abs(int64_t index, uint4& e) const {  // resolve_dynamic_abs :201-213
+    __device__ __forceinline__ bool resolve_abs(int64_t index, QEntry& e) const {  // resolve_dynamic_abs :201-213
         if (index < s.base_offset || index - s.base_offset >= (int64_t)s.num) return false;
         e = get((uint32_t)(index - s.base_offset));
         return true;
     }
-    __device__ __forceinline__ uint32_t at(uint32_t off) const {  // off < 2 RB
-        return ring[off >= RB ? off - RB : off];
-    }
     __device__ void evict(uint64_t delta) {  // header_table_evict (:153-164)
         while (s.num != 0 && s.num_bytes + delta > s.max_size) {
-            const uint4 e = get(0);
-            s.num_bytes -= (uint64_t)e.y + e.z + kEntryOverhead;
+            const uint2 l = *reinterpret_cast<const uint2*>(&ent[s.start].nl);
+            s.num_bytes -= (uint64_t)l.x + l.y + kEntryOverhead;
             s.start = s.start + 1 == E ? 0u : s.start + 1;
             --s.num;
             ++s.base_offset;
         }
     }
-    // book an entry whose nlen + vlen bytes were written at ring[w0...] (header_table_insert :166-190)
-    __device__ void commit(uint32_t w0, uint32_t nlen, uint32_t vlen, uint32_t soft) {
-        const uint64_t add = (uint64_t)nlen + vlen + kEntryOverhead;
+    // header_table_insert (:166-190): the entry's bytes are references; the table pass writes them
+    __device__ void commit(const QEntry& e) {
+        const uint64_t add = (uint64_t)e.nl + e.vl + kEntryOverhead;
         evict(add);
-        const uint32_t i = s.start + s.num;
-        ent[i >= E ? i - E : i] = make_uint4(w0, nlen, vlen, soft);
+        ent[slot(s.num)] = e;
         ++s.num;
         s.num_bytes += add;
         ++s.total_inserts;
-        s.whead = (uint32_t)(((uint64_t)w0 + nlen + vlen) % RB);
+        s.dirty = 1;
     }
 };
 
@@ -255,50 +258,53 @@ struct QTable {  // one connection's table, as the kernels see it
 // (input regions that overlap), or a verdict other than success (the in-place path then reproduces the
 // reference's exact failure)
 __device__ __forceinline__ int64_t q_pre(const QpkArgs& A, uint64_t p, uint32_t prefix) {
-    if (!A.lit_bits) return -1;
     const uint32_t w = A.lit_bits[p >> 5], m = 1u << (p & 31);
     if (!(w & m)) return -1;
     const uint32_t r = A.word_pre[p >> 5] + (uint32_t)__builtin_popcount(w & (m - 1u));
     return ((A.lit_st[r] >> 2) & 7u) == 0 && A.lit_pfx[r] == prefix ? (int64_t)r : -1;
 }
 
-// writes n bytes get(0..n-1) at ring[pos...], at most `room` of them
-template <class Get>
-__device__ void ring_put(QTable& t, uint32_t pos, Get get, uint64_t n, uint32_t room) {
-    const uint32_t m = (uint32_t)(n < room ? n : room), RB = t.RB;
-    uint8_t* ring = t.ring;
-    copy16([&](uint32_t i) { return (uint8_t)get(i); },
-           [&](uint32_t i, uint8_t v) { ring[pos + i >= RB ? pos + i - RB : pos + i] = v; }, m);
+// An encoder-stream string literal (H flag at bit `prefix`, length, payload at p after the header): its
+// source and length.  Pre-decoded (pre >= 0): the pre-pass results.  Otherwise decoded here -- a Huffman
+// payload into lit_out at the place the pre-pass would have used (floor(8 p / 5)), a raw one validated
+// and referenced in the input -- with the reference's verdicts (qpack.c:222-237, :362-378).
+__device__ bool q_enc_string(const QpkArgs& A, bool huff, bool is_name, uint64_t p, uint64_t n, int64_t pre,
+                             uint64_t& src, uint32_t& len, uint32_t& soft, const DecTables& T) {
+    if (pre >= 0) {
+        len = A.lit_len[pre];
+        soft |= A.lit_st[pre] & 3u;
+        src = huff ? kQLit | ((p * 8u) / 5u) : kQIn | p;
+        return true;
+    }
+    if (huff) {
+        if (n > kMaxStrLen) return false;
+        ArenaSinkFL sk{RegSink{}, 0u, 0u};
+        sk.s.init(const_cast<uint8_t*>(A.lit_out) + (p * 8u) / 5u);
+        const DecResult d = decode_core(GlobalSource{A.in, A.in_size}, (uint32_t)p, (uint32_t)n, sk, T);
+        if (!d.ok) return false;
+        sk.s.finish();
+        soft |= soft_bits(is_name, d.len, d.flags, sk.first, sk.last);
+        len = d.len;
+        src = kQLit | ((p * 8u) / 5u);
+        return true;
+    }
+    const uint8_t* s = A.in + p;
+    if (is_name) {
+        if (!q_valid_name([&](uint64_t i) { return (uint32_t)s[i]; }, n, soft)) return false;
+    } else {
+        q_valid_value([&](uint64_t i) { return (uint32_t)s[i]; }, n, soft);
+    }
+    len = (uint32_t)n;
+    src = kQIn | p;
+    return true;
 }
 
-// the value half of an insert (decode_value_and_insert :273-287) once the name sits at ring[w0, +nlen)
-// (pre: the value's pre-decoded literal, or -1)
-__device__ int32_t q_value_and_insert(QTable& t, const QpkArgs& A, uint32_t w0, uint64_t nlen, uint32_t soft,
-                                      bool vhuff, uint64_t vp, uint64_t vlen, int64_t pre, const DecTables& T) {
-    const uint32_t cap = A.T;
-    const uint32_t room = nlen < cap ? cap - (uint32_t)nlen : 0u;
-    const uint32_t vpos = (uint32_t)(((uint64_t)w0 + (nlen < cap ? nlen : cap)) % t.RB);
-    uint64_t r;
-    if (pre >= 0) {
-        r = A.lit_len[pre];
-        soft |= A.lit_st[pre] & 3u;
-        const uint8_t* src = vhuff ? A.lit_out + (vp * 8u) / 5u : A.in + vp;
-        ring_put(t, vpos, [&](uint64_t i) { return (uint32_t)src[i]; }, r, room);
-    } else if (vhuff) {
-        if (vlen > kMaxStrLen) return kDF;
-        RingSinkFL sk{t.ring, t.RB, vpos, 0u, room, 0u, 0u};
-        const DecResult d = decode_core(GlobalSource{A.in, A.in_size}, (uint32_t)vp, (uint32_t)vlen, sk, T);
-        if (!d.ok) return kDF;
-        soft |= soft_bits(false, d.len, d.flags, sk.first, sk.last);
-        r = d.len;
-    } else {
-        const uint8_t* src = A.in + vp;
-        q_valid_value([&](uint64_t i) { return (uint32_t)src[i]; }, vlen, soft);
-        ring_put(t, vpos, [&](uint64_t i) { return (uint32_t)src[i]; }, vlen, room);
-        r = vlen;
-    }
-    if (nlen + r + kEntryOverhead > t.s.max_size) return kDF;  // header exceeds table size (:278-281)
-    t.commit(w0, (uint32_t)nlen, (uint32_t)r, soft);
+// the value half of an insert (decode_value_and_insert :273-287)
+__device__ int32_t q_value_and_insert(QTable& t, const QpkArgs& A, QEntry e, bool vhuff, uint64_t vp, uint64_t vlen,
+                                      int64_t pre, const DecTables& T) {
+    if (!q_enc_string(A, vhuff, false, vp, vlen, pre, e.vsrc, e.vl, e.soft, T)) return kDF;
+    if ((uint64_t)e.nl + e.vl + kEntryOverhead > t.s.max_size) return kDF;  // header exceeds table size (:278-281)
+    t.commit(e);
     return 0;
 }
 
@@ -323,24 +329,26 @@ __device__ int32_t q_handle_input(QTable& t, const QpkArgs& A, uint64_t p, uint6
                 const bool vhuff = (in[p] & 0x80u) != 0;
                 if ((ret = q_int(value_len, in, p, end, 7)) != 0) goto Exit;
                 if (!((uint64_t)value_len <= end - p)) goto Exit;
-                const uint32_t w0 = t.s.whead;
+                QEntry e{};
                 if (name_is_static) {  // insert_token_header (:289-300): soft starts at 0
                     if ((uint64_t)name_index >= kQStaticCount) {
                         ret = kDF;
                     } else {
                         const uint32_t k = 4u * (uint32_t)name_index;
-                        const uint32_t no = q_static_ent[k], nl = q_static_ent[k + 1];
-                        ring_put(t, w0, [&](uint64_t i) { return (uint32_t)q_static_bytes[no + i]; }, nl, A.T);
-                        ret = q_value_and_insert(t, A, w0, nl, 0u, vhuff, p, (uint64_t)value_len, vpre, T);
+                        e.nsrc = kQStatic | q_static_ent[k];
+                        e.nl = q_static_ent[k + 1];
+                        ret = q_value_and_insert(t, A, e, vhuff, p, (uint64_t)value_len, vpre, T);
                     }
                 } else {  // dynamic (:335-348): token names carry no name bit, literal names keep theirs
                     const int64_t base_index = t.total() - 1;
-                    uint4 e;
-                    if (name_index > base_index || !t.resolve_abs(base_index - name_index, e)) {
+                    QEntry r;
+                    if (name_index > base_index || !t.resolve_abs(base_index - name_index, r)) {
                         ret = kDF;
                     } else {
-                        ring_put(t, w0, [&](uint64_t i) { return t.at(e.x + (uint32_t)i); }, e.y, A.T);
-                        ret = q_value_and_insert(t, A, w0, e.y, e.w & 0x1u, vhuff, p, (uint64_t)value_len, vpre, T);
+                        e.nsrc = r.nsrc;
+                        e.nl = r.nl;
+                        e.soft = r.soft & 0x1u;
+                        ret = q_value_and_insert(t, A, e, vhuff, p, (uint64_t)value_len, vpre, T);
                     }
                 }
                 p += (uint64_t)value_len;
@@ -358,53 +366,26 @@ __device__ int32_t q_handle_input(QTable& t, const QpkArgs& A, uint64_t p, uint6
                 const bool vhuff = (in[p] & 0x80u) != 0;
                 if ((ret = q_int(value_len, in, p, end, 7)) != 0) goto Exit;
                 if (!((uint64_t)value_len <= end - p)) goto Exit;
-                uint32_t soft = 0;
-                const uint32_t w0 = t.s.whead;
-                uint64_t nl = 0;
-                bool ok = true;
-                if (npre >= 0) {  // decoded and validated by the pre-pass
-                    nl = A.lit_len[npre];
-                    soft = A.lit_st[npre] & 3u;
-                    const uint8_t* src = nhuff ? A.lit_out + (qn * 8u) / 5u : in + qn;
-                    ring_put(t, w0, [&](uint64_t i) { return (uint32_t)src[i]; }, nl, A.T);
-                } else if (nhuff) {
-                    if ((uint64_t)name_len > kMaxStrLen) {
-                        ok = false;
-                    } else {
-                        RingSinkFL sk{t.ring, t.RB, w0, 0u, A.T, 0u, 0u};
-                        const DecResult d =
-                            decode_core(GlobalSource{A.in, A.in_size}, (uint32_t)qn, (uint32_t)name_len, sk, T);
-                        ok = d.ok;
-                        if (ok) soft |= soft_bits(true, d.len, d.flags, sk.first, sk.last);
-                        nl = d.len;
-                    }
-                } else {
-                    const uint8_t* src = in + qn;
-                    ok = q_valid_name([&](uint64_t i) { return (uint32_t)src[i]; }, (uint64_t)name_len, soft);
-                    if (ok) ring_put(t, w0, [&](uint64_t i) { return (uint32_t)src[i]; }, (uint64_t)name_len, A.T);
-                    nl = (uint64_t)name_len;
-                }
-                if (!ok) {
+                QEntry e{};
+                if (!q_enc_string(A, nhuff, true, qn, (uint64_t)name_len, npre, e.nsrc, e.nl, e.soft, T)) {
                     ret = kDF;
                 } else {
                     // a name h2o_lookup_token knows goes in as a token header with soft bits 0 (:383-384)
-                    if (soft && nl <= A.T && q_pseudo_token([&](uint64_t i) { return t.at(w0 + (uint32_t)i); }, nl))
-                        soft = 0;
-                    ret = q_value_and_insert(t, A, w0, nl, soft, vhuff, p, (uint64_t)value_len, vpre, T);
+                    if (e.soft) {
+                        const uint8_t* nb = q_src(A, e.nsrc);
+                        if (q_pseudo_token([&](uint64_t i) { return (uint32_t)nb[i]; }, e.nl)) e.soft = 0;
+                    }
+                    ret = q_value_and_insert(t, A, e, vhuff, p, (uint64_t)value_len, vpre, T);
                 }
                 p += (uint64_t)value_len;
             } break;
             case 0: {  // duplicate (:463-468, :395-406)
                 int64_t index;
                 if ((ret = q_int(index, in, p, end, 5)) != 0) goto Exit;
-                if (index >= (int64_t)t.s.num) {
+                if (index >= (int64_t)t.s.num)
                     ret = kDF;
-                } else {
-                    const uint4 e = t.get(t.s.num - 1u - (uint32_t)index);
-                    const uint32_t w0 = t.s.whead;
-                    ring_put(t, w0, [&](uint64_t i) { return t.at(e.x + (uint32_t)i); }, (uint64_t)e.y + e.z, A.T);
-                    t.commit(w0, e.y, e.z, e.w);
-                }
+                else
+                    t.commit(t.get(t.s.num - 1u - (uint32_t)index));
             } break;
             case 1: {  // set dynamic table capacity (:469-474, :408-418)
                 int64_t max_size;
@@ -428,9 +409,7 @@ Exit:
 
 __device__ __forceinline__ QTable q_table(const QpkArgs& A, uint64_t c) {
     uint8_t* scr = A.scratch + c * A.conn_scratch;
-    const uint32_t RB = qpk_ring_bytes(A.T);
-    uint8_t* ring = scr + sizeof(QState);
-    QTable t{ring, reinterpret_cast<uint4*>(ring + RB), RB, A.T / kEntryOverhead + 1u, {}};
+    QTable t{reinterpret_cast<QEntry*>(scr + sizeof(QState)), qpk_entries(A.T), {}};
     t.s = *reinterpret_cast<const QState*>(scr);
     return t;
 }
@@ -461,6 +440,7 @@ __global__ __launch_bounds__(256) void qpack_encoder_kernel(QpkArgs A) {
             *ps = s0;
         }
         QTable t = q_table(A, c);
+        t.s.dirty = 0;
         int32_t st = 0;
         uint32_t consumed = 0;
         uint64_t ic = 0;
@@ -476,6 +456,43 @@ __global__ __launch_bounds__(256) void qpack_encoder_kernel(QpkArgs A) {
         A.insert_count[c] = ic;
         *ps = t.s;
     }
+}
+
+// Table pass: one wave per connection whose table took entries this call writes the live entries' bytes,
+// oldest first, back to back into the ring they do not use now and points the entries there; the field
+// sections (and the next call, HHUFF_QPK_CONTINUE) read only scratch.
+__global__ __launch_bounds__(256) void qpack_table_kernel(QpkArgs A) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (c >= A.nconn) return;
+    const uint64_t base = c * A.conn_scratch;
+    QState* ps = reinterpret_cast<QState*>(A.scratch + base);
+    const QState s = *ps;
+    if (!s.dirty) return;
+    const uint32_t E = qpk_entries(A.T);
+    QEntry* ent = reinterpret_cast<QEntry*>(A.scratch + base + sizeof(QState));
+    const uint32_t nring = s.ring ^ 1u;
+    const uint64_t rbase = base + sizeof(QState) + (uint64_t)E * sizeof(QEntry) + nring * (uint64_t)qpk_ring_bytes(A.T);
+    uint32_t carry = 0;
+    for (uint32_t k0 = 0; k0 < s.num; k0 += 64) {
+        const uint32_t k = k0 + (uint32_t)lane;
+        const bool live = k < s.num;
+        uint32_t i = s.start + k;
+        i = i >= E ? i - E : i;
+        QEntry e{};
+        if (live) e = ent[i];
+        const uint32_t sz = live ? e.nl + e.vl : 0u;
+        const uint32_t dst = carry + wave_excl_scan(sz, lane);
+        carry += (uint32_t)__builtin_amdgcn_readlane((int)(dst - carry + sz), 63);
+        uint8_t* d = A.scratch + rbase + dst;
+        wave_copy64(q_src(A, e.nsrc), d, live ? e.nl : 0u, lane);
+        wave_copy64(q_src(A, e.vsrc), d + e.nl, live ? e.vl : 0u, lane);
+        if (live) {
+            ent[i].nsrc = kQScr | (rbase + dst);
+            ent[i].vsrc = kQScr | (rbase + dst + e.nl);
+        }
+    }
+    if (lane == 0) ps->ring = nring;
 }
 
 // ---- field sections ----
@@ -514,7 +531,7 @@ __device__ int32_t q_parse_context(const QTable& t, uint32_t max_entries, QCtx& 
 
 // resolve_dynamic / resolve_dynamic_postbase (qpack.c:523-557)
 __device__ bool q_dyn(const QTable& t, const QCtx& ctx, const uint8_t* in, uint64_t& p, uint64_t end, uint32_t prefix,
-                      bool postbase, uint4& e) {
+                      bool postbase, QEntry& e) {
     int64_t off, index;
     if (q_int(off, in, p, end, prefix) != 0) return false;
     if (postbase) {
@@ -533,43 +550,14 @@ struct QArena {
     uint64_t cur, end;
 };
 
-// a field string's bytes go to arena[off, off + n): recorded for qpack_copy_kernel (fs = their address), or
-// copied now (no deferred copies)
-__device__ __forceinline__ void q_put(const QpkArgs& A, const uint8_t* src, uint32_t off, uint32_t n, uint64_t& fs) {
-    if (A.fsrc_n) {
-        fs = (uint64_t)(uintptr_t)src;
-        return;
-    }
-    uint8_t* d = A.arena + off;
-    copy16([&](uint32_t i) { return src[i]; }, [&](uint32_t i, uint8_t v) { d[i] = v; }, n);
-    fs = 0;
-}
-
-__device__ __forceinline__ int32_t q_copy_static(const QpkArgs& A, QArena& R, uint32_t so, uint32_t n, uint32_t& off,
-                                                 uint64_t& fs) {
+// a field string's n bytes at source `src` go to arena[off, off + n): qpack_copy_kernel moves them
+// (fs = their address)
+__device__ __forceinline__ int32_t q_copy(const QpkArgs& A, QArena& R, uint64_t src, uint32_t n, uint32_t& off,
+                                          uint64_t& fs) {
     if (R.cur + n > R.end) return HHUFF_QPK_ARENA;
     off = (uint32_t)R.cur;
-    q_put(A, q_static_bytes + so, off, n, fs);
+    fs = (uint64_t)(uintptr_t)q_src(A, src);
     R.cur += n;
-    return 0;
-}
-
-__device__ __forceinline__ int32_t q_copy_ring(const QpkArgs& A, QArena& R, const QTable& t, uint32_t ro, uint32_t n,
-                                               uint32_t& off, uint64_t& fs) {
-    if (R.cur + n > R.end) return HHUFF_QPK_ARENA;
-    if (ro >= t.RB) ro -= t.RB;
-    off = (uint32_t)R.cur;
-    R.cur += n;
-    const uint32_t RB = t.RB;
-    if (ro + n <= RB) {
-        q_put(A, t.ring + ro, off, n, fs);
-        return 0;
-    }
-    uint8_t* d = A.arena + off;  // wraps around the ring end: copied here
-    const uint8_t* ring = t.ring;
-    copy16([&](uint32_t i) { return ring[ro + i >= RB ? ro + i - RB : ro + i]; }, [&](uint32_t i, uint8_t v) { d[i] = v; },
-           n);
-    fs = 0;
     return 0;
 }
 
@@ -590,7 +578,7 @@ __device__ int32_t q_literal(const QpkArgs& A, QArena& R, uint32_t& soft, uint64
         len = A.lit_len[pre];
         soft |= A.lit_st[pre] & 3u;
         off = (uint32_t)R.cur;
-        q_put(A, huff ? A.lit_out + (p * 8u) / 5u : in + p, off, len, fs);
+        fs = (uint64_t)(uintptr_t)(huff ? A.lit_out + (p * 8u) / 5u : in + p);
         R.cur += len;
         p += (uint64_t)n;
         return 0;
@@ -631,7 +619,7 @@ __device__ int32_t q_field(const QpkArgs& A, const QTable& t, const QCtx& ctx, u
     const uint8_t* in = A.in;
     uint32_t soft = 0;
     int32_t r;
-    uint4 e;
+    QEntry e;
     const uint32_t kind = in[p] >> 4;
     switch (kind) {
         case 12:
@@ -642,9 +630,9 @@ __device__ int32_t q_field(const QpkArgs& A, const QTable& t, const QCtx& ctx, u
             if (q_int(si, in, p, end, 6) != 0 || (uint64_t)si >= kQStaticCount) return kDF;
             const uint32_t k = 4u * (uint32_t)si;
             nlen = q_static_ent[k + 1];
-            if ((r = q_copy_static(A, R, q_static_ent[k], nlen, noff, fn)) != 0) return r;
+            if ((r = q_copy(A, R, kQStatic | q_static_ent[k], nlen, noff, fn)) != 0) return r;
             vlen = q_static_ent[k + 3];
-            if ((r = q_copy_static(A, R, q_static_ent[k + 2], vlen, voff, fv)) != 0) return r;
+            if ((r = q_copy(A, R, kQStatic | q_static_ent[k + 2], vlen, voff, fv)) != 0) return r;
         } break;
         case 8:
         case 9:
@@ -652,11 +640,11 @@ __device__ int32_t q_field(const QpkArgs& A, const QTable& t, const QCtx& ctx, u
         case 11:  // indexed field line, dynamic (:670-682)
         case 1:   // indexed field line, post-base (:713-722)
             if (!q_dyn(t, ctx, in, p, end, kind == 1 ? 4u : 6u, kind == 1, e)) return kDF;
-            if ((r = q_copy_ring(A, R, t, e.x, e.y, noff, fn)) != 0) return r;
-            if ((r = q_copy_ring(A, R, t, e.x + e.y, e.z, voff, fv)) != 0) return r;
-            nlen = e.y;
-            vlen = e.z;
-            soft = e.w;
+            if ((r = q_copy(A, R, e.nsrc, e.nl, noff, fn)) != 0) return r;
+            if ((r = q_copy(A, R, e.vsrc, e.vl, voff, fv)) != 0) return r;
+            nlen = e.nl;
+            vlen = e.vl;
+            soft = e.soft;
             break;
         case 5:
         case 7: {  // literal field line, static name reference (:683-692)
@@ -664,16 +652,16 @@ __device__ int32_t q_field(const QpkArgs& A, const QTable& t, const QCtx& ctx, u
             if (q_int(si, in, p, end, 4) != 0 || (uint64_t)si >= kQStaticCount) return kDF;
             const uint32_t k = 4u * (uint32_t)si;
             nlen = q_static_ent[k + 1];
-            if ((r = q_copy_static(A, R, q_static_ent[k], nlen, noff, fn)) != 0) return r;
+            if ((r = q_copy(A, R, kQStatic | q_static_ent[k], nlen, noff, fn)) != 0) return r;
             if ((r = q_literal(A, R, soft, p, end, false, voff, vlen, fv, T)) != 0) return r;
         } break;
         case 4:
         case 6:  // literal field line, dynamic name reference (:693-704)
         case 0:  // literal field line, post-base name reference (:723-733)
             if (!q_dyn(t, ctx, in, p, end, kind == 0 ? 3u : 4u, kind == 0, e)) return kDF;
-            if ((r = q_copy_ring(A, R, t, e.x, e.y, noff, fn)) != 0) return r;
-            nlen = e.y;
-            soft = e.w & 0x1u;
+            if ((r = q_copy(A, R, e.nsrc, e.nl, noff, fn)) != 0) return r;
+            nlen = e.nl;
+            soft = e.soft & 0x1u;
             if ((r = q_literal(A, R, soft, p, end, false, voff, vlen, fv, T)) != 0) return r;
             break;
         default:  // 2, 3: literal field line with a literal name (:705-712)
@@ -733,10 +721,8 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
                 st = rc;
                 break;
             }
-            if (A.fsrc_n) {
-                A.fsrc_n[slot + nf] = fn;
-                A.fsrc_v[slot + nf] = fv;
-            }
+            A.fsrc_n[slot + nf] = fn;
+            A.fsrc_v[slot + nf] = fv;
             A.name_off[slot + nf] = no;
             A.name_len[slot + nf] = nl;
             A.value_off[slot + nf] = vo;
@@ -859,7 +845,8 @@ __global__ __launch_bounds__(256) void qpack_mark_kernel(QpkArgs A, QMarks M) {
 }
 
 uint64_t qpack_conn_scratch(uint32_t header_table_size) {
-    return sizeof(QState) + qpk_ring_bytes(header_table_size) + 16ull * (header_table_size / kEntryOverhead + 1u);
+    return sizeof(QState) + (uint64_t)qpk_entries(header_table_size) * sizeof(QEntry) +
+           2ull * qpk_ring_bytes(header_table_size);
 }
 
 hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off, const uint32_t* enc_len,
@@ -874,10 +861,10 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
               max_blocked, arena, arena_off, name_off, name_len, value_off, value_len, fflags, nfields, sstatus,
               req_insert_count, enc_status, enc_consumed, insert_count, scratch, qpack_conn_scratch(header_table_size),
               flags, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    // literal pre-pass workspace (inputs below 4 GiB: u32 positions): bitmaps, word prefixes, chunk sums, the
-    // literal list with each literal's prefix, the literal kernels' results, the decoded bytes
-    const bool prepass = in_size > 0 && in_size < (1ull << 32);
-    const uint64_t nwords = (in_size + 31) / 32, nchunks = literal_list_chunks(nwords);
+    // workspace: the literal pre-pass's bitmaps, word prefixes, chunk sums, the literal list with each
+    // literal's prefix, the literal kernels' results and decoded bytes (positions are u32: in_size < 2^32,
+    // checked by the C ABI), and the field slots' byte sources
+    const uint64_t nwords = in_size / 32 + 1, nchunks = literal_list_chunks(nwords);
     const uint64_t n_max = in_size + 2;  // every literal header takes a byte
     auto up = [](uint64_t x) { return (x + 255) & ~255ull; };
     const uint64_t o_lit = 0, o_name = o_lit + up(4 * nwords), o_p3 = o_name + up(4 * nwords);
@@ -891,7 +878,7 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
     const uint64_t wbytes = o_fsv + up(8 * in_size + 8);  // field slots: one per input byte
     uint8_t* work = nullptr;
     hipError_t e = hipSuccess;
-    if (prepass) {
+    {
         e = work_alloc((void**)&work, wbytes, stream);
         if (e == hipSuccess) e = hipMemsetAsync(work, 0, zero_end, stream);
         uint32_t* lit_bits = reinterpret_cast<uint32_t*>(work + o_lit);
@@ -926,11 +913,12 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
     }
     if (e == hipSuccess) {
         hipLaunchKernelGGL(qpack_encoder_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
+        hipLaunchKernelGGL(qpack_table_kernel, dim3((uint32_t)(((uint64_t)nconn + 3) / 4)), dim3(256), 0, stream, A);
         e = hipGetLastError();
     }
     if (e == hipSuccess && nsec != 0) {
         hipLaunchKernelGGL(qpack_sections_kernel, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
-        if (A.fsrc_n) hipLaunchKernelGGL(qpack_copy_kernel, dim3(4096), dim3(256), 0, stream, A);
+        hipLaunchKernelGGL(qpack_copy_kernel, dim3(4096), dim3(256), 0, stream, A);
         hipLaunchKernelGGL(qpack_blocked_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
         e = hipGetLastError();
     }
