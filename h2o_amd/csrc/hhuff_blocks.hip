@@ -12,7 +12,7 @@
 //      table lookups and inserts, arena offsets, verdicts.  A field's name and value are *references* to
 //      where their bytes already are -- a decoded literal, the static table, the connection's ring, or
 //      (literals decoded in place) the arena -- and a table entry is such a pair of references;
-//   3. the copy pass (blk_copy_kernel, one thread per 32 field slots) moves every field's bytes into the
+//   3. the copy pass (blk_copy_kernel, 64 blocks per wave) moves every field's bytes into the
 //      arena, and the table pass (blk_table_kernel, one wave per connection) writes each connection's live
 //      entries into its other ring, so the next call (HHUFF_BLK_CONTINUE) finds them there.
 // The walk stores little and waits on few loads; the byte traffic runs in the parallel passes.
@@ -659,27 +659,22 @@ __global__ __launch_bounds__(kBlkThreads) void hpack_walk_kernel(BlkArgs A) {
     }
 }
 
-// Copy pass: one wave per block (grid-stride), 32 fields (64 name / value segments) per round through
-// wave_copy64 (literals decoded in place already sit in the arena).
+// Copy pass: 64 blocks per wave (wave_copy_fields), their fields' name / value bytes into the arena
+// (literals decoded in place already sit there).
 __global__ __launch_bounds__(256) void blk_copy_kernel(BlkArgs A) {
     const int lane = threadIdx.x & 63;
     const uint32_t nblk = A.conn_first[A.nconn];
     const uint32_t nw = gridDim.x * 4u;
-    for (uint32_t b = blockIdx.x * 4u + (threadIdx.x >> 6); b < nblk; b += nw) {
-        const uint32_t s0 = A.blk_off[b], nf = A.nfields[b];
-        for (uint32_t g = 0; g < nf; g += 32) {
-            const uint32_t fi = g + ((uint32_t)lane >> 1), f = s0 + fi;
-            const bool val = lane & 1;
-            uint32_t len = 0, off = 0;
-            uint64_t src = 0;
-            if (fi < nf) {
-                len = val ? A.value_len[f] : A.name_len[f];
-                off = val ? A.value_off[f] : A.name_off[f];
-                src = val ? A.fsrc_v[f] : A.fsrc_n[f];
-                if (src == (kSrcArena | off)) len = 0;
-            }
-            wave_copy64(src_ptr(A, src), A.arena + off, len, lane);
-        }
+    for (uint32_t b0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 64u; b0 < nblk; b0 += nw * 64u) {
+        const uint32_t b = b0 + (uint32_t)lane;
+        const uint32_t s0 = b < nblk ? A.blk_off[b] : 0u, nf = b < nblk ? A.nfields[b] : 0u;
+        wave_copy_fields(s0, nf, lane, [&](uint32_t f, bool val, const uint8_t*& src, uint8_t*& dst, uint32_t& len) {
+            const uint32_t off = val ? A.value_off[f] : A.name_off[f];
+            const uint64_t fs = val ? A.fsrc_v[f] : A.fsrc_n[f];
+            src = src_ptr(A, fs);
+            dst = A.arena + off;
+            len = fs == (kSrcArena | off) ? 0u : (val ? A.value_len[f] : A.name_len[f]);
+        });
     }
 }
 

@@ -352,7 +352,7 @@ __device__ __forceinline__ void copy16(Src src, Dst dst, uint32_t n) {
 }
 
 // The wave copies 64 byte segments at once (lane i holds segment i: src, dst, len; len 0 = none) in 16-byte
-// pieces spread over all lanes, so a long segment does not serialise one lane: every 64 pieces cost one
+// pieces spread over all lanes (whole pieces as unaligned 16-B accesses, tails bytewise), so a long segment does not serialise one lane: every 64 pieces cost one
 // round trip.  Piece t belongs to the last lane k whose piece prefix excl[k] <= t (binary search by lanes).
 __device__ void wave_copy64(const uint8_t* src, uint8_t* dst, uint32_t len, int lane) {
     const uint32_t chunks = (len + 15u) >> 4;
@@ -372,14 +372,47 @@ __device__ void wave_copy64(const uint8_t* src, uint8_t* dst, uint32_t len, int 
         const uint32_t n = (uint32_t)__shfl((int)len, k);
         if (t < total) {
             const uint32_t a = 16u * c, m = min(16u, n - a);
-            uint8_t v[16];
+            if (m == 16) {  // a whole piece: one unaligned 16-B load and store (inside both strings)
+                uint4 w;
+                __builtin_memcpy(&w, s + a, 16);
+                __builtin_memcpy(d + a, &w, 16);
+            } else {  // the tail: bytes, so nothing outside the two strings is touched
+                uint8_t v[16];
 #pragma unroll
-            for (uint32_t j = 0; j < 16; ++j)
-                if (j < m) v[j] = s[a + j];
+                for (uint32_t j = 0; j < 15; ++j)
+                    if (j < m) v[j] = s[a + j];
 #pragma unroll
-            for (uint32_t j = 0; j < 16; ++j)
-                if (j < m) d[a + j] = v[j];
+                for (uint32_t j = 0; j < 15; ++j)
+                    if (j < m) d[a + j] = v[j];
+            }
         }
+    }
+}
+
+// Field copies of up to 64 consecutive field lists (header blocks / sections) per wave: lane j holds list
+// j's first field slot s0 and field count nf (0 for no list); the lists' 2 nf name / value segments are
+// numbered back to back and handed to wave_copy64 64 at a time, so a wave stays full however few fields a
+// list has.  seg(slot, val, src, dst, len) describes one segment (len 0: nothing to copy).
+template <class Seg>
+__device__ __forceinline__ void wave_copy_fields(uint32_t s0, uint32_t nf, int lane, Seg seg) {
+    const uint32_t cnt = 2u * nf;
+    const uint32_t excl = wave_excl_scan(cnt, lane);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(excl + cnt), 63);
+    for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+        const uint32_t t = r0 + (uint32_t)lane;
+        int k = 0;  // the last lane whose segment prefix is <= t
+#pragma unroll
+        for (int step = 32; step > 0; step >>= 1) {
+            const uint32_t e = (uint32_t)__shfl((int)excl, k + step);
+            k += e <= t ? step : 0;
+        }
+        const uint32_t w = t - (uint32_t)__shfl((int)excl, k);
+        const uint32_t slot = (uint32_t)__shfl((int)s0, k) + (w >> 1);
+        const uint8_t* src = nullptr;
+        uint8_t* dst = nullptr;
+        uint32_t len = 0;
+        if (t < total) seg(slot, (w & 1u) != 0, src, dst, len);
+        wave_copy64(src, dst, len, lane);
     }
 }
 

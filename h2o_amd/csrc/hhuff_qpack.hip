@@ -735,25 +735,19 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
     }
 }
 
-// Copy pass (with the pre-pass): one wave per section, 32 fields (64 name / value segments) per round
-// through wave_copy64.  A failed section's fields up to the failure are copied too, as the in-lane path does.
+// Copy pass: 64 sections per wave (wave_copy_fields), their fields' name / value bytes into the arena.
 __global__ __launch_bounds__(256) void qpack_copy_kernel(QpkArgs A) {
     const int lane = threadIdx.x & 63;
     const uint32_t nw = gridDim.x * 4u;
-    for (uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6); k < A.nsec; k += nw) {
-        const uint32_t s0 = A.sec_off[k], nf = A.nfields[k];
-        for (uint32_t g = 0; g < nf; g += 32) {
-            const uint32_t fi = g + ((uint32_t)lane >> 1), f = s0 + fi;
-            const bool val = lane & 1;
-            uint32_t len = 0, off = 0;
-            uint64_t src = 0;
-            if (fi < nf) {
-                src = val ? A.fsrc_v[f] : A.fsrc_n[f];
-                len = src ? (val ? A.value_len[f] : A.name_len[f]) : 0u;
-                off = val ? A.value_off[f] : A.name_off[f];
-            }
-            wave_copy64(reinterpret_cast<const uint8_t*>(src), A.arena + off, len, lane);
-        }
+    for (uint32_t k0 = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 64u; k0 < A.nsec; k0 += nw * 64u) {
+        const uint32_t k = k0 + (uint32_t)lane;
+        const uint32_t s0 = k < A.nsec ? A.sec_off[k] : 0u, nf = k < A.nsec ? A.nfields[k] : 0u;
+        wave_copy_fields(s0, nf, lane, [&](uint32_t f, bool val, const uint8_t*& src, uint8_t*& dst, uint32_t& len) {
+            const uint64_t fs = val ? A.fsrc_v[f] : A.fsrc_n[f];
+            src = reinterpret_cast<const uint8_t*>(fs);
+            dst = A.arena + (val ? A.value_off[f] : A.name_off[f]);
+            len = fs ? (val ? A.value_len[f] : A.name_len[f]) : 0u;
+        });
     }
 }
 
@@ -918,7 +912,7 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
     }
     if (e == hipSuccess && nsec != 0) {
         hipLaunchKernelGGL(qpack_sections_kernel, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
-        hipLaunchKernelGGL(qpack_copy_kernel, dim3(4096), dim3(256), 0, stream, A);
+        hipLaunchKernelGGL(qpack_copy_kernel, dim3(std::min((nsec + 255u) / 256u, 4096u)), dim3(256), 0, stream, A);
         hipLaunchKernelGGL(qpack_blocked_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
         e = hipGetLastError();
     }
