@@ -338,6 +338,7 @@ def main():
         if world == 1 and not args.pmc_child:
             if not args.no_extra:
                 line["configs"] = other_configs(torch, codec, synth)
+                line["f4"] = f4_lines(torch, codec)
                 line["per_string_latency_us"] = per_string_latency(codec)
             if not args.no_host:
                 line["host_inclusive"] = host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch)
@@ -379,6 +380,22 @@ def other_configs(torch, codec, synth):
             r.update(flatten_ms=round(t, 4), flatten_gibps=round(P / GIB / (t * 1e-3), 2))
         res[cfg] = r
         del b
+        torch.cuda.empty_cache()
+    return res
+
+
+def f4_lines(torch, codec):
+    """whole header blocks (65,536 browser-like HTTP/2 connections, h2o_hpack_decode_header per field
+    with one dynamic table each, and h2o_hpack_parse_request's rules) and one QPACK decoder step (65,536 HTTP/3
+    connections: encoder streams, then field sections), with their CPU baselines (tools/bench_configs.py)"""
+    import bench_configs as BC
+
+    res = {}
+    for name, fn in (("blocks", BC.blocks_line), ("qpack", BC.qpack_line)):
+        try:
+            res[name] = fn(torch, codec, 65536)
+        except Exception as e:  # a report, not a gate
+            res[name] = {"error": str(e)}
         torch.cuda.empty_cache()
     return res
 

@@ -279,9 +279,13 @@ int hhuff_hpack_parse_requests(const uint8_t *in, uint64_t in_size, const uint32
  *      Device arrays; scratch = hhuff_qpack_scratch_size(nconn, header_table_size) bytes of device memory
  *      (16-byte aligned) that holds the tables: pass HHUFF_QPK_CONTINUE to carry them (and the failed
  *      state) over from the previous call -- connection c of this call is connection c of that one;
- *      without it every connection starts with a fresh decoder.  nsec = conn_first[nconn] (host copy).
- *      Asynchronous on `stream` (two launches: encoder streams one lane per connection, then sections
- *      one lane per section). */
+ *      without it every connection starts with a fresh decoder; the tables hold scratch offsets, not
+ *      addresses, so scratch may be moved between calls.  nsec = conn_first[nconn] (host copy).
+ *      in_size < 2^32 (offsets are u32).  Encoder streams and sections must not overlap in `in`.
+ *      Asynchronous on `stream`: a literal pre-pass (every literal of the step decoded at once), the
+ *      encoder streams (one lane per connection, entries booked as references), a table pass, the
+ *      sections (one lane per section) and a copy pass; ~30 bytes of stream-ordered pool workspace per
+ *      input byte. */
 #define HHUFF_QPK_CONTINUE 1u
 #define HHUFF_QPK_DECOMPRESSION_FAILED 0x30200 /* H2O_HTTP3_ERROR_QPACK_DECOMPRESSION_FAILED, http3_common.h:73 */
 #define HHUFF_QPK_ARENA (-300)
