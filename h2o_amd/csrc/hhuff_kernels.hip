@@ -1067,22 +1067,44 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
         return P;
     };
 
+    // Software pipeline: cur = being encoded (span in the stage), nxt = planned, span in flight in pf,
+    // ti = offsets of the tile after nxt.  Every wait on a global load sits between a tile's encode and its
+    // stores, never right after stores: vmcnt counts stores too, so a load consumed after the stores
+    // would wait for their writes to land.
     SpanPrefetch<(STAGE + 1023) / 1024> pf;
     TileIn ti = issue_tile(base, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
     Plan cur = plan(base, ti);
     if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
     if (base + stride < A.n) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
     if (cur.fits) pf.commit(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+    Plan nxt;
+    bool nxt_pf = false;  // nxt's span is in pf (issued, not committed)
+    if (base + stride < A.n) {
+        nxt = plan(base + stride, ti);
+        if (nxt.fits) {
+            pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+            nxt_pf = true;
+        }
+    }
     PROF_DECL
     for (;;) {
         const uint64_t nbase = base + stride;
-        const bool have_next = nbase < A.n;
-        Plan nxt;
-        if (have_next) {
-            nxt = plan(nbase, ti);
-            if (nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
-            if (nbase + stride < A.n) ti = issue_tile(nbase + stride, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
-        }
+        const bool have_next = nbase < A.n, have_nn = nbase + stride < A.n;
+        if (have_nn) ti = issue_tile(nbase + stride, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
+        Plan nn;
+        bool nn_pf = false, advanced = false;
+        // commit nxt's span into the (free) stage, then plan the tile after it and put its span in flight
+        auto advance = [&]() {
+            if (nxt_pf) pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+            if (have_nn) {
+                nn = plan(nbase + stride, ti);
+                if (nn.fits) {
+                    pf.issue(A.in, A.in_size, nn.a0, nn.span, lane);
+                    nn_pf = true;
+                }
+            }
+            advanced = true;
+        };
         // ---- the current tile ----
         const Tile& t = cur.t;
         uint32_t ol = kFailLen;
@@ -1121,9 +1143,9 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
                     if (t.i == A.n - 1) A.pk_off[A.n] = (uint32_t)(G + place + keep);
                 }
             } else {
-                // the input stage is free: commit the next span BEFORE this tile's stores, so the commit's
-                // vmcnt wait covers only loads issued a tile ago, not the stores (vmcnt counts both)
-                if (have_next && nxt.fits) pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+                // the input stage is free: commit the next span and plan the one after BEFORE this tile's
+                // stores, so their vmcnt waits cover loads issued a tile ago, not the stores
+                advance();
                 wave_lds_sync();
                 if (!(region && A.edges)) stage_bswap(obuf32, (cur.ospan + 15u) & ~15u, lane);
                 wave_lds_sync();
@@ -1176,8 +1198,10 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
             PROF_FLUSH(1);
             break;
         }
-        if (nxt.fits && (PACKED || !cur.fits)) pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+        if (!advanced) advance();  // packed mode (the stage held the compaction) and direct tiles
         cur = nxt;
+        nxt = nn;
+        nxt_pf = nn_pf;
         base = nbase;
     }
 }
