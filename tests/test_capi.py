@@ -88,3 +88,24 @@ def test_c_translation_unit_on_the_gpu():
     r = subprocess.run([build_capi_check()], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "capi_check: ok" in r.stdout
+
+
+def test_argument_checks_need_no_gpu():
+    """the C ABI rejects bad arguments before touching the device: QPACK inputs of 2^32 bytes or more (u32
+    offsets), scratch too small or misaligned -- HHUFF_EINVAL with the reason in hhuff_last_error_string()"""
+    from h2o_amd import codec
+
+    L = codec.lib()
+    p = 1 << 20  # a 16-byte aligned dummy address: never dereferenced on these paths
+    ss = int(L.hhuff_qpack_scratch_size(1, 4096))
+
+    def qpack(in_size, scratch, scratch_size):
+        return L.hhuff_qpack_decode(p, in_size, p, p, p, p, 1, 0, 4096, 100, None, None, None, None, None, None,
+                                    None, None, None, None, None, p, p, p, scratch, scratch_size, 0, None)
+
+    assert qpack(1 << 32, p, ss) == -1
+    assert b"2^32" in L.hhuff_last_error_string()
+    assert qpack(100, p, ss - 1) == -1
+    assert b"scratch" in L.hhuff_last_error_string()
+    assert qpack(100, p + 8, ss) == -1
+    assert b"aligned" in L.hhuff_last_error_string()

@@ -255,9 +255,11 @@ def test_gpu_empty_and_degenerate_batches(torch_cuda, oracle_codec):
 
 
 @pytest.mark.gpu
-def test_gpu_tables_carry_over_between_calls(torch_cuda, oracle_codec):
+@pytest.mark.parametrize("move", [False, True])
+def test_gpu_tables_carry_over_between_calls(torch_cuda, oracle_codec, move):
     """HHUFF_BLK_CONTINUE: each connection's blocks split over two calls sharing the scratch decode exactly
-    like one call over all of them (dynamic tables and the failed state persist)"""
+    like one call over all of them (dynamic tables and the failed state persist).  move: the scratch is
+    copied to a new buffer between the calls and the old one overwritten (tables hold offsets, not addresses)"""
     from h2o_amd import codec
 
     b = HS.make_connections(2000, seed=47, adversarial_frac=0.2)
@@ -277,6 +279,11 @@ def test_gpu_tables_carry_over_between_calls(torch_cuda, oracle_codec):
                                       4096, in_size=int(part["data"].size), scratch=scratch, cont=cont)
         torch.cuda.synchronize()
         scratch = r["scratch"]
+        if move:
+            moved = torch.empty_like(scratch)
+            moved.copy_(scratch)
+            scratch.fill_(0x5A)  # stays allocated: a stale address would read this
+            old, scratch = scratch, moved  # noqa: F841
         h = {k: v.cpu().numpy() for k, v in r.items() if k != "scratch"}
         for k in ("name_off", "name_len", "value_off", "value_len", "nfields"):
             h[k] = h[k].view(np.uint32)

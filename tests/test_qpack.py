@@ -129,8 +129,9 @@ def torch_cuda():
     return torch
 
 
-def gpu_session(torch, nconn, hts, mb, nbl, steps):
-    """every step through hhuff_qpack_decode, the tables carried over in the scratch -> list of host dicts"""
+def gpu_session(torch, nconn, hts, mb, nbl, steps, move=False):
+    """every step through hhuff_qpack_decode, the tables carried over in the scratch -> list of host dicts
+    (move: the scratch is copied to a new buffer between steps and the old one overwritten)"""
     from h2o_amd import codec
 
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
@@ -145,6 +146,11 @@ def gpu_session(torch, nconn, hts, mb, nbl, steps):
                                in_size=int(st["data"].size), scratch=scratch, cont=k > 0)
         torch.cuda.synchronize()
         scratch = r["scratch"]
+        if move:
+            moved = torch.empty_like(scratch)
+            moved.copy_(scratch)
+            scratch.fill_(0x5A)  # stays allocated: a stale address would read this
+            old, scratch = scratch, moved  # noqa: F841
         h = {}
         for key, v in r.items():
             if key == "scratch":
@@ -187,6 +193,25 @@ def test_gpu_matches_restatement_field_by_field(torch_cuda, oracle_codec, seed, 
             o, n = int(st["sec_off"][s]), int(a["nfields"][s])
             for k in ("name_off", "name_len", "value_off", "value_len", "fflags"):
                 np.testing.assert_array_equal(g[k][o:o + n], a[k][o:o + n], err_msg="%s section %d" % (k, s))
+        fg, fa = fields_of(g, st["sec_off"], ns), fields_of(a, st["sec_off"], ns)
+        assert fg[0] == fa[0] and fg[1] == fa[1]
+
+
+@pytest.mark.gpu
+def test_gpu_scratch_moves_between_steps(torch_cuda, oracle_codec):
+    """the tables hold scratch offsets: a scratch copied to another buffer between steps continues exactly"""
+    nconn = 1000
+    steps = QS.make_session(nconn, steps=3, seed=87, adversarial_frac=0.05)
+    for st in steps:
+        st["arena_off"] = QS.arena_offsets(st["sec_off"], 4096)
+    ro = run_oracle_session(oracle_codec, nconn, 4096, 8, None, steps)
+    rg = gpu_session(torch_cuda, nconn, 4096, 8, None, steps, move=True)
+    for a, g, st in zip(ro, rg, steps):
+        ns = len(st["sec_off"]) - 1
+        for k in SEC_KEYS:
+            np.testing.assert_array_equal(g[k][:ns], a[k][:ns], err_msg=k)
+        for k in CONN_KEYS:
+            np.testing.assert_array_equal(g[k][:nconn], a[k][:nconn], err_msg=k)
         fg, fa = fields_of(g, st["sec_off"], ns), fields_of(a, st["sec_off"], ns)
         assert fg[0] == fa[0] and fg[1] == fa[1]
 
