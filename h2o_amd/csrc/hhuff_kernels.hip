@@ -1095,7 +1095,9 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
         bool nn_pf = false, advanced = false;
         // commit nxt's span into the (free) stage, then plan the tile after it and put its span in flight
         auto advance = [&]() {
+            PROF_MARK(2);
             if (nxt_pf) pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+            PROF_MARK(3);  // commit
             if (have_nn) {
                 nn = plan(nbase + stride, ti);
                 if (nn.fits) {
@@ -1103,6 +1105,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
                     nn_pf = true;
                 }
             }
+            PROF_MARK(7);  // plan + issue of the tile after next
             advanced = true;
         };
         // ---- the current tile ----

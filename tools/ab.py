@@ -116,7 +116,7 @@ def run(names, cfg="c4", rounds=5, steps=10):
                 ref = chk
             assert chk == ref or nm.startswith("x_"), (nm, chk, ref)  # x_*: ablation builds, output not checked
     # profile builds (-DHHUFF_PROFILE): per-phase shader cycles of one launch of each kernel
-    phases = ["plan+issue", "steps", "verdicts/bswap", "commit", "out copy", "len/status", "direct", "-"]
+    phases = ["plan+issue", "steps", "verdicts/bswap", "commit", "out copy", "len/status", "direct", "plan next"]
     for nm in names:
         L = libs[nm]
         if not hasattr(L, "hhuff_debug_prof"):
