@@ -729,6 +729,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
     uint64_t bnext = 0, bend = 0;
     bool qdone = false;
     const uint64_t nwork = A.n_dev ? (uint64_t)*A.n_dev : (uint64_t)A.n;
+    PROF_DECL  // profile builds: phases take / window / bulk / tail / flush in slot 0 (the staged kernel's)
 
     for (;;) {
         // ---- 1. idle lanes take strings ----
@@ -768,9 +769,13 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
             bnext = min(bend, bnext + (uint64_t)__builtin_popcountll(need));
         }
         if (!__any(busy)) {
-            if (qdone) break;
+            if (qdone) {
+                PROF_FLUSH(0);
+                break;
+            }
             continue;
         }
+        PROF_MARK(0);
 
         // ---- 2. the lane's window: NW dwords from its current byte (dword-aligned) ----
         // A round that does not finish its string stops with its next byte at wb + 4 (NW - 3) (bulk steps
@@ -800,6 +805,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
         }
         int32_t pm = busy ? (int32_t)(8u * (uint32_t)(cur - wb) + (P & 7u)) - 1 : -1;
         const int32_t pm0 = pm;
+        PROF_MARK(1);
         const int32_t end = busy ? (int32_t)min((uint64_t)(pm + 1) + rem, (uint64_t)0x40000000u) : 0;
         const bool fin = busy && end <= kFinal;
         const uint32_t h0 = (uint32_t)((dst + ocnt) & 15u);  // buffer offset of this round's first byte
@@ -867,6 +873,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
             bstep(true);
             if (!__any(pm < lim)) break;
         }
+        PROF_MARK(2);
 
         // ---- 3b. tail: lanes whose string ends in this window ----
         int32_t c = (fin && !parked) ? pm - end : 0x40000000;
@@ -931,6 +938,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
             }
         }
 
+        PROF_MARK(3);
         // ---- 4. flush whole chunks, carry the partial one; finish strings ----
         if (busy) {
             flags |= ((accb >> 24) | (accb >> 26) | (acc1 >> 24) | (acc2 >> 26) | (accl >> 14)) & 3u;
@@ -972,6 +980,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                 busy = false;
             }
         }
+        PROF_MARK(4);
     }
 }
 
