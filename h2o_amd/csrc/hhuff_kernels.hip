@@ -104,21 +104,30 @@ struct TileIn {  // per-lane prefetched fields of one tile
     uint32_t s, len, name_word, dst;
 };
 
+// No VALU writes on purpose: the index is clamped (a lane past n loads string n - 1's fields, which
+// finish_tile then ignores) and absent arrays read in_off instead, so every load issues unconditionally
+// and its register is written by the load alone; consume_tile() then uses all four words where the
+// tile is planned.  With the loads under `if (i < n)` and zero defaults, or with a loaded word left
+// unused, the compiler copied (PHI), re-zeroed or reused those registers and put a vmcnt wait in front
+// of each write -- a memory round trip per tile, behind the span loads just issued or the stores.
 __device__ __forceinline__ TileIn issue_tile(uint64_t base, int lane, uint32_t n, const uint32_t* __restrict__ in_off,
                                              const uint32_t* __restrict__ in_len, const uint32_t* __restrict__ name_bits,
                                              const uint32_t* __restrict__ out_off) {
-    TileIn r{0u, 0u, 0u, 0u};
-    const uint64_t i = base + lane;
-    if (i < n) {
-        r.s = in_off[i];
-        r.len = in_len ? in_len[i] : in_off[i + 1];  // end offset for the contiguous layout (minus s later)
-        if (name_bits) r.name_word = name_bits[i >> 5];
-        if (out_off) r.dst = out_off[i];
-    }
+    const uint64_t i = min(base + (uint64_t)lane, (uint64_t)n - 1u);  // n >= 1 in every kernel
+    TileIn r;
+    r.s = in_off[i];
+    r.len = in_len ? in_len[i] : in_off[i + 1];  // end offset for the contiguous layout (minus s later)
+    r.name_word = name_bits ? name_bits[i >> 5] : in_off[i];
+    r.dst = out_off ? out_off[i] : in_off[i];
     return r;
+}
+// the words of a prefetched tile are all waited for here, where its offsets are needed anyway
+__device__ __forceinline__ void consume_tile(const TileIn& t) {
+    __asm__ volatile("" : : "v"(t.s), "v"(t.len), "v"(t.name_word), "v"(t.dst));
 }
 
 __device__ __forceinline__ Tile finish_tile(uint64_t base, int lane, uint32_t n, const TileIn& in, bool pairs) {
+    consume_tile(in);
     Tile t;
     t.i = (uint32_t)base + lane;
     t.valid = (uint64_t)base + lane < n;
@@ -457,7 +466,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     uint32_t cur_name = ti.name_word;
     if (cur.fits) pf.issue(A.in, A.in_size, cur.a0(), cur.span(), lane);
     bool have_next = base + stride < A.n;
-    if (have_next) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
+    ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
     if (cur.fits) pf.template commit<true>(reinterpret_cast<uint32_t*>(buf + cur.ib), A.in, A.in_size, cur.a0(), cur.span(), lane);
     Plan nxt;
     uint32_t nxt_name = 0;
@@ -465,8 +474,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         nxt = plan(base + stride, ti, PACKED ? 1u : 0u);
         nxt_name = ti.name_word;
         if (nxt.fits) pf.issue(A.in, A.in_size, nxt.a0(), nxt.span(), lane);
-        if (base + 2 * stride < A.n)
-            ti = issue_tile(base + 2 * stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
+        ti = issue_tile(base + 2 * stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
     }
     PROF_DECL
     for (;;) {
@@ -570,18 +578,15 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         Plan nn;
         uint32_t nn_name = 0;
         bool have_nn = false;
-        if (have_next) {
-            if (nxt.fits)
-                pf.template commit<true>(reinterpret_cast<uint32_t*>(buf + nxt.ib), A.in, A.in_size, nxt.a0(), nxt.span(), lane);
-            have_nn = nbase + stride < A.n;
-            if (have_nn) {
-                nn = plan(nbase + stride, ti, PACKED ? par : 0u);
-                nn_name = ti.name_word;
-                if (nn.fits) pf.issue(A.in, A.in_size, nn.a0(), nn.span(), lane);
-                if (nbase + 2 * stride < A.n)
-                    ti = issue_tile(nbase + 2 * stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
-            }
-        }
+        if (have_next && nxt.fits)
+            pf.template commit<true>(reinterpret_cast<uint32_t*>(buf + nxt.ib), A.in, A.in_size, nxt.a0(), nxt.span(), lane);
+        have_nn = have_next && nbase + stride < A.n;
+        // planned and reloaded on every path (issue_tile clamps its index): ti is consumed and redefined
+        // at one place, so no wait for it lands behind the span loads issued here
+        nn = plan(nbase + stride, ti, PACKED ? par : 0u);
+        nn_name = ti.name_word;
+        if (have_nn && nn.fits) pf.issue(A.in, A.in_size, nn.a0(), nn.span(), lane);
+        ti = issue_tile(nbase + 2 * stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
         PROF_MARK(3);  // commit + plan
         // ---- the current tile: stores ----
         if (cur.fits) {
@@ -1084,7 +1089,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
     TileIn ti = issue_tile(base, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
     Plan cur = plan(base, ti);
     if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
-    if (base + stride < A.n) ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
+    ti = issue_tile(base + stride, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
     if (cur.fits) pf.commit(stage, A.in, A.in_size, cur.a0, cur.span, lane);
     Plan nxt;
     bool nxt_pf = false;  // nxt's span is in pf (issued, not committed)
@@ -1099,7 +1104,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
     for (;;) {
         const uint64_t nbase = base + stride;
         const bool have_next = nbase < A.n, have_nn = nbase + stride < A.n;
-        if (have_nn) ti = issue_tile(nbase + stride, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);
+        ti = issue_tile(nbase + stride, lane, A.n, A.in_off, A.in_len, nullptr, A.out_off);  // clamped: always safe
         Plan nn;
         bool nn_pf = false, advanced = false;
         // commit nxt's span into the (free) stage, then plan the tile after it and put its span in flight
@@ -1107,12 +1112,10 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
             PROF_MARK(2);
             if (nxt_pf) pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
             PROF_MARK(3);  // commit
-            if (have_nn) {
-                nn = plan(nbase + stride, ti);
-                if (nn.fits) {
-                    pf.issue(A.in, A.in_size, nn.a0, nn.span, lane);
-                    nn_pf = true;
-                }
+            nn = plan(nbase + stride, ti);  // on every path: ti is consumed at one place (see issue_tile)
+            if (have_nn && nn.fits) {
+                pf.issue(A.in, A.in_size, nn.a0, nn.span, lane);
+                nn_pf = true;
             }
             PROF_MARK(7);  // plan + issue of the tile after next
             advanced = true;
