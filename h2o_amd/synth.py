@@ -135,6 +135,8 @@ def make_batch_torch(config, n=None, seed=0, device="cuda", adversarial_frac=0.0
     else:
         L = torch.arange(lo, hi + 1, device=device, dtype=torch.float64)
         lens = torch.multinomial(1.0 / L, n, replacement=True, generator=g) + lo
+        if kind == "zipf_desc":  # ablation (tools/ab.py): the same lengths, longest first
+            lens = torch.sort(lens, descending=True).values
     off = torch.zeros(n + 1, dtype=torch.int64, device=device)
     off[1:] = torch.cumsum(lens, 0)
     total = int(off[-1].item())

@@ -33,6 +33,7 @@ def run(names, cfg="c4", rounds=5, steps=10):
 
     # ablation configs (not product configs): fixed-length strings isolate lane imbalance
     synth.CONFIGS.setdefault("c4u", dict(n=1 << 24, lengths=("uniform", 48, 48), alphabet="header"))
+    synth.CONFIGS.setdefault("c3desc", dict(n=1 << 20, lengths=("zipf_desc", 8, 512), alphabet="header"))
     for L in (64, 80, 96, 120, 200, 400):  # fixed lengths at the c3 scale: what length-sorted tiles could reach
         synth.CONFIGS.setdefault("u%d" % L, dict(n=1 << 20, lengths=("uniform", L, L), alphabet="header"))
     torch.cuda.set_device(0)
