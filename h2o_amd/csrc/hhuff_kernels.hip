@@ -681,19 +681,23 @@ __device__ __forceinline__ uint4 load16_bounded(const uint8_t* __restrict__ in, 
     return load16_tail(in, in_size, a);
 }
 
-// bytes [lo, hi) of the 16-B LDS chunk `c` to global `g` (16-B aligned): dword stores where whole
+// bytes [lo, hi) of the 16-B LDS chunk `c` to global `g` (16-B aligned): whole dwords as dword stores, the
+// partial dword at each end (at most 3 bytes each) as byte stores -- a fixed set of at most 10 predicated
+// stores, where per-dword byte loops issued up to 16 (the wave runs the union of its lanes' paths)
 __device__ __forceinline__ void store_range16(uint8_t* __restrict__ g, const uint8_t* c, uint32_t lo, uint32_t hi) {
     const uint4 v = *reinterpret_cast<const uint4*>(c);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t bl = max(lo, 4u * k), bh = min(hi, 4u * k + 4u);
-        if (bl >= bh) continue;
-        if (bh - bl == 4u) {
-            *reinterpret_cast<uint32_t*>(g + 4u * k) = w[k];
-        } else {
-            for (uint32_t x = bl; x < bh; ++x) g[x] = (uint8_t)(w[k] >> (8u * (x & 3u)));
-        }
+    for (uint32_t k = 0; k < 4; ++k)
+        if (lo <= 4u * k && 4u * k + 4u <= hi) *reinterpret_cast<uint32_t*>(g + 4u * k) = w[k];
+    const uint64_t q0 = (uint64_t)v.y << 32 | v.x, q1 = (uint64_t)v.w << 32 | v.z;
+    auto byte_at = [&](uint32_t a) { return (uint32_t)((a < 8u ? q0 : q1) >> (8u * (a & 7u))); };
+    const uint32_t e0 = min(hi, (lo + 3u) & ~3u);            // head partial dword: [lo, e0)
+    const uint32_t s1 = max(max(lo, hi & ~3u), e0);           // tail partial dword: [s1, hi)
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) {
+        if (lo + j < e0) g[lo + j] = (uint8_t)byte_at(lo + j);
+        if (s1 + j < hi) g[s1 + j] = (uint8_t)byte_at(s1 + j);
     }
 }
 
