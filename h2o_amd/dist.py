@@ -101,6 +101,18 @@ def scatter_batch(batch, root=0, group=None, device=None):
     return out
 
 
+def exchange_sizes_async(n_strings, out_bytes, group=None, device=None):
+    """exchange_sizes issued asynchronously: returns (work, parts).  With RCCL the all_gather runs on the
+    collective's own stream once the work queued before it (the kernel that produced `out_bytes`) is done,
+    so kernels launched after it on the compute stream overlap it; work.wait() makes the compute stream
+    wait for it (no host block).  torch.stack(parts) then gives the sizes."""
+    dev = torch.device(device) if device is not None else _default_device(group)
+    mine = torch.stack([torch.as_tensor(n_strings, dtype=torch.int64, device=dev),
+                        torch.as_tensor(out_bytes, dtype=torch.int64, device=dev).reshape(())])
+    parts = [torch.empty(2, dtype=torch.int64, device=dev) for _ in range(dist.get_world_size(group))]
+    return dist.all_gather(parts, mine, group=group, async_op=True), parts
+
+
 def exchange_sizes(n_strings, out_bytes, group=None, device=None):
     """all_gather of every shard's (strings, output bytes): returns (sizes int64 [world, 2], this shard's
     global string index and global output byte offset).  `out_bytes` may be a device tensor (a sum the

@@ -75,6 +75,10 @@ def _worker(rank, world, port, q, with_names, gpu=False):
         sizes, first, obase = hd.exchange_sizes(local[0], local[1])
         exp = sum(r + 1 for r in range(rank)), sum(10 * (r + 1) for r in range(rank))
         assert (int(first), int(obase)) == exp and sizes.shape == (world, 2)
+        # the asynchronous form bench.py overlaps with the decode: same sizes once waited for
+        work, parts = hd.exchange_sizes_async(local[0], local[1])
+        work.wait()
+        assert torch.equal(torch.stack(parts), sizes)
         if rank == 0:
             q.put(tuple(np.asarray(x).tobytes() for x in res))
     finally:
