@@ -40,7 +40,8 @@ METRIC = "GiB/s device-resident Huffman decode+encode, 16M header strings mean 4
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) on this node; without a launcher's WORLD_SIZE, N > 1 starts N ranks itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4")
@@ -173,9 +174,67 @@ def mean(x):
     return sum(x) / len(x)
 
 
+def launch_plan(gpus, env, backend, device_count):
+    """How this invocation runs: ("rank", world) -- this process is one rank of `world` (a launcher set
+    WORLD_SIZE, or N = 1) -- or ("spawn", N) -- start N ranks (torch.distributed.run as a child process; this
+    process has not touched the GPU) and exit with their status.  Raises SystemExit with a message when the
+    request cannot be met: --gpus disagreeing with the launcher's WORLD_SIZE, or more RCCL ranks than GPUs.
+    `device_count` is a callable (torch.cuda.device_count, which does not initialise the GPU on this image)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        ws = int(ws)
+        if gpus is not None and gpus != ws:
+            raise SystemExit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%d ranks" % (gpus, ws))
+        return ("rank", ws)
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1 (got %d)" % n)
+    if n == 1:
+        return ("rank", 1)
+    if backend == "nccl":
+        have = device_count()
+        if have < n:
+            raise SystemExit("bench.py: --gpus %d needs %d GPUs for RCCL, this node shows %d "
+                             "(HHUFF_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs)" % (n, n, have))
+    return ("spawn", n)
+
+
+def rank_command(n, argv, port):
+    """the child command that starts n ranks of this script: torch.distributed.run sets RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_* for each; every rank sees the same arguments and --gpus n"""
+    args = [a for a in argv]
+    if not any(a == "--gpus" or a.startswith("--gpus=") for a in args):
+        args += ["--gpus", str(n)]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + args
+
+
+def spawn_ranks(n, argv):
+    """start n ranks of this script on this node (one per GPU) as a child process tree and return their exit
+    status; rank 0 prints the JSON line"""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "16")
+    return subprocess.run(rank_command(n, argv, port), env=env).returncode
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    backend = os.environ.get("HHUFF_DIST_BACKEND", "nccl")  # gloo: rehearse N ranks on fewer GPUs
+
+    def _count():
+        import torch
+        return torch.cuda.device_count()
+
+    mode, world = launch_plan(args.gpus, os.environ, backend, _count)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
+    args.gpus = world
     pmc = {}
     if not args.pmc_child and not args.no_traffic and world == 1:
         pmc = pmc_passes(args)  # child processes; this process has not touched the GPU yet
@@ -187,7 +246,6 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    backend = os.environ.get("HHUFF_DIST_BACKEND", "nccl")  # gloo: rehearse N ranks on fewer GPUs
     if world > 1:
         torch.cuda.set_device(local % torch.cuda.device_count())
         if backend == "nccl":
@@ -236,19 +294,25 @@ def main():
     do_enc = args.only in (None, "encode")
     do_dec = args.only in (None, "decode")
     # N > 1: the batch split's all_gather of (strings, output bytes), from device-resident sums.  With both
-    # kernels in the step it is issued behind the encode (its output bytes) and overlaps the decode on the
-    # collective's stream; the decode's end event is recorded after the compute stream waits for it.
+    # kernels in the step it is issued behind the encode (its output bytes) and waited for after the decode.
+    # Every piece has its own event pair on the compute stream, so encode_ms / decode_ms are the codec
+    # launches alone: "issue" covers the output-byte sum and the all_gather's enqueue, "wait" the part of the
+    # exchange the decode did not hide.  With RCCL the collective runs on its own stream; with gloo the
+    # device-to-host copy of the sum blocks the host until the encode is done (host-synchronous, no overlap).
     overlap = world > 1 and do_enc and do_dec
     pending = []
 
     def run_encode():
         codec.encode_batch(b["data"], off32, n, out=enc_out, out_len=enc_len, status=enc_st, in_size=P)
-        if overlap:
-            pending.append(hd.exchange_sizes_async(n, torch.clamp(enc_len, min=0).to(torch.int64).sum())[0])
+
+    def run_exchange_issue():
+        pending.append(hd.exchange_sizes_async(n, torch.clamp(enc_len, min=0).to(torch.int64).sum())[0])
 
     def run_decode():
         codec.decode_batch(huff, h_off32, n_ok, is_name_bits=names_bits, out=dec_out, out_len=dec_len, status=dec_st,
                            in_size=H)
+
+    def run_exchange_wait():
         while pending:
             pending.pop().wait()
 
@@ -260,11 +324,16 @@ def main():
     torch.cuda.synchronize()
     assert bool((dec_len == lens[idx].to(torch.int32)).all()), "decode does not invert encode"
 
-    fns = ([run_encode] if do_enc else []) + ([run_decode] if do_dec else []) + \
-        ([run_exchange] if world > 1 and not overlap else [])
+    if overlap:
+        fns = [run_encode, run_exchange_issue, run_decode, run_exchange_wait]
+        slot_enc, slot_dec = 0, 2
+    else:
+        fns = ([run_encode] if do_enc else []) + ([run_decode] if do_dec else []) + \
+            ([run_exchange] if world > 1 else [])
+        slot_enc, slot_dec = 0, (1 if do_enc else 0)
     ms_step, per = timed_events(torch, fns, args.steps, args.warmup, world, dist)
-    t_enc = mean(per[0]) if do_enc else 0.0
-    t_dec = mean(per[1 if do_enc else 0]) if do_dec else 0.0
+    t_enc = mean(per[slot_enc]) if do_enc else 0.0
+    t_dec = mean(per[slot_dec]) if do_dec else 0.0
 
     # ---- packed-output mode on the same shard (hhuff_{de,en}code_batch_packed) ----------------------------
     packed = None
@@ -286,12 +355,18 @@ def main():
         torch.cuda.synchronize()
         assert bool((dec_len == lens[idx].to(torch.int32)).all()), "packed decode does not invert encode"
         pk_ms, pk = timed_events(torch, [run_encode_packed, run_decode_packed], args.steps, args.warmup, world, dist)
+        # value: the whole batch over the slowest rank's kernel time (the same rule as the headline)
         packed = {"encode_ms": round(mean(pk[0]), 4), "decode_ms": round(mean(pk[1]), 4), "ms_per_step": round(pk_ms, 4),
-                  "value": round(P / GIB / ((mean(pk[0]) + mean(pk[1])) * 1e-3), 3)}
+                  "_kernel_ms": mean(pk[0]) + mean(pk[1])}
     if world > 1:
-        t = torch.tensor([ms_step], device="cuda" if backend == "nccl" else "cpu", dtype=torch.float64)
+        vals = [ms_step] + ([packed["_kernel_ms"]] if packed is not None else [])
+        t = torch.tensor(vals, device="cuda" if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms_step = float(t.item())
+        ms_step = float(t[0].item())
+        if packed is not None:
+            packed["_kernel_ms"] = float(t[1].item())
+    if packed is not None:
+        packed["value"] = round(P_all / GIB / (packed.pop("_kernel_ms") * 1e-3), 3)
 
     if rank == 0:
         B_dec = H + P_ok + 9 * n_ok + 4 + (n_ok + 7) // 8
@@ -337,7 +412,12 @@ def main():
         if world > 1 and not overlap:
             line["exchange_ms"] = round(mean(per[-1]), 4)
         elif world > 1:
-            line["exchange"] = "all_gather of (strings, encode output bytes) issued behind the encode, overlapping the decode"
+            line["exchange_issue_ms"] = round(mean(per[1]), 4)
+            line["exchange_wait_ms"] = round(mean(per[3]), 4)
+            line["exchange"] = ("all_gather of (strings, encode output bytes) issued behind the encode on the RCCL "
+                                "stream and waited for after the decode" if backend == "nccl" else
+                                "gloo rehearsal: host-synchronous all_gather after the encode (no overlap)")
+            line["dist_backend"] = backend
         if packed is not None:
             B_dec_pk = B_dec + 4 * (n_ok + 1)  # + out_off[n + 1]
             B_enc_pk = B_enc + 4 * (n + 1)

@@ -39,8 +39,12 @@ def lib():
             raise HhuffError("libhhuff.so not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
         # torch first: its ROCm wheel ships its own libamdhip64.so, and libhhuff.so's dependency must
         # resolve to that already-loaded runtime -- one HIP runtime per process (loaded the other way round,
-        # two runtimes end up sharing the device and the per-string path fails)
-        import torch  # noqa: F401
+        # two runtimes end up sharing the device and the per-string path fails).  Without torch (the
+        # numpy-only host and per-string bindings) the library's own HIP runtime dependency is used.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
 
         L = ctypes.CDLL(LIB_PATH)
         L.h2o_hpack_decode_huffman.restype = ctypes.c_size_t
@@ -95,6 +99,8 @@ def lib():
         L.hhuff_grid_size.restype = ctypes.c_int
         L.hhuff_per_string_calls.restype = ctypes.c_uint64
         L.hhuff_grid_size.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.hhuff_pool_trim.restype = ctypes.c_int
+        L.hhuff_pool_trim.argtypes = []
         _lib = L
     return _lib
 
@@ -107,7 +113,7 @@ EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decod
             "hhuff_qpack_decode", "hhuff_qpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string", "hhuff_per_string_calls",
-            "hhuff_grid_size")
+            "hhuff_grid_size", "hhuff_pool_trim")
 
 
 def _check(rc, what):

@@ -258,7 +258,8 @@ HHUFF_API int hhuff_qpack_decode(const uint8_t* in, uint64_t in_size, const uint
                  !sstatus || !req_insert_count))
         return arg_fail("NULL array");
     if (header_table_size > (1u << 30)) return arg_fail("header_table_size above 2^30");
-    if (in_size >= (1ull << 32)) return arg_fail("in_size must be below 2^32 (u32 offsets)");
+    // u32 offsets, and the literal workspace is sized for in_size + 2 literals in 32 bits
+    if (in_size > (1ull << 32) - 3) return arg_fail("in_size must be at most 2^32 - 3 (u32 offsets)");
     if (scratch_size < hhuff_qpack_scratch_size(nconn, header_table_size))
         return arg_fail("scratch smaller than hhuff_qpack_scratch_size");
     if (((uintptr_t)scratch & 15u) != 0) return arg_fail("scratch must be 16-byte aligned");
@@ -663,6 +664,10 @@ HHUFF_API int hhuff_debug_prof(unsigned long long* out16, int reset) {
 #endif
 HHUFF_API const char* hhuff_version(void) { return "hhuff 0.1.0 (gfx950)"; }
 HHUFF_API const char* hhuff_last_error_string(void) { return t_err; }
+HHUFF_API int hhuff_pool_trim(void) {
+    hipError_t e = hhuff::pool_trim();
+    return e == hipSuccess ? HHUFF_OK : hip_fail(e, "pool trim");
+}
 HHUFF_API int hhuff_grid_size(int device, int which) {
     DeviceGuard guard(device);
     if (guard.err != hipSuccess) return -1;

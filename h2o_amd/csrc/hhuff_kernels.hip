@@ -2077,9 +2077,12 @@ static uint64_t edge_recs(uint32_t n) { return 2 * (((uint64_t)n + 63) / 64); }
 
 // Edge records come from a library-owned stream-ordered pool that keeps its memory between calls (the
 // default pool's release threshold of 0 would hand it back to the driver at every synchronisation).
+// hhuff_pool_trim() hands the kept memory back.
+static std::mutex g_pool_mu;
+static hipMemPool_t g_pools[64] = {};
 static hipError_t pool_alloc(void** p, uint64_t bytes, hipStream_t stream) {
-    static std::mutex mu;
-    static hipMemPool_t pools[64] = {};
+    std::mutex& mu = g_pool_mu;
+    hipMemPool_t* pools = g_pools;
     const int dev = current_device();
     if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
     hipMemPool_t pool;
@@ -2482,6 +2485,15 @@ hipError_t launch_literals_dev(const uint8_t* in, uint64_t in_size, const uint32
 uint64_t literals_dev_ws(uint32_t n_max, uint64_t in_size) { return 5ull * n_max + 8 + 16 + 4 * (in_size / kLongRaw + 1); }
 
 hipError_t work_alloc(void** p, uint64_t bytes, hipStream_t stream) { return pool_alloc(p, bytes, stream); }
+
+hipError_t pool_trim() {
+    const int dev = current_device();
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    if (!g_pools[dev]) return hipSuccess;
+    hipError_t e = hipDeviceSynchronize();  // memory freed on a stream returns to the pool once the stream passes it
+    return e == hipSuccess ? hipMemPoolTrimTo(g_pools[dev], 0) : e;
+}
 
 int grid_size(int device, int which) { return grid_for(which == 0 ? kDecS : kEncS, device, 0xFFFFFFFFu); }
 

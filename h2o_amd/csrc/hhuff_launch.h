@@ -50,6 +50,8 @@ hipError_t launch_literal_list(const uint32_t* lit_bits, const uint32_t* name_bi
                                uint8_t* prefix_of, hipStream_t stream);
 // stream-ordered device memory from the library's pool (free with hipFreeAsync on the same stream)
 hipError_t work_alloc(void** p, uint64_t bytes, hipStream_t stream);
+// hand the pool's kept memory on the current device back to the driver (hhuff_pool_trim)
+hipError_t pool_trim();
 
 // HPACK header blocks (f4): see include/hhuff.h hhuff_hpack_decode_blocks; scratch = nconn x
 // hpack_conn_scratch(table_size) bytes of device memory

@@ -182,9 +182,12 @@ int hhuff_decode_literals(const uint8_t *in, uint64_t in_size, const uint32_t *l
  *      earlier block of the connection failed: h2o drops the connection).  Fields before the error stand.
  *      Device arrays; scratch = device memory of hhuff_hpack_scratch_size(nconn, table_size) bytes (the
  *      dynamic tables, 16-byte aligned), kept by the caller between calls for HHUFF_BLK_CONTINUE;
- *      asynchronous on `stream`.  The call also takes a stream-ordered workspace of about 16 bytes per input
- *      byte from the library's device memory pool (the literal pre-pass and the field sources; released
- *      on the stream, kept by the pool for the next call). */
+ *      asynchronous on `stream`.  The call also takes a stream-ordered workspace from the library's device
+ *      memory pool: 16 bytes per input byte of field sources plus, for inputs below 4 GiB, the literal
+ *      pre-pass -- 22 bytes per possible literal (up to 2/3 of the input bytes) plus 1.6 per input byte of
+ *      decoded output -- about 33 bytes per input byte in all.  It is released on the stream; the pool
+ *      keeps released memory for the next call (it never returns it to the driver by itself):
+ *      hhuff_pool_trim() hands it back. */
 #define HHUFF_BLK_CONTINUE 1u /* flags: the tables (and failed state) the previous call left in scratch
                                  carry over -- connection c of this call is connection c of that one; without
                                  it every connection starts with an empty table */
@@ -281,11 +284,12 @@ int hhuff_hpack_parse_requests(const uint8_t *in, uint64_t in_size, const uint32
  *      state) over from the previous call -- connection c of this call is connection c of that one;
  *      without it every connection starts with a fresh decoder; the tables hold scratch offsets, not
  *      addresses, so scratch may be moved between calls.  nsec = conn_first[nconn] (host copy).
- *      in_size < 2^32 (offsets are u32).  Encoder streams and sections must not overlap in `in`.
+ *      in_size <= 2^32 - 3 (offsets are u32).  Encoder streams and sections must not overlap in `in`.
  *      Asynchronous on `stream`: a literal pre-pass (every literal of the step decoded at once), the
  *      encoder streams (one lane per connection, entries booked as references), a table pass, the
- *      sections (one lane per section) and a copy pass; ~30 bytes of stream-ordered pool workspace per
- *      input byte. */
+ *      sections (one lane per section) and a copy pass.  Stream-ordered pool workspace: 16 bytes per input
+ *      byte of field sources, 22 per possible literal (one per input byte) and 1.6 of decoded output --
+ *      about 40 bytes per input byte; kept by the pool after the call (hhuff_pool_trim). */
 #define HHUFF_QPK_CONTINUE 1u
 #define HHUFF_QPK_DECOMPRESSION_FAILED 0x30200 /* H2O_HTTP3_ERROR_QPACK_DECOMPRESSION_FAILED, http3_common.h:73 */
 #define HHUFF_QPK_ARENA (-300)
@@ -323,6 +327,9 @@ const char *hhuff_version(void);
 const char *hhuff_last_error_string(void);
 /* Number of workgroups the decode / encode launches use on `device` (grid sizing, for profiling). */
 int hhuff_grid_size(int device, int which /* 0 decode, 1 encode */);
+/* Return the memory the library's stream-ordered pool on the caller's current device keeps between calls
+ * (batch workspaces, edge records) to the driver.  Synchronises the device first.  HHUFF_OK or an error. */
+int hhuff_pool_trim(void);
 
 #ifdef __cplusplus
 }

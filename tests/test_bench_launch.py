@@ -1,0 +1,53 @@
+"""bench.py --gpus N: the launcher's decisions (no GPU needed).  A bare `bench.py --gpus N` starts N ranks
+itself through torch.distributed.run; under a launcher the rank checks that --gpus agrees with WORLD_SIZE;
+RCCL ranks beyond the node's GPUs are refused with a message."""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _never():
+    raise AssertionError("device_count must not be consulted")
+
+
+def test_single_gpu_runs_in_process():
+    assert bench.launch_plan(None, {}, "nccl", _never) == ("rank", 1)
+    assert bench.launch_plan(1, {}, "nccl", _never) == ("rank", 1)
+
+
+def test_n_gpus_spawns_when_no_launcher():
+    assert bench.launch_plan(8, {}, "nccl", lambda: 8) == ("spawn", 8)
+    assert bench.launch_plan(2, {}, "gloo", _never) == ("spawn", 2)  # gloo rehearsal on fewer GPUs
+
+
+def test_too_few_gpus_for_rccl_is_refused():
+    with pytest.raises(SystemExit) as e:
+        bench.launch_plan(8, {}, "nccl", lambda: 1)
+    assert "needs 8 GPUs" in str(e.value)
+
+
+def test_launcher_world_size_must_match():
+    assert bench.launch_plan(4, {"WORLD_SIZE": "4"}, "nccl", _never) == ("rank", 4)
+    assert bench.launch_plan(None, {"WORLD_SIZE": "2"}, "nccl", _never) == ("rank", 2)
+    with pytest.raises(SystemExit) as e:
+        bench.launch_plan(8, {"WORLD_SIZE": "2"}, "nccl", _never)
+    assert "WORLD_SIZE=2" in str(e.value)
+    with pytest.raises(SystemExit):
+        bench.launch_plan(0, {}, "nccl", _never)
+
+
+def test_rank_command():
+    cmd = bench.rank_command(4, ["--steps", "5"], 29511)
+    i = cmd.index("torch.distributed.run")
+    assert cmd[i - 1] == "-m" and "--nproc-per-node" in cmd and cmd[cmd.index("--nproc-per-node") + 1] == "4"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[cmd.index("--master-port") + 1] == "29511"
+    assert cmd[-4:] == ["--steps", "5", "--gpus", "4"]
+    assert cmd.count("--gpus") == 1
+    assert bench.rank_command(2, ["--gpus", "2"], 1).count("--gpus") == 1
+    assert bench.rank_command(2, ["--gpus=2"], 1)[-1] == "--gpus=2"

@@ -104,6 +104,8 @@ def test_argument_checks_need_no_gpu():
                                     None, None, None, None, None, p, p, p, scratch, scratch_size, 0, None)
 
     assert qpack(1 << 32, p, ss) == -1
+    assert qpack((1 << 32) - 2, p, ss) == -1  # n_max = in_size + 2 would wrap the u32 literal count
+    assert qpack((1 << 32) - 1, p, ss) == -1
     assert b"2^32" in L.hhuff_last_error_string()
     assert qpack(100, p, ss - 1) == -1
     assert b"scratch" in L.hhuff_last_error_string()
