@@ -64,8 +64,11 @@ def kernel_key(name):
     packed = ", true>" in name
     if "decode_staged_kernel" in name or "decode_stream_kernel" in name or "decode_direct_kernel" in name:
         return "decode_packed" if packed else "decode"
-    if "encode_staged_kernel" in name or "encode_pl_kernel" in name or "encode_direct_kernel" in name:
+    if ("encode_staged_kernel" in name or "encode_pl_kernel" in name or "encode_direct_kernel" in name or
+            "encode_cp_kernel" in name):
         return "encode_packed" if packed else "encode"
+    if "flatten_pl_kernel" in name or "flatten_direct_kernel" in name:
+        return "flatten"
     if "edge_fix" in name:
         return "edge_fix"
     return None
@@ -75,10 +78,12 @@ SQ_GROUP = ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_S
             "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
 
 
-def pmc_passes(args):
+def pmc_passes(args, config=None, groups=None):
     """Per-launch PMC counters of each hhuff kernel: one rocprofv3 run per counter group (FETCH_SIZE,
-    WRITE_SIZE, the SQ group, GRBM_GUI_ACTIVE) over this script as a child, BEFORE this process touches the
-    GPU.  Returns {kernel key: {counter: mean per launch}} or {} when rocprofv3 is unavailable."""
+    WRITE_SIZE, the SQ group, GRBM_GUI_ACTIVE) over this script as a child on `config` (default: the bench's
+    own), BEFORE this process touches the GPU.  Returns {kernel key: {counter: per launch}} or {} when
+    rocprofv3 is unavailable.  A launch may run several kernels under one key (the mixed-length decode: the
+    staged and the stream kernel, one of which exits at once): their counters add up."""
     import csv
     import shutil
     import subprocess
@@ -88,11 +93,13 @@ def pmc_passes(args):
     if not os.path.exists(exe):
         return {}
     child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "2", "--warmup", "1",
-             "--no-cpu-baseline", "--no-traffic", "--no-host", "--no-extra", "--config", args.config]
-    if args.n:
+             "--no-cpu-baseline", "--no-traffic", "--no-host", "--no-extra", "--config", config or args.config]
+    if args.n and config is None:
         child += ["--n", str(args.n)]
+    if config is not None:
+        child += ["--no-packed"]
     vals = {}
-    for group in (("FETCH_SIZE",), ("WRITE_SIZE",), SQ_GROUP, ("GRBM_GUI_ACTIVE",)):
+    for group in groups or (("FETCH_SIZE",), ("WRITE_SIZE",), SQ_GROUP, ("GRBM_GUI_ACTIVE",)):
         d = tempfile.mkdtemp(prefix="hhuff_pmc_")
         try:
             subprocess.run([exe, "--pmc"] + list(group) + ["--output-format", "csv", "-d", d, "-o", "pmc", "--"] + child,
@@ -104,8 +111,10 @@ def pmc_passes(args):
                         for r in csv.DictReader(open(os.path.join(root, f))):
                             k = kernel_key(r["Kernel_Name"])
                             if k is not None:
-                                vals.setdefault(k, {}).setdefault((r["Dispatch_Id"], r["Counter_Name"]), 0.0)
-                                vals[k][(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+                                kn = r["Kernel_Name"]
+                                key = (kn, int(r["Dispatch_Id"]), r["Counter_Name"])
+                                vals.setdefault(k, {}).setdefault(key, 0.0)
+                                vals[k][key] += float(r["Counter_Value"])
         except Exception:
             return {}
         finally:
@@ -113,10 +122,15 @@ def pmc_passes(args):
     out = {}
     for k, per in vals.items():
         agg = {}
-        for (_, cname), v in per.items():
-            agg.setdefault(cname, []).append(v)
-        # the last two dispatches are the child's timed steps (the first ones build the wire)
-        out[k] = {c: sum(v[-2:]) / len(v[-2:]) for c, v in agg.items()}
+        for (kn, disp, cname), v in per.items():
+            agg.setdefault((kn, cname), []).append((disp, v))
+        # per kernel: the last two dispatches are the child's timed steps (the first ones build the wire);
+        # the kernels of one key add up
+        tot = {}
+        for (kn, cname), dv in agg.items():
+            last = [v for _, v in sorted(dv)[-2:]]
+            tot[cname] = tot.get(cname, 0.0) + sum(last) / len(last)
+        out[k] = tot
     return out
 
 
@@ -235,9 +249,11 @@ def main():
     if mode == "spawn":
         sys.exit(spawn_ranks(world, sys.argv[1:]))
     args.gpus = world
-    pmc = {}
+    pmc, pmc_cfg = {}, {}
     if not args.pmc_child and not args.no_traffic and world == 1:
         pmc = pmc_passes(args)  # child processes; this process has not touched the GPU yet
+        if not args.no_extra:  # HBM traffic of the other configs' kernels (two passes each)
+            pmc_cfg = {c: pmc_passes(args, config=c, groups=(("FETCH_SIZE",), ("WRITE_SIZE",))) for c in ("c2", "c3", "c5")}
     import torch
     import torch.distributed as dist
 
@@ -332,6 +348,12 @@ def main():
             ([run_exchange] if world > 1 else [])
         slot_enc, slot_dec = 0, (1 if do_enc else 0)
     ms_step, per = timed_events(torch, fns, args.steps, args.warmup, world, dist)
+    if args.pmc_child and args.config == "c5":  # c5's own operation, flatten_string framing, for its PMC pass
+        f_out = torch.empty(P + 11 * n + 16, dtype=torch.uint8, device="cuda")
+        f_len = torch.empty(n, dtype=torch.int32, device="cuda")
+        for _ in range(3):
+            codec.flatten_batch(b["data"], off32, n, 7, out=f_out, out_len=f_len, in_size=P)
+        torch.cuda.synchronize()
     t_enc = mean(per[slot_enc]) if do_enc else 0.0
     t_dec = mean(per[slot_dec]) if do_dec else 0.0
 
@@ -431,7 +453,7 @@ def main():
             line["packed"] = packed
         if world == 1 and not args.pmc_child:
             if not args.no_extra:
-                line["configs"] = other_configs(torch, codec, synth)
+                line["configs"] = other_configs(torch, codec, synth, pmc_cfg)
                 line["f4"] = f4_lines(torch, codec)
                 line["per_string_latency_us"] = per_string_latency(codec)
             if not args.no_host:
@@ -443,11 +465,22 @@ def main():
         dist.destroy_process_group()
 
 
-def other_configs(torch, codec, synth):
+def kernel_roofline(B, t_ms, pmc, key):
+    """{algorithmic bytes, achieved GB/s, fraction of HBM peak, PMC traffic per launch} of one kernel"""
+    ach = B / (t_ms * 1e-3) / 1e9
+    tr = traffic_bytes(pmc.get(key, {})) if pmc else None
+    return {"algorithmic_bytes": int(B), "achieved": round(ach, 2), "frac": round(ach / HBM_PEAK_GBPS, 4),
+            "traffic": round(tr) if tr else None, "traffic_over_algorithmic": round(tr / B, 4) if tr else None}
+
+
+def other_configs(torch, codec, synth, pmc_cfg=None):
     """BASELINE configs 2, 3, 5 (device-resident, HIP-event medians; tools/bench_configs.py): encode to slots,
-    decode of the compressible strings' Huffman packed back to back, and for c5 the flatten_string framing"""
+    decode of the compressible strings' Huffman packed back to back, and for c5 the flatten_string framing.
+    Each leg carries its roofline (SURVEY 8d bytes; traffic from this config's own PMC passes):
+    decode H + P_ok + 9 N_ok + 4, encode P + E + 9 N + 4, framing P + F + 8 N + 4 (F: framed bytes)."""
     import bench_configs as BC
 
+    pmc_cfg = pmc_cfg or {}
     res = {}
     for cfg in ("c2", "c3", "c5"):
         b = synth.make_batch_torch(cfg, seed=7)
@@ -463,15 +496,21 @@ def other_configs(torch, codec, synth):
         e_out = torch.empty(P + 16, dtype=torch.uint8, device="cuda")
         e_len = torch.empty(n, dtype=torch.int32, device="cuda")
         t_enc = BC.timed(torch, lambda: codec.encode_batch(b["data"], off32, n, out=e_out, out_len=e_len, in_size=P))
+        E = int(torch.clamp(e_len, min=0).to(torch.int64).sum().item())
+        pm = pmc_cfg.get(cfg, {})
         r.update(decode_ms=round(t_dec, 4), decode_gibps=round(P_ok / GIB / (t_dec * 1e-3), 2),
                  encode_ms=round(t_enc, 4), encode_gibps=round(P / GIB / (t_enc * 1e-3), 2),
-                 round_trip_gibps=round(P / GIB / ((t_enc + t_dec) * 1e-3), 2))
+                 round_trip_gibps=round(P / GIB / ((t_enc + t_dec) * 1e-3), 2),
+                 decode_roofline=kernel_roofline(H + P_ok + 9 * n_ok + 4, t_dec, pm, "decode"),
+                 encode_roofline=kernel_roofline(P + E + 9 * n + 4, t_enc, pm, "encode"))
         del huff, h_off, d_out, e_out
         if cfg == "c5":  # QPACK values: flatten_string(prefix 7) framing, the config's own operation
             f_out = torch.empty(P + 11 * n + 16, dtype=torch.uint8, device="cuda")
             f_len = torch.empty(n, dtype=torch.int32, device="cuda")
             t = BC.timed(torch, lambda: codec.flatten_batch(b["data"], off32, n, 7, out=f_out, out_len=f_len, in_size=P))
-            r.update(flatten_ms=round(t, 4), flatten_gibps=round(P / GIB / (t * 1e-3), 2))
+            F = int(f_len.to(torch.int64).sum().item())
+            r.update(flatten_ms=round(t, 4), flatten_gibps=round(P / GIB / (t * 1e-3), 2),
+                     flatten_roofline=kernel_roofline(P + F + 8 * n + 4, t, pm, "flatten"))
         res[cfg] = r
         del b
         torch.cuda.empty_cache()

@@ -431,6 +431,88 @@ def test_c4_full_size_round_trip(torch_cuda):
     assert bool((d_out[dec_idx][okb] == b["data"][okb]).all())
 
 
+def _slot_bytes_equal(torch, a, b, slot_off, slot_len, used):
+    """bytes [slot_off[i], slot_off[i] + used[i]) of buffers a and b agree for every i (used = FAIL: none);
+    slots are back to back from slot_off[0] (slot_len[i] bytes each) -- compared on the device"""
+    used = torch.where(used == -1, torch.zeros_like(used), used).to(torch.int64)
+    slot_len = slot_len.to(torch.int64)
+    total = int(slot_len.sum().item())
+    base = int(slot_off[0].item())
+    rel = torch.arange(total, device="cuda", dtype=torch.int64) - torch.repeat_interleave(
+        torch.cumsum(slot_len, 0) - slot_len, slot_len)
+    mask = rel < torch.repeat_interleave(used, slot_len)
+    return bool((a[base:base + total][mask] == b[base:base + total][mask]).all())
+
+
+def test_c4_full_size_vs_oracle(torch_cuda, oracle_codec):
+    """config 4 at its full size (16M strings, U[24,72], 805 MB) against the restatement (16 threads), through
+    the bench's layouts: encode to slots = in_off; decode of the compressible strings' Huffman packed back
+    to back with their is-name bits (lengths, status and every byte of every output)."""
+    import torch
+
+    from h2o_amd import codec
+    from h2o_amd import dist as hd
+
+    b = synth.make_batch_torch("c4", seed=2025)
+    n, P = b["n"], int(b["total"])
+    off32 = b["off"].to(torch.int32)
+    lens = (b["off"][1:] - b["off"][:-1]).to(torch.int32)
+    data_h = b["data"].cpu().numpy()
+    off_h = off32.cpu().numpy().view(np.uint32)
+    e_out, e_len, e_st = codec.encode_batch(b["data"], off32, n, in_size=P)
+    torch.cuda.synchronize()
+    o_out, o_len, o_st = oracle_codec.encode_batch(data_h, off_h, n, nthreads=16)
+    o_len_t = torch.from_numpy(o_len.view(np.int32)).cuda()
+    assert bool((e_len == o_len_t).all()), "encode lengths differ from the restatement"
+    assert bool((e_st == torch.from_numpy(o_st).cuda()).all())
+    o_out_t = torch.from_numpy(o_out).cuda()
+    assert _slot_bytes_equal(torch, e_out, o_out_t, off32.to(torch.int64), lens, e_len), "encoded bytes differ"
+    del o_out_t
+    # the wire: successful strings back to back; decode with their is-name bits
+    ok = e_len != -1
+    idx = torch.nonzero(ok).squeeze(1)
+    m = int(idx.numel())
+    hl = e_len[idx].to(torch.int64)
+    h_off = torch.zeros(m + 1, dtype=torch.int64, device="cuda")
+    h_off[1:] = torch.cumsum(hl, 0)
+    H = int(h_off[-1].item())
+    huff = torch.empty(H + 16, dtype=torch.uint8, device="cuda")
+    rel = torch.arange(H, device="cuda") - torch.repeat_interleave(h_off[:-1], hl)
+    huff[:H] = e_out[torch.repeat_interleave(b["off"][:-1][idx], hl) + rel]
+    del rel
+    names = hd.bool_to_bits(hd.bits_to_bool(b["is_name_bits"], n)[idx])
+    h32 = h_off.to(torch.int32)
+    d_out, d_len, d_st = codec.decode_batch(huff, h32, m, is_name_bits=names, in_size=H)
+    torch.cuda.synchronize()
+    od, odl, ods = oracle_codec.decode_batch(huff[:H].cpu().numpy(), h32.cpu().numpy().view(np.uint32), m,
+                                             is_name_bits=names.cpu().numpy().view(np.uint32), nthreads=16)
+    assert bool((d_len == torch.from_numpy(odl.view(np.int32)).cuda()).all()), "decode lengths differ"
+    assert bool((d_st == torch.from_numpy(ods).cuda()).all()), "decode status differs"
+    slots = (h_off * 8) // 5
+    assert _slot_bytes_equal(torch, d_out, torch.from_numpy(od).cuda(), slots[:-1], slots[1:] - slots[:-1], d_len)
+    assert bool((d_len == lens[idx]).all())  # every encoder output decodes to its string
+
+
+def test_c5_full_size_framing_vs_oracle(torch_cuda, oracle_codec):
+    """config 5's own operation at its full size: flatten_string(value, len, 7, 0) (qpack.c:1042-1066) over
+    512K cookie/URI values (mean 512 B, 268 MB), against the restatement (16 threads)"""
+    import torch
+
+    from h2o_amd import codec
+
+    b = synth.make_batch_torch("c5", seed=2026)
+    n, P = b["n"], int(b["total"])
+    off32 = b["off"].to(torch.int32)
+    f_out, f_len = codec.flatten_batch(b["data"], off32, n, 7, in_size=P)
+    torch.cuda.synchronize()
+    o_out, o_len = oracle_codec.flatten_batch(b["data"].cpu().numpy(), off32.cpu().numpy().view(np.uint32), n, 7,
+                                              nthreads=16)
+    assert bool((f_len[:n] == torch.from_numpy(o_len.view(np.int32)).cuda()).all())
+    slot_off = b["off"][:-1] + 11 * torch.arange(n, device="cuda", dtype=torch.int64)  # in_off[i] + 11 i
+    slot_len = (b["off"][1:] - b["off"][:-1]) + 11
+    assert _slot_bytes_equal(torch, f_out, torch.from_numpy(o_out).cuda(), slot_off, slot_len, f_len[:n])
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 def test_pipelined_host_path(torch_cuda, pinned):
     """chunked pageable/pinned -> device -> host path == the device-resident path, over many chunks"""
