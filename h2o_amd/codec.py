@@ -94,6 +94,10 @@ def lib():
         L.hhuff_qpack_decode.argtypes = ([_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32,
                                           ctypes.c_uint32, ctypes.c_uint64] + [_vp] * 15 +
                                          [ctypes.c_uint64, ctypes.c_uint, _vp])
+        L.hhuff_qpack_parse_requests.restype = ctypes.c_int
+        L.hhuff_qpack_parse_requests.argtypes = ([_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32,
+                                                  ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64] + [_vp] * 17 +
+                                                 [ctypes.c_uint64, ctypes.c_uint, _vp])
         L.hhuff_version.restype = ctypes.c_char_p
         L.hhuff_last_error_string.restype = ctypes.c_char_p
         L.hhuff_grid_size.restype = ctypes.c_int
@@ -110,7 +114,7 @@ EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decod
             "hhuff_decode_batch_packed", "hhuff_encode_batch_packed",
             "hhuff_flatten_batch", "hhuff_decode_literals", "hhuff_hpack_decode_blocks", "hhuff_hpack_scratch_size",
             "hhuff_hpack_parse_requests",
-            "hhuff_qpack_decode", "hhuff_qpack_scratch_size",
+            "hhuff_qpack_decode", "hhuff_qpack_parse_requests", "hhuff_qpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string", "hhuff_per_string_calls",
             "hhuff_grid_size", "hhuff_pool_trim")
@@ -357,14 +361,20 @@ def hpack_decode_blocks(data, blk_off, conn_first, table_size=4096, arena_off=No
 QPK_CONTINUE = 1
 
 
+QREQ_BYTES = 72  # sizeof(hhuff_qpack_request_t)
+
+
 def qpack_decode(data, enc_off, enc_len, sec_off, conn_first, nsec, header_table_size=4096, max_blocked=100,
-                 num_blocked=None, arena_off=None, in_size=None, stream=None, scratch=None, cont=False, arena=None):
+                 num_blocked=None, arena_off=None, in_size=None, stream=None, scratch=None, cont=False, arena=None,
+                 stream_id=None):
     """QPACK decoder step (include/hhuff.h hhuff_qpack_decode) on device tensors: enc_off / enc_len (per
     connection), sec_off / conn_first / num_blocked int32 tensors (u32 bits), arena_off int64; nsec =
     conn_first[-1] as a host int.  Returns a dict of device tensors: arena, name_off, name_len, value_off,
     value_len, fflags (per field slot), nfields, sstatus, req_insert_count (per section), enc_status,
     enc_consumed, insert_count (per connection), and the scratch holding the tables (pass it back with
-    cont=True for the next step)."""
+    cont=True for the next step).  stream_id (int64 tensor, one per section): the HTTP/3 request step,
+    hhuff_qpack_parse_requests (h2o_qpack_parse_request per section), plus "req": uint8 [nsec, 72] records
+    (hhuff_qpack_request_t)."""
     import torch
 
     dev = data.device
@@ -384,14 +394,18 @@ def qpack_decode(data, enc_off, enc_len, sec_off, conn_first, nsec, header_table
     ss = int(lib().hhuff_qpack_scratch_size(nconn, header_table_size))
     if scratch is None:
         scratch = torch.empty(max(16, ss), dtype=torch.uint8, device=dev)
-    _check(lib().hhuff_qpack_decode(_dp(data), in_size, _dp(enc_off), _dp(enc_len), _dp(sec_off), _dp(conn_first),
-                                    nconn, nsec, header_table_size, max_blocked,
-                                    None if num_blocked is None else _dp(num_blocked), _dp(r["arena"]), _dp(arena_off),
-                                    _dp(r["name_off"]), _dp(r["name_len"]), _dp(r["value_off"]), _dp(r["value_len"]),
-                                    _dp(r["fflags"]), _dp(r["nfields"]), _dp(r["sstatus"]), _dp(r["req_insert_count"]),
-                                    _dp(r["enc_status"]), _dp(r["enc_consumed"]), _dp(r["insert_count"]), _dp(scratch),
-                                    scratch.numel(), QPK_CONTINUE if cont else 0, _stream(stream)),
-           "hhuff_qpack_decode")
+    args = [_dp(data), in_size, _dp(enc_off), _dp(enc_len), _dp(sec_off), _dp(conn_first), nconn, nsec,
+            header_table_size, max_blocked, None if num_blocked is None else _dp(num_blocked), _dp(r["arena"]),
+            _dp(arena_off), _dp(r["name_off"]), _dp(r["name_len"]), _dp(r["value_off"]), _dp(r["value_len"]),
+            _dp(r["fflags"]), _dp(r["nfields"]), _dp(r["sstatus"]), _dp(r["req_insert_count"]), _dp(r["enc_status"]),
+            _dp(r["enc_consumed"]), _dp(r["insert_count"])]
+    tail = [_dp(scratch), scratch.numel(), QPK_CONTINUE if cont else 0, _stream(stream)]
+    if stream_id is None:
+        _check(lib().hhuff_qpack_decode(*(args + tail)), "hhuff_qpack_decode")
+    else:
+        r["req"] = torch.empty((max(1, nsec), QREQ_BYTES), dtype=torch.uint8, device=dev)
+        _check(lib().hhuff_qpack_parse_requests(*(args + [_dp(stream_id), _dp(r["req"])] + tail)),
+               "hhuff_qpack_parse_requests")
     r["scratch"] = scratch
     return r
 

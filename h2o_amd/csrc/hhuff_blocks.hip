@@ -22,6 +22,7 @@
 #include "hhuff_device.h"
 #include "hhuff.h"
 #include "hhuff_launch.h"
+#include "hhuff_request.h"
 
 namespace hhuff {
 namespace {
@@ -174,197 +175,7 @@ struct DynTable {  // one connection's dynamic table (newest entry = dynamic ind
 
 enum : int { kStrOk = 0, kStrFail = 1, kStrUpper = 2, kStrArena = 3 };
 
-// ---------------------------------------------------------------------------------------------------
-// h2o_hpack_parse_request's rules (hpack.c:502-637), applied to each field right after it is decoded.
-// h2o compares name POINTERS with its tokens; a name is a token exactly when its bytes are a token's
-// (static-table names are tokens, literal names are interned through h2o_lookup_token, hpack.c:398-400,
-// dynamic entries keep what they were given), so the classes below compare bytes.
-// ---------------------------------------------------------------------------------------------------
-enum : uint32_t {
-    kNRegular = 0,     // anything h2o_add_header takes as it is
-    kNAuthority,       // H2O_TOKEN_AUTHORITY
-    kNMethod,          // H2O_TOKEN_METHOD
-    kNPath,            // H2O_TOKEN_PATH
-    kNProtocol,        // H2O_TOKEN_PROTOCOL
-    kNScheme,          // H2O_TOKEN_SCHEME
-    kNPseudoOther,     // ':' + anything else (:status included)
-    kNContentLength,   // the is_hpack_special tokens (lib/common/token_table.h, 5th flag)
-    kNExpect,
-    kNHost,
-    kNTe,
-    kNCacheDigest,
-    kNDatagramFlowId,
-    kNConnSpecific,    // connection, http2-settings, transfer-encoding, upgrade
-};
-
-__device__ __forceinline__ bool bytes_eq(const uint8_t* s, const char* lit, uint32_t n) {
-    for (uint32_t i = 0; i < n; ++i)
-        if (s[i] != (uint8_t)lit[i]) return false;
-    return true;
-}
-
-__device__ uint32_t req_name_class(const uint8_t* s, uint32_t n) {
-    if (n != 0 && s[0] == ':') {
-        switch (n) {
-            case 5: return bytes_eq(s, ":path", 5) ? kNPath : kNPseudoOther;
-            case 7: return bytes_eq(s, ":method", 7) ? kNMethod : bytes_eq(s, ":scheme", 7) ? kNScheme : kNPseudoOther;
-            case 9: return bytes_eq(s, ":protocol", 9) ? kNProtocol : kNPseudoOther;
-            case 10: return bytes_eq(s, ":authority", 10) ? kNAuthority : kNPseudoOther;
-            default: return kNPseudoOther;
-        }
-    }
-    switch (n) {
-        case 2: return bytes_eq(s, "te", 2) ? kNTe : kNRegular;
-        case 4: return bytes_eq(s, "host", 4) ? kNHost : kNRegular;
-        case 6: return bytes_eq(s, "expect", 6) ? kNExpect : kNRegular;
-        case 7: return bytes_eq(s, "upgrade", 7) ? kNConnSpecific : kNRegular;
-        case 10: return bytes_eq(s, "connection", 10) ? kNConnSpecific : kNRegular;
-        case 12: return bytes_eq(s, "cache-digest", 12) ? kNCacheDigest : kNRegular;
-        case 14:
-            return bytes_eq(s, "content-length", 14) ? kNContentLength
-                   : bytes_eq(s, "http2-settings", 14) ? kNConnSpecific
-                                                        : kNRegular;
-        case 16: return bytes_eq(s, "datagram-flow-id", 16) ? kNDatagramFlowId : kNRegular;
-        case 17: return bytes_eq(s, "transfer-encoding", 17) ? kNConnSpecific : kNRegular;
-        default: return kNRegular;
-    }
-}
-
-// h2o_strtosize (lib/common/string.c:86-113): at most 19 decimal digits, nothing else; ~0 on failure
-__device__ uint64_t req_strtosize(const uint8_t* s, uint32_t n) {
-    if (n == 0 || n > 19) return ~0ull;
-    uint64_t v = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t d = (uint32_t)s[i] - '0';
-        if (d > 9u) return ~0ull;
-        v = v * 10u + d;
-    }
-    return v;
-}
-
-struct ReqState {  // one block's h2o_hpack_parse_request locals and out-parameters
-    uint64_t content_length;
-    int32_t method, scheme, authority, path, protocol, expect;
-    uint32_t map, nheaders, err, scheme_kind, ndecoded;
-    bool pseudo_ok;  // pseudo_header_exists_map != NULL: no regular field yet
-    __device__ void reset() {
-        content_length = ~0ull;
-        method = scheme = authority = path = protocol = expect = -1;
-        map = nheaders = err = scheme_kind = ndecoded = 0;
-        pseudo_ok = true;
-    }
-};
-
-constexpr uint32_t kMaxHeadersHard = 1000;  // H2O_HPACK_MAX_HEADERS_HARD_LIMIT (include/h2o/hpack.h:36)
-constexpr uint32_t kMaxHeaders = 100;       // H2O_MAX_HEADERS (include/h2o/header.h:37)
-
-// one decoded field k of the block (hpack.c:515-635); returns 0 or the hard error; sets *header when
-// h2o_add_header takes the field
-__device__ int32_t req_field(ReqState& r, uint32_t cls, const uint8_t* value, uint32_t vl, uint32_t soft, int32_t k,
-                             bool& header) {
-    header = false;
-    if (soft != 0 && r.err == HHUFF_HERR_NONE) r.err = (soft & 1u) ? HHUFF_HERR_SOFT_NAME : HHUFF_HERR_SOFT_VALUE;
-    if (++r.ndecoded > kMaxHeadersHard) {
-        r.err = HHUFF_HERR_HEADERS_TOO_LONG;
-        return kErrCompression;
-    }
-    if (cls >= kNAuthority && cls <= kNPseudoOther) {  // a pseudo-header name (first byte a colon)
-        if (!r.pseudo_ok) {
-            r.err = HHUFF_HERR_INVALID_PSEUDO;
-            return kErrProtocol;
-        }
-        switch (cls) {
-            case kNAuthority:
-                if (r.authority >= 0) break;
-                r.authority = k;
-                r.map |= 8u;
-                return 0;
-            case kNMethod:
-                if (r.method >= 0) break;
-                r.method = k;
-                r.map |= 1u;
-                return 0;
-            case kNProtocol:  // a duplicate is rejected without an err_desc (:546-548)
-                if (r.protocol >= 0) return kErrProtocol;
-                r.protocol = k;
-                r.map |= 16u;
-                return 0;
-            case kNPath:
-                if (r.path >= 0 || vl == 0) break;
-                r.path = k;
-                r.map |= 4u;
-                return 0;
-            case kNScheme:
-                if (r.scheme >= 0) break;
-                r.scheme = k;
-                r.scheme_kind = (vl == 5 && bytes_eq(value, "https", 5)) ? 2u : (vl == 6 && bytes_eq(value, "masque", 6)) ? 3u : 1u;
-                r.map |= 2u;
-                return 0;
-            default:  // unknown pseudo-header: rejected without an err_desc (:579-581)
-                return kErrProtocol;
-        }
-        r.err = HHUFF_HERR_INVALID_PSEUDO;
-        return kErrProtocol;
-    }
-    r.pseudo_ok = false;
-    switch (cls) {
-        case kNContentLength:
-            if ((r.content_length = req_strtosize(value, vl)) == ~0ull) {
-                r.err = HHUFF_HERR_CONTENT_LENGTH;
-                return kErrProtocol;
-            }
-            return 0;
-        case kNExpect:
-            r.expect = k;
-            return 0;
-        case kNHost:
-            if (r.authority < 0) r.authority = k;
-            return 0;
-        case kNDatagramFlowId:  // datagram_flow_id == NULL for HTTP/2 (connection.c:629)
-            return 0;
-        case kNTe: {  // h2o_lcstris(value, "trailers")
-            bool trailers = vl == 8;
-            for (uint32_t i = 0; trailers && i < 8; ++i) {
-                uint32_t c = value[i];
-                c = (c - 'A' < 26u) ? c + 32u : c;
-                trailers = c == (uint8_t)"trailers"[i];
-            }
-            if (!trailers) {
-                r.err = HHUFF_HERR_CONNECTION_SPECIFIC;
-                return kErrProtocol;
-            }
-            break;
-        }
-        case kNCacheDigest:  // digests != NULL for HTTP/2 (connection.c:629): loaded, then listed
-            break;
-        case kNConnSpecific:
-            r.err = HHUFF_HERR_CONNECTION_SPECIFIC;
-            return kErrProtocol;
-        default:
-            break;
-    }
-    if (r.nheaders < kMaxHeaders) {
-        ++r.nheaders;
-        header = true;
-    } else if (r.err == HHUFF_HERR_NONE) {
-        r.err = HHUFF_HERR_HEADERS_TOO_LONG;
-    }
-    return 0;
-}
-
-__device__ __forceinline__ void req_store(hhuff_request_t* out, const ReqState& r) {
-    out->content_length = r.content_length;
-    out->method = r.method;
-    out->scheme = r.scheme;
-    out->authority = r.authority;
-    out->path = r.path;
-    out->protocol = r.protocol;
-    out->expect = r.expect;
-    out->exists_map = r.map;
-    out->nheaders = r.nheaders;
-    out->err = r.err;
-    out->scheme_kind = r.scheme_kind;
-}
+// h2o_hpack_parse_request's rules: hhuff_request.h (shared with the QPACK sections, qpack.c:848)
 
 // decode_string (hpack.c:223-261) at position p: the string's arena place [off, off + len) and the source of
 // its bytes (a pre-decoded literal; or, decoded in place, the arena itself)

@@ -242,14 +242,14 @@ HHUFF_API uint64_t hhuff_qpack_scratch_size(uint32_t nconn, uint32_t header_tabl
     return (uint64_t)nconn * hhuff::qpack_conn_scratch(header_table_size);
 }
 
-HHUFF_API int hhuff_qpack_decode(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off, const uint32_t* enc_len,
-                                 const uint32_t* sec_off, const uint32_t* conn_first, uint32_t nconn, uint32_t nsec,
-                                 uint32_t header_table_size, uint64_t max_blocked, const uint32_t* num_blocked,
-                                 uint8_t* arena, const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len,
-                                 uint32_t* value_off, uint32_t* value_len, uint8_t* fflags, uint32_t* nfields,
-                                 int32_t* sstatus, uint64_t* req_insert_count, int32_t* enc_status,
-                                 uint32_t* enc_consumed, uint64_t* insert_count, void* scratch, uint64_t scratch_size,
-                                 unsigned flags, void* stream) {
+namespace {
+int qpack_step(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off, const uint32_t* enc_len,
+               const uint32_t* sec_off, const uint32_t* conn_first, uint32_t nconn, uint32_t nsec,
+               uint32_t header_table_size, uint64_t max_blocked, const uint32_t* num_blocked, uint8_t* arena,
+               const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len, uint32_t* value_off,
+               uint32_t* value_len, uint8_t* fflags, uint32_t* nfields, int32_t* sstatus, uint64_t* req_insert_count,
+               int32_t* enc_status, uint32_t* enc_consumed, uint64_t* insert_count, const uint64_t* stream_id,
+               hhuff_qpack_request_t* req, void* scratch, uint64_t scratch_size, unsigned flags, void* stream) {
     if (nconn == 0) return HHUFF_OK;
     if (!in || !enc_off || !enc_len || !sec_off || !conn_first || !enc_status || !enc_consumed || !insert_count ||
         !scratch)
@@ -266,8 +266,41 @@ HHUFF_API int hhuff_qpack_decode(const uint8_t* in, uint64_t in_size, const uint
     hipError_t e = hhuff::launch_qpack(in, in_size, enc_off, enc_len, sec_off, conn_first, nconn, nsec,
                                        header_table_size, max_blocked, num_blocked, arena, arena_off, name_off, name_len,
                                        value_off, value_len, fflags, nfields, sstatus, req_insert_count, enc_status,
-                                       enc_consumed, insert_count, (uint8_t*)scratch, flags, (hipStream_t)stream);
+                                       enc_consumed, insert_count, (uint8_t*)scratch, flags, (hipStream_t)stream,
+                                       stream_id, req);
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "qpack launch");
+}
+}  // namespace
+
+HHUFF_API int hhuff_qpack_decode(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off, const uint32_t* enc_len,
+                                 const uint32_t* sec_off, const uint32_t* conn_first, uint32_t nconn, uint32_t nsec,
+                                 uint32_t header_table_size, uint64_t max_blocked, const uint32_t* num_blocked,
+                                 uint8_t* arena, const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len,
+                                 uint32_t* value_off, uint32_t* value_len, uint8_t* fflags, uint32_t* nfields,
+                                 int32_t* sstatus, uint64_t* req_insert_count, int32_t* enc_status,
+                                 uint32_t* enc_consumed, uint64_t* insert_count, void* scratch, uint64_t scratch_size,
+                                 unsigned flags, void* stream) {
+    return qpack_step(in, in_size, enc_off, enc_len, sec_off, conn_first, nconn, nsec, header_table_size, max_blocked,
+                      num_blocked, arena, arena_off, name_off, name_len, value_off, value_len, fflags, nfields, sstatus,
+                      req_insert_count, enc_status, enc_consumed, insert_count, nullptr, nullptr, scratch, scratch_size,
+                      flags, stream);
+}
+
+HHUFF_API int hhuff_qpack_parse_requests(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off,
+                                         const uint32_t* enc_len, const uint32_t* sec_off, const uint32_t* conn_first,
+                                         uint32_t nconn, uint32_t nsec, uint32_t header_table_size, uint64_t max_blocked,
+                                         const uint32_t* num_blocked, uint8_t* arena, const uint64_t* arena_off,
+                                         uint32_t* name_off, uint32_t* name_len, uint32_t* value_off, uint32_t* value_len,
+                                         uint8_t* fflags, uint32_t* nfields, int32_t* sstatus, uint64_t* req_insert_count,
+                                         int32_t* enc_status, uint32_t* enc_consumed, uint64_t* insert_count,
+                                         const uint64_t* stream_id, hhuff_qpack_request_t* req, void* scratch,
+                                         uint64_t scratch_size, unsigned flags, void* stream) {
+    if (nconn != 0 && nsec != 0 && (!stream_id || !req)) return arg_fail("NULL array");
+    if (((uintptr_t)req & 7u) != 0) return arg_fail("req must be 8-byte aligned");
+    return qpack_step(in, in_size, enc_off, enc_len, sec_off, conn_first, nconn, nsec, header_table_size, max_blocked,
+                      num_blocked, arena, arena_off, name_off, name_len, value_off, value_len, fflags, nfields, sstatus,
+                      req_insert_count, enc_status, enc_consumed, insert_count, stream_id, req, scratch, scratch_size,
+                      flags, stream);
 }
 
 // ---------------------------------------------------------------------------------------------------

@@ -70,6 +70,7 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
                         const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len, uint32_t* value_off,
                         uint32_t* value_len, uint8_t* fflags, uint32_t* nfields, int32_t* sstatus,
                         uint64_t* req_insert_count, int32_t* enc_status, uint32_t* enc_consumed, uint64_t* insert_count,
-                        uint8_t* scratch, uint32_t flags, hipStream_t stream);
+                        uint8_t* scratch, uint32_t flags, hipStream_t stream, const uint64_t* stream_id = nullptr,
+                        hhuff_qpack_request_t* qreq = nullptr);
 int grid_size(int device, int which);
 }  // namespace hhuff

@@ -33,6 +33,7 @@
 #include "hhuff_device.h"
 #include "hhuff.h"
 #include "hhuff_launch.h"
+#include "hhuff_request.h"
 
 namespace hhuff {
 namespace {
@@ -86,6 +87,9 @@ struct QpkArgs {
     // bytes (0: already in the arena); qpack_copy_kernel moves them.  NULL: the sections kernel copies.
     uint64_t* fsrc_n;
     uint64_t* fsrc_v;
+    // h2o_qpack_parse_request mode (hhuff_qpack_parse_requests): per section its stream id and record
+    const uint64_t* stream_id;
+    hhuff_qpack_request_t* qreq;
 };
 
 // Byte sources of table entries and field strings: kind in the top 3 bits, offset below.  Every source stays
@@ -673,6 +677,41 @@ __device__ int32_t q_field(const QpkArgs& A, const QTable& t, const QCtx& ctx, u
     return soft ? kErrInvalidChar : 0;
 }
 
+// h2o_hpack_encode_int (hpack.c:757-772) of v with a 7-bit prefix behind 0x80: send_header_ack (qpack.c:642-649)
+__device__ __forceinline__ uint32_t q_header_ack(uint64_t v, uint8_t* out) {
+    uint32_t n = 0;
+    if (v < 127u) {
+        out[n++] = (uint8_t)(0x80u | v);
+        return n;
+    }
+    out[n++] = 0xFFu;
+    v -= 127u;
+    while (v >= 128u) {
+        out[n++] = (uint8_t)(0x80u | (v & 0x7Fu));
+        v >>= 7;
+    }
+    out[n++] = (uint8_t)v;
+    return n;
+}
+
+__device__ __forceinline__ void q_req_store(hhuff_qpack_request_t* out, const ReqState& r, int32_t st, uint64_t ric,
+                                            uint64_t stream_id) {
+    req_store(&out->req, r);
+    out->datagram_flow_id = r.dfid;
+    uint8_t ack[16] = {};
+    const uint32_t n = ((st == 0 || st == kErrInvalidChar) && ric != 0) ? q_header_ack(stream_id, ack) : 0u;
+    out->ack_len = n;
+    uint2* a2 = reinterpret_cast<uint2*>(out->ack);  // 8-byte aligned records: two 8-byte stores
+    uint32_t w[4];
+    __builtin_memcpy(w, ack, 16);
+    a2[0] = make_uint2(w[0], w[1]);
+    a2[1] = make_uint2(w[2], w[3]);
+}
+
+// REQ: h2o_qpack_parse_request (qpack.c:830-858) -- each field also runs h2o_hpack_parse_request's rules
+// (hhuff_request.h, the HTTP/3 arguments of lib/http3/server.c:1540-1545), a rule's hard error is
+// normalised to DECOMPRESSION_FAILED (:852-853), and the record gets the Section Acknowledgment (:856)
+template <bool REQ>
 __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
     __shared__ uint32_t s_kinfo[32];
@@ -696,8 +735,11 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
         const QTable t = q_table(A, lo);
         A.nfields[k] = 0;
         A.req_insert_count[k] = 0;
+        ReqState rq;
+        if (REQ) rq.reset();
         if (t.s.failed) {
             A.sstatus[k] = HHUFF_QPK_SKIPPED;
+            if (REQ) q_req_store(A.qreq + k, rq, HHUFF_QPK_SKIPPED, 0u, 0u);
             continue;
         }
         uint64_t p = A.sec_off[k];
@@ -719,7 +761,16 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
             const int32_t rc = q_field(A, t, ctx, p, end, R, no, nl, vo, vl, soft, fn, fv, T);
             if (rc != 0 && rc != kErrInvalidChar) {
                 st = rc;
+                // h2o_hpack_parse_request: *err_desc = decode_err (hpack.c:523-525)
+                if (REQ) rq.err = rc == HHUFF_QPK_ARENA ? HHUFF_HERR_NONE : HHUFF_HERR_DECODE;
                 break;
+            }
+            bool header = false;
+            int32_t rr = 0;
+            if (REQ) {  // the bytes where they lie: a source (fn / fv), or the arena (decoded in place)
+                const uint8_t* np = fn ? reinterpret_cast<const uint8_t*>(fn) : A.arena + no;
+                const uint8_t* vp = fv ? reinterpret_cast<const uint8_t*>(fv) : A.arena + vo;
+                rr = req_field<true>(rq, req_name_class(np, nl), vp, vl, soft, (int32_t)nf, header);
             }
             A.fsrc_n[slot + nf] = fn;
             A.fsrc_v[slot + nf] = fv;
@@ -727,8 +778,16 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
             A.name_len[slot + nf] = nl;
             A.value_off[slot + nf] = vo;
             A.value_len[slot + nf] = vl;
-            A.fflags[slot + nf] = (uint8_t)soft;
+            A.fflags[slot + nf] = (uint8_t)(soft | (header ? HHUFF_FIELD_HEADER : 0u));
             ++nf;
+            if (rr != 0) {  // normalize_error_code (qpack.c:822-828): a rule's H2 error fails the section
+                st = kDF;
+                break;
+            }
+        }
+        if (REQ) {
+            if (st == 0 && rq.err != HHUFF_HERR_NONE) st = kErrInvalidChar;  // hpack.c:636-637
+            q_req_store(A.qreq + k, rq, st, (uint64_t)ctx.ric, A.stream_id[k]);
         }
         A.nfields[k] = nf;
         A.sstatus[k] = st;
@@ -849,12 +908,13 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
                         const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len, uint32_t* value_off,
                         uint32_t* value_len, uint8_t* fflags, uint32_t* nfields, int32_t* sstatus,
                         uint64_t* req_insert_count, int32_t* enc_status, uint32_t* enc_consumed, uint64_t* insert_count,
-                        uint8_t* scratch, uint32_t flags, hipStream_t stream) {
+                        uint8_t* scratch, uint32_t flags, hipStream_t stream, const uint64_t* stream_id,
+                        hhuff_qpack_request_t* qreq) {
     if (nconn == 0) return hipSuccess;
     QpkArgs A{in, in_size, enc_off, enc_len, sec_off, conn_first, num_blocked, nconn, nsec, header_table_size,
               max_blocked, arena, arena_off, name_off, name_len, value_off, value_len, fflags, nfields, sstatus,
               req_insert_count, enc_status, enc_consumed, insert_count, scratch, qpack_conn_scratch(header_table_size),
-              flags, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+              flags, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream_id, qreq};
     // workspace: the literal pre-pass's bitmaps, word prefixes, chunk sums, the literal list with each
     // literal's prefix, the literal kernels' results and decoded bytes (positions are u32: in_size < 2^32,
     // checked by the C ABI), and the field slots' byte sources
@@ -911,7 +971,11 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
         e = hipGetLastError();
     }
     if (e == hipSuccess && nsec != 0) {
-        hipLaunchKernelGGL(qpack_sections_kernel, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
+        if (qreq)
+            hipLaunchKernelGGL(qpack_sections_kernel<true>, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
+        else
+            hipLaunchKernelGGL(qpack_sections_kernel<false>, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0,
+                               stream, A);
         hipLaunchKernelGGL(qpack_copy_kernel, dim3(std::min((nsec + 255u) / 256u, 4096u)), dim3(256), 0, stream, A);
         hipLaunchKernelGGL(qpack_blocked_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
         e = hipGetLastError();

@@ -304,6 +304,34 @@ int hhuff_qpack_decode(const uint8_t *in, uint64_t in_size, const uint32_t *enc_
                        uint64_t *req_insert_count, int32_t *enc_status, uint32_t *enc_consumed, uint64_t *insert_count,
                        void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
 
+/* (2e') HTTP/3 request sections: the same step with h2o_qpack_parse_request (lib/http3/qpack.c:830-858)
+ *      applied to every section as h2o's HTTP/3 server calls it (lib/http3/server.c:1540-1545): the
+ *      section's fields go through h2o_hpack_parse_request's rules (qpack.c:848, hpack.c:502-637) with no
+ *      cache-digest receiver (a cache-digest field is rejected like the other special fields) and a
+ *      datagram-flow-id out-parameter; hard errors other than H2O_HTTP2_ERROR_INVALID_HEADER_CHAR become
+ *      HHUFF_QPK_DECOMPRESSION_FAILED (normalize_error_code, :822-828); a section that decoded (0 or
+ *      -254) with a Required Insert Count other than 0 gets its Section Acknowledgment (send_header_ack,
+ *      :642-649: 0x80 | stream_id[k] as a 7-bit prefix integer) in req[k].ack.
+ *      sstatus[k] is h2o_qpack_parse_request's return value: 0, -254 (a soft error, *err_desc in
+ *      req[k].req.err), HHUFF_QPK_DECOMPRESSION_FAILED, or HHUFF_QPK_BLOCKED / _ARENA / _SKIPPED as for
+ *      hhuff_qpack_decode.  fflags carries HHUFF_FIELD_HEADER for the fields h2o_add_header took.
+ *      req[k].req.err is HHUFF_HERR_DECODE when decode_header itself failed (its own description). */
+typedef struct hhuff_qpack_request {
+    hhuff_request_t req;      /* h2o_hpack_parse_request's out-parameters, as for HTTP/2 */
+    int32_t datagram_flow_id; /* the field whose value h2o stored in *datagram_flow_id, or -1 */
+    uint32_t ack_len;         /* *outbufsize: bytes of ack (0: no acknowledgment) */
+    uint8_t ack[16];          /* the Section Acknowledgment instruction */
+} hhuff_qpack_request_t;      /* 72 bytes */
+#define HHUFF_HERR_DECODE 8u /* a hard error inside QPACK's decode_header (qpack.c:652-752) */
+int hhuff_qpack_parse_requests(const uint8_t *in, uint64_t in_size, const uint32_t *enc_off, const uint32_t *enc_len,
+                               const uint32_t *sec_off, const uint32_t *conn_first, uint32_t nconn, uint32_t nsec,
+                               uint32_t header_table_size, uint64_t max_blocked, const uint32_t *num_blocked,
+                               uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off, uint32_t *name_len,
+                               uint32_t *value_off, uint32_t *value_len, uint8_t *fflags, uint32_t *nfields,
+                               int32_t *sstatus, uint64_t *req_insert_count, int32_t *enc_status, uint32_t *enc_consumed,
+                               uint64_t *insert_count, const uint64_t *stream_id, hhuff_qpack_request_t *req,
+                               void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
+
 /* (3b) Pipelined host path (the socket-buffer -> pinned -> device -> pinned -> pool staging of
  *     SURVEY f3; replaces the caller-side copies around lib/http2/hpack.c:240-241).  Contiguous layout
  *     (in_off[n + 1], implicit output slots) only.  The batch is cut into chunks of about

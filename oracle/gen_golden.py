@@ -562,11 +562,22 @@ def blocks_sets():
     return out
 
 
-QPACK_SESSIONS = [  # name, seed, connections, steps, header_table_size, max_blocked, adversarial fraction
-    ("q4096", 61, 300, 4, 4096, 4, 0.3),
-    ("q256", 62, 150, 3, 256, 2, 0.3),
-    ("q0", 63, 100, 2, 0, 0, 0.2),
+QPACK_SESSIONS = [  # name, seed, connections, steps, header_table_size, max_blocked, adversarial fraction,
+    # fraction of requests with one of h2o_hpack_parse_request's cases
+    ("q4096", 61, 300, 4, 4096, 4, 0.3, 0.0),
+    ("q256", 62, 150, 3, 256, 2, 0.3, 0.0),
+    ("q0", 63, 100, 2, 0, 0, 0.2, 0.0),
+    ("qreq", 64, 500, 3, 4096, 4, 0.05, 0.3),
 ]
+
+
+def qpack_stream_ids(ns, step):
+    """client-initiated bidirectional stream ids (multiples of 4), a quarter of them large enough that the
+    Section Acknowledgment's 7-bit prefix integer takes 2 to 9 bytes"""
+    k = np.arange(ns, dtype=np.uint64)
+    big = np.uint64(1) << (np.uint64(7) * (k % np.uint64(9)) + np.uint64(4))
+    sid = np.uint64(4) * (k + np.uint64(1000 * step)) + np.where(k % 4 == 3, big * np.uint64(4), np.uint64(0))
+    return sid & np.uint64((1 << 62) - 4)
 
 
 def qpack_edge_session():
@@ -627,11 +638,14 @@ def qpack_set():
     from h2o_amd import qpack_synth as QS
 
     out = {}
-    sessions = [(n, QS.make_session(nc, steps=st, seed=sd, header_table_size=h, adversarial_frac=adv), nc, h, mb)
-                for n, sd, nc, st, h, mb, adv in QPACK_SESSIONS]
+    sessions = [(n, QS.make_session(nc, steps=st, seed=sd, header_table_size=h, adversarial_frac=adv,
+                                    request_frac=rf), nc, h, mb)
+                for n, sd, nc, st, h, mb, adv, rf in QPACK_SESSIONS]
     sessions.append(("qedge", qpack_edge_session(), 14, 4096, 2))
     for name, steps, nconn, hts, mb in sessions:
         sr = O.QpackSession(O.ref(), nconn, hts, mb)
+        # the same session through h2o_qpack_parse_request (a second decoder: the encoder streams act alike)
+        sq = O.QpackSession(O.ref(), nconn, hts, mb)
         nbl = (np.arange(nconn) % 6).astype(np.uint32)
         out[name + "_meta"] = np.asarray([nconn, hts, mb, len(steps)], np.uint32)
         out[name + "_num_blocked"] = nbl
@@ -658,7 +672,27 @@ def qpack_set():
                 out[p + key] = r[key][:nconn]
             out[p + "fld_name"], out[p + "fld_name_off"], out[p + "fld_value"], out[p + "fld_value_off"] = nd, no, vd, vo
             out[p + "fld_soft"] = np.asarray(soft, np.uint8)
+            # h2o_qpack_parse_request: verdicts, request records, acks, the fields' flags (their names and
+            # values are a prefix of the decode-only fields above, checked here)
+            sid = qpack_stream_ids(ns, k)
+            q = sq.step(st["data"], st["enc_off"], st["enc_len"], st["sec_off"], st["conn_first"], ao, nbl, stream_id=sid)
+            fl = []
+            for s_ in range(ns):
+                o, kq = int(st["sec_off"][s_]), int(q["nfields"][s_])
+                assert kq <= int(r["nfields"][s_]) or int(r["sstatus"][s_]) != 0
+                for f in range(o, o + kq):
+                    assert q["arena"][q["name_off"][f]:q["name_off"][f] + q["name_len"][f]].tobytes() == \
+                        r["arena"][r["name_off"][f]:r["name_off"][f] + r["name_len"][f]].tobytes()
+                    assert q["arena"][q["value_off"][f]:q["value_off"][f] + q["value_len"][f]].tobytes() == \
+                        r["arena"][r["value_off"][f]:r["value_off"][f] + r["value_len"][f]].tobytes()
+                    fl.append(q["fflags"][f])
+            out[p + "rq_stream_id"] = sid
+            out[p + "rq_nfields"] = q["nfields"][:ns]
+            out[p + "rq_sstatus"] = q["sstatus"][:ns]
+            out[p + "rq_req"] = q["req"][:ns].view(np.uint32).reshape(ns, 18)
+            out[p + "rq_fflags"] = np.asarray(fl, np.uint8)
         sr.close()
+        sq.close()
     return out
 
 

@@ -13,6 +13,7 @@
 
 #include "huff_oracle.h"
 #include "huff_tables.h"
+#include "orc_request.h"
 
 #define ENTRY_OVERHEAD 32u /* HEADER_TABLE_ENTRY_SIZE_OFFSET, hpack.c:30 */
 #define STATIC_COUNT 61u   /* HEADER_TABLE_OFFSET - 1, hpack.c:27 */
@@ -257,32 +258,28 @@ static uint64_t rq_strtosize(const uint8_t *s, uint32_t n)
     return v;
 }
 
-typedef struct {
-    uint64_t content_length;
-    int32_t slot[6]; /* method, scheme, authority, path, protocol, expect */
-    uint32_t map, nheaders, err, scheme_kind, ndecoded;
-    int pseudo_ok;
-} orc_req_t;
-
-static void rq_init(orc_req_t *r)
+void orc_rq_init(orc_req_t *r)
 {
     memset(r, 0, sizeof(*r));
     r->content_length = UINT64_MAX;
     for (int i = 0; i < 6; ++i)
         r->slot[i] = -1;
+    r->dfid = -1;
     r->pseudo_ok = 1;
 }
 
-static void rq_store(uint32_t *w, const orc_req_t *r)
+void orc_rq_store(uint32_t *w, const orc_req_t *r)
 {
     memcpy(w, &r->content_length, 8);
     memcpy(w + 2, r->slot, 24);
     w[8] = r->map, w[9] = r->nheaders, w[10] = r->err, w[11] = r->scheme_kind;
 }
 
-/* field k decoded with soft bits `soft`: 0, or the hard error; *header = h2o_add_header took it */
-static int rq_field(orc_req_t *r, const uint8_t *name, uint32_t nl, const uint8_t *value, uint32_t vl, unsigned soft,
-                    int32_t k, int *header)
+/* field k decoded with soft bits `soft`: 0, or the hard error; *header = h2o_add_header took it.  h3: the
+ * arguments of h2o's HTTP/3 server (lib/http3/server.c:1540-1545): digests == NULL (a cache-digest field is
+ * rejected, hpack.c:606-617) and a datagram-flow-id out-parameter (the field is stored, :610-613) */
+int orc_rq_field(orc_req_t *r, const uint8_t *name, uint32_t nl, const uint8_t *value, uint32_t vl, unsigned soft,
+                 int32_t k, int *header, int h3)
 {
     enum { M = 0, S = 1, A = 2, P = 3, PR = 4, E = 5 };
     *header = 0;
@@ -337,7 +334,15 @@ static int rq_field(orc_req_t *r, const uint8_t *name, uint32_t nl, const uint8_
             r->slot[A] = k;
         return 0;
     case RQ_DATAGRAM_FLOW_ID:
+        if (h3)
+            r->dfid = k;
         return 0;
+    case RQ_CACHE_DIGEST:
+        if (h3) {
+            r->err = 6;
+            return ORC_ERR_PROTOCOL;
+        }
+        break;
     case RQ_TE:
         if (vl == 8 && strncasecmp((const char *)value, "trailers", 8) == 0)
             break;
@@ -376,12 +381,12 @@ static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
     int failed = 0;
     for (uint32_t b = j->conn_first[c]; b < j->conn_first[c + 1]; ++b) {
         orc_req_t rq;
-        rq_init(&rq);
+        orc_rq_init(&rq);
         j->nfields[b] = 0;
         if (failed) {
             j->bstatus[b] = ORC_BLK_SKIPPED;
             if (j->req)
-                rq_store(j->req + 12 * (size_t)b, &rq);
+                orc_rq_store(j->req + 12 * (size_t)b, &rq);
             continue;
         }
         const uint8_t *p = j->in + j->blk_off[b], *end = j->in + j->blk_off[b + 1];
@@ -400,7 +405,7 @@ static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
             }
             int header = 0, rr = 0;
             if (j->req)
-                rr = rq_field(&rq, j->arena + no, nl, j->arena + vo, vl, soft, (int32_t)nf, &header);
+                rr = orc_rq_field(&rq, j->arena + no, nl, j->arena + vo, vl, soft, (int32_t)nf, &header, 0);
             j->name_off[slot + nf] = no;
             j->name_len[slot + nf] = nl;
             j->value_off[slot + nf] = vo;
@@ -415,7 +420,7 @@ static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
         if (j->req) {
             if (st == 0 && rq.err != 0)
                 st = ORC_ERR_INVALID_CHAR; /* hpack.c:636-637 */
-            rq_store(j->req + 12 * (size_t)b, &rq);
+            orc_rq_store(j->req + 12 * (size_t)b, &rq);
         }
         j->nfields[b] = nf;
         j->bstatus[b] = st;

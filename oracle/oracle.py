@@ -20,6 +20,11 @@ STATUS_FAIL = 0x80
 REQ_DTYPE = np.dtype([("content_length", "<u8"), ("method", "<i4"), ("scheme", "<i4"), ("authority", "<i4"),
                       ("path", "<i4"), ("protocol", "<i4"), ("expect", "<i4"), ("exists_map", "<u4"),
                       ("nheaders", "<u4"), ("err", "<u4"), ("scheme_kind", "<u4")])
+# include/hhuff.h hhuff_qpack_request_t (72 bytes): the request record, the datagram-flow-id field, the ack
+QREQ_DTYPE = np.dtype([("content_length", "<u8"), ("method", "<i4"), ("scheme", "<i4"), ("authority", "<i4"),
+                       ("path", "<i4"), ("protocol", "<i4"), ("expect", "<i4"), ("exists_map", "<u4"),
+                       ("nheaders", "<u4"), ("err", "<u4"), ("scheme_kind", "<u4"), ("datagram_flow_id", "<i4"),
+                       ("ack_len", "<u4"), ("ack", "u1", (16,))])
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 
@@ -229,6 +234,9 @@ class QpackSession:
         self._open.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64]
         self._close.argtypes = [ctypes.c_void_p]
         self._step.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 19
+        self._step_req = getattr(L, P + "_qpack_step_req")
+        self._step_req.restype = ctypes.c_int
+        self._step_req.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 21
         self.nconn = nconn
         self.h = self._open(nconn, header_table_size, max_blocked)
 
@@ -239,9 +247,12 @@ class QpackSession:
 
     __del__ = close
 
-    def step(self, data, enc_off, enc_len, sec_off, conn_first, arena_off, num_blocked=None):
+    def step(self, data, enc_off, enc_len, sec_off, conn_first, arena_off, num_blocked=None, stream_id=None):
         """-> dict: arena, name_off, name_len, value_off, value_len, fflags (per field slot), nfields, sstatus,
-        req_insert_count (per section), enc_status, enc_consumed, insert_count (per connection)"""
+        req_insert_count (per section), enc_status, enc_consumed, insert_count (per connection).  With
+        stream_id (u64 per section): h2o_qpack_parse_request per section (hhuff_qpack_parse_requests'
+        contract), plus "req" (QREQ_DTYPE records); the reference harness also checks every section against
+        the real h2o_qpack_parse_request and fails on a disagreement."""
         c = lambda a, t: np.ascontiguousarray(a, dtype=t)  # noqa: E731
         data, enc_off, enc_len, sec_off, conn_first = (c(data, np.uint8), c(enc_off, np.uint32), c(enc_len, np.uint32),
                                                        c(sec_off, np.uint32), c(conn_first, np.uint32))
@@ -260,11 +271,19 @@ class QpackSession:
                  enc_status=np.zeros(nc, np.int32), enc_consumed=np.zeros(nc, np.uint32),
                  insert_count=np.zeros(nc, np.uint64))
         d = lambda a: None if a is None else a.ctypes.data  # noqa: E731
-        rc = self._step(self.h, d(data), d(enc_off), d(enc_len), d(sec_off), d(conn_first), d(nb), d(r["arena"]),
-                        d(arena_off), d(r["name_off"]), d(r["name_len"]), d(r["value_off"]), d(r["value_len"]),
-                        d(r["fflags"]), d(r["nfields"]), d(r["sstatus"]), d(r["req_insert_count"]), d(r["enc_status"]),
-                        d(r["enc_consumed"]), d(r["insert_count"]))
-        assert rc == 0
+        args = [self.h, d(data), d(enc_off), d(enc_len), d(sec_off), d(conn_first), d(nb), d(r["arena"]),
+                d(arena_off), d(r["name_off"]), d(r["name_len"]), d(r["value_off"]), d(r["value_len"]),
+                d(r["fflags"]), d(r["nfields"]), d(r["sstatus"]), d(r["req_insert_count"]), d(r["enc_status"]),
+                d(r["enc_consumed"]), d(r["insert_count"])]
+        if stream_id is None:
+            rc = self._step(*args)
+            assert rc == 0
+            return r
+        sid = c(stream_id, np.uint64)
+        words = np.zeros((max(1, ns), 18), np.uint32)
+        rc = self._step_req(*args, d(sid), d(words))
+        assert rc == 0, "%d section(s) disagree with the real h2o_qpack_parse_request" % rc
+        r["req"] = words.view(QREQ_DTYPE).reshape(-1)
         return r
 
 

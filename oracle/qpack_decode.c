@@ -13,6 +13,7 @@
 
 #include "huff_oracle.h"
 #include "huff_tables.h"
+#include "orc_request.h"
 
 #define QPK_ENTRY_OVERHEAD 32u                /* HEADER_ENTRY_SIZE_OFFSET, qpack.c:32 */
 #define QPK_STATIC_COUNT 99u                  /* h2o_qpack_static_table[99], include/h2o/token_table.h:114 */
@@ -514,17 +515,27 @@ void orc_qpack_close(void *h)
     free(s);
 }
 
+/* send_header_ack (qpack.c:642-649): 0x80 | stream_id as a 7-bit prefix integer (h2o_hpack_encode_int) */
+static uint32_t qpk_header_ack(uint64_t stream_id, uint8_t *out)
+{
+    out[0] = 0x80;
+    return (uint32_t)(orc_encode_int(out, (int64_t)stream_id, 7) - out);
+}
+
 /* One step for every connection c: its encoder-stream bytes in[enc_off[c], + enc_len[c]), then its field
  * sections conn_first[c] .. conn_first[c+1]-1 (section k = in[sec_off[k], sec_off[k+1])) against the table
  * as the encoder stream left it; num_blocked[c] (NULL = 0) is the caller's count of the connection's
- * blocked streams (h2o's conn->num_qpack_blocked, lib/http3/server.c:1544). */
-int orc_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, const uint32_t *enc_len, const uint32_t *sec_off,
-                   const uint32_t *conn_first, const uint32_t *num_blocked, uint8_t *arena, const uint64_t *arena_off,
-                   uint32_t *name_off, uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,
-                   uint32_t *nfields, int32_t *sstatus, uint64_t *req_insert_count, int32_t *enc_status,
-                   uint32_t *enc_consumed, uint64_t *insert_count)
+ * blocked streams (h2o's conn->num_qpack_blocked, lib/http3/server.c:1544).  With req != NULL every section
+ * goes through h2o_qpack_parse_request (qpack.c:830-858): h2o_hpack_parse_request's rules with the HTTP/3
+ * arguments, normalize_error_code, send_header_ack; req = 18 u32 words per section: the hhuff_request_t
+ * words, datagram_flow_id, ack_len, ack[16]. */
+static int qpk_step(qpk_session_t *s, const uint8_t *in, const uint32_t *enc_off, const uint32_t *enc_len,
+                    const uint32_t *sec_off, const uint32_t *conn_first, const uint32_t *num_blocked, uint8_t *arena,
+                    const uint64_t *arena_off, uint32_t *name_off, uint32_t *name_len, uint32_t *value_off,
+                    uint32_t *value_len, uint8_t *fflags, uint32_t *nfields, int32_t *sstatus, uint64_t *req_insert_count,
+                    int32_t *enc_status, uint32_t *enc_consumed, uint64_t *insert_count, const uint64_t *stream_id,
+                    uint32_t *req)
 {
-    qpk_session_t *s = (qpk_session_t *)h;
     for (uint32_t c = 0; c < s->nconn; ++c) {
         qpk_conn_t *t = &s->c[c];
         enc_status[c] = 0;
@@ -543,41 +554,87 @@ int orc_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, const ui
         for (uint32_t k = conn_first[c]; k < conn_first[c + 1]; ++k) {
             nfields[k] = 0;
             req_insert_count[k] = 0;
+            orc_req_t rq;
+            orc_rq_init(&rq);
+            int st = 0;
+            qpk_ctx_t ctx = {t, 0, 0};
+            uint32_t nf = 0;
             if (t->failed) {
-                sstatus[k] = ORC_BLK_SKIPPED;
-                continue;
-            }
-            const uint8_t *p = in + sec_off[k], *end = in + sec_off[k + 1];
-            qpk_ctx_t ctx;
-            int st = qpk_parse_context(t, &ctx, &p, end);
-            if (st == 0) {
-                req_insert_count[k] = (uint64_t)ctx.req_insert_count;
-                /* check_decode_context_blocked (:801-820) */
-                if (!(ctx.req_insert_count < qpk_table_total(t))) {
-                    st = nb >= s->max_blocked ? ORC_QPK_DECOMPRESSION_FAILED : ORC_QPK_BLOCKED;
-                    nb += st == ORC_QPK_BLOCKED;
+                st = ORC_BLK_SKIPPED;
+            } else {
+                const uint8_t *p = in + sec_off[k], *end = in + sec_off[k + 1];
+                st = qpk_parse_context(t, &ctx, &p, end);
+                if (st == 0) {
+                    req_insert_count[k] = (uint64_t)ctx.req_insert_count;
+                    /* check_decode_context_blocked (:801-820) */
+                    if (!(ctx.req_insert_count < qpk_table_total(t))) {
+                        st = nb >= s->max_blocked ? ORC_QPK_DECOMPRESSION_FAILED : ORC_QPK_BLOCKED;
+                        nb += st == ORC_QPK_BLOCKED;
+                    }
                 }
-            }
-            uint32_t nf = 0, slot = sec_off[k];
-            qpk_arena_t A = {arena, arena_off[k], arena_off[k + 1] < (1ull << 32) ? arena_off[k + 1] : (1ull << 32)};
-            while (st == 0 && p != end) {
-                uint32_t no = 0, nl = 0, vo = 0, vl = 0;
-                unsigned soft = 0;
-                int rc = qpk_field(&ctx, &p, end, &A, &no, &nl, &vo, &vl, &soft);
-                if (rc != 0 && rc != ORC_ERR_INVALID_CHAR) {
-                    st = rc;
-                    break;
+                uint32_t slot = sec_off[k];
+                qpk_arena_t A = {arena, arena_off[k], arena_off[k + 1] < (1ull << 32) ? arena_off[k + 1] : (1ull << 32)};
+                while (st == 0 && p != end) {
+                    uint32_t no = 0, nl = 0, vo = 0, vl = 0;
+                    unsigned soft = 0;
+                    int rc = qpk_field(&ctx, &p, end, &A, &no, &nl, &vo, &vl, &soft);
+                    if (rc != 0 && rc != ORC_ERR_INVALID_CHAR) {
+                        st = rc;
+                        rq.err = rc == ORC_BLK_ARENA ? 0 : 8; /* HHUFF_HERR_DECODE: decode_header's own error */
+                        break;
+                    }
+                    int header = 0, rr = 0;
+                    if (req)
+                        rr = orc_rq_field(&rq, arena + no, nl, arena + vo, vl, soft, (int32_t)nf, &header, 1);
+                    name_off[slot + nf] = no;
+                    name_len[slot + nf] = nl;
+                    value_off[slot + nf] = vo;
+                    value_len[slot + nf] = vl;
+                    fflags[slot + nf] = (uint8_t)(soft | (header ? 4u : 0u));
+                    ++nf;
+                    if (rr != 0) { /* normalize_error_code (:822-828) */
+                        st = ORC_QPK_DECOMPRESSION_FAILED;
+                        break;
+                    }
                 }
-                name_off[slot + nf] = no;
-                name_len[slot + nf] = nl;
-                value_off[slot + nf] = vo;
-                value_len[slot + nf] = vl;
-                fflags[slot + nf] = (uint8_t)soft;
-                ++nf;
+                if (req && st == 0 && rq.err != 0)
+                    st = ORC_ERR_INVALID_CHAR; /* hpack.c:636-637 */
             }
             nfields[k] = nf;
             sstatus[k] = st;
+            if (req) {
+                uint32_t *w = req + 18 * (size_t)k;
+                orc_rq_store(w, &rq);
+                w[12] = (uint32_t)rq.dfid;
+                uint8_t ack[16] = {0};
+                w[13] = (st == 0 || st == ORC_ERR_INVALID_CHAR) && ctx.req_insert_count != 0
+                            ? qpk_header_ack(stream_id[k], ack) : 0;
+                memcpy(w + 14, ack, 16);
+            }
         }
     }
     return 0;
+}
+
+int orc_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, const uint32_t *enc_len, const uint32_t *sec_off,
+                   const uint32_t *conn_first, const uint32_t *num_blocked, uint8_t *arena, const uint64_t *arena_off,
+                   uint32_t *name_off, uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,
+                   uint32_t *nfields, int32_t *sstatus, uint64_t *req_insert_count, int32_t *enc_status,
+                   uint32_t *enc_consumed, uint64_t *insert_count)
+{
+    return qpk_step((qpk_session_t *)h, in, enc_off, enc_len, sec_off, conn_first, num_blocked, arena, arena_off, name_off,
+                    name_len, value_off, value_len, fflags, nfields, sstatus, req_insert_count, enc_status, enc_consumed,
+                    insert_count, NULL, NULL);
+}
+
+int orc_qpack_step_req(void *h, const uint8_t *in, const uint32_t *enc_off, const uint32_t *enc_len,
+                       const uint32_t *sec_off, const uint32_t *conn_first, const uint32_t *num_blocked, uint8_t *arena,
+                       const uint64_t *arena_off, uint32_t *name_off, uint32_t *name_len, uint32_t *value_off,
+                       uint32_t *value_len, uint8_t *fflags, uint32_t *nfields, int32_t *sstatus,
+                       uint64_t *req_insert_count, int32_t *enc_status, uint32_t *enc_consumed, uint64_t *insert_count,
+                       const uint64_t *stream_id, uint32_t *req)
+{
+    return qpk_step((qpk_session_t *)h, in, enc_off, enc_len, sec_off, conn_first, num_blocked, arena, arena_off, name_off,
+                    name_len, value_off, value_len, fflags, nfields, sstatus, req_insert_count, enc_status, enc_consumed,
+                    insert_count, stream_id, req);
 }

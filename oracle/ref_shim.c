@@ -220,3 +220,238 @@ REF_API int ref_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, 
     }
     return 0;
 }
+
+/* ---- h2o_qpack_parse_request (qpack.c:830-858) as h2o's HTTP/3 server calls it ----
+ * lib/http3/server.c:1540-1545: no cache digests, a datagram-flow-id out-parameter, the connection's
+ * num_qpack_blocked.  Per section the request record (include/hhuff.h hhuff_qpack_request_t, 18 u32
+ * words) is produced by h2o_qpack_parse_request's own steps -- parse_decode_context,
+ * check_decode_context_blocked, h2o_hpack_parse_request over decode_header (through a wrapper that copies
+ * each field to the arena and, from the out-parameters' changes between calls, learns which field each
+ * one took and which went to the header list), normalize_error_code, send_header_ack -- and every section
+ * is ALSO run through the real h2o_qpack_parse_request on the same decoder, whose return value, header
+ * acknowledgment, content length, pseudo-header map, header count, err_desc, scheme and out-parameter
+ * bytes must agree (the count of disagreeing sections is the return value). */
+#define Q3_OUTS 7 /* method, (scheme), authority, path, protocol, expect, datagram_flow_id */
+typedef struct {
+    struct st_h2o_qpack_decode_header_ctx_t *dctx;
+    uint8_t *arena;
+    uint64_t cur, aend;
+    uint32_t *name_off, *name_len, *value_off, *value_len, slot, nf;
+    uint8_t *fflags;
+    h2o_iovec_t *out[Q3_OUTS];
+    const h2o_url_scheme_t **scheme;
+    h2o_headers_t *headers;
+    h2o_iovec_t snap[Q3_OUTS];
+    const h2o_url_scheme_t *scheme_snap;
+    size_t hsize_snap;
+    int32_t taken[Q3_OUTS];
+    int hard, arena_full;
+} q3_ctx_t;
+
+static void q3_settle(q3_ctx_t *x)
+{
+    if (x->nf == 0)
+        return;
+    int32_t k = (int32_t)x->nf - 1;
+    if (x->headers->size > x->hsize_snap)
+        x->fflags[x->slot + k] |= 4;
+    for (int i = 0; i < Q3_OUTS; ++i) {
+        if (i == 1) {
+            if (*x->scheme != x->scheme_snap)
+                x->taken[1] = k;
+            continue;
+        }
+        if (x->out[i]->base != x->snap[i].base || x->out[i]->len != x->snap[i].len)
+            x->taken[i] = k;
+    }
+}
+
+static void q3_snapshot(q3_ctx_t *x)
+{
+    for (int i = 0; i < Q3_OUTS; ++i)
+        if (i != 1)
+            x->snap[i] = *x->out[i];
+    x->scheme_snap = *x->scheme;
+    x->hsize_snap = x->headers->size;
+}
+
+static int q3_decode_cb(h2o_mem_pool_t *pool, void *ctx, h2o_iovec_t **name, h2o_iovec_t *value, const uint8_t **src,
+                        const uint8_t *src_end, const char **err_desc)
+{
+    q3_ctx_t *x = ctx;
+    q3_settle(x);
+    q3_snapshot(x);
+    int ret = decode_header(pool, x->dctx, name, value, src, src_end, err_desc);
+    if (ret != 0 && ret != H2O_HTTP2_ERROR_INVALID_HEADER_CHAR) {
+        x->hard = 1;
+        return ret;
+    }
+    if (x->cur + (*name)->len + value->len > x->aend) {
+        x->arena_full = 1;
+        *err_desc = NULL;
+        return REF_QPK_ARENA;
+    }
+    uint32_t f = x->slot + x->nf;
+    memcpy(x->arena + x->cur, (*name)->base, (*name)->len);
+    x->name_off[f] = (uint32_t)x->cur;
+    x->name_len[f] = (uint32_t)(*name)->len;
+    x->cur += (*name)->len;
+    memcpy(x->arena + x->cur, value->base, value->len);
+    x->value_off[f] = (uint32_t)x->cur;
+    x->value_len[f] = (uint32_t)value->len;
+    x->cur += value->len;
+    x->fflags[f] = ret == 0 ? 0 : (*err_desc == h2o_hpack_soft_err_found_invalid_char_in_header_name ? 1 : 2);
+    ++x->nf;
+    return ret;
+}
+
+static uint32_t q3_err_code(const char *e)
+{
+    if (e == NULL)
+        return 0;
+    if (e == h2o_hpack_soft_err_found_invalid_char_in_header_name)
+        return 1;
+    if (e == h2o_hpack_soft_err_found_invalid_char_in_header_value)
+        return 2;
+    if (e == h2o_hpack_err_headers_too_long)
+        return 3;
+    if (e == h2o_hpack_err_invalid_pseudo_header)
+        return 4;
+    if (e == h2o_hpack_err_invalid_content_length_header)
+        return 5;
+    if (e == h2o_hpack_err_unexpected_connection_specific_header)
+        return 6;
+    if (e == h2o_hpack_err_found_upper_case_in_header_name)
+        return 7;
+    return 99;
+}
+
+static int q3_iov_eq(h2o_iovec_t a, h2o_iovec_t b)
+{
+    return a.len == b.len && (a.len == 0 || memcmp(a.base, b.base, a.len) == 0);
+}
+
+REF_API int ref_qpack_step_req(void *h, const uint8_t *in, const uint32_t *enc_off, const uint32_t *enc_len,
+                               const uint32_t *sec_off, const uint32_t *conn_first, const uint32_t *num_blocked,
+                               uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off, uint32_t *name_len,
+                               uint32_t *value_off, uint32_t *value_len, uint8_t *fflags, uint32_t *nfields,
+                               int32_t *sstatus, uint64_t *req_insert_count, int32_t *enc_status, uint32_t *enc_consumed,
+                               uint64_t *insert_count, const uint64_t *stream_id, uint32_t *req)
+{
+    ref_qpk_session_t *s = h;
+    int mismatches = 0;
+    for (uint32_t c = 0; c < s->nconn; ++c) {
+        h2o_qpack_decoder_t *q = s->d[c];
+        enc_status[c] = 0;
+        enc_consumed[c] = 0;
+        insert_count[c] = 0;
+        if (s->failed[c]) {
+            enc_status[c] = REF_QPK_SKIPPED;
+        } else if (enc_len[c]) {
+            const uint8_t *src = in + enc_off[c], *end = src + enc_len[c];
+            const char *err_desc = NULL;
+            int r = h2o_qpack_decoder_handle_input(q, &insert_count[c], &src, end, &err_desc);
+            enc_consumed[c] = (uint32_t)(src - (in + enc_off[c]));
+            enc_status[c] = r;
+            s->failed[c] = r != 0;
+        }
+        uint64_t nb = num_blocked ? num_blocked[c] : 0; /* +1 per parked stream (lib/http3/server.c:1553) */
+        for (uint32_t k = conn_first[c]; k < conn_first[c + 1]; ++k) {
+            uint32_t *w = req + 18 * (size_t)k;
+            nfields[k] = 0;
+            req_insert_count[k] = 0;
+            h2o_iovec_t method = {NULL, 0}, authority = {NULL, 0}, path = {NULL, 0}, protocol = {NULL, 0}, expect = {NULL, 0},
+                        dfid = {NULL, 0};
+            const h2o_url_scheme_t *scheme = NULL;
+            h2o_headers_t headers = {NULL, 0, 0};
+            int exists_map = 0;
+            size_t content_length = SIZE_MAX, outbufsize = 0;
+            uint8_t outbuf[16] = {0};
+            const char *err_desc = NULL;
+            q3_ctx_t x;
+            memset(&x, 0, sizeof(x));
+            for (int i = 0; i < Q3_OUTS; ++i)
+                x.taken[i] = -1;
+            int st;
+            h2o_mem_pool_t pool;
+            h2o_mem_init_pool(&pool);
+            const uint8_t *src0 = in + sec_off[k], *end = in + sec_off[k + 1];
+            if (s->failed[c]) {
+                st = REF_QPK_SKIPPED;
+            } else {
+                /* h2o_qpack_parse_request's own steps */
+                const uint8_t *src = src0;
+                struct st_h2o_qpack_decode_header_ctx_t ctx;
+                h2o_qpack_section_stats_t stats = {0};
+                uint64_t blocked_ref = 0;
+                st = parse_decode_context(q, &ctx, &src, end);
+                if (st == 0) {
+                    req_insert_count[k] = (uint64_t)ctx.req_insert_count;
+                    st = check_decode_context_blocked(q, &ctx, nb, &blocked_ref);
+                }
+                int blocked = st == 0 && blocked_ref != 0;
+                if (st == 0 && !blocked) {
+                    ctx.stats = &stats;
+                    x.dctx = &ctx, x.arena = arena, x.cur = arena_off[k];
+                    x.aend = arena_off[k + 1] < (1ull << 32) ? arena_off[k + 1] : (1ull << 32);
+                    x.name_off = name_off, x.name_len = name_len, x.value_off = value_off, x.value_len = value_len;
+                    x.fflags = fflags, x.slot = sec_off[k];
+                    x.out[0] = &method, x.out[1] = &method, x.out[2] = &authority, x.out[3] = &path;
+                    x.out[4] = &protocol, x.out[5] = &expect, x.out[6] = &dfid;
+                    x.scheme = &scheme, x.headers = &headers;
+                    st = h2o_hpack_parse_request(&pool, q3_decode_cb, &x, &method, &scheme, &authority, &path, &protocol,
+                                                 &headers, &exists_map, &content_length, &expect, NULL, &dfid, src,
+                                                 end - src, &err_desc);
+                    q3_settle(&x);
+                    if (x.arena_full)
+                        st = REF_QPK_ARENA;
+                    else if (st != 0 && st != H2O_HTTP2_ERROR_INVALID_HEADER_CHAR)
+                        st = normalize_error_code(st);
+                    else
+                        outbufsize = send_header_ack(q, &ctx, outbuf, (int64_t)stream_id[k]);
+                }
+                /* the real function, on the same decoder and the same blocked count */
+                h2o_iovec_t m2 = {NULL, 0}, a2 = {NULL, 0}, p2 = {NULL, 0}, pr2 = {NULL, 0}, e2 = {NULL, 0}, d2 = {NULL, 0};
+                const h2o_url_scheme_t *sc2 = NULL;
+                h2o_headers_t hd2 = {NULL, 0, 0};
+                int map2 = 0;
+                size_t cl2 = SIZE_MAX, obs2 = 0;
+                uint8_t ob2[16] = {0};
+                uint64_t bref2 = 0;
+                h2o_qpack_section_stats_t st2 = {0};
+                const char *ed2 = NULL;
+                h2o_mem_pool_t pool2;
+                h2o_mem_init_pool(&pool2);
+                int ret2 = h2o_qpack_parse_request(&pool2, q, (int64_t)stream_id[k], &m2, &sc2, &a2, &p2, &pr2, &hd2, &map2,
+                                                   &cl2, &e2, NULL, &d2, nb, &bref2, &st2, ob2, &obs2, src0, end - src0, &ed2);
+                if (!x.arena_full) {
+                    int ok = (blocked ? (ret2 == 0 && bref2 != 0) : (ret2 == st && bref2 == 0)) && obs2 == outbufsize &&
+                             memcmp(ob2, outbuf, 16) == 0 && cl2 == content_length && map2 == exists_map &&
+                             hd2.size == headers.size && ed2 == err_desc && sc2 == scheme && q3_iov_eq(m2, method) &&
+                             q3_iov_eq(a2, authority) && q3_iov_eq(p2, path) && q3_iov_eq(pr2, protocol) &&
+                             q3_iov_eq(e2, expect) && q3_iov_eq(d2, dfid);
+                    mismatches += !ok;
+                }
+                h2o_mem_clear_pool(&pool2);
+                if (blocked) {
+                    st = REF_QPK_BLOCKED;
+                    ++nb;
+                }
+            }
+            h2o_mem_clear_pool(&pool);
+            nfields[k] = x.nf;
+            sstatus[k] = st;
+            uint64_t cl = content_length;
+            memcpy(w, &cl, 8);
+            memcpy(w + 2, x.taken, 24);
+            w[8] = (uint32_t)exists_map;
+            w[9] = (uint32_t)headers.size;
+            w[10] = x.hard ? 8u /* HHUFF_HERR_DECODE */ : q3_err_code(err_desc);
+            w[11] = scheme == NULL ? 0 : scheme == &H2O_URL_SCHEME_HTTP ? 1 : scheme == &H2O_URL_SCHEME_HTTPS ? 2 : 3;
+            w[12] = (uint32_t)x.taken[6];
+            w[13] = (uint32_t)outbufsize;
+            memcpy(w + 14, outbuf, 16);
+        }
+    }
+    return mismatches;
+}
