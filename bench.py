@@ -58,10 +58,21 @@ def parse():
     return ap.parse_args()
 
 
+def _template_args(name):
+    """the template arguments of a demangled kernel name: 'k<16, 3584, true, false>(...)' -> [16, 3584, true, false]"""
+    i = name.find("<")
+    j = name.find(">", i)
+    return [a.strip() for a in name[i + 1:j].split(",")] if i >= 0 and j > i else []
+
+
 def kernel_key(name):
     if "hhuff::" not in name:
         return None
-    packed = ", true>" in name
+    args = _template_args(name)
+    # the PACKED template argument: decode_staged_kernel<WAVES, IN, OUT, PACKED>,
+    # encode_staged_kernel<WAVES, STAGE, PACKED, CP>
+    pos = 3 if "decode_staged_kernel" in name else 2 if "encode_staged_kernel" in name else None
+    packed = pos is not None and len(args) > pos and args[pos] == "true"
     if "decode_staged_kernel" in name or "decode_stream_kernel" in name or "decode_direct_kernel" in name:
         return "decode_packed" if packed else "decode"
     if ("encode_staged_kernel" in name or "encode_pl_kernel" in name or "encode_direct_kernel" in name or

@@ -708,6 +708,15 @@ __device__ __forceinline__ void q_req_store(hhuff_qpack_request_t* out, const Re
     a2[1] = make_uint2(w[2], w[3]);
 }
 
+// The HTTP/3 rules as a call of their own: inlined into the sections kernel (11K instructions, SGPRs spilled
+// to VGPR lanes), the compiler lost the err_desc code of a rejected connection-specific field on gfx950
+// (the request record said 0 where h2o says h2o_hpack_err_unexpected_connection_specific_header), while the
+// same source compiled for the host, and inlined into the HPACK walk, is right.
+__device__ __noinline__ int32_t req_field_h3(ReqState& r, uint32_t cls, const uint8_t* value, uint32_t vl, uint32_t soft,
+                                             int32_t k, bool& header) {
+    return req_field<true>(r, cls, value, vl, soft, k, header);
+}
+
 // REQ: h2o_qpack_parse_request (qpack.c:830-858) -- each field also runs h2o_hpack_parse_request's rules
 // (hhuff_request.h, the HTTP/3 arguments of lib/http3/server.c:1540-1545), a rule's hard error is
 // normalised to DECOMPRESSION_FAILED (:852-853), and the record gets the Section Acknowledgment (:856)
@@ -770,7 +779,7 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
             if (REQ) {  // the bytes where they lie: a source (fn / fv), or the arena (decoded in place)
                 const uint8_t* np = fn ? reinterpret_cast<const uint8_t*>(fn) : A.arena + no;
                 const uint8_t* vp = fv ? reinterpret_cast<const uint8_t*>(fv) : A.arena + vo;
-                rr = req_field<true>(rq, req_name_class(np, nl), vp, vl, soft, (int32_t)nf, header);
+                rr = req_field_h3(rq, req_name_class(np, nl), vp, vl, soft, (int32_t)nf, header);
             }
             A.fsrc_n[slot + nf] = fn;
             A.fsrc_v[slot + nf] = fv;

@@ -193,6 +193,18 @@ def qpack_line(torch, codec, nconn=65536):
             "arena_short_sections": int((r["sstatus"][:nsec] == -300).sum().item()), "decode_ms": round(t, 4),
             "sections_per_s": round(nsec / (t * 1e-3), 1), "fields_per_s": round(nf / (t * 1e-3), 1),
             "input_gibps": round(W / GIB / (t * 1e-3), 3)}
+    # the same step as HTTP/3 requests: h2o_qpack_parse_request per section (hhuff_qpack_parse_requests)
+    sid = dev(np.arange(nsec, dtype=np.int64) * 4)
+
+    def run_req():
+        res["q"] = codec.qpack_decode(d, eo, el, so, cf, nsec, 4096, 100, arena_off=ao, in_size=int(st["data"].size),
+                                      scratch=scratch, stream_id=sid)
+
+    t_req = timed(torch, run_req, steps=10, warmup=2)
+    q = res["q"]
+    line.update(requests_ms=round(t_req, 4), requests_sections_per_s=round(nsec / (t_req * 1e-3), 1),
+                ok_requests=int((q["sstatus"][:nsec] == 0).sum().item()),
+                acks=int((q["req"][:nsec, 52] != 0).sum().item()))
     try:
         sys.path.insert(0, ROOT)
         from oracle import oracle as O
