@@ -117,7 +117,7 @@ EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decod
             "hhuff_qpack_decode", "hhuff_qpack_parse_requests", "hhuff_qpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string", "hhuff_per_string_calls",
-            "hhuff_grid_size", "hhuff_pool_trim")
+            "hhuff_grid_size", "hhuff_pool_trim", "hhuff_service_stamps")
 
 
 def _check(rc, what):

@@ -8,6 +8,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -317,6 +320,128 @@ namespace {
 constexpr size_t kMeta = 32;
 uint64_t g_per_string_calls = 0;  // process-wide, atomic adds (hhuff_per_string_calls)
 
+// ---- the resident per-string service (service_kernel, hhuff_kernels.hip), one per device ----
+// A call posts its string in its thread's mailbox (slot = thread number mod kSvcSlots, a mutex per slot for
+// more threads than slots), raises the slot's request counter and spins on the slot's done counter.  The
+// service wave exits after kSvcIdle of idleness; a call that finds its request unserved and the wave gone
+// (ctrl->alive 0, the service stream idle) launches it again.  atexit stops every service before the HIP
+// runtime goes away.  HHUFF_NO_SERVICE=1 in the environment keeps the launch-per-string path.
+constexpr uint64_t kSvcIdle = 200000;      // real-time counter ticks (100 MHz): 2 ms without a request
+constexpr uint64_t kSvcLife = 1000000000;  // 10 s in all, then a fresh launch
+struct Service {
+    std::mutex mu;
+    bool ready = false, broken = false;
+    hipStream_t stream = nullptr;
+    hhuff::SvcSlot* slots = nullptr;  // host view (pinned, mapped, coherent)
+    hhuff::SvcSlot* d_slots = nullptr;
+    hhuff::SvcCtrl* ctrl = nullptr;
+    hhuff::SvcCtrl* d_ctrl = nullptr;
+    uint32_t seq[hhuff::kSvcSlots] = {};
+    std::mutex slot_mu[hhuff::kSvcSlots];
+};
+Service g_svc[64];
+std::atomic<uint32_t> g_svc_threads{0};
+thread_local int t_svc_slot = -1;
+
+void svc_shutdown() {
+    for (auto& S : g_svc) {
+        std::lock_guard<std::mutex> g(S.mu);
+        if (!S.ready) continue;
+        __atomic_store_n(&S.ctrl->stop, 1u, __ATOMIC_RELEASE);
+        (void)hipStreamSynchronize(S.stream);  // the wave polls stop: it exits within a poll
+        S.ready = false;
+    }
+}
+
+bool svc_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("HHUFF_NO_SERVICE");
+        return !(e && *e && *e != '0');
+    }();
+    return on;
+}
+
+// make sure device dev's service is set up and running (stream idle -> launch); caller holds nothing
+int svc_kick(Service& S, int dev) {
+    std::lock_guard<std::mutex> g(S.mu);
+    if (S.broken) return HHUFF_EHIP;
+    if (!S.ready) {
+        int cur = 0;
+        HIP_TRY(hipGetDevice(&cur), "hipGetDevice");
+        if (cur != dev) HIP_TRY(hipSetDevice(dev), "hipSetDevice");
+        hipError_t e = hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking);
+        void* h = nullptr;
+        const size_t bytes = sizeof(hhuff::SvcSlot) * hhuff::kSvcSlots + sizeof(hhuff::SvcCtrl);
+        if (e == hipSuccess) e = hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent);
+        void* d = nullptr;
+        if (e == hipSuccess) {
+            memset(h, 0, bytes);
+            e = hipHostGetDevicePointer(&d, h, 0);
+        }
+        if (cur != dev) (void)hipSetDevice(cur);
+        if (e != hipSuccess) {
+            S.broken = true;
+            return hip_fail(e, "per-string service setup");
+        }
+        S.slots = static_cast<hhuff::SvcSlot*>(h);
+        S.d_slots = static_cast<hhuff::SvcSlot*>(d);
+        S.ctrl = reinterpret_cast<hhuff::SvcCtrl*>(S.slots + hhuff::kSvcSlots);
+        S.d_ctrl = reinterpret_cast<hhuff::SvcCtrl*>(S.d_slots + hhuff::kSvcSlots);
+        static std::once_flag once;
+        std::call_once(once, [] { atexit(svc_shutdown); });
+        S.ready = true;
+    }
+    const hipError_t q = hipStreamQuery(S.stream);
+    if (q == hipErrorNotReady) return HHUFF_OK;  // running (or starting)
+    if (q != hipSuccess) return hip_fail(q, "per-string service query");
+    __atomic_store_n(&S.ctrl->stop, 0u, __ATOMIC_RELEASE);
+    const hipError_t e = hhuff::launch_service(S.d_slots, S.d_ctrl, kSvcIdle, kSvcLife, S.stream);
+    return e == hipSuccess ? HHUFF_OK : hip_fail(e, "per-string service launch");
+}
+
+// 1: served (result in *res), 0: not taken (the caller uses the launch path), -1: HIP failure
+int svc_call(int dev, bool encode, const uint8_t* src, size_t len, int is_name, uint8_t* dst, uint32_t* res,
+             uint32_t* status) {
+    if (dev < 0 || dev >= 64 || len > hhuff::kSvcMax || !svc_enabled()) return 0;
+    Service& S = g_svc[dev];
+    if (S.broken) return 0;
+    if (!S.ready && svc_kick(S, dev) != HHUFF_OK) return S.broken ? 0 : -1;
+    if (t_svc_slot < 0) t_svc_slot = (int)(g_svc_threads.fetch_add(1) % hhuff::kSvcSlots);
+    const int k = t_svc_slot;
+    std::lock_guard<std::mutex> g(S.slot_mu[k]);
+    hhuff::SvcSlot* sl = S.slots + k;
+    sl->op = encode ? 1u : 0u;
+    sl->len = (uint32_t)len;
+    sl->is_name = is_name ? 1u : 0u;
+    memcpy(sl->in, src, len);
+    const uint32_t n = ++S.seq[k];
+    __atomic_store_n(&sl->req, n, __ATOMIC_RELEASE);
+    // spin for the result.  While the wave is alive nothing else is done; a wave that is gone (idle exit,
+    // or exiting just as this request arrived) is launched again -- checked every 64 spins, so a wave that
+    // is still starting up is not launched twice (svc_kick sees its stream busy)
+    if (__atomic_load_n(&S.ctrl->alive, __ATOMIC_ACQUIRE) == 0u && svc_kick(S, dev) != HHUFF_OK) return -1;
+    uint64_t spins = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    while (__atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) != n) {
+        ++spins;
+        if ((spins & 63u) == 0u) {
+            if (__atomic_load_n(&S.ctrl->alive, __ATOMIC_ACQUIRE) == 0u && svc_kick(S, dev) != HHUFF_OK) return -1;
+            if ((spins & 4095u) == 0u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+                snprintf(t_err, sizeof(t_err), "per-string service: no answer in 5 s");
+                std::lock_guard<std::mutex> gg(S.mu);
+                S.broken = true;  // later calls take the launch path
+                return -1;
+            }
+        }
+        __builtin_ia32_pause();
+    }
+    const uint32_t r = sl->result;
+    *res = r;
+    *status = sl->status;
+    if (r != HHUFF_FAIL_LEN) memcpy(dst, sl->out, r);
+    return 1;
+}
+
 size_t per_string(bool encode, uint8_t* dst, const uint8_t* src, size_t len, int is_name, unsigned* soft_errors) {
     __atomic_fetch_add(&g_per_string_calls, 1, __ATOMIC_RELAXED);
     Ctx& c = t_ctx;
@@ -325,6 +450,16 @@ size_t per_string(bool encode, uint8_t* dst, const uint8_t* src, size_t len, int
         return SIZE_MAX;
     }
     if (c.bind(-1)) return SIZE_MAX;
+    {
+        uint32_t r = 0, st = 0;
+        const int sv = svc_call(c.dev, encode, src, len, is_name, dst, &r, &st);
+        if (sv < 0) return SIZE_MAX;
+        if (sv > 0) {
+            if (r == HHUFF_FAIL_LEN) return SIZE_MAX;
+            if (!encode) *soft_errors |= st & 3u;
+            return r;
+        }
+    }
     const size_t in_cap = up16(len ? len : 1);
     if (len <= hhuff::kOneMax) {
         const size_t out_cap = up16(len * 8 / 5 + 4);
@@ -383,6 +518,16 @@ HHUFF_API size_t h2o_hpack_encode_huffman(uint8_t* dst, const uint8_t* src, size
 }
 
 HHUFF_API uint64_t hhuff_per_string_calls(void) { return __atomic_load_n(&g_per_string_calls, __ATOMIC_RELAXED); }
+
+HHUFF_API int hhuff_service_stamps(uint32_t* out4) {
+    int dev = 0;
+    if (!out4 || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return HHUFF_EINVAL;
+    const Service& S = g_svc[dev];
+    if (!S.ready || t_svc_slot < 0) return HHUFF_EINVAL;
+    const hhuff::SvcSlot* sl = S.slots + t_svc_slot;
+    out4[0] = sl->t_seen, out4[1] = sl->t_data, out4[2] = sl->t_coded, out4[3] = sl->t_out;
+    return HHUFF_OK;
+}
 
 // ---------------------------------------------------------------------------------------------------
 // (3) host batch API: copy in, run, copy out (synchronous)

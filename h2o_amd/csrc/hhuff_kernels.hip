@@ -2579,6 +2579,113 @@ hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, b
 }
 
 // ------------------------------------------------------------------------------------------------
+// Resident per-string service.  A launch per string costs ~18 us (launch + stream synchronisation); here
+// one wave stays resident and polls kSvcSlots mailboxes in coherent host memory (one per calling thread):
+// lane l watches slot l's request counter with system-scope loads.  A posted request is served by the
+// whole wave: its header and input come over PCIe in one round of 16-B loads into LDS, lane 0 runs the
+// codec from LDS (decode_core / encode_core, the tables staged once per launch), the wave writes the
+// output back, then a system-scope release and the slot's `done` counter.  The wave exits when the host
+// sets ctrl->stop, after idle_ticks of the real-time counter (100 MHz) without a request, or after
+// max_ticks in all -- every exit is reached without the host, so the grid always drains -- and the host
+// relaunches it on the next request it finds unserved.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
+                                                     uint64_t idle_ticks, uint64_t max_ticks) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
+    __shared__ uint32_t s_kinfo[32];
+    __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
+    __shared__ __attribute__((aligned(16))) uint2 s_enc[256];
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[kSvcMax / 4 + 16];  // [16 header words][input]
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[(kSvcMax * 8) / 5 + 64];
+    __shared__ uint32_t s_res[2];
+    static_assert(64 + kSvcMax == 64 * 16, "one 16-B load per lane reads a mailbox's header and input");
+    const uint32_t lane = threadIdx.x;
+    load_dec_tables(s_lut, s_kinfo, s_ones, 64);
+    for (uint32_t k = lane; k < 256; k += 64) s_enc[k] = make_uint2(g_enc_code[k], g_enc_nbits[k]);
+    __syncthreads();
+    if (lane == 0) sys_store(&ctrl->alive, 1u);
+    uint32_t handled = sys_load(&slots[lane].done);  // lane l keeps slot l's last served request
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t last = t0;
+    for (;;) {
+        const uint32_t req = sys_load(&slots[lane].req);
+        uint64_t pend = __builtin_amdgcn_ballot_w64(req != handled);
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        if (pend == 0) {
+            const uint32_t stop = sys_load(&ctrl->stop);
+            if (stop != 0 || now - last > idle_ticks || now - t0 > max_ticks) break;
+            continue;  // each poll is a PCIe round trip already: no sleep between them
+        }
+        last = now;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the request's bytes were written before its counter
+        while (pend) {
+            const uint32_t s = (uint32_t)__builtin_ctzll(pend);
+            pend &= pend - 1;
+            SvcSlot* sl = slots + s;
+            const uint32_t r = (uint32_t)__shfl((int)req, (int)s);
+            const uint32_t t_seen = (uint32_t)now;
+            // header (16 words) and the whole input area in one round of 16-B loads: no wait on `len` first
+            const uint8_t* src = reinterpret_cast<const uint8_t*>(sl);
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_in) + 16u * lane) =
+                *reinterpret_cast<const uint4*>(src + 16u * lane);
+            __syncthreads();
+            const uint32_t t_data = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            if (lane == 0) {
+                const uint32_t op = s_in[2], len = min(s_in[3], kSvcMax), is_name = s_in[4];
+                const LdsSource lsrc{s_in + 16, len ? ((len + 3u) & ~3u) - 4u : 0u};
+                LdsSink sink{s_out, 0u, 0u, (kSvcMax * 8) / 5 + 60};
+                uint32_t ol, st = 0;
+                if (op == 1u) {
+                    ol = encode_core(lsrc, 0u, len, sink, s_enc);
+                    st = ol == kFailLen ? kStatusFail : 0u;
+                } else {
+                    const DecResult d = decode_core(lsrc, 0u, len, sink, DecTables{s_lut, s_kinfo, s_ones});
+                    ol = d.ok ? d.len : kFailLen;
+                    st = d.ok ? soft_bits(is_name != 0, d.len, d.flags, d.len ? s_out[0] : 0u, d.len ? s_out[d.len - 1] : 0u)
+                              : kStatusFail;
+                }
+                s_res[0] = ol;
+                s_res[1] = st;
+            }
+            __syncthreads();
+            const uint32_t t_coded = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            const uint32_t ol = s_res[0];
+            const uint32_t n = ol == kFailLen ? 0u : ol;
+            for (uint32_t k = 4u * lane; k < n; k += 256u)
+                *reinterpret_cast<uint32_t*>(sl->out + k) = *reinterpret_cast<const uint32_t*>(s_out + k);
+            if (lane == 0) {
+                sl->result = ol;
+                sl->status = s_res[1];
+                sl->t_seen = t_seen;
+                sl->t_data = t_data;
+                sl->t_coded = t_coded;
+                sl->t_out = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the result before its counter
+            if (lane == 0) sys_store(&sl->done, r);
+            if (lane == s) handled = r;
+            __syncthreads();
+        }
+    }
+    if (lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        sys_store(&ctrl->alive, 0u);
+    }
+}
+
+hipError_t launch_service(SvcSlot* slots, SvcCtrl* ctrl, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream) {
+    hipLaunchKernelGGL(service_kernel, dim3(1), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
 // Packed output for the variants without a native packed mode (long strings: stream / direct decode,
 // proportional-lane encode): the kernel writes the slot layout into a stream-ordered scratch buffer,
 // then pack_tiles_kernel moves each 64-string tile's outputs to their places (one wave per tile: wave

@@ -16,6 +16,25 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
 // [u32 len, is_name, result len, status][input, in_cap bytes (16-aligned)][output]; len <= kOneMax
 constexpr uint32_t kOneMax = 8192;
 hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, bool encode, hipStream_t stream);
+// Resident per-string service (hhuff_capi.hip per_string): one wave polls kSvcSlots mailboxes in pinned,
+// device-visible, coherent host memory and codes each posted string in place; it exits when `stop` is set,
+// after idle_ticks of the 100 MHz real-time counter without a request, or after max_ticks in all.
+constexpr uint32_t kSvcSlots = 64;
+constexpr uint32_t kSvcMax = 960;  // longest string a mailbox takes (longer ones: launch_one / batch kernels);
+                                   // header + input = 1 KiB: one round of the wave's 16-B loads
+struct alignas(16) SvcSlot {       // one mailbox (host writes req after the request; device writes done after the result)
+    uint32_t req, done, op, len;   // op: 0 decode, 1 encode
+    uint32_t is_name, result, status, pad;
+    uint32_t t_seen, t_data, t_coded, t_out;  // the wave's real-time stamps (100 MHz, low 32 bits): profiling
+    uint32_t pad2[4];
+    uint8_t in[kSvcMax];
+    uint8_t out[1600];  // >= floor(8 kSvcMax / 5) + 60
+};
+static_assert(sizeof(SvcSlot) % 16 == 0 && sizeof(SvcSlot) == 1024 + 1600, "mailbox layout");
+struct SvcCtrl {
+    uint32_t stop, alive, pad[2];
+};
+hipError_t launch_service(SvcSlot* slots, SvcCtrl* ctrl, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream);
 // Packed output (include/hhuff.h hhuff_{de,en}code_batch_packed): contiguous layout, pk_off u32[n + 1]
 hipError_t launch_decode_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
                                 const uint32_t* is_name_bits, uint8_t* out, uint32_t* pk_off, uint32_t* out_len,

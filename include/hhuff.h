@@ -67,6 +67,10 @@ size_t h2o_hpack_encode_huffman(uint8_t *dst, const uint8_t *src, size_t len);
  * check: after linking h2o against this library, a non-zero count after decoding a Huffman literal shows
  * h2o's callers (decode_string, h2o_hpack_encode_string, QPACK's flatten_string ...) bound here. */
 uint64_t hhuff_per_string_calls(void);
+/* Profiling: the resident per-string service's real-time stamps (100 MHz counter, low 32 bits) of the calling
+ * thread's last served call on its current device: request seen, input in LDS, coded, output written.
+ * HHUFF_OK, or HHUFF_EINVAL when this thread has no served call. */
+int hhuff_service_stamps(uint32_t *out4);
 
 /* ---------------------------------------------------------------------------------------------
  * (2) batch API, device-resident arrays (hot path).  Asynchronous on `stream`.
