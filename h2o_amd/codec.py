@@ -98,6 +98,12 @@ def lib():
         L.hhuff_qpack_parse_requests.argtypes = ([_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32,
                                                   ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64] + [_vp] * 17 +
                                                  [ctypes.c_uint64, ctypes.c_uint, _vp])
+        L.hhuff_hpack_enc_scratch_size.restype = ctypes.c_uint64
+        L.hhuff_hpack_enc_scratch_size.argtypes = [ctypes.c_uint32]
+        L.hhuff_hpack_flatten_responses.restype = ctypes.c_int
+        L.hhuff_hpack_flatten_responses.argtypes = ([_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, _vp,
+                                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+                                                    + [_vp] * 6 + [ctypes.c_uint64, ctypes.c_uint, _vp])
         L.hhuff_version.restype = ctypes.c_char_p
         L.hhuff_last_error_string.restype = ctypes.c_char_p
         L.hhuff_grid_size.restype = ctypes.c_int
@@ -117,7 +123,8 @@ EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decod
             "hhuff_qpack_decode", "hhuff_qpack_parse_requests", "hhuff_qpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string", "hhuff_per_string_calls",
-            "hhuff_grid_size", "hhuff_pool_trim", "hhuff_service_stamps")
+            "hhuff_grid_size", "hhuff_pool_trim", "hhuff_service_stamps", "hhuff_hpack_enc_scratch_size",
+            "hhuff_hpack_flatten_responses")
 
 
 def _check(rc, what):
@@ -406,6 +413,53 @@ def qpack_decode(data, enc_off, enc_len, sec_off, conn_first, nsec, header_table
         r["req"] = torch.empty((max(1, nsec), QREQ_BYTES), dtype=torch.uint8, device=dev)
         _check(lib().hhuff_qpack_parse_requests(*(args + [_dp(stream_id), _dp(r["req"])] + tail)),
                "hhuff_qpack_parse_requests")
+    r["scratch"] = scratch
+    return r
+
+
+# include/hhuff.h hhuff_hpack_header_t / hhuff_hpack_response_t as numpy records
+HPE_HEADER_DTYPE = np.dtype([("name_off", "<u4"), ("name_len", "<u4"), ("value_off", "<u4"), ("value_len", "<u4"),
+                             ("flags", "<u4")])
+HPE_RESPONSE_DTYPE = np.dtype([("content_length", "<u8"), ("stream_id", "<u4"), ("status", "<u4"),
+                               ("hdr_first", "<u4"), ("nhdr", "<u4"), ("header_table_size", "<u4"),
+                               ("max_frame_size", "<u4"), ("flags", "<u4"), ("reserved", "<u4")])
+HDR_DONT_COMPRESS, HDR_TOKEN = 1, 2
+RES_END_STREAM, RES_SERVER, RES_TRAILERS = 1, 2, 4
+ENC_CONTINUE = 1
+RES_SPACE, RES_SKIPPED, RES_EINVAL = -300, -301, -303
+
+
+def hpack_response_bound(name_value_bytes, nhdr, server_len, max_frame_size):
+    """include/hhuff.h hhuff_hpack_response_bound (numpy arrays or ints)"""
+    payload = name_value_bytes + 21 * np.asarray(nhdr, np.int64) + 10 + 23 + np.where(
+        np.asarray(server_len) != 0, np.asarray(server_len, np.int64) + 26, 0)
+    return 9 + payload + 9 * (payload // np.maximum(np.asarray(max_frame_size, np.int64), 1) + 1)
+
+
+def hpack_flatten_responses(data, hdr, res, conn_first, nres, out_off, server_off=0, server_len=0, in_size=None,
+                            out=None, scratch=None, cont=False, stream=None):
+    """HTTP/2 response header blocks (include/hhuff.h hhuff_hpack_flatten_responses) on device tensors:
+    hdr = uint8 tensor of HPE_HEADER_DTYPE records (20 B each), res = uint8 tensor of HPE_RESPONSE_DTYPE
+    records (40 B), conn_first int32 (u32 bits), out_off int64 [nres + 1]; nres = conn_first[-1] as a host int.
+    Returns a dict of device tensors: out, out_len, headers_size, rstatus, and the scratch holding the encoder
+    tables (pass it back with cont=True for the connections' next responses)."""
+    import torch
+
+    dev = data.device
+    in_size = data.numel() if in_size is None else in_size
+    nconn = conn_first.numel() - 1
+    nhdr = hdr.numel() // HPE_HEADER_DTYPE.itemsize
+    if out is None:
+        out = torch.empty(max(1, int(out_off[-1].item())), dtype=torch.uint8, device=dev)
+    i32 = lambda n: torch.empty(max(1, n), dtype=torch.int32, device=dev)  # noqa: E731
+    r = dict(out=out, out_len=i32(nres), headers_size=i32(nres), rstatus=i32(nres))
+    ss = int(lib().hhuff_hpack_enc_scratch_size(nconn))
+    if scratch is None:
+        scratch = torch.empty(max(16, ss), dtype=torch.uint8, device=dev)
+    _check(lib().hhuff_hpack_flatten_responses(
+        _dp(data), in_size, _dp(hdr) if nhdr else None, nhdr, _dp(res), _dp(conn_first), nconn, nres, server_off,
+        server_len, _dp(out), _dp(out_off), _dp(r["out_len"]), _dp(r["headers_size"]), _dp(r["rstatus"]),
+        _dp(scratch), scratch.numel(), ENC_CONTINUE if cont else 0, _stream(stream)), "hhuff_hpack_flatten_responses")
     r["scratch"] = scratch
     return r
 

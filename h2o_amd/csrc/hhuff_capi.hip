@@ -241,6 +241,29 @@ HHUFF_API int hhuff_hpack_parse_requests(const uint8_t* in, uint64_t in_size, co
                         value_off, value_len, fflags, nfields, bstatus, req, scratch, scratch_size, flags, stream);
 }
 
+HHUFF_API uint64_t hhuff_hpack_enc_scratch_size(uint32_t nconn) { return (uint64_t)nconn * hhuff::hpenc_conn_scratch(); }
+
+HHUFF_API int hhuff_hpack_flatten_responses(const uint8_t* in, uint64_t in_size, const hhuff_hpack_header_t* hdr,
+                                            uint32_t nhdr, const hhuff_hpack_response_t* res, const uint32_t* conn_first,
+                                            uint32_t nconn, uint32_t nres, uint32_t server_off, uint32_t server_len,
+                                            uint8_t* out, const uint64_t* out_off, uint32_t* out_len,
+                                            uint32_t* headers_size, int32_t* rstatus, void* scratch, uint64_t scratch_size,
+                                            unsigned flags, void* stream) {
+    if (nconn == 0) return HHUFF_OK;
+    if (!conn_first || !scratch || (nres && (!res || !out || !out_off || !out_len || !headers_size || !rstatus)) ||
+        (nhdr && (!hdr || !in)))
+        return arg_fail("NULL array");
+    if (in_size >= (1ull << 32)) return arg_fail("in_size must stay below 2^32 (u32 offsets)");
+    if (scratch_size < hhuff_hpack_enc_scratch_size(nconn)) return arg_fail("scratch smaller than hhuff_hpack_enc_scratch_size");
+    if (((uintptr_t)scratch & 15u) != 0) return arg_fail("scratch must be 16-byte aligned");
+    if (((uintptr_t)res & 7u) != 0 || ((uintptr_t)hdr & 3u) != 0 || ((uintptr_t)out_off & 7u) != 0)
+        return arg_fail("misaligned hdr / res / out_off");
+    hipError_t e = hhuff::launch_hpack_flatten(in, in_size, hdr, nhdr, res, conn_first, nconn, nres, server_off, server_len,
+                                               out, out_off, out_len, headers_size, rstatus, (uint8_t*)scratch, flags,
+                                               (hipStream_t)stream);
+    return e == hipSuccess ? HHUFF_OK : hip_fail(e, "hpack flatten launch");
+}
+
 HHUFF_API uint64_t hhuff_qpack_scratch_size(uint32_t nconn, uint32_t header_table_size) {
     return (uint64_t)nconn * hhuff::qpack_conn_scratch(header_table_size);
 }

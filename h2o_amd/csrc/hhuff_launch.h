@@ -72,6 +72,15 @@ hipError_t work_alloc(void** p, uint64_t bytes, hipStream_t stream);
 // hand the pool's kept memory on the current device back to the driver (hhuff_pool_trim)
 hipError_t pool_trim();
 
+// HTTP/2 response header blocks, encode side (hhuff_hpenc.hip): include/hhuff.h hhuff_hpack_flatten_responses;
+// scratch = nconn x hpenc_conn_scratch() bytes
+uint64_t hpenc_conn_scratch();
+hipError_t launch_hpack_flatten(const uint8_t* in, uint64_t in_size, const hhuff_hpack_header_t* hdr, uint32_t nhdr,
+                                const hhuff_hpack_response_t* res, const uint32_t* conn_first, uint32_t nconn, uint32_t nres,
+                                uint32_t server_off, uint32_t server_len, uint8_t* out, const uint64_t* out_off,
+                                uint32_t* out_len, uint32_t* headers_size, int32_t* rstatus, uint8_t* scratch,
+                                uint32_t flags, hipStream_t stream);
+
 // HPACK header blocks (f4): see include/hhuff.h hhuff_hpack_decode_blocks; scratch = nconn x
 // hpack_conn_scratch(table_size) bytes of device memory
 uint64_t hpack_conn_scratch(uint32_t table_size);

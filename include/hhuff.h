@@ -336,6 +336,71 @@ int hhuff_qpack_parse_requests(const uint8_t *in, uint64_t in_size, const uint32
                                uint64_t *insert_count, const uint64_t *stream_id, hhuff_qpack_request_t *req,
                                void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
 
+/* (2f) HTTP/2 response header blocks, encode side (SURVEY f4 encode half): h2o_hpack_flatten_response
+ *      (lib/http2/hpack.c:1137-1177) and h2o_hpack_flatten_trailers (:1179-1196) for many responses of many
+ *      connections, with one encoder dynamic table per connection (conn->_output_header_table; do_encode_header
+ *      :858-937, at most 32 entries, initial capacity 4096 as lib/http2/connection.c:1847 sets it) kept in
+ *      scratch between calls.  A call flattens the responses conn_first[c] .. conn_first[c+1]-1 of every
+ *      connection c in order, as lib/http2/stream.c:311-314 / :404-406 and connection.c:1580-1582 call them.
+ *        header h    hdr[h]: name in[name_off .. + name_len), value in[value_off .. + value_len), flags:
+ *                    HHUFF_HDR_DONT_COMPRESS = h2o_header_t.flags.dont_compress; HHUFF_HDR_TOKEN = the name is
+ *                    an h2o token (h2o_iovec_is_token: the header was added with its h2o_token_t) -- set it only
+ *                    for names listed in lib/common/token_table.h
+ *        response r  res[r] (below): the headers hdr_first .. hdr_first + nhdr - 1 in order; HHUFF_RES_SERVER
+ *                    sends server_name (in[server_off .. + server_len), h2o's globalconf->server_name; clear
+ *                    it where h2o passes NULL: informational responses); HHUFF_RES_TRAILERS makes r a trailers
+ *                    block (flatten_trailers: no :status, server or content-length, END_STREAM)
+ *        out         response r's frames (HEADERS, then CONTINUATIONs past max_frame_size, fixup_frame_headers
+ *                    :1012-1042) at out + out_off[r]; region [out_off[r], out_off[r+1]) (u64, nres + 1 entries);
+ *                    hhuff_hpack_response_bound() is enough for any table state
+ *      Per response: out_len[r] = bytes written (frame headers included), headers_size[r] = the payload bytes
+ *      (h2o_hpack_flatten_response's return value), rstatus[r] = 0, HHUFF_RES_SPACE (the frames do not fit
+ *      the region), HHUFF_RES_EINVAL (status outside 100..999, max_frame_size outside 16384..2^24-1, a string
+ *      past in_size) or HHUFF_RES_SKIPPED (an earlier response of the connection failed: its table is no
+ *      longer the peer's, h2o would have dropped the connection).  A failed response writes nothing.
+ *      Device arrays; scratch = hhuff_hpack_enc_scratch_size(nconn) bytes (16-byte aligned) holding the
+ *      tables: HHUFF_ENC_CONTINUE carries them (and the failed state) over from the previous call; without it
+ *      every connection starts with an empty table.  nhdr = headers in hdr, nres = conn_first[nconn] (host
+ *      copies).  in_size < 2^32.  Asynchronous on `stream`; stream-ordered pool workspace of 36 bytes per
+ *      header and 16 per response (hhuff_pool_trim). */
+typedef struct hhuff_hpack_header {
+    uint32_t name_off, name_len, value_off, value_len;
+    uint32_t flags; /* HHUFF_HDR_* */
+} hhuff_hpack_header_t; /* 20 bytes */
+#define HHUFF_HDR_DONT_COMPRESS 1u
+#define HHUFF_HDR_TOKEN 2u
+typedef struct hhuff_hpack_response {
+    uint64_t content_length;    /* res.content_length: SIZE_MAX (all ones) sends none */
+    uint32_t stream_id, status; /* status: res.status (ignored for trailers) */
+    uint32_t hdr_first, nhdr;
+    uint32_t header_table_size; /* conn->peer_settings.header_table_size (header_table_adjust_size, :839-856) */
+    uint32_t max_frame_size;    /* conn->peer_settings.max_frame_size */
+    uint32_t flags;             /* HHUFF_RES_* */
+    uint32_t reserved;          /* 0 */
+} hhuff_hpack_response_t;       /* 40 bytes */
+#define HHUFF_RES_END_STREAM 1u /* is_end_stream */
+#define HHUFF_RES_SERVER 2u     /* server_name != NULL */
+#define HHUFF_RES_TRAILERS 4u   /* h2o_hpack_flatten_trailers */
+#define HHUFF_ENC_CONTINUE 1u
+#define HHUFF_RES_SPACE (-300)
+#define HHUFF_RES_SKIPPED (-301)
+#define HHUFF_RES_EINVAL (-303)
+/* A region size that holds response r whatever its connection's table: name_value_bytes = the sum of its
+ * headers' name_len + value_len, server_len = 0 without HHUFF_RES_SERVER.  (h2o's own reservation,
+ * hpack.c:1141-1152 with calc_capacity :998-1001, plus the CONTINUATION frame headers.) */
+static inline uint64_t hhuff_hpack_response_bound(uint64_t name_value_bytes, uint32_t nhdr, uint32_t server_len,
+                                                  uint32_t max_frame_size)
+{
+    uint64_t payload = name_value_bytes + 21ull * nhdr + 5 + 5 + (server_len ? 5ull + server_len + 21 : 0) + 23;
+    return 9 + payload + 9 * (payload / (max_frame_size ? max_frame_size : 1) + 1);
+}
+uint64_t hhuff_hpack_enc_scratch_size(uint32_t nconn);
+int hhuff_hpack_flatten_responses(const uint8_t *in, uint64_t in_size, const hhuff_hpack_header_t *hdr, uint32_t nhdr,
+                                  const hhuff_hpack_response_t *res, const uint32_t *conn_first, uint32_t nconn,
+                                  uint32_t nres, uint32_t server_off, uint32_t server_len, uint8_t *out,
+                                  const uint64_t *out_off, uint32_t *out_len, uint32_t *headers_size, int32_t *rstatus,
+                                  void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
+
 /* (3b) Pipelined host path (the socket-buffer -> pinned -> device -> pinned -> pool staging of
  *     SURVEY f3; replaces the caller-side copies around lib/http2/hpack.c:240-241).  Contiguous layout
  *     (in_off[n + 1], implicit output slots) only.  The batch is cut into chunks of about

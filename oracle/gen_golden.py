@@ -23,6 +23,10 @@ Fixture sets (numpy .npz, arrays only, no pickles):
                    truncated integers, invalid Huffman), and QPACK name literals (prefix 3/5) -- the
                    reference's decode_int / decode_huffman / validators / h2o_lookup_token composed as
                    decode_string and decode_header_{name,value}_literal call them (oracle/ref_shim.c)
+  hpenc.npz        HTTP/2 response header blocks (f4 encode half): synthetic sessions of responses flattened by
+                   the real h2o_hpack_flatten_response / _trailers with one encoder table per connection
+                   (oracle/ref_hpenc.c), the restatement checked against them as they are written; one session
+                   with invalid arguments and short output regions
 
 Usage:  python3 oracle/gen_golden.py            (rewrites tests/golden/)
 """
@@ -696,7 +700,72 @@ def qpack_set():
     return out
 
 
+HPENC_SESSIONS = [  # name, seed, connections, steps, knobs (h2o_amd.hpenc_synth.make_session), error mutations
+    ("h4096", 301, 160, 3, dict(), False),
+    ("hedge", 302, 120, 3, dict(small_table_frac=0.3, trailers_frac=0.1, big_frac=0.01, notoken_frac=0.1,
+                                dont_compress_frac=0.15, frame_frac=0.3), False),
+    ("herr", 303, 120, 2, dict(small_table_frac=0.1, big_frac=0.005, dont_compress_frac=0.05), True),
+]
+
+
+def hpenc_errors(rng, st):
+    """invalid arguments and short output regions -> HHUFF_RES_EINVAL / _SPACE, and the connection's later
+    responses HHUFF_RES_SKIPPED"""
+    res, hdr = st["res"], st["hdr"]
+    n = res.size
+    regions = np.diff(st["out_off"].astype(np.int64))
+    for r in rng.choice(n, max(1, n // 40), replace=False):
+        regions[r] = int(rng.integers(0, 24))
+    for r in rng.choice(n, max(1, n // 80), replace=False):
+        if not res["flags"][r] & 4:
+            res["status"][r] = int(rng.choice([0, 99, 1000]))
+    for r in rng.choice(n, max(1, n // 150), replace=False):
+        res["max_frame_size"][r] = int(rng.choice([100, 16383, 1 << 24]))
+    if hdr.size:
+        for h in rng.choice(hdr.size, max(1, hdr.size // 400), replace=False):
+            hdr["value_off"][h] = st["data"].size - int(rng.integers(0, 3))
+            hdr["value_len"][h] = 5
+    st["out_off"] = np.concatenate([[0], np.cumsum(regions)]).astype(np.uint64)
+
+
+def hpenc_set():
+    """HTTP/2 response header blocks (f4 encode half): sessions of synthetic responses flattened by the
+    real h2o_hpack_flatten_response / _trailers (oracle/ref_hpenc.c), one encoder table per connection
+    across the steps; per step the inputs and the reference's frames (compacted), lengths and statuses"""
+    from h2o_amd import hpenc_synth as HE
+
+    out = {}
+    for name, seed, nconn, nsteps, knobs, errors in HPENC_SESSIONS:
+        steps = HE.make_session(nconn, steps=nsteps, seed=seed, **knobs)
+        rng = np.random.default_rng(seed + 7)
+        sr, so = O.HpeSession(O.ref(), nconn), O.HpeSession(O.oracle(), nconn)
+        out[name + "_meta"] = np.array([nconn, nsteps], np.uint32)
+        for k, st in enumerate(steps):
+            if errors:
+                hpenc_errors(rng, st)
+            args = (st["data"], st["hdr"], st["res"], st["conn_first"], st["out_off"], st["server_off"],
+                    st["server_len"])
+            r, q = sr.step(*args), so.step(*args)
+            for key in ("out_len", "headers_size", "rstatus"):
+                assert (r[key] == q[key]).all(), (name, k, key)
+            frames = b"".join(r["out"][int(o):int(o) + int(L)].tobytes() for o, L in zip(st["out_off"], r["out_len"]))
+            assert frames == b"".join(q["out"][int(o):int(o) + int(L)].tobytes()
+                                      for o, L in zip(st["out_off"], q["out_len"])), (name, k)
+            p = "%s_%d_" % (name, k)
+            out.update({p + "data": st["data"], p + "hdr": st["hdr"].view(np.uint32).reshape(-1),
+                        p + "res": st["res"].view(np.uint32).reshape(-1), p + "conn_first": st["conn_first"],
+                        p + "server": np.array([st["server_off"], st["server_len"]], np.uint32),
+                        p + "out_off": st["out_off"], p + "frames": np.frombuffer(frames, np.uint8),
+                        p + "out_len": r["out_len"], p + "headers_size": r["headers_size"], p + "rstatus": r["rstatus"]})
+        sr.close()
+        so.close()
+    return out
+
+
 def main():
+    if "--only-hpenc" in sys.argv:
+        np.savez_compressed(os.path.join(GOLDEN, "hpenc.npz"), **hpenc_set())
+        return
     if "--only-qpack" in sys.argv:
         np.savez_compressed(os.path.join(GOLDEN, "qpack.npz"), **qpack_set())
         return
@@ -719,6 +788,7 @@ def main():
     sets["literals"] = literals_set()
     sets.update(blocks_sets())
     sets["qpack"] = qpack_set()
+    sets["hpenc"] = hpenc_set()
     for name, arrays in sets.items():
         path = os.path.join(GOLDEN, name + ".npz")
         np.savez_compressed(path, **arrays)

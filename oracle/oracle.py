@@ -287,6 +287,55 @@ class QpackSession:
         return r
 
 
+class HpeSession:
+    """HTTP/2 response encoder session (include/hhuff.h hhuff_hpack_flatten_responses contract): one encoder
+    dynamic table per connection, kept between step() calls.  codec = oracle() (restatement, hpack_encode.c)
+    or ref() (h2o's h2o_hpack_flatten_response / _trailers, ref_hpenc.c)."""
+
+    def __init__(self, codec, nconn):
+        L, P = codec.lib, codec.prefix
+        self._open, self._close, self._step = (getattr(L, P + "_hpe_open"), getattr(L, P + "_hpe_close"),
+                                               getattr(L, P + "_hpe_step"))
+        self._open.restype = ctypes.c_void_p
+        self._open.argtypes = [ctypes.c_uint32]
+        self._close.argtypes = [ctypes.c_void_p]
+        self._step.restype = ctypes.c_int
+        self._step.argtypes = ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32] + [ctypes.c_void_p] * 5)
+        self.nconn = nconn
+        self.h = self._open(nconn)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._close(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def step(self, data, hdr, res, conn_first, out_off, server_off=0, server_len=0):
+        """hdr / res: numpy record arrays (h2o_amd.codec HPE_HEADER_DTYPE / HPE_RESPONSE_DTYPE); -> dict out,
+        out_len, headers_size, rstatus"""
+        c = lambda a, t: np.ascontiguousarray(a, dtype=t)  # noqa: E731
+        data = c(data, np.uint8)
+        in_size = data.size
+        if data.size == 0:
+            data = np.zeros(1, np.uint8)
+        hdr = np.ascontiguousarray(hdr)
+        res = np.ascontiguousarray(res)
+        conn_first, out_off = c(conn_first, np.uint32), c(out_off, np.uint64)
+        nres = max(1, int(conn_first[-1]))
+        r = dict(out=np.zeros(max(1, int(out_off[-1])), np.uint8), out_len=np.zeros(nres, np.uint32),
+                 headers_size=np.zeros(nres, np.uint32), rstatus=np.zeros(nres, np.int32))
+        if hdr.size == 0:
+            hdr = np.zeros(1, hdr.dtype)
+        hp = hdr.ctypes.data
+        rc = self._step(self.h, data.ctypes.data, in_size, hp, res.ctypes.data, conn_first.ctypes.data, server_off,
+                        server_len, r["out"].ctypes.data, out_off.ctypes.data, r["out_len"].ctypes.data,
+                        r["headers_size"].ctypes.data, r["rstatus"].ctypes.data)
+        assert rc == 0, "%d header(s) flagged as tokens are not h2o tokens" % rc
+        return r
+
+
 def default_arena_off(blk_off, table_size=4096):
     """A block of L bytes produces at most L fields; each field's name + value is at most 8/5 of its
     literal bytes or a copy of one table entry (<= table_size bytes): a generous bound per block."""
