@@ -104,6 +104,9 @@ def lib():
         L.hhuff_hpack_flatten_responses.argtypes = ([_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, _vp,
                                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
                                                     + [_vp] * 6 + [ctypes.c_uint64, ctypes.c_uint, _vp])
+        L.hhuff_qpack_flatten_responses.restype = ctypes.c_int
+        L.hhuff_qpack_flatten_responses.argtypes = ([_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32,
+                                                     ctypes.c_uint32, ctypes.c_uint32] + [_vp] * 6)
         L.hhuff_version.restype = ctypes.c_char_p
         L.hhuff_last_error_string.restype = ctypes.c_char_p
         L.hhuff_grid_size.restype = ctypes.c_int
@@ -124,7 +127,7 @@ EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decod
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string", "hhuff_per_string_calls",
             "hhuff_grid_size", "hhuff_pool_trim", "hhuff_service_stamps", "hhuff_hpack_enc_scratch_size",
-            "hhuff_hpack_flatten_responses")
+            "hhuff_hpack_flatten_responses", "hhuff_qpack_flatten_responses")
 
 
 def _check(rc, what):
@@ -434,6 +437,39 @@ def hpack_response_bound(name_value_bytes, nhdr, server_len, max_frame_size):
     payload = name_value_bytes + 21 * np.asarray(nhdr, np.int64) + 10 + 23 + np.where(
         np.asarray(server_len) != 0, np.asarray(server_len, np.int64) + 26, 0)
     return 9 + payload + 9 * (payload // np.maximum(np.asarray(max_frame_size, np.int64), 1) + 1)
+
+
+QPE_RESPONSE_DTYPE = np.dtype([("content_length", "<u8"), ("status", "<u4"), ("hdr_first", "<u4"), ("nhdr", "<u4"),
+                               ("flags", "<u4"), ("dfid_off", "<u4"), ("dfid_len", "<u4")])
+QRES_DATAGRAM = 8
+
+
+def qpack_response_bound(name_value_bytes, nhdr, server_len, dfid_len):
+    """include/hhuff.h hhuff_qpack_response_bound (numpy arrays or ints)"""
+    sl = np.asarray(server_len, np.int64)
+    return (9 + 2 + 8 + 23 + 26 + np.asarray(dfid_len, np.int64) + np.where(sl != 0, sl + 12, 0) +
+            21 * np.asarray(nhdr, np.int64) + name_value_bytes)
+
+
+def qpack_flatten_responses(data, hdr, res, nres, out_off, server_off=0, server_len=0, in_size=None, out=None,
+                            stream=None):
+    """HTTP/3 response HEADERS frames (include/hhuff.h hhuff_qpack_flatten_responses) on device tensors: hdr =
+    uint8 tensor of HPE_HEADER_DTYPE records, res = uint8 tensor of QPE_RESPONSE_DTYPE records (32 B), out_off
+    int64 [nres + 1].  Returns a dict of device tensors: out, out_len, header_len, rstatus."""
+    import torch
+
+    dev = data.device
+    in_size = data.numel() if in_size is None else in_size
+    nhdr = hdr.numel() // HPE_HEADER_DTYPE.itemsize
+    if out is None:
+        out = torch.empty(max(1, int(out_off[-1].item())), dtype=torch.uint8, device=dev)
+    i32 = lambda n: torch.empty(max(1, n), dtype=torch.int32, device=dev)  # noqa: E731
+    r = dict(out=out, out_len=i32(nres), header_len=i32(nres), rstatus=i32(nres))
+    _check(lib().hhuff_qpack_flatten_responses(
+        _dp(data), in_size, _dp(hdr) if nhdr else None, nhdr, _dp(res), nres, server_off, server_len, _dp(out),
+        _dp(out_off), _dp(r["out_len"]), _dp(r["header_len"]), _dp(r["rstatus"]), _stream(stream)),
+        "hhuff_qpack_flatten_responses")
+    return r
 
 
 def hpack_flatten_responses(data, hdr, res, conn_first, nres, out_off, server_off=0, server_len=0, in_size=None,

@@ -264,6 +264,20 @@ HHUFF_API int hhuff_hpack_flatten_responses(const uint8_t* in, uint64_t in_size,
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "hpack flatten launch");
 }
 
+HHUFF_API int hhuff_qpack_flatten_responses(const uint8_t* in, uint64_t in_size, const hhuff_hpack_header_t* hdr,
+                                            uint32_t nhdr, const hhuff_qpack_response_t* res, uint32_t nres,
+                                            uint32_t server_off, uint32_t server_len, uint8_t* out, const uint64_t* out_off,
+                                            uint32_t* out_len, uint32_t* header_len, int32_t* rstatus, void* stream) {
+    if (nres == 0) return HHUFF_OK;
+    if (!res || !out || !out_off || !out_len || !header_len || !rstatus || (nhdr && !hdr) || !in) return arg_fail("NULL array");
+    if (in_size >= (1ull << 32)) return arg_fail("in_size must stay below 2^32 (u32 offsets)");
+    if (((uintptr_t)res & 7u) != 0 || ((uintptr_t)hdr & 3u) != 0 || ((uintptr_t)out_off & 7u) != 0)
+        return arg_fail("misaligned hdr / res / out_off");
+    hipError_t e = hhuff::launch_qpack_flatten(in, in_size, hdr, nhdr, res, nres, server_off, server_len, out, out_off, out_len,
+                                               header_len, rstatus, (hipStream_t)stream);
+    return e == hipSuccess ? HHUFF_OK : hip_fail(e, "qpack flatten launch");
+}
+
 HHUFF_API uint64_t hhuff_qpack_scratch_size(uint32_t nconn, uint32_t header_table_size) {
     return (uint64_t)nconn * hhuff::qpack_conn_scratch(header_table_size);
 }

@@ -81,6 +81,12 @@ hipError_t launch_hpack_flatten(const uint8_t* in, uint64_t in_size, const hhuff
                                 uint32_t* out_len, uint32_t* headers_size, int32_t* rstatus, uint8_t* scratch,
                                 uint32_t flags, hipStream_t stream);
 
+// HTTP/3 response HEADERS frames (hhuff_hpenc.hip): include/hhuff.h hhuff_qpack_flatten_responses
+hipError_t launch_qpack_flatten(const uint8_t* in, uint64_t in_size, const hhuff_hpack_header_t* hdr, uint32_t nhdr,
+                                const hhuff_qpack_response_t* res, uint32_t nres, uint32_t server_off, uint32_t server_len,
+                                uint8_t* out, const uint64_t* out_off, uint32_t* out_len, uint32_t* header_len,
+                                int32_t* rstatus, hipStream_t stream);
+
 // HPACK header blocks (f4): see include/hhuff.h hhuff_hpack_decode_blocks; scratch = nconn x
 // hpack_conn_scratch(table_size) bytes of device memory
 uint64_t hpack_conn_scratch(uint32_t table_size);

@@ -17,8 +17,8 @@ Several steps of one session continue the same connections (HHUFF_ENC_CONTINUE).
 """
 import numpy as np
 
-from .codec import HPE_HEADER_DTYPE, HPE_RESPONSE_DTYPE, HDR_DONT_COMPRESS, HDR_TOKEN, RES_END_STREAM, RES_SERVER, \
-    RES_TRAILERS, hpack_response_bound
+from .codec import HPE_HEADER_DTYPE, HPE_RESPONSE_DTYPE, QPE_RESPONSE_DTYPE, HDR_DONT_COMPRESS, HDR_TOKEN, \
+    QRES_DATAGRAM, RES_END_STREAM, RES_SERVER, RES_TRAILERS, hpack_response_bound, qpack_response_bound
 
 SERVER = b"h2o/2.3.0-dev"
 _CTYPES = [b"text/html; charset=utf-8", b"text/css", b"application/javascript", b"image/png", b"image/jpeg",
@@ -228,3 +228,42 @@ def tile(b, k):
     conn_first = np.concatenate([cf[:-1] + j * nres for j in range(k)] + [[k * nres]]).astype(np.uint32)
     return dict(data=b["data"], hdr=hdr, res=res, conn_first=conn_first, server_off=b["server_off"],
                 server_len=b["server_len"], out_off=out_offsets(hdr, res, b["server_len"]))
+
+
+def to_qpack(b, seed=0, dfid_frac=0.02, odd_status_frac=0.01):
+    """The same responses as HTTP/3 responses (include/hhuff.h hhuff_qpack_response_t; trailers dropped --
+    h2o's HTTP/3 server sends them through the same flatten), a few with a datagram flow id or a status outside
+    the HTTP status range: -> dict data, hdr, res, server_off, server_len, out_off"""
+    rng = np.random.default_rng(seed)
+    keep = (b["res"]["flags"] & RES_TRAILERS) == 0
+    src = b["res"][keep]
+    res = np.zeros(src.size, QPE_RESPONSE_DTYPE)
+    for k in ("content_length", "status", "hdr_first", "nhdr"):
+        res[k] = src[k]
+    res["flags"] = src["flags"] & RES_SERVER
+    data = b["data"]
+    extra = []
+    dfid = rng.random(src.size) < dfid_frac
+    for r in np.flatnonzero(dfid):
+        v = b"%d" % int(rng.integers(0, 1 << 40))
+        res["dfid_off"][r] = data.size + sum(len(e) for e in extra)
+        res["dfid_len"][r] = len(v)
+        extra.append(v)
+    res["flags"][dfid] |= QRES_DATAGRAM
+    odd = rng.random(src.size) < odd_status_frac
+    res["status"][odd] = rng.choice([0, 7, 99, 599, 1000, 65535, 65536 + 200], int(odd.sum()))
+    if extra:
+        data = np.concatenate([data, np.frombuffer(b"".join(extra), np.uint8)])
+    return dict(data=data, hdr=b["hdr"], res=res, server_off=b["server_off"], server_len=b["server_len"],
+                out_off=qpack_out_offsets(b["hdr"], res, b["server_len"]))
+
+
+def qpack_out_offsets(hdr, res, server_len):
+    nv = (hdr["name_len"].astype(np.int64) + hdr["value_len"]) if hdr.size else np.zeros(0, np.int64)
+    csum = np.concatenate([[0], np.cumsum(nv)])
+    first = res["hdr_first"].astype(np.int64)
+    nh = res["nhdr"].astype(np.int64)
+    sl = np.where(res["flags"] & RES_SERVER, server_len, 0)
+    b = qpack_response_bound(csum[first + nh] - csum[first], nh, sl, res["dfid_len"].astype(np.int64))
+    b = (b + 15) // 16 * 16
+    return np.concatenate([[0], np.cumsum(b)]).astype(np.uint64)

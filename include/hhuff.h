@@ -346,7 +346,8 @@ int hhuff_qpack_parse_requests(const uint8_t *in, uint64_t in_size, const uint32
  *                    HHUFF_HDR_DONT_COMPRESS = h2o_header_t.flags.dont_compress; HHUFF_HDR_TOKEN = the name is
  *                    an h2o token (h2o_iovec_is_token: the header was added with its h2o_token_t) -- set it only
  *                    for names listed in lib/common/token_table.h
- *        response r  res[r] (below): the headers hdr_first .. hdr_first + nhdr - 1 in order; HHUFF_RES_SERVER
+ *        response r  res[r] (below): the headers hdr_first .. hdr_first + nhdr - 1 in order (the ranges of two
+ *                    responses must not overlap; headers outside every range are ignored); HHUFF_RES_SERVER
  *                    sends server_name (in[server_off .. + server_len), h2o's globalconf->server_name; clear
  *                    it where h2o passes NULL: informational responses); HHUFF_RES_TRAILERS makes r a trailers
  *                    block (flatten_trailers: no :status, server or content-length, END_STREAM)
@@ -400,6 +401,40 @@ int hhuff_hpack_flatten_responses(const uint8_t *in, uint64_t in_size, const hhu
                                   uint32_t nres, uint32_t server_off, uint32_t server_len, uint8_t *out,
                                   const uint64_t *out_off, uint32_t *out_len, uint32_t *headers_size, int32_t *rstatus,
                                   void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
+
+/* (2g) HTTP/3 response HEADERS frames (QPACK encode half): h2o_qpack_flatten_response
+ *      (lib/http3/qpack.c:1352-1399) as h2o's HTTP/3 server calls it (lib/http3/server.c:1680-1683): without an
+ *      encoder-stream buffer, so the encoder never inserts into its dynamic table (:1175-1176) and every response
+ *      stands alone -- :status, server (HHUFF_RES_SERVER), content-length, the headers (static-table references
+ *      through h2o_qpack_lookup_static for token names, literals otherwise; do_flatten_header :1148-1213),
+ *      datagram-flow-id (HHUFF_QRES_DATAGRAM: in[dfid_off .. + dfid_len)), behind the section prefix 00 00 and
+ *      the HEADERS frame header (type 0x01, QUIC varint length; finalize_flatten :1265-1310).
+ *        header h    hdr[h] as for hhuff_hpack_flatten_responses (HHUFF_HDR_TOKEN, HHUFF_HDR_DONT_COMPRESS); the
+ *                    ranges hdr_first .. + nhdr of two responses must not overlap
+ *        out         frame r at out + out_off[r]; region [out_off[r], out_off[r+1]) (u64, nres + 1 entries):
+ *                    hhuff_qpack_response_bound() always fits
+ *      out_len[r] = frame bytes, header_len[r] = *serialized_header_len (the field section, frame header
+ *      excluded), rstatus[r] = 0, HHUFF_RES_SPACE or HHUFF_RES_EINVAL (a string past in_size); a failed
+ *      response writes nothing.  Device arrays; in_size < 2^32; asynchronous on `stream`; stream-ordered pool
+ *      workspace of 24 bytes per header and 32 per response. */
+typedef struct hhuff_qpack_response {
+    uint64_t content_length; /* res.content_length: SIZE_MAX (all ones) sends none */
+    uint32_t status;         /* res.status: a static entry, else the decimal of (uint16_t)status against :status */
+    uint32_t hdr_first, nhdr;
+    uint32_t flags;          /* HHUFF_RES_SERVER, HHUFF_QRES_DATAGRAM */
+    uint32_t dfid_off, dfid_len;
+} hhuff_qpack_response_t;    /* 32 bytes */
+#define HHUFF_QRES_DATAGRAM 8u
+static inline uint64_t hhuff_qpack_response_bound(uint64_t name_value_bytes, uint32_t nhdr, uint32_t server_len,
+                                                  uint32_t dfid_len)
+{
+    return 9 + 2 + 8 + 23 + 26 + (uint64_t)dfid_len + (server_len ? 12ull + server_len : 0) + 21ull * nhdr +
+           name_value_bytes;
+}
+int hhuff_qpack_flatten_responses(const uint8_t *in, uint64_t in_size, const hhuff_hpack_header_t *hdr, uint32_t nhdr,
+                                  const hhuff_qpack_response_t *res, uint32_t nres, uint32_t server_off,
+                                  uint32_t server_len, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
+                                  uint32_t *header_len, int32_t *rstatus, void *stream);
 
 /* (3b) Pipelined host path (the socket-buffer -> pinned -> device -> pinned -> pool staging of
  *     SURVEY f3; replaces the caller-side copies around lib/http2/hpack.c:240-241).  Contiguous layout

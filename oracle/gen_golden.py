@@ -27,6 +27,9 @@ Fixture sets (numpy .npz, arrays only, no pickles):
                    the real h2o_hpack_flatten_response / _trailers with one encoder table per connection
                    (oracle/ref_hpenc.c), the restatement checked against them as they are written; one session
                    with invalid arguments and short output regions
+  qpenc.npz        HTTP/3 response HEADERS frames (f4, QPACK encode half): synthetic responses (datagram flow ids,
+                   statuses outside the static table, dont_compress, names added without their token) flattened by
+                   the real h2o_qpack_flatten_response as h2o's HTTP/3 server calls it (ref_shim.c ref_qpe_step)
 
 Usage:  python3 oracle/gen_golden.py            (rewrites tests/golden/)
 """
@@ -762,7 +765,52 @@ def hpenc_set():
     return out
 
 
+QPENC_SETS = [  # name, seed, connections, knobs (make_session), to_qpack knobs, error mutations
+    ("q1", 401, 300, dict(), dict(), False),
+    ("qedge", 402, 200, dict(big_frac=0.01, notoken_frac=0.1, dont_compress_frac=0.15),
+     dict(dfid_frac=0.2, odd_status_frac=0.1), False),
+    ("qerr", 403, 200, dict(big_frac=0.005), dict(dfid_frac=0.05), True),
+]
+
+
+def qpenc_set():
+    """HTTP/3 response HEADERS frames (f4, QPACK encode half): synthetic responses flattened by the real
+    h2o_qpack_flatten_response as h2o's HTTP/3 server calls it (oracle/ref_shim.c ref_qpe_step), the restatement
+    checked against them as they are written"""
+    from h2o_amd import hpenc_synth as HE
+
+    out = {}
+    for name, seed, nconn, knobs, qknobs, errors in QPENC_SETS:
+        q = HE.to_qpack(HE.make_session(nconn, seed=seed, **knobs)[0], seed=seed, **qknobs)
+        if errors:
+            rng = np.random.default_rng(seed + 7)
+            n = q["res"].size
+            regions = np.diff(q["out_off"].astype(np.int64))
+            for r in rng.choice(n, max(1, n // 40), replace=False):
+                regions[r] = int(rng.integers(0, 24))
+            q["out_off"] = np.concatenate([[0], np.cumsum(regions)]).astype(np.uint64)
+            for h in rng.choice(q["hdr"].size, max(1, q["hdr"].size // 400), replace=False):
+                q["hdr"]["value_off"][h] = q["data"].size - int(rng.integers(0, 3))
+                q["hdr"]["value_len"][h] = 5
+        args = (q["data"], q["hdr"], q["res"], q["out_off"], q["server_off"], q["server_len"])
+        r, o = O.qpe_step(O.ref(), *args), O.qpe_step(O.oracle(), *args)
+        for key in ("out_len", "header_len", "rstatus"):
+            assert (r[key] == o[key]).all(), (name, key)
+        frames = b"".join(r["out"][int(a):int(a) + int(L)].tobytes() for a, L in zip(q["out_off"], r["out_len"]))
+        assert frames == b"".join(o["out"][int(a):int(a) + int(L)].tobytes() for a, L in zip(q["out_off"], o["out_len"]))
+        p = name + "_"
+        out.update({p + "data": q["data"], p + "hdr": q["hdr"].view(np.uint32).reshape(-1),
+                    p + "res": q["res"].view(np.uint32).reshape(-1),
+                    p + "server": np.array([q["server_off"], q["server_len"]], np.uint32), p + "out_off": q["out_off"],
+                    p + "frames": np.frombuffer(frames, np.uint8), p + "out_len": r["out_len"][:q["res"].size],
+                    p + "header_len": r["header_len"][:q["res"].size], p + "rstatus": r["rstatus"][:q["res"].size]})
+    return out
+
+
 def main():
+    if "--only-qpenc" in sys.argv:
+        np.savez_compressed(os.path.join(GOLDEN, "qpenc.npz"), **qpenc_set())
+        return
     if "--only-hpenc" in sys.argv:
         np.savez_compressed(os.path.join(GOLDEN, "hpenc.npz"), **hpenc_set())
         return
@@ -789,6 +837,7 @@ def main():
     sets.update(blocks_sets())
     sets["qpack"] = qpack_set()
     sets["hpenc"] = hpenc_set()
+    sets["qpenc"] = qpenc_set()
     for name, arrays in sets.items():
         path = os.path.join(GOLDEN, name + ".npz")
         np.savez_compressed(path, **arrays)

@@ -336,6 +336,32 @@ class HpeSession:
         return r
 
 
+def qpe_step(codec, data, hdr, res, out_off, server_off=0, server_len=0):
+    """HTTP/3 response HEADERS frames (include/hhuff.h hhuff_qpack_flatten_responses contract); codec = oracle()
+    (restatement, qpack_encode.c) or ref() (h2o_qpack_flatten_response, ref_shim.c).  hdr / res: numpy record
+    arrays (h2o_amd.codec HPE_HEADER_DTYPE / QPE_RESPONSE_DTYPE) -> dict out, out_len, header_len, rstatus"""
+    f = getattr(codec.lib, codec.prefix + "_qpe_step")
+    f.restype = ctypes.c_int
+    f.argtypes = ([ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
+                   ctypes.c_uint32] + [ctypes.c_void_p] * 5)
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    in_size = data.size
+    if data.size == 0:
+        data = np.zeros(1, np.uint8)
+    hdr, res = np.ascontiguousarray(hdr), np.ascontiguousarray(res)
+    if hdr.size == 0:
+        hdr = np.zeros(1, hdr.dtype)
+    out_off = np.ascontiguousarray(out_off, dtype=np.uint64)
+    n = res.size
+    r = dict(out=np.zeros(max(1, int(out_off[-1])), np.uint8), out_len=np.zeros(max(1, n), np.uint32),
+             header_len=np.zeros(max(1, n), np.uint32), rstatus=np.zeros(max(1, n), np.int32))
+    rc = f(data.ctypes.data, in_size, hdr.ctypes.data, res.ctypes.data if n else None, n, server_off, server_len,
+           r["out"].ctypes.data, out_off.ctypes.data, r["out_len"].ctypes.data, r["header_len"].ctypes.data,
+           r["rstatus"].ctypes.data)
+    assert rc == 0, "%d header(s) flagged as tokens are not h2o tokens" % rc
+    return r
+
+
 def default_arena_off(blk_off, table_size=4096):
     """A block of L bytes produces at most L fields; each field's name + value is at most 8/5 of its
     literal bytes or a copy of one table entry (<= table_size bytes): a generous bound per block."""

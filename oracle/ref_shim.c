@@ -455,3 +455,100 @@ REF_API int ref_qpack_step_req(void *h, const uint8_t *in, const uint32_t *enc_o
     }
     return mismatches;
 }
+
+/* ---- h2o_qpack_flatten_response (qpack.c:1352-1399) as h2o's HTTP/3 server calls it ----
+ * lib/http3/server.c:1680-1683: the connection's encoder, no encoder-stream buffer (so nothing is ever inserted
+ * into the encoder's table), the globalconf server name, the response's content length and datagram flow id.
+ * One response after another into the caller's output slots: the include/hhuff.h hhuff_qpack_flatten_responses
+ * contract (res = hhuff_qpack_response_t, 8 u32 words; hdr = hhuff_hpack_header_t, 5 words). */
+REF_API int ref_qpe_step(const uint8_t *in, uint64_t in_size, const uint32_t *hdr, const uint32_t *res, uint32_t nres,
+                         uint32_t server_off, uint32_t server_len, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
+                         uint32_t *header_len, int32_t *rstatus)
+{
+    h2o_qpack_encoder_t *enc = h2o_qpack_create_encoder(4096, 100);
+    h2o_iovec_t server_name = h2o_iovec_init(in + server_off, server_len);
+    int bad_tokens = 0;
+    for (uint32_t r = 0; r < nres; ++r) {
+        const uint32_t *R = res + 8 * (size_t)r;
+        uint64_t content_length;
+        memcpy(&content_length, R, 8);
+        uint32_t status = R[2], hfirst = R[3], nh = R[4], fl = R[5], doff = R[6], dlen = R[7];
+        int server = (fl & 2u) && server_len != 0, dfid = (fl & 8u) != 0;
+        out_len[r] = header_len[r] = 0;
+        int bad = (server && (uint64_t)server_off + server_len > in_size) || (dfid && (uint64_t)doff + dlen > in_size);
+        h2o_iovec_t *names = calloc(nh ? nh : 1, sizeof(h2o_iovec_t));
+        h2o_header_t *headers = calloc(nh ? nh : 1, sizeof(h2o_header_t));
+        for (uint32_t i = 0; i < nh && !bad; ++i) {
+            const uint32_t *H = hdr + 5 * (size_t)(hfirst + i);
+            if ((uint64_t)H[0] + H[1] > in_size || (uint64_t)H[2] + H[3] > in_size) {
+                bad = 1;
+                break;
+            }
+            const h2o_token_t *tok = (H[4] & 2u) ? h2o_lookup_token((const char *)in + H[0], H[1]) : NULL;
+            bad_tokens += (H[4] & 2u) && tok == NULL;
+            names[i] = h2o_iovec_init(in + H[0], H[1]);
+            headers[i].name = tok != NULL ? (h2o_iovec_t *)&tok->buf : &names[i];
+            headers[i].value = h2o_iovec_init(in + H[2], H[3]);
+            headers[i].flags.dont_compress = (H[4] & 1u) != 0;
+        }
+        if (bad) {
+            rstatus[r] = -303;
+        } else {
+            h2o_mem_pool_t pool;
+            h2o_mem_init_pool(&pool);
+            h2o_qpack_section_stats_t stats = {0};
+            size_t shl = 0;
+            h2o_iovec_t dv = dfid ? h2o_iovec_init(in + doff, dlen) : h2o_iovec_init(NULL, 0);
+            if (dfid && dv.base == NULL)
+                dv.base = (char *)"";
+            h2o_iovec_t f = h2o_qpack_flatten_response(enc, &pool, 4 * (int64_t)r, NULL, (int)status, headers, nh,
+                                                       server ? &server_name : NULL,
+                                                       content_length == UINT64_MAX ? SIZE_MAX : (size_t)content_length, dv,
+                                                       &stats, &shl);
+            if (f.len > out_off[r + 1] - out_off[r]) {
+                rstatus[r] = -300;
+            } else {
+                memcpy(out + out_off[r], f.base, f.len);
+                out_len[r] = (uint32_t)f.len;
+                header_len[r] = (uint32_t)shl;
+                rstatus[r] = 0;
+            }
+            h2o_mem_clear_pool(&pool);
+        }
+        free(names);
+        free(headers);
+    }
+    h2o_qpack_destroy_encoder(enc);
+    return bad_tokens;
+}
+
+/* The rule the restatement and the GPU path use for h2o_qpack_lookup_static[token] (lib/common/token_table.h):
+ * the h2o_qpack_static_table entry with the token's name and the same value (is_exact), else the first entry
+ * with the name, else -1.  Checked for every token against every static value plus two others; returns the
+ * number of disagreements. */
+REF_API int ref_qpe_lookup_check(void)
+{
+    int bad = 0;
+    for (size_t t = 0; t < h2o__num_tokens; ++t) {
+        const h2o_token_t *tok = &h2o__tokens[t];
+        for (int v = -2; v < 99; ++v) {
+            h2o_iovec_t value = v == -2 ? h2o_iovec_init(H2O_STRLIT("")) : v == -1 ? h2o_iovec_init(H2O_STRLIT("zz-other"))
+                                                                                   : h2o_qpack_static_table[v].value;
+            int exact = -1, want_exact = 0;
+            int32_t got = h2o_qpack_lookup_static[t](value, &exact), want = -1;
+            for (int32_t i = 0; i < 99; ++i) {
+                if (h2o_qpack_static_table[i].name != tok)
+                    continue;
+                if (want < 0)
+                    want = i;
+                if (h2o_memis(h2o_qpack_static_table[i].value.base, h2o_qpack_static_table[i].value.len, value.base, value.len)) {
+                    want = i;
+                    want_exact = 1;
+                    break;
+                }
+            }
+            bad += got != want || (got >= 0 && exact != want_exact);
+        }
+    }
+    return bad;
+}

@@ -3,6 +3,8 @@
   c2  1M strings mean 32 B, decode only
   c3  1M strings Zipf 8..512 B, encode + decode round trip, P / (t_enc + t_dec)
   c5  512K QPACK values mean 512 B (cookie/URI charset), encode only with flatten_string(prefix 7) framing
+  hpenc[N]   f4 encode half: HTTP/2 responses of N connections (default 65536) flattened with their encoder
+             tables (hhuff_hpack_flatten_responses)
   blocks[N]  f4: N synthetic HPACK connections (default 65536), header blocks decoded with a dynamic
       table per connection; CPU baselines: the reference (1 thread) and the restatement (16 threads)
   lit 16M c4 strings framed as HPACK literals (h2o_hpack_encode_string), then decoded as literals
@@ -229,6 +231,61 @@ def qpack_line(torch, codec, nconn=65536):
     return line
 
 
+def hpenc_line(torch, codec, nconn=65536):
+    """f4 encode half: HTTP/2 response header blocks (h2o_amd/hpenc_synth.py: 4,096 synthetic connections of 1-8
+    responses tiled to nconn, 1 % edge cases) flattened as h2o_hpack_flatten_response / _trailers do, one encoder
+    table per connection; the CPU baselines run the 4,096 distinct connections through the reference's
+    h2o_hpack_flatten_response (oracle/_ref, 1 thread) and the restatement (1 thread)"""
+    import time
+
+    from h2o_amd import hpenc_synth as HE
+
+    big = float(os.environ.get("HHUFF_HPENC_BIG", "0.001"))  # A/B knob: share of responses past max_frame_size
+    base = HE.make_session(4096, seed=13, big_frac=big)[0]
+    b = HE.tile(base, max(1, nconn // 4096))
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
+    d, hd, rs = dev(b["data"]), dev(b["hdr"].view(np.uint8)), dev(b["res"].view(np.uint8))
+    cf, oo = dev(b["conn_first"].view(np.int32)), dev(b["out_off"].view(np.int64))
+    nres, nhdr, nc = int(b["res"].size), int(b["hdr"].size), int(b["conn_first"].size - 1)
+    out = torch.empty(int(b["out_off"][-1]), dtype=torch.uint8, device="cuda")
+    scratch = torch.empty(int(codec.lib().hhuff_hpack_enc_scratch_size(nc)), dtype=torch.uint8, device="cuda")
+    res = {}
+
+    def run():
+        res["r"] = codec.hpack_flatten_responses(d, hd, rs, cf, nres, oo, b["server_off"], b["server_len"],
+                                                 in_size=int(b["data"].size), out=out, scratch=scratch)
+
+    t = timed(torch, run, steps=10, warmup=2)
+    r = res["r"]
+    frame_bytes = int(r["out_len"][:nres].to(torch.int64).sum().item())
+    field_bytes = int(b["hdr"]["name_len"].astype(np.int64).sum() + b["hdr"]["value_len"].astype(np.int64).sum())
+    line = {"config": "hpenc", "connections": nc, "responses": nres, "fields": nhdr, "field_bytes": field_bytes,
+            "frame_bytes": frame_bytes, "ok_responses": int((r["rstatus"][:nres] == 0).sum().item()),
+            "flatten_ms": round(t, 4), "responses_per_s": round(nres / (t * 1e-3), 1),
+            "fields_per_s": round(nhdr / (t * 1e-3), 1), "field_gibps": round(field_bytes / GIB / (t * 1e-3), 3)}
+    try:
+        sys.path.insert(0, ROOT)
+        from oracle import oracle as O
+
+        cpu = {}
+        n0 = int(base["res"].size)
+        args = (base["data"], base["hdr"], base["res"], base["conn_first"], base["out_off"], base["server_off"],
+                base["server_len"])
+        for kind, lib in (("reference", O.ref() if O.ref_available() else None), ("restatement", O.oracle())):
+            if lib is None:
+                continue
+            s = O.HpeSession(lib, 4096)
+            t0 = time.perf_counter()
+            s.step(*args)
+            dt = time.perf_counter() - t0
+            s.close()
+            cpu[kind + "_1thread_responses_per_s"] = round(n0 / dt, 1)
+        line["cpu"] = cpu
+    except Exception as e:  # the CPU baseline is a report, not a gate
+        line["cpu_error"] = str(e)
+    return line
+
+
 def main():
     import torch
 
@@ -245,6 +302,10 @@ def main():
         if cfg.startswith("qpack"):
             n = int(cfg[5:]) if len(cfg) > 5 else 65536
             print(json.dumps(qpack_line(torch, codec, n)), flush=True)
+            continue
+        if cfg.startswith("hpenc"):
+            n = int(cfg[5:]) if len(cfg) > 5 else 65536
+            print(json.dumps(hpenc_line(torch, codec, n)), flush=True)
             continue
         if cfg.startswith("blocks"):
             n = int(cfg[6:]) if len(cfg) > 6 else 65536
