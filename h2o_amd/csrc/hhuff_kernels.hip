@@ -2582,13 +2582,124 @@ hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, b
 // Resident per-string service.  A launch per string costs ~18 us (launch + stream synchronisation); here
 // one wave stays resident and polls kSvcSlots mailboxes in coherent host memory (one per calling thread):
 // lane l watches slot l's request counter with system-scope loads.  A posted request is served by the
-// whole wave: its header and input come over PCIe in one round of 16-B loads into LDS, lane 0 runs the
-// codec from LDS (decode_core / encode_core, the tables staged once per launch), the wave writes the
-// output back, then a system-scope release and the slot's `done` counter.  The wave exits when the host
+// whole wave: its header and input come over PCIe in one round of system-scope loads into LDS, the wave
+// codes it (wave_encode / wave_decode, the tables staged once per launch), writes the output back with
+// system-scope stores, waits for them, then stores the slot's `done` counter.  The wave exits when the host
 // sets ctrl->stop, after idle_ticks of the real-time counter (100 MHz) without a request, or after
 // max_ticks in all -- every exit is reached without the host, so the grid always drains -- and the host
 // relaunches it on the next request it finds unserved.
 // ------------------------------------------------------------------------------------------------
+// ------------------------------------------------------------------------------------------------
+// Wave-parallel codecs for one string (the per-string service; same results as encode_core / decode_core).
+//   encode: 64 bytes per round, one per lane: table entry, wave prefix sum of the code lengths, each code
+//           OR-ed into the MSB-first output stage at its bit (place_bits); the verdict from the total.
+//   decode: the code stream is a chain of steps (each step: one window-LUT entry, 1-2 symbols, or a long
+//           code).  Per round every lane takes the step that would start at bit W + lane (all 64 of them in
+//           parallel, one LUT round trip), then the wave follows the chain through those 64 candidates with
+//           scalar reads (v_readlane at the chain position: no memory round trip per step) until it leaves
+//           the window; the lanes on the chain write their symbols at a wave prefix sum of their counts.
+//           A lone lane decoding the string waits on one LUT read per step (~35 steps for 48 B).
+// ------------------------------------------------------------------------------------------------
+// encode s_in bytes [0, len) into out32 (LDS, MSB-first words); returns the code bits or kFailLen
+__device__ __forceinline__ uint32_t wave_encode(const uint8_t* in, uint32_t len, uint32_t* out32, const uint2* s_enc,
+                                                uint32_t lane) {
+    for (uint32_t k = lane; k < len / 4u + 4u; k += 64u) out32[k] = 0u;
+    wave_lds_sync();
+    const uint32_t obase = lds_addr(out32);
+    const uint32_t lim = len ? 8u * len - 8u : 0u;  // hpack.c:799-800: ceil(bits / 8) < len
+    uint32_t bits = 0;                               // wave-uniform
+    bool fail = len == 0 || len > kSvcMax;
+    for (uint32_t j0 = 0; j0 < len && !fail; j0 += 64u) {
+        const uint32_t j = j0 + lane;
+        const uint2 e = j < len ? s_enc[in[j]] : make_uint2(0u, 0u);
+        const uint32_t incl = wave_incl_scan(e.y);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (bits + tot > lim) {
+            fail = true;  // already longer than the input allows: the rest cannot shorten it
+            break;
+        }
+        if (e.y) place_bits(obase, bits + incl - e.y, e.x, e.y);
+        bits += tot;
+    }
+    if (fail) return kFailLen;
+    const uint32_t p = (0u - bits) & 7u;  // fill the last byte with ones (EOS prefix, hpack.c:795-798)
+    if (lane == 0 && p) place_bits(obase, bits, (1ull << p) - 1ull, p);
+    wave_lds_sync();
+    return bits;
+}
+
+// decode s_in bytes [0, len) into out (LDS bytes)
+__device__ __forceinline__ DecResult wave_decode(const uint8_t* in, uint32_t len, uint8_t* out, const DecTables& T,
+                                                 uint32_t lane) {
+    constexpr uint32_t kPad = 1u << 10, kFail = 1u << 11;  // chain ends: incomplete code (padding) / EOS
+    const uint32_t TB = 8u * len;
+    uint32_t W = 0, opos = 0, flags = 0;
+    DecResult r;
+    r.ok = false;
+    for (;;) {
+        const uint32_t p = W + lane;
+        const uint32_t q = (p >> 5) * 4u;  // the aligned dword holding bit p; bits past the string are don't-care
+        const uint64_t x = (uint64_t)bswap32(*reinterpret_cast<const uint32_t*>(in + q)) << 32 |
+                           bswap32(*reinterpret_cast<const uint32_t*>(in + q + 4u));
+        const uint32_t w = (uint32_t)((x << (p & 31u)) >> 32);
+        const uint32_t R = p < TB ? TB - p : 0u;
+        const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+        uint32_t info, syms, fl;
+        if (e & kLong) {  // leading-ones table (as decode_core)
+            const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+            const uint32_t ki = T.kinfo[k];
+            const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+            const uint32_t L = (le >> 9) & 31u, sym = le & 0x1FFu;
+            info = L > R ? kPad : sym == kEos ? kFail : (L | 1u << 8);
+            syms = sym;
+            fl = (le >> 14) & 3u;
+        } else {
+            const uint32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+            const bool two = (e & kHas2) && L12 <= R;
+            info = L1 > R ? kPad : ((two ? L12 : L1) | (two ? 2u : 1u) << 8);
+            syms = e & 0xFFFFu;
+            fl = (e >> 24) & (two ? 15u : 3u);
+        }
+        // follow the chain through this round's candidates (scalar: c is wave-uniform)
+        uint64_t on = 0;
+        uint32_t c = 0, end = 0;
+        while (c < 64u) {
+            const uint32_t xi = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)c);
+            if (xi & (kPad | kFail)) {
+                end = xi & (kPad | kFail);
+                break;
+            }
+            on |= 1ull << c;
+            c += xi & 0xFFu;
+        }
+        const bool mine = ((on >> lane) & 1u) != 0u;
+        const uint32_t ns = mine ? (info >> 8) & 3u : 0u;
+        const uint32_t incl = wave_incl_scan(ns);
+        if (mine) {
+            out[opos + incl - ns] = (uint8_t)syms;
+            if (ns == 2u) out[opos + incl - 1u] = (uint8_t)(syms >> 8);
+            flags |= fl;
+        }
+        opos += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (end) {
+            // padding: at most 7 bits, all ones (mkhufftbl.py:374-381, hpack.c:132-133); EOS fails
+            const uint32_t wc = (uint32_t)__builtin_amdgcn_readlane((int)w, (int)c);
+            const uint32_t Rc = (uint32_t)__builtin_amdgcn_readlane((int)R, (int)c);
+            r.ok = end == kPad && Rc <= 7u && ((wc >> 24) | (0xFFu >> Rc)) == 0xFFu;
+            break;
+        }
+        W += c;
+    }
+    uint32_t fa = 0;  // OR over the wave (4 flag bits)
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b) fa |= __builtin_amdgcn_ballot_w64(((flags >> b) & 1u) != 0u) != 0 ? 1u << b : 0u;
+    flags = fa;
+    r.len = opos;
+    r.flags = (flags | (flags >> 2)) & 3u;
+    r.status = 0;
+    return r;
+}
+
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -2602,9 +2713,8 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
     __shared__ uint32_t s_kinfo[32];
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
     __shared__ __attribute__((aligned(16))) uint2 s_enc[256];
-    __shared__ __attribute__((aligned(16))) uint32_t s_in[kSvcMax / 4 + 16];  // [16 header words][input]
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[kSvcMax / 4 + 16 + 8];  // [16 header words][input][slack]
     __shared__ __attribute__((aligned(16))) uint8_t s_out[(kSvcMax * 8) / 5 + 64];
-    __shared__ uint32_t s_res[2];
     static_assert(64 + kSvcMax == 64 * 16, "one 16-B load per lane reads a mailbox's header and input");
     const uint32_t lane = threadIdx.x;
     load_dec_tables(s_lut, s_kinfo, s_ones, 64);
@@ -2624,51 +2734,53 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
             continue;  // each poll is a PCIe round trip already: no sleep between them
         }
         last = now;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the request's bytes were written before its counter
         while (pend) {
             const uint32_t s = (uint32_t)__builtin_ctzll(pend);
             pend &= pend - 1;
             SvcSlot* sl = slots + s;
             const uint32_t r = (uint32_t)__shfl((int)req, (int)s);
             const uint32_t t_seen = (uint32_t)now;
-            // header (16 words) and the whole input area in one round of 16-B loads: no wait on `len` first
-            const uint8_t* src = reinterpret_cast<const uint8_t*>(sl);
-            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_in) + 16u * lane) =
-                *reinterpret_cast<const uint4*>(src + 16u * lane);
-            __syncthreads();
+            // header (16 words) and the whole input area in one round of system-scope loads (they bypass the
+            // caches, so no acquire fence is needed: the request's bytes were written before its counter)
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(sl) + 4u * lane;
+            uint32_t v4[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j) v4[j] = sys_load(src + j);
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_in) + 16u * lane) = make_uint4(v4[0], v4[1], v4[2], v4[3]);
+            wave_lds_sync();
             const uint32_t t_data = (uint32_t)__builtin_amdgcn_s_memrealtime();
-            if (lane == 0) {
-                const uint32_t op = s_in[2], len = min(s_in[3], kSvcMax), is_name = s_in[4];
-                const LdsSource lsrc{s_in + 16, len ? ((len + 3u) & ~3u) - 4u : 0u};
-                LdsSink sink{s_out, 0u, 0u, (kSvcMax * 8) / 5 + 60};
-                uint32_t ol, st = 0;
-                if (op == 1u) {
-                    ol = encode_core(lsrc, 0u, len, sink, s_enc);
-                    st = ol == kFailLen ? kStatusFail : 0u;
-                } else {
-                    const DecResult d = decode_core(lsrc, 0u, len, sink, DecTables{s_lut, s_kinfo, s_ones});
-                    ol = d.ok ? d.len : kFailLen;
-                    st = d.ok ? soft_bits(is_name != 0, d.len, d.flags, d.len ? s_out[0] : 0u, d.len ? s_out[d.len - 1] : 0u)
-                              : kStatusFail;
-                }
-                s_res[0] = ol;
-                s_res[1] = st;
+            const uint32_t op = s_in[2], len = min(s_in[3], kSvcMax), is_name = s_in[4];
+            const uint8_t* in = reinterpret_cast<const uint8_t*>(s_in + 16);
+            uint32_t ol, st = 0;
+            if (op == 1u) {
+                ol = wave_encode(in, len, reinterpret_cast<uint32_t*>(s_out), s_enc, lane);
+                st = ol == kFailLen ? kStatusFail : 0u;
+                if (ol != kFailLen) ol = (ol + 7u) >> 3;
+            } else {
+                const DecResult d = wave_decode(in, len, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane);
+                wave_lds_sync();
+                ol = d.ok ? d.len : kFailLen;
+                st = d.ok ? soft_bits(is_name != 0, d.len, d.flags, d.len ? s_out[0] : 0u, d.len ? s_out[d.len - 1] : 0u)
+                          : kStatusFail;
             }
-            __syncthreads();
             const uint32_t t_coded = (uint32_t)__builtin_amdgcn_s_memrealtime();
-            const uint32_t ol = s_res[0];
             const uint32_t n = ol == kFailLen ? 0u : ol;
-            for (uint32_t k = 4u * lane; k < n; k += 256u)
-                *reinterpret_cast<uint32_t*>(sl->out + k) = *reinterpret_cast<const uint32_t*>(s_out + k);
-            if (lane == 0) {
-                sl->result = ol;
-                sl->status = s_res[1];
-                sl->t_seen = t_seen;
-                sl->t_data = t_data;
-                sl->t_coded = t_coded;
-                sl->t_out = (uint32_t)__builtin_amdgcn_s_memrealtime();
+            uint32_t* dst = reinterpret_cast<uint32_t*>(sl->out);
+            for (uint32_t k = lane; 4u * k < n; k += 64u) {  // encode's stage holds MSB-first words
+                const uint32_t wv = reinterpret_cast<const uint32_t*>(s_out)[k];
+                sys_store(dst + k, op == 1u ? bswap32(wv) : wv);
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the result before its counter
+            if (lane == 0) {
+                sys_store(&sl->result, ol);
+                sys_store(&sl->status, st);
+                sys_store(&sl->t_seen, t_seen);
+                sys_store(&sl->t_data, t_data);
+                sys_store(&sl->t_coded, t_coded);
+                sys_store(&sl->t_out, (uint32_t)__builtin_amdgcn_s_memrealtime());
+            }
+            // the result before its counter: the stores above are system-scope (write-through), so waiting
+            // for their completion orders them before `done` (no L2 write-back needed)
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) sys_store(&sl->done, r);
             if (lane == s) handled = r;
             __syncthreads();
