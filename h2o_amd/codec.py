@@ -88,6 +88,14 @@ def lib():
         L.hhuff_hpack_parse_requests.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp,
                                                  _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_uint64,
                                                  ctypes.c_uint, _vp]
+        L.hhuff_hpack_parse_responses.restype = ctypes.c_int
+        L.hhuff_hpack_parse_responses.argtypes = [_vp, ctypes.c_uint64, _vp, _vp, ctypes.c_uint32, ctypes.c_uint32, _vp,
+                                                  _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                                  ctypes.c_uint64, ctypes.c_uint, _vp]
+        L.hhuff_qpack_parse_responses.restype = ctypes.c_int
+        L.hhuff_qpack_parse_responses.argtypes = ([_vp, ctypes.c_uint64, _vp, _vp, _vp, _vp, ctypes.c_uint32,
+                                                   ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64] + [_vp] * 17 +
+                                                  [ctypes.c_uint64, ctypes.c_uint, _vp])
         L.hhuff_qpack_scratch_size.restype = ctypes.c_uint64
         L.hhuff_qpack_scratch_size.argtypes = [ctypes.c_uint32, ctypes.c_uint32]
         L.hhuff_qpack_decode.restype = ctypes.c_int
@@ -122,8 +130,8 @@ def lib():
 EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decode_batch", "hhuff_encode_batch",
             "hhuff_decode_batch_packed", "hhuff_encode_batch_packed",
             "hhuff_flatten_batch", "hhuff_decode_literals", "hhuff_hpack_decode_blocks", "hhuff_hpack_scratch_size",
-            "hhuff_hpack_parse_requests",
-            "hhuff_qpack_decode", "hhuff_qpack_parse_requests", "hhuff_qpack_scratch_size",
+            "hhuff_hpack_parse_requests", "hhuff_hpack_parse_responses",
+            "hhuff_qpack_decode", "hhuff_qpack_parse_requests", "hhuff_qpack_parse_responses", "hhuff_qpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string", "hhuff_per_string_calls",
             "hhuff_grid_size", "hhuff_pool_trim", "hhuff_service_stamps", "hhuff_hpack_enc_scratch_size",
@@ -326,15 +334,20 @@ BLK_CONTINUE = 1
 REQUEST_FIELDS = ("content_length", "method", "scheme", "authority", "path", "protocol", "expect", "exists_map",
                   "nheaders", "err", "scheme_kind")
 FIELD_HEADER = 0x4
+# include/hhuff.h hhuff_response_t: 4 words per block; hhuff_qpack_response_head_t: 40 bytes per section
+RESPONSE_FIELDS = ("status", "nheaders", "err", "datagram_flow_id")
+QRES_BYTES = 40
 
 
 def hpack_decode_blocks(data, blk_off, conn_first, table_size=4096, arena_off=None, in_size=None, stream=None,
-                        scratch=None, cont=False, requests=False):
+                        scratch=None, cont=False, requests=False, responses=False, trailers=None):
     """HPACK header blocks (include/hhuff.h hhuff_hpack_decode_blocks) on device tensors: blk_off / conn_first
     int32 tensors (u32 bits), arena_off int64.  Returns a dict of device tensors: arena, name_off, name_len,
     value_off, value_len, fflags (per field slot), nfields, bstatus (per block).  requests=True runs
     hhuff_hpack_parse_requests (h2o_hpack_parse_request per block) and adds req: int32 [nblk, 12], the
-    hhuff_request_t words (REQUEST_FIELDS; content_length is words 0-1)."""
+    hhuff_request_t words (REQUEST_FIELDS; content_length is words 0-1).  responses=True runs
+    hhuff_hpack_parse_responses (h2o_hpack_parse_response per block; trailers: uint8 tensor, nonzero for a
+    trailers block, or None) and adds res: int32 [nblk, 4], the hhuff_response_t words (RESPONSE_FIELDS)."""
     import torch
 
     dev = data.device
@@ -359,7 +372,11 @@ def hpack_decode_blocks(data, blk_off, conn_first, table_size=4096, arena_off=No
             _dp(r["name_off"]), _dp(r["name_len"]), _dp(r["value_off"]), _dp(r["value_len"]), _dp(r["fflags"]),
             _dp(r["nfields"]), _dp(r["bstatus"])]
     tail = [_dp(scratch), scratch.numel(), BLK_CONTINUE if cont else 0, _stream(stream)]
-    if requests:
+    if responses:
+        r["res"] = torch.empty((max(1, nblk), 4), dtype=torch.int32, device=dev)
+        _check(lib().hhuff_hpack_parse_responses(*args[:6], None if trailers is None else _dp(trailers), *args[6:],
+                                                 _dp(r["res"]), *tail), "hhuff_hpack_parse_responses")
+    elif requests:
         r["req"] = torch.empty((max(1, nblk), 12), dtype=torch.int32, device=dev)
         _check(lib().hhuff_hpack_parse_requests(*args, _dp(r["req"]), *tail), "hhuff_hpack_parse_requests")
     else:
@@ -376,7 +393,7 @@ QREQ_BYTES = 72  # sizeof(hhuff_qpack_request_t)
 
 def qpack_decode(data, enc_off, enc_len, sec_off, conn_first, nsec, header_table_size=4096, max_blocked=100,
                  num_blocked=None, arena_off=None, in_size=None, stream=None, scratch=None, cont=False, arena=None,
-                 stream_id=None):
+                 stream_id=None, responses=False):
     """QPACK decoder step (include/hhuff.h hhuff_qpack_decode) on device tensors: enc_off / enc_len (per
     connection), sec_off / conn_first / num_blocked int32 tensors (u32 bits), arena_off int64; nsec =
     conn_first[-1] as a host int.  Returns a dict of device tensors: arena, name_off, name_len, value_off,
@@ -384,7 +401,9 @@ def qpack_decode(data, enc_off, enc_len, sec_off, conn_first, nsec, header_table
     enc_consumed, insert_count (per connection), and the scratch holding the tables (pass it back with
     cont=True for the next step).  stream_id (int64 tensor, one per section): the HTTP/3 request step,
     hhuff_qpack_parse_requests (h2o_qpack_parse_request per section), plus "req": uint8 [nsec, 72] records
-    (hhuff_qpack_request_t)."""
+    (hhuff_qpack_request_t).  responses=True (with stream_id): the HTTP/3 client's step,
+    hhuff_qpack_parse_responses (h2o_qpack_parse_response per section), plus "res": uint8 [nsec, 40] records
+    (hhuff_qpack_response_head_t)."""
     import torch
 
     dev = data.device
@@ -412,6 +431,10 @@ def qpack_decode(data, enc_off, enc_len, sec_off, conn_first, nsec, header_table
     tail = [_dp(scratch), scratch.numel(), QPK_CONTINUE if cont else 0, _stream(stream)]
     if stream_id is None:
         _check(lib().hhuff_qpack_decode(*(args + tail)), "hhuff_qpack_decode")
+    elif responses:
+        r["res"] = torch.empty((max(1, nsec), QRES_BYTES), dtype=torch.uint8, device=dev)
+        _check(lib().hhuff_qpack_parse_responses(*(args + [_dp(stream_id), _dp(r["res"])] + tail)),
+               "hhuff_qpack_parse_responses")
     else:
         r["req"] = torch.empty((max(1, nsec), QREQ_BYTES), dtype=torch.uint8, device=dev)
         _check(lib().hhuff_qpack_parse_requests(*(args + [_dp(stream_id), _dp(r["req"])] + tail)),

@@ -75,7 +75,10 @@ struct BlkArgs {
     // per field slot: the byte sources of its name and value (read by the copy pass)
     uint64_t* fsrc_n;
     uint64_t* fsrc_v;
+    hhuff_response_t* res;   // response mode (hhuff_hpack_parse_responses): h2o_hpack_parse_response per block
+    const uint8_t* trailers;  // response mode: per block, nonzero = trailers (status == NULL); NULL = none
 };
+constexpr int kWalkPlain = 0, kWalkReq = 1, kWalkResp = 2;  // hpack_walk_kernel modes
 
 // Byte sources: kind in the top three bits, offset below.  All stay valid until the call's passes have run.
 constexpr uint64_t kSrcLit = 0;              // lit_out offset (a pre-decoded Huffman literal)
@@ -382,8 +385,9 @@ __device__ int32_t blk_field(const BlkArgs& A, const Win& W, DynTable& t, uint64
     return soft ? kErrInvalidChar : 0;
 }
 
-template <bool REQ>
+template <int MODE>
 __global__ __launch_bounds__(kBlkThreads) void hpack_walk_kernel(BlkArgs A) {
+    constexpr bool REQ = MODE == kWalkReq, RESP = MODE == kWalkResp;
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];  // literals decoded in place
     __shared__ uint32_t s_kinfo[32];
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
@@ -417,11 +421,14 @@ __global__ __launch_bounds__(kBlkThreads) void hpack_walk_kernel(BlkArgs A) {
         bool failed = s0.failed != 0;
         for (uint32_t b = A.conn_first[c]; b < A.conn_first[c + 1]; ++b) {
             ReqState rq;
+            RespState rs;
             if (REQ) rq.reset();
+            if (RESP) rs.reset(A.trailers != nullptr && A.trailers[b] != 0);
             if (failed) {
                 A.nfields[b] = 0;
                 A.bstatus[b] = kBlkSkipped;
                 if (REQ) req_store(A.req + b, rq);
+                if (RESP) resp_store(A.res + b, rs);
                 continue;
             }
             uint64_t p = A.blk_off[b];
@@ -431,19 +438,27 @@ __global__ __launch_bounds__(kBlkThreads) void hpack_walk_kernel(BlkArgs A) {
             const uint32_t slot = A.blk_off[b];
             uint32_t nf = 0;
             int32_t st = 0;
-            while (p != end) {
+            // h2o_hpack_parse_response: a head must hold :status (:652-655); it loops do-while, so an empty
+            // trailers block meets decode_header's end-of-input check (hpack.c:328-329)
+            if (RESP && p == end) {
+                if (!rs.trailers) rs.err = HHUFF_HERR_MISSING_PSEUDO;
+                st = rs.trailers ? kErrCompression : kErrProtocol;
+            }
+            while (st == 0 && p != end) {
                 FieldDesc F{0u, 0u, 0u, 0u, 0u, 0u, 0ull, 0ull};
-                const int32_t rc = blk_field(A, W, t, p, end, cur, aend, F, T, s_sent, s_scls, REQ);
+                const int32_t rc = blk_field(A, W, t, p, end, cur, aend, F, T, s_sent, s_scls, MODE != kWalkPlain);
                 if (rc != 0 && rc != kErrInvalidChar) {
                     st = rc;
-                    // h2o_hpack_parse_request: *err_desc = decode_err (:523-525) -- only the upper-case name
-                    // error carries one
+                    // h2o_hpack_parse_request / _response: *err_desc = decode_err (:523-525, :663-665) -- only
+                    // the upper-case name error carries one
                     if (REQ) rq.err = rc == kErrProtocol ? HHUFF_HERR_UPPER_CASE_NAME : HHUFF_HERR_NONE;
+                    if (RESP) rs.err = rc == kErrProtocol ? HHUFF_HERR_UPPER_CASE_NAME : HHUFF_HERR_NONE;
                     break;
                 }
                 bool header = false;
                 int32_t rr = 0;
                 if (REQ) rr = req_field(rq, F.cls, src_ptr(A, F.vsrc), F.vl, F.soft, (int32_t)nf, header);
+                if (RESP) rr = resp_field(rs, F.cls, src_ptr(A, F.vsrc), F.vl, F.soft, (int32_t)nf, header);
                 const uint32_t f = slot + nf;
                 A.name_off[f] = F.noff;
                 A.name_len[f] = F.nl;
@@ -461,6 +476,10 @@ __global__ __launch_bounds__(kBlkThreads) void hpack_walk_kernel(BlkArgs A) {
             if (REQ) {
                 if (st == 0 && rq.err != HHUFF_HERR_NONE) st = kErrInvalidChar;  // :636-637
                 req_store(A.req + b, rq);
+            }
+            if (RESP) {
+                if (st == 0 && rs.err != HHUFF_HERR_NONE) st = kErrInvalidChar;  // :745-747
+                resp_store(A.res + b, rs);
             }
             A.nfields[b] = nf;
             A.bstatus[b] = st;
@@ -694,11 +713,12 @@ hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32
                                uint32_t nconn, uint32_t table_size, uint8_t* arena, const uint64_t* arena_off,
                                uint32_t* name_off, uint32_t* name_len, uint32_t* value_off, uint32_t* value_len,
                                uint8_t* fflags, uint32_t* nfields, int32_t* bstatus, hhuff_request_t* req,
-                               uint8_t* scratch, uint32_t flags, hipStream_t stream) {
+                               hhuff_response_t* res, const uint8_t* trailers, uint8_t* scratch, uint32_t flags,
+                               hipStream_t stream) {
     if (nconn == 0) return hipSuccess;
     BlkArgs A{in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len, value_off,
               value_len, fflags, nfields, bstatus, scratch, hpack_conn_scratch(table_size), flags, req,
-              nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+              nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, res, trailers};
     // workspace (the library's stream-ordered pool): field sources for every slot (block byte);
     // with the literal pre-pass (inputs below 4 GiB: u32 positions) its bitmaps, word prefixes, chunk sums,
     // the literal list and results, and the decoded bytes
@@ -762,9 +782,11 @@ hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32
     if (e == hipSuccess) {
         const uint32_t blocks = min((nconn + kBlkThreads - 1u) / kBlkThreads, 65535u);
         if (req)
-            hipLaunchKernelGGL(hpack_walk_kernel<true>, dim3(blocks), dim3(kBlkThreads), 0, stream, A);
+            hipLaunchKernelGGL(hpack_walk_kernel<kWalkReq>, dim3(blocks), dim3(kBlkThreads), 0, stream, A);
+        else if (res)
+            hipLaunchKernelGGL(hpack_walk_kernel<kWalkResp>, dim3(blocks), dim3(kBlkThreads), 0, stream, A);
         else
-            hipLaunchKernelGGL(hpack_walk_kernel<false>, dim3(blocks), dim3(kBlkThreads), 0, stream, A);
+            hipLaunchKernelGGL(hpack_walk_kernel<kWalkPlain>, dim3(blocks), dim3(kBlkThreads), 0, stream, A);
         hipLaunchKernelGGL(blk_copy_kernel, dim3(4096), dim3(256), 0, stream, A);
         hipLaunchKernelGGL(blk_table_kernel, dim3((uint32_t)(((uint64_t)nconn + 3) / 4)), dim3(256), 0, stream, A);
         e = hipGetLastError();

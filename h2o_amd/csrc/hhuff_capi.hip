@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <immintrin.h>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -205,7 +206,8 @@ namespace {
 int hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off, const uint32_t* conn_first, uint32_t nconn,
                  uint32_t table_size, uint8_t* arena, const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len,
                  uint32_t* value_off, uint32_t* value_len, uint8_t* fflags, uint32_t* nfields, int32_t* bstatus,
-                 hhuff_request_t* req, void* scratch, uint64_t scratch_size, unsigned flags, void* stream) {
+                 hhuff_request_t* req, hhuff_response_t* res, const uint8_t* trailers, void* scratch,
+                 uint64_t scratch_size, unsigned flags, void* stream) {
     if (nconn == 0) return HHUFF_OK;
     if (!in || !blk_off || !conn_first || !arena || !arena_off || !name_off || !name_len || !value_off || !value_len ||
         !fflags || !nfields || !bstatus || !scratch)
@@ -213,8 +215,9 @@ int hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off, c
     if (scratch_size < hhuff_hpack_scratch_size(nconn, table_size)) return arg_fail("scratch smaller than hhuff_hpack_scratch_size");
     if (((uintptr_t)scratch & 15u) != 0) return arg_fail("scratch must be 16-byte aligned");
     if (((uintptr_t)req & 7u) != 0) return arg_fail("req must be 8-byte aligned");
+    if (((uintptr_t)res & 3u) != 0) return arg_fail("res must be 4-byte aligned");
     hipError_t e = hhuff::launch_hpack_blocks(in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off,
-                                              name_len, value_off, value_len, fflags, nfields, bstatus, req,
+                                              name_len, value_off, value_len, fflags, nfields, bstatus, req, res, trailers,
                                               (uint8_t*)scratch, flags, (hipStream_t)stream);
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "hpack block launch");
 }
@@ -227,7 +230,8 @@ HHUFF_API int hhuff_hpack_decode_blocks(const uint8_t* in, uint64_t in_size, con
                                         int32_t* bstatus, void* scratch, uint64_t scratch_size, unsigned flags,
                                         void* stream) {
     return hpack_blocks(in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len,
-                        value_off, value_len, fflags, nfields, bstatus, nullptr, scratch, scratch_size, flags, stream);
+                        value_off, value_len, fflags, nfields, bstatus, nullptr, nullptr, nullptr, scratch, scratch_size,
+                        flags, stream);
 }
 
 HHUFF_API int hhuff_hpack_parse_requests(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off,
@@ -238,7 +242,20 @@ HHUFF_API int hhuff_hpack_parse_requests(const uint8_t* in, uint64_t in_size, co
                                          unsigned flags, void* stream) {
     if (nconn != 0 && !req) return arg_fail("NULL array");
     return hpack_blocks(in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len,
-                        value_off, value_len, fflags, nfields, bstatus, req, scratch, scratch_size, flags, stream);
+                        value_off, value_len, fflags, nfields, bstatus, req, nullptr, nullptr, scratch, scratch_size,
+                        flags, stream);
+}
+
+HHUFF_API int hhuff_hpack_parse_responses(const uint8_t* in, uint64_t in_size, const uint32_t* blk_off,
+                                          const uint32_t* conn_first, uint32_t nconn, uint32_t table_size,
+                                          const uint8_t* trailers, uint8_t* arena, const uint64_t* arena_off,
+                                          uint32_t* name_off, uint32_t* name_len, uint32_t* value_off, uint32_t* value_len,
+                                          uint8_t* fflags, uint32_t* nfields, int32_t* bstatus, hhuff_response_t* res,
+                                          void* scratch, uint64_t scratch_size, unsigned flags, void* stream) {
+    if (nconn != 0 && !res) return arg_fail("NULL array");
+    return hpack_blocks(in, in_size, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len,
+                        value_off, value_len, fflags, nfields, bstatus, nullptr, res, trailers, scratch, scratch_size,
+                        flags, stream);
 }
 
 HHUFF_API uint64_t hhuff_hpack_enc_scratch_size(uint32_t nconn) { return (uint64_t)nconn * hhuff::hpenc_conn_scratch(); }
@@ -289,7 +306,8 @@ int qpack_step(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off, con
                const uint64_t* arena_off, uint32_t* name_off, uint32_t* name_len, uint32_t* value_off,
                uint32_t* value_len, uint8_t* fflags, uint32_t* nfields, int32_t* sstatus, uint64_t* req_insert_count,
                int32_t* enc_status, uint32_t* enc_consumed, uint64_t* insert_count, const uint64_t* stream_id,
-               hhuff_qpack_request_t* req, void* scratch, uint64_t scratch_size, unsigned flags, void* stream) {
+               hhuff_qpack_request_t* req, hhuff_qpack_response_head_t* res, void* scratch, uint64_t scratch_size,
+               unsigned flags, void* stream) {
     if (nconn == 0) return HHUFF_OK;
     if (!in || !enc_off || !enc_len || !sec_off || !conn_first || !enc_status || !enc_consumed || !insert_count ||
         !scratch)
@@ -307,7 +325,7 @@ int qpack_step(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off, con
                                        header_table_size, max_blocked, num_blocked, arena, arena_off, name_off, name_len,
                                        value_off, value_len, fflags, nfields, sstatus, req_insert_count, enc_status,
                                        enc_consumed, insert_count, (uint8_t*)scratch, flags, (hipStream_t)stream,
-                                       stream_id, req);
+                                       stream_id, req, res);
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "qpack launch");
 }
 }  // namespace
@@ -322,8 +340,8 @@ HHUFF_API int hhuff_qpack_decode(const uint8_t* in, uint64_t in_size, const uint
                                  unsigned flags, void* stream) {
     return qpack_step(in, in_size, enc_off, enc_len, sec_off, conn_first, nconn, nsec, header_table_size, max_blocked,
                       num_blocked, arena, arena_off, name_off, name_len, value_off, value_len, fflags, nfields, sstatus,
-                      req_insert_count, enc_status, enc_consumed, insert_count, nullptr, nullptr, scratch, scratch_size,
-                      flags, stream);
+                      req_insert_count, enc_status, enc_consumed, insert_count, nullptr, nullptr, nullptr, scratch,
+                      scratch_size, flags, stream);
 }
 
 HHUFF_API int hhuff_qpack_parse_requests(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off,
@@ -339,8 +357,25 @@ HHUFF_API int hhuff_qpack_parse_requests(const uint8_t* in, uint64_t in_size, co
     if (((uintptr_t)req & 7u) != 0) return arg_fail("req must be 8-byte aligned");
     return qpack_step(in, in_size, enc_off, enc_len, sec_off, conn_first, nconn, nsec, header_table_size, max_blocked,
                       num_blocked, arena, arena_off, name_off, name_len, value_off, value_len, fflags, nfields, sstatus,
-                      req_insert_count, enc_status, enc_consumed, insert_count, stream_id, req, scratch, scratch_size,
-                      flags, stream);
+                      req_insert_count, enc_status, enc_consumed, insert_count, stream_id, req, nullptr, scratch,
+                      scratch_size, flags, stream);
+}
+
+HHUFF_API int hhuff_qpack_parse_responses(const uint8_t* in, uint64_t in_size, const uint32_t* enc_off,
+                                          const uint32_t* enc_len, const uint32_t* sec_off, const uint32_t* conn_first,
+                                          uint32_t nconn, uint32_t nsec, uint32_t header_table_size, uint64_t max_blocked,
+                                          const uint32_t* num_blocked, uint8_t* arena, const uint64_t* arena_off,
+                                          uint32_t* name_off, uint32_t* name_len, uint32_t* value_off, uint32_t* value_len,
+                                          uint8_t* fflags, uint32_t* nfields, int32_t* sstatus, uint64_t* req_insert_count,
+                                          int32_t* enc_status, uint32_t* enc_consumed, uint64_t* insert_count,
+                                          const uint64_t* stream_id, hhuff_qpack_response_head_t* res, void* scratch,
+                                          uint64_t scratch_size, unsigned flags, void* stream) {
+    if (nconn != 0 && nsec != 0 && (!stream_id || !res)) return arg_fail("NULL array");
+    if (((uintptr_t)res & 7u) != 0) return arg_fail("res must be 8-byte aligned");
+    return qpack_step(in, in_size, enc_off, enc_len, sec_off, conn_first, nconn, nsec, header_table_size, max_blocked,
+                      num_blocked, arena, arena_off, name_off, name_len, value_off, value_len, fflags, nfields, sstatus,
+                      req_insert_count, enc_status, enc_consumed, insert_count, stream_id, nullptr, res, scratch,
+                      scratch_size, flags, stream);
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -447,12 +482,16 @@ int svc_call(int dev, bool encode, const uint8_t* src, size_t len, int is_name, 
     const int k = t_svc_slot;
     std::lock_guard<std::mutex> g(S.slot_mu[k]);
     hhuff::SvcSlot* sl = S.slots + k;
-    sl->op = encode ? 1u : 0u;
-    sl->len = (uint32_t)len;
-    sl->is_name = is_name ? 1u : 0u;
-    memcpy(sl->in, src, len);
     const uint32_t n = ++S.seq[k];
-    __atomic_store_n(&sl->req, n, __ATOMIC_RELEASE);
+    // chunks first, each one 16-B store {n, 12 bytes}; then the header, one 16-B store (see SvcSlot)
+    for (size_t i = 0; 12 * i < len; ++i) {
+        uint32_t w[4] = {n, 0u, 0u, 0u};
+        memcpy(&w[1], src + 12 * i, len - 12 * i < 12 ? len - 12 * i : 12);
+        _mm_store_si128(reinterpret_cast<__m128i*>(sl->chunk[i]), _mm_loadu_si128(reinterpret_cast<const __m128i*>(w)));
+    }
+    __atomic_thread_fence(__ATOMIC_RELEASE);
+    const uint32_t h[4] = {n, encode ? 1u : 0u, (uint32_t)len, is_name ? 1u : 0u};
+    _mm_store_si128(reinterpret_cast<__m128i*>(&sl->req), _mm_loadu_si128(reinterpret_cast<const __m128i*>(h)));
     // spin for the result.  While the wave is alive nothing else is done; a wave that is gone (idle exit,
     // or exiting just as this request arrived) is launched again -- checked every 64 spins, so a wave that
     // is still starting up is not launched twice (svc_kick sees its stream busy)

@@ -2628,74 +2628,101 @@ __device__ __forceinline__ uint32_t wave_encode(const uint8_t* in, uint32_t len,
     return bits;
 }
 
-// decode s_in bytes [0, len) into out (LDS bytes)
+// decode s_in bytes [0, len) into out (LDS bytes).  Two candidates per lane: bits W + lane and W + 64 + lane.
+struct WaveStep {  // the step that would start at one candidate bit
+    uint32_t nx;    // chain offset of the next step (offset + bits taken), or kStop
+    uint32_t syms;  // 1-2 symbol bytes
+    uint32_t ns;    // symbols (1-2; 0 at a chain end)
+    uint32_t fl;    // invalid-char flags (decode_core's)
+    uint32_t w, R;  // window at the candidate, string bits left there
+    bool eos;       // EOS symbol (a chain end that fails)
+};
+constexpr uint32_t kStop = 255u;
+__device__ __forceinline__ WaveStep wave_step(const uint8_t* in, uint32_t TB, uint32_t p, uint32_t off, const DecTables& T) {
+    WaveStep s;
+    const uint32_t q = (p >> 5) * 4u;  // the aligned dword holding bit p; bits past the string are don't-care
+    const uint64_t x = (uint64_t)bswap32(*reinterpret_cast<const uint32_t*>(in + q)) << 32 |
+                       bswap32(*reinterpret_cast<const uint32_t*>(in + q + 4u));
+    s.w = (uint32_t)((x << (p & 31u)) >> 32);
+    s.R = p < TB ? TB - p : 0u;
+    const uint32_t e = T.lut[s.w >> (32 - HHUFF_LUT_BITS)];
+    s.eos = false;
+    if (e & kLong) {  // leading-ones table (as decode_core)
+        const uint32_t k = min((uint32_t)__builtin_clz(~s.w | 1u), 30u);
+        const uint32_t ki = T.kinfo[k];
+        const uint32_t le = T.ones[(ki & 0xFFFFu) + (((s.w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+        const uint32_t L = (le >> 9) & 31u, sym = le & 0x1FFu;
+        const bool stop = L > s.R || sym == kEos;
+        s.eos = L <= s.R && sym == kEos;
+        s.nx = stop ? kStop : off + L;
+        s.ns = stop ? 0u : 1u;
+        s.syms = sym;
+        s.fl = (le >> 14) & 3u;
+    } else {
+        const uint32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+        const bool two = (e & kHas2) && L12 <= s.R;
+        const bool stop = L1 > s.R;
+        s.nx = stop ? kStop : off + (two ? L12 : L1);
+        s.ns = stop ? 0u : (two ? 2u : 1u);
+        s.syms = e & 0xFFFFu;
+        s.fl = (e >> 24) & (two ? 15u : 3u);
+    }
+    return s;
+}
 __device__ __forceinline__ DecResult wave_decode(const uint8_t* in, uint32_t len, uint8_t* out, const DecTables& T,
                                                  uint32_t lane) {
-    constexpr uint32_t kPad = 1u << 10, kFail = 1u << 11;  // chain ends: incomplete code (padding) / EOS
     const uint32_t TB = 8u * len;
     uint32_t W = 0, opos = 0, flags = 0;
     DecResult r;
     r.ok = false;
     for (;;) {
-        const uint32_t p = W + lane;
-        const uint32_t q = (p >> 5) * 4u;  // the aligned dword holding bit p; bits past the string are don't-care
-        const uint64_t x = (uint64_t)bswap32(*reinterpret_cast<const uint32_t*>(in + q)) << 32 |
-                           bswap32(*reinterpret_cast<const uint32_t*>(in + q + 4u));
-        const uint32_t w = (uint32_t)((x << (p & 31u)) >> 32);
-        const uint32_t R = p < TB ? TB - p : 0u;
-        const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
-        uint32_t info, syms, fl;
-        if (e & kLong) {  // leading-ones table (as decode_core)
-            const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
-            const uint32_t ki = T.kinfo[k];
-            const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
-            const uint32_t L = (le >> 9) & 31u, sym = le & 0x1FFu;
-            info = L > R ? kPad : sym == kEos ? kFail : (L | 1u << 8);
-            syms = sym;
-            fl = (le >> 14) & 3u;
-        } else {
-            const uint32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
-            const bool two = (e & kHas2) && L12 <= R;
-            info = L1 > R ? kPad : ((two ? L12 : L1) | (two ? 2u : 1u) << 8);
-            syms = e & 0xFFFFu;
-            fl = (e >> 24) & (two ? 15u : 3u);
-        }
-        // follow the chain through this round's candidates (scalar: c is wave-uniform)
-        uint64_t on = 0;
-        uint32_t c = 0, end = 0;
-        while (c < 64u) {
-            const uint32_t xi = (uint32_t)__builtin_amdgcn_readlane((int)info, (int)c);
-            if (xi & (kPad | kFail)) {
-                end = xi & (kPad | kFail);
+        const WaveStep a = wave_step(in, TB, W + lane, lane, T), b = wave_step(in, TB, W + 64u + lane, 64u + lane, T);
+        // follow the chain through this round's 128 candidates (scalar: c is wave-uniform)
+        uint64_t on0 = 0, on1 = 0;
+        uint32_t c = 0;
+        bool end = false;
+        while (c < 128u) {
+            const uint32_t nx = c < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)a.nx, (int)c)
+                                        : (uint32_t)__builtin_amdgcn_readlane((int)b.nx, (int)(c - 64u));
+            if (nx == kStop) {
+                end = true;
                 break;
             }
-            on |= 1ull << c;
-            c += xi & 0xFFu;
+            if (c < 64u) on0 |= 1ull << c;
+            else on1 |= 1ull << (c - 64u);
+            c = nx;
         }
-        const bool mine = ((on >> lane) & 1u) != 0u;
-        const uint32_t ns = mine ? (info >> 8) & 3u : 0u;
-        const uint32_t incl = wave_incl_scan(ns);
-        if (mine) {
-            out[opos + incl - ns] = (uint8_t)syms;
-            if (ns == 2u) out[opos + incl - 1u] = (uint8_t)(syms >> 8);
-            flags |= fl;
+        const uint32_t n0 = ((on0 >> lane) & 1u) ? a.ns : 0u, n1 = ((on1 >> lane) & 1u) ? b.ns : 0u;
+        const uint32_t i0 = wave_incl_scan(n0), i1 = wave_incl_scan(n1);
+        const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
+        if (n0) {
+            out[opos + i0 - n0] = (uint8_t)a.syms;
+            if (n0 == 2u) out[opos + i0 - 1u] = (uint8_t)(a.syms >> 8);
+            flags |= a.fl;
         }
-        opos += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        if (n1) {
+            out[opos + t0 + i1 - n1] = (uint8_t)b.syms;
+            if (n1 == 2u) out[opos + t0 + i1 - 1u] = (uint8_t)(b.syms >> 8);
+            flags |= b.fl;
+        }
+        opos += t0 + (uint32_t)__builtin_amdgcn_readlane((int)i1, 63);
         if (end) {
-            // padding: at most 7 bits, all ones (mkhufftbl.py:374-381, hpack.c:132-133); EOS fails
-            const uint32_t wc = (uint32_t)__builtin_amdgcn_readlane((int)w, (int)c);
-            const uint32_t Rc = (uint32_t)__builtin_amdgcn_readlane((int)R, (int)c);
-            r.ok = end == kPad && Rc <= 7u && ((wc >> 24) | (0xFFu >> Rc)) == 0xFFu;
+            // padding: at most 7 bits, all ones (mkhufftbl.py:374-381, hpack.c:132-133); EOS fails (hpack.c:88-89)
+            const bool lo = c < 64u;
+            const uint32_t cl = lo ? c : c - 64u;
+            const uint32_t wc = (uint32_t)__builtin_amdgcn_readlane((int)(lo ? a.w : b.w), (int)cl);
+            const uint32_t Rc = (uint32_t)__builtin_amdgcn_readlane((int)(lo ? a.R : b.R), (int)cl);
+            const uint32_t ec = (uint32_t)__builtin_amdgcn_readlane((int)((lo ? a.eos : b.eos) ? 1u : 0u), (int)cl);
+            r.ok = ec == 0u && Rc <= 7u && ((wc >> 24) | (0xFFu >> Rc)) == 0xFFu;
             break;
         }
         W += c;
     }
     uint32_t fa = 0;  // OR over the wave (4 flag bits)
 #pragma unroll
-    for (uint32_t b = 0; b < 4; ++b) fa |= __builtin_amdgcn_ballot_w64(((flags >> b) & 1u) != 0u) != 0 ? 1u << b : 0u;
-    flags = fa;
+    for (uint32_t k = 0; k < 4; ++k) fa |= __builtin_amdgcn_ballot_w64(((flags >> k) & 1u) != 0u) != 0 ? 1u << k : 0u;
     r.len = opos;
-    r.flags = (flags | (flags >> 2)) & 3u;
+    r.flags = (fa | (fa >> 2)) & 3u;
     r.status = 0;
     return r;
 }
@@ -2707,15 +2734,25 @@ __device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// two 16-B system-scope loads (each is seen whole: old or new, see SvcSlot), waited for here
+__device__ __forceinline__ void sys_load16x2(const void* pa, const void* pb, uint4& a, uint4& b) {
+    __asm__ volatile(
+        "global_load_dwordx4 %0, %2, off sc0 sc1\n\t"
+        "global_load_dwordx4 %1, %3, off sc0 sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(a), "=&v"(b)
+        : "v"(pa), "v"(pb)
+        : "memory");
+}
+
 __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
                                                      uint64_t idle_ticks, uint64_t max_ticks) {
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
     __shared__ uint32_t s_kinfo[32];
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
     __shared__ __attribute__((aligned(16))) uint2 s_enc[256];
-    __shared__ __attribute__((aligned(16))) uint32_t s_in[kSvcMax / 4 + 16 + 8];  // [16 header words][input][slack]
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[kSvcMax / 4 + 8];  // [input][slack]
     __shared__ __attribute__((aligned(16))) uint8_t s_out[(kSvcMax * 8) / 5 + 64];
-    static_assert(64 + kSvcMax == 64 * 16, "one 16-B load per lane reads a mailbox's header and input");
     const uint32_t lane = threadIdx.x;
     load_dec_tables(s_lut, s_kinfo, s_ones, 64);
     for (uint32_t k = lane; k < 256; k += 64) s_enc[k] = make_uint2(g_enc_code[k], g_enc_nbits[k]);
@@ -2724,33 +2761,50 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
     uint32_t handled = sys_load(&slots[lane].done);  // lane l keeps slot l's last served request
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t last = t0;
+    uint32_t hot = 0, polls = 0;  // hot: the mailbox served last, whose chunks every poll reads too
     for (;;) {
-        const uint32_t req = sys_load(&slots[lane].req);
+        // one round: lane l reads mailbox l's header and chunk l of the hot mailbox
+        uint4 hdr, ck;
+        sys_load16x2(&slots[lane].req, slots[hot].chunk[lane], hdr, ck);
+        const uint32_t req = hdr.x;
         uint64_t pend = __builtin_amdgcn_ballot_w64(req != handled);
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         if (pend == 0) {
-            const uint32_t stop = sys_load(&ctrl->stop);
-            if (stop != 0 || now - last > idle_ticks || now - t0 > max_ticks) break;
+            if ((++polls & 15u) == 0u) {  // the stop flag costs a round trip of its own: every 16th poll
+                const uint32_t stop = sys_load(&ctrl->stop);
+                if (stop != 0) break;
+            }
+            if (now - last > idle_ticks || now - t0 > max_ticks) break;
             continue;  // each poll is a PCIe round trip already: no sleep between them
         }
         last = now;
+        int ck_slot = (int)hot;  // the mailbox whose chunks `ck` holds
         while (pend) {
             const uint32_t s = (uint32_t)__builtin_ctzll(pend);
             pend &= pend - 1;
             SvcSlot* sl = slots + s;
             const uint32_t r = (uint32_t)__shfl((int)req, (int)s);
+            const uint32_t op = (uint32_t)__shfl((int)hdr.y, (int)s);
+            const uint32_t len = min((uint32_t)__shfl((int)hdr.z, (int)s), kSvcMax);
+            const uint32_t is_name = (uint32_t)__shfl((int)hdr.w, (int)s);
             const uint32_t t_seen = (uint32_t)now;
-            // header (16 words) and the whole input area in one round of system-scope loads (they bypass the
-            // caches, so no acquire fence is needed: the request's bytes were written before its counter)
-            const uint32_t* src = reinterpret_cast<const uint32_t*>(sl) + 4u * lane;
-            uint32_t v4[4];
-#pragma unroll
-            for (uint32_t j = 0; j < 4; ++j) v4[j] = sys_load(src + j);
-            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_in) + 16u * lane) = make_uint4(v4[0], v4[1], v4[2], v4[3]);
+            const bool need = 12u * lane < len;
+            // the chunks read with the headers serve if every one needed carries this request's number;
+            // else read them now: the header was stored after them, so this read sees them all
+            if ((int)s != ck_slot || __builtin_amdgcn_ballot_w64(need && ck.x != r) != 0) {
+                uint4 unused;
+                sys_load16x2(sl->chunk[lane], &sl->req, ck, unused);
+            }
+            ck_slot = -1;
+            if (need) {
+                uint32_t* d = s_in + 3u * lane;
+                d[0] = ck.y;
+                d[1] = ck.z;
+                d[2] = ck.w;
+            }
             wave_lds_sync();
             const uint32_t t_data = (uint32_t)__builtin_amdgcn_s_memrealtime();
-            const uint32_t op = s_in[2], len = min(s_in[3], kSvcMax), is_name = s_in[4];
-            const uint8_t* in = reinterpret_cast<const uint8_t*>(s_in + 16);
+            const uint8_t* in = reinterpret_cast<const uint8_t*>(s_in);
             uint32_t ol, st = 0;
             if (op == 1u) {
                 ol = wave_encode(in, len, reinterpret_cast<uint32_t*>(s_out), s_enc, lane);
@@ -2783,7 +2837,8 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
             __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
             if (lane == 0) sys_store(&sl->done, r);
             if (lane == s) handled = r;
-            __syncthreads();
+            hot = s;
+            wave_lds_sync();
         }
     }
     if (lane == 0) {

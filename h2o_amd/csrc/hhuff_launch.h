@@ -20,17 +20,23 @@ hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, b
 // device-visible, coherent host memory and codes each posted string in place; it exits when `stop` is set,
 // after idle_ticks of the 100 MHz real-time counter without a request, or after max_ticks in all.
 constexpr uint32_t kSvcSlots = 64;
-constexpr uint32_t kSvcMax = 960;  // longest string a mailbox takes (longer ones: launch_one / batch kernels);
-                                   // header + input = 1 KiB: one round of the wave's 16-B loads
-struct alignas(16) SvcSlot {       // one mailbox (host writes req after the request; device writes done after the result)
-    uint32_t req, done, op, len;   // op: 0 decode, 1 encode
-    uint32_t is_name, result, status, pad;
+constexpr uint32_t kSvcMax = 768;  // longest string a mailbox takes (longer ones: launch_one / batch kernels):
+                                   // 64 chunks of 12 input bytes, one 16-B load per lane
+// One mailbox.  The host writes the input as 16-B chunks {request number, 12 bytes} with single 16-B stores,
+// then the header {req, op, len, is_name} as one 16-B store.  A device load of a chunk sees it whole, old or
+// new, so a chunk is current iff it carries the request number: the service wave can read the data of the
+// mailbox it served last in the same round as the headers it polls, and use it when every chunk it needs
+// is current (else it reads the chunks again, after the header -- then they are all current).
+struct alignas(16) SvcSlot {
+    uint32_t req, op, len, is_name;       // host, one 16-B store after the chunks; op: 0 decode, 1 encode
+    uint32_t done, result, status, pad;   // device: done after the result
     uint32_t t_seen, t_data, t_coded, t_out;  // the wave's real-time stamps (100 MHz, low 32 bits): profiling
     uint32_t pad2[4];
-    uint8_t in[kSvcMax];
-    uint8_t out[1600];  // >= floor(8 kSvcMax / 5) + 60
+    uint32_t chunk[64][4];                // {req, input bytes [12 i, 12 i + 12)}
+    uint8_t out[1600];                    // >= floor(8 kSvcMax / 5) + 60
 };
-static_assert(sizeof(SvcSlot) % 16 == 0 && sizeof(SvcSlot) == 1024 + 1600, "mailbox layout");
+static_assert(sizeof(SvcSlot) % 16 == 0 && sizeof(SvcSlot) == 64 + 1024 + 1600, "mailbox layout");
+static_assert(12 * 64 == kSvcMax && (kSvcMax * 8) / 5 + 60 <= 1600, "mailbox sizes");
 struct SvcCtrl {
     uint32_t stop, alive, pad[2];
 };
@@ -94,7 +100,8 @@ hipError_t launch_hpack_blocks(const uint8_t* in, uint64_t in_size, const uint32
                                uint32_t nconn, uint32_t table_size, uint8_t* arena, const uint64_t* arena_off,
                                uint32_t* name_off, uint32_t* name_len, uint32_t* value_off, uint32_t* value_len,
                                uint8_t* fflags, uint32_t* nfields, int32_t* bstatus, hhuff_request_t* req,
-                               uint8_t* scratch, uint32_t flags, hipStream_t stream);
+                               hhuff_response_t* res, const uint8_t* trailers, uint8_t* scratch, uint32_t flags,
+                               hipStream_t stream);
 // QPACK decoder (f4): see include/hhuff.h hhuff_qpack_decode; scratch = nconn x
 // qpack_conn_scratch(header_table_size) bytes of device memory
 uint64_t qpack_conn_scratch(uint32_t header_table_size);
@@ -105,6 +112,6 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
                         uint32_t* value_len, uint8_t* fflags, uint32_t* nfields, int32_t* sstatus,
                         uint64_t* req_insert_count, int32_t* enc_status, uint32_t* enc_consumed, uint64_t* insert_count,
                         uint8_t* scratch, uint32_t flags, hipStream_t stream, const uint64_t* stream_id = nullptr,
-                        hhuff_qpack_request_t* qreq = nullptr);
+                        hhuff_qpack_request_t* qreq = nullptr, hhuff_qpack_response_head_t* qres = nullptr);
 int grid_size(int device, int which);
 }  // namespace hhuff

@@ -90,6 +90,8 @@ struct QpkArgs {
     // h2o_qpack_parse_request mode (hhuff_qpack_parse_requests): per section its stream id and record
     const uint64_t* stream_id;
     hhuff_qpack_request_t* qreq;
+    // h2o_qpack_parse_response mode (hhuff_qpack_parse_responses): per section its record (and stream_id)
+    hhuff_qpack_response_head_t* qres;
 };
 
 // Byte sources of table entries and field strings: kind in the top 3 bits, offset below.  Every source stays
@@ -717,11 +719,36 @@ __device__ __noinline__ int32_t req_field_h3(ReqState& r, uint32_t cls, const ui
     return req_field<true>(r, cls, value, vl, soft, k, header);
 }
 
+__device__ __noinline__ int32_t resp_field_h3(RespState& r, uint32_t cls, const uint8_t* value, uint32_t vl, uint32_t soft,
+                                              int32_t k, bool& header) {
+    return resp_field<true>(r, cls, value, vl, soft, k, header);
+}
+
+// h2o_qpack_parse_response's record: the Section Acknowledgment only after a clean parse (qpack.c:876-881)
+__device__ __forceinline__ void q_res_store(hhuff_qpack_response_head_t* out, const RespState& r, int32_t st, uint64_t ric,
+                                            uint64_t stream_id) {
+    resp_store(&out->res, r);
+    uint8_t ack[16] = {};
+    const uint32_t n = (st == 0 && ric != 0) ? q_header_ack(stream_id, ack) : 0u;
+    out->ack_len = n;
+    out->reserved = 0u;
+    uint2* a2 = reinterpret_cast<uint2*>(out->ack);
+    uint32_t w[4];
+    __builtin_memcpy(w, ack, 16);
+    a2[0] = make_uint2(w[0], w[1]);
+    a2[1] = make_uint2(w[2], w[3]);
+}
+
+constexpr int kSecPlain = 0, kSecReq = 1, kSecResp = 2;  // qpack_sections_kernel modes
+
 // REQ: h2o_qpack_parse_request (qpack.c:830-858) -- each field also runs h2o_hpack_parse_request's rules
 // (hhuff_request.h, the HTTP/3 arguments of lib/http3/server.c:1540-1545), a rule's hard error is
-// normalised to DECOMPRESSION_FAILED (:852-853), and the record gets the Section Acknowledgment (:856)
-template <bool REQ>
+// normalised to DECOMPRESSION_FAILED (:852-853), and the record gets the Section Acknowledgment (:856).
+// RESP: h2o_qpack_parse_response (:860-882) as lib/common/http3client.c:542 calls it -- a response head,
+// h2o_hpack_parse_response's rules (a status and a datagram-flow-id out-parameter), the same normalisation
+template <int MODE>
 __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
+    constexpr bool REQ = MODE == kSecReq, RESP = MODE == kSecResp;
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
     __shared__ uint32_t s_kinfo[32];
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
@@ -745,10 +772,13 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
         A.nfields[k] = 0;
         A.req_insert_count[k] = 0;
         ReqState rq;
+        RespState rs;
         if (REQ) rq.reset();
+        if (RESP) rs.reset(false);
         if (t.s.failed) {
             A.sstatus[k] = HHUFF_QPK_SKIPPED;
             if (REQ) q_req_store(A.qreq + k, rq, HHUFF_QPK_SKIPPED, 0u, 0u);
+            if (RESP) q_res_store(A.qres + k, rs, HHUFF_QPK_SKIPPED, 0u, 0u);
             continue;
         }
         uint64_t p = A.sec_off[k];
@@ -764,6 +794,10 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
         QArena R{A.arena, A.arena_off[k], min(A.arena_off[k + 1], kArenaLimit)};  // field offsets are u32
         const uint32_t slot = A.sec_off[k];
         uint32_t nf = 0;
+        if (RESP && st == 0 && p == end) {  // a head without fields: missing :status (hpack.c:652-655), normalised
+            rs.err = HHUFF_HERR_MISSING_PSEUDO;
+            st = kDF;
+        }
         while (st == 0 && p != end) {
             uint32_t no = 0, nl = 0, vo = 0, vl = 0, soft = 0;
             uint64_t fn = 0, fv = 0;
@@ -772,14 +806,16 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
                 st = rc;
                 // h2o_hpack_parse_request: *err_desc = decode_err (hpack.c:523-525)
                 if (REQ) rq.err = rc == HHUFF_QPK_ARENA ? HHUFF_HERR_NONE : HHUFF_HERR_DECODE;
+                if (RESP) rs.err = rc == HHUFF_QPK_ARENA ? HHUFF_HERR_NONE : HHUFF_HERR_DECODE;
                 break;
             }
             bool header = false;
             int32_t rr = 0;
-            if (REQ) {  // the bytes where they lie: a source (fn / fv), or the arena (decoded in place)
+            if (REQ || RESP) {  // the bytes where they lie: a source (fn / fv), or the arena (decoded in place)
                 const uint8_t* np = fn ? reinterpret_cast<const uint8_t*>(fn) : A.arena + no;
                 const uint8_t* vp = fv ? reinterpret_cast<const uint8_t*>(fv) : A.arena + vo;
-                rr = req_field_h3(rq, req_name_class(np, nl), vp, vl, soft, (int32_t)nf, header);
+                if (REQ) rr = req_field_h3(rq, req_name_class(np, nl), vp, vl, soft, (int32_t)nf, header);
+                if (RESP) rr = resp_field_h3(rs, req_name_class(np, nl), vp, vl, soft, (int32_t)nf, header);
             }
             A.fsrc_n[slot + nf] = fn;
             A.fsrc_v[slot + nf] = fv;
@@ -797,6 +833,10 @@ __global__ __launch_bounds__(256) void qpack_sections_kernel(QpkArgs A) {
         if (REQ) {
             if (st == 0 && rq.err != HHUFF_HERR_NONE) st = kErrInvalidChar;  // hpack.c:636-637
             q_req_store(A.qreq + k, rq, st, (uint64_t)ctx.ric, A.stream_id[k]);
+        }
+        if (RESP) {
+            if (st == 0 && rs.err != HHUFF_HERR_NONE) st = kErrInvalidChar;  // hpack.c:745-747
+            q_res_store(A.qres + k, rs, st, (uint64_t)ctx.ric, A.stream_id[k]);
         }
         A.nfields[k] = nf;
         A.sstatus[k] = st;
@@ -918,12 +958,12 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
                         uint32_t* value_len, uint8_t* fflags, uint32_t* nfields, int32_t* sstatus,
                         uint64_t* req_insert_count, int32_t* enc_status, uint32_t* enc_consumed, uint64_t* insert_count,
                         uint8_t* scratch, uint32_t flags, hipStream_t stream, const uint64_t* stream_id,
-                        hhuff_qpack_request_t* qreq) {
+                        hhuff_qpack_request_t* qreq, hhuff_qpack_response_head_t* qres) {
     if (nconn == 0) return hipSuccess;
     QpkArgs A{in, in_size, enc_off, enc_len, sec_off, conn_first, num_blocked, nconn, nsec, header_table_size,
               max_blocked, arena, arena_off, name_off, name_len, value_off, value_len, fflags, nfields, sstatus,
               req_insert_count, enc_status, enc_consumed, insert_count, scratch, qpack_conn_scratch(header_table_size),
-              flags, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream_id, qreq};
+              flags, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream_id, qreq, qres};
     // workspace: the literal pre-pass's bitmaps, word prefixes, chunk sums, the literal list with each
     // literal's prefix, the literal kernels' results and decoded bytes (positions are u32: in_size < 2^32,
     // checked by the C ABI), and the field slots' byte sources
@@ -980,10 +1020,12 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
         e = hipGetLastError();
     }
     if (e == hipSuccess && nsec != 0) {
-        if (qreq)
-            hipLaunchKernelGGL(qpack_sections_kernel<true>, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
+        if (qres)
+            hipLaunchKernelGGL(qpack_sections_kernel<kSecResp>, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
+        else if (qreq)
+            hipLaunchKernelGGL(qpack_sections_kernel<kSecReq>, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);
         else
-            hipLaunchKernelGGL(qpack_sections_kernel<false>, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0,
+            hipLaunchKernelGGL(qpack_sections_kernel<kSecPlain>, dim3(std::min((nsec + 255u) / 256u, 65535u)), dim3(256), 0,
                                stream, A);
         hipLaunchKernelGGL(qpack_copy_kernel, dim3(std::min((nsec + 255u) / 256u, 4096u)), dim3(256), 0, stream, A);
         hipLaunchKernelGGL(qpack_blocked_kernel, dim3(std::min((nconn + 255u) / 256u, 65535u)), dim3(256), 0, stream, A);

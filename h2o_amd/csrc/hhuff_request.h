@@ -1,6 +1,7 @@
-// h2o_hpack_parse_request's rules (lib/http2/hpack.c:502-637) on the GPU, shared by the HPACK block walk
-// (hhuff_blocks.hip, as lib/http2/connection.c:626-629 calls it) and the QPACK sections (hhuff_qpack.hip, as
-// h2o_qpack_parse_request calls it for HTTP/3, lib/http3/qpack.c:848).
+// h2o_hpack_parse_request's rules (lib/http2/hpack.c:502-637) and h2o_hpack_parse_response's
+// (:642-750) on the GPU, shared by the HPACK block walk (hhuff_blocks.hip, as lib/http2/connection.c:626-629
+// and lib/common/http2client.c:332, :421 call them) and the QPACK sections (hhuff_qpack.hip, as
+// h2o_qpack_parse_request / h2o_qpack_parse_response call them for HTTP/3, lib/http3/qpack.c:848, :876).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,7 +26,8 @@ enum : uint32_t {
     kNPath,            // H2O_TOKEN_PATH
     kNProtocol,        // H2O_TOKEN_PROTOCOL
     kNScheme,          // H2O_TOKEN_SCHEME
-    kNPseudoOther,     // ':' + anything else (:status included)
+    kNStatus,          // H2O_TOKEN_STATUS (an unknown pseudo-header to the request rules)
+    kNPseudoOther,     // ':' + anything else
     kNContentLength,   // the is_hpack_special tokens (lib/common/token_table.h, 5th flag)
     kNExpect,
     kNHost,
@@ -45,7 +47,11 @@ __device__ uint32_t req_name_class(const uint8_t* s, uint32_t n) {
     if (n != 0 && s[0] == ':') {
         switch (n) {
             case 5: return bytes_eq(s, ":path", 5) ? kNPath : kNPseudoOther;
-            case 7: return bytes_eq(s, ":method", 7) ? kNMethod : bytes_eq(s, ":scheme", 7) ? kNScheme : kNPseudoOther;
+            case 7:
+                return bytes_eq(s, ":method", 7)   ? kNMethod
+                       : bytes_eq(s, ":scheme", 7) ? kNScheme
+                       : bytes_eq(s, ":status", 7) ? kNStatus
+                                                   : kNPseudoOther;
             case 9: return bytes_eq(s, ":protocol", 9) ? kNProtocol : kNPseudoOther;
             case 10: return bytes_eq(s, ":authority", 10) ? kNAuthority : kNPseudoOther;
             default: return kNPseudoOther;
@@ -197,6 +203,85 @@ __device__ int32_t req_field(ReqState& r, uint32_t cls, const uint8_t* value, ui
         r.err = HHUFF_HERR_HEADERS_TOO_LONG;
     }
     return 0;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// h2o_hpack_parse_response's rules (hpack.c:642-750): a response head (status != NULL) or trailers
+// (status == NULL, http2client.c:421).  H3: the datagram flow id out-parameter h2o's HTTP/3 client passes
+// (lib/common/http3client.c:542); HTTP/2 passes NULL (http2client.c:332).
+// ---------------------------------------------------------------------------------------------------
+struct RespState {
+    int32_t status, dfid;
+    uint32_t nheaders, err, ndecoded;
+    bool trailers;
+    __device__ void reset(bool tr) {
+        status = 0;
+        dfid = -1;
+        nheaders = err = ndecoded = 0;
+        trailers = tr;
+    }
+};
+
+template <bool H3 = false>
+__device__ int32_t resp_field(RespState& r, uint32_t cls, const uint8_t* value, uint32_t vl, uint32_t soft, int32_t k,
+                              bool& header) {
+    header = false;
+    if (soft != 0 && r.err == HHUFF_HERR_NONE) r.err = (soft & 1u) ? HHUFF_HERR_SOFT_NAME : HHUFF_HERR_SOFT_VALUE;
+    if (++r.ndecoded > kMaxHeadersHard) {  // :668-671
+        r.err = HHUFF_HERR_HEADERS_TOO_LONG;
+        return kReqErrCompression;
+    }
+    if (cls >= kNAuthority && cls <= kNPseudoOther) {  // name->base[0] == ':' (:672-704)
+        if (r.trailers || cls != kNStatus || r.status != 0 || vl != 3) {
+            r.err = HHUFF_HERR_INVALID_PSEUDO;
+            return kReqErrProtocol;
+        }
+        // PARSE_DIGIT(100, 1), (10, 0), (1, 0): a digit is added to *status before the next one is checked
+        const uint32_t mul[3] = {100u, 10u, 1u};
+        for (uint32_t i = 0; i < 3; ++i) {
+            const uint32_t d = (uint32_t)value[i] - '0';
+            if (d > 9u || (i == 0 && d == 0u)) {
+                r.err = HHUFF_HERR_INVALID_PSEUDO;
+                return kReqErrProtocol;
+            }
+            r.status += (int32_t)(d * mul[i]);
+        }
+        return 0;
+    }
+    if (!r.trailers && r.status == 0) {  // :706-709
+        r.err = HHUFF_HERR_MISSING_PSEUDO;
+        return kReqErrProtocol;
+    }
+    switch (cls) {  // the is_hpack_special tokens (:712-725)
+        case kNContentLength:
+        case kNCacheDigest:
+        case kNHost:
+            break;  // passed through
+        case kNDatagramFlowId:
+            if (H3) r.dfid = k;
+            return 0;  // goto Next: not listed
+        case kNExpect:
+        case kNTe:
+        case kNConnSpecific:
+            r.err = HHUFF_HERR_CONNECTION_SPECIFIC;
+            return kReqErrProtocol;
+        default:
+            break;
+    }
+    if (r.nheaders < kMaxHeaders) {  // :726-738
+        ++r.nheaders;
+        header = true;
+    } else if (r.err == HHUFF_HERR_NONE) {
+        r.err = HHUFF_HERR_HEADERS_TOO_LONG;
+    }
+    return 0;
+}
+
+__device__ __forceinline__ void resp_store(hhuff_response_t* out, const RespState& r) {
+    out->status = r.status;
+    out->nheaders = r.nheaders;
+    out->err = r.err;
+    out->datagram_flow_id = r.dfid;
 }
 
 __device__ __forceinline__ void req_store(hhuff_request_t* out, const ReqState& r) {

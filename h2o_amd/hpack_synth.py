@@ -274,3 +274,108 @@ def pack_connections(conns, table_size=4096):
     off[1:] = np.cumsum([len(b) for b in blocks])
     return dict(data=np.frombuffer(b"".join(blocks), np.uint8).copy(), blk_off=off.astype(np.uint32),
                 conn_first=np.asarray(conn_first, np.uint32), table_size=table_size)
+
+
+# ---- response header blocks (the client side: h2o_hpack_parse_response, lib/http2/hpack.c:642-750) ----
+def _response(rng, V):
+    """a server response head as a client receives it: :status first, then regular fields"""
+    hosts, paths, agents, cookies, accepts = V
+    st = [b"200", b"200", b"200", b"204", b"206", b"301", b"302", b"304", b"404", b"500", b"103"][int(rng.integers(11))]
+    f = [(b":status", st), (b"content-type", [b"text/html; charset=utf-8", b"application/json", b"image/webp"]
+                                              [int(rng.integers(3))]),
+         (b"date", b"Sat, 17 Oct 2026 %02d:%02d:%02d GMT" % (int(rng.integers(24)), int(rng.integers(60)),
+                                                              int(rng.integers(60)))),
+         (b"server", b"h2o/2.3.0-dev")]
+    if rng.random() < 0.6:
+        f.append((b"cache-control", [b"max-age=3600", b"no-cache", b"private, max-age=0"][int(rng.integers(3))]))
+    if rng.random() < 0.5:
+        f.append((b"etag", b'"%016x"' % int(rng.integers(1 << 62))))
+    if rng.random() < 0.3:
+        f.append((b"set-cookie", cookies[int(rng.integers(len(cookies)))]))
+    if rng.random() < 0.2:
+        f.append((b"location", b"https://" + hosts[int(rng.integers(len(hosts)))] + paths[int(rng.integers(len(paths)))]))
+    return f
+
+
+def _trailers(rng):
+    f = [(b"x-checksum", b"%08x" % int(rng.integers(1 << 31)))]
+    if rng.random() < 0.5:
+        f.append((b"grpc-status", b"%d" % int(rng.integers(17))))
+    if rng.random() < 0.3:
+        f.append((b"grpc-message", b"ok"))
+    return f
+
+
+def _response_rules(rng, f, trailers):
+    """one of h2o_hpack_parse_response's cases applied to a head's (or trailers') field list"""
+    kind = int(rng.integers(14))
+    if kind == 0:  # :status variants (three digits, the first 1-9; PARSE_DIGIT keeps the digits before a bad one)
+        v = [b"099", b"1000", b"20", b"2x0", b"20x", b"x00", b"999", b"100", b"", b"0200", b"2 0"][int(rng.integers(11))]
+        if trailers:
+            f.insert(0, (b":status", v))
+        else:
+            f[0] = (b":status", v)
+    elif kind == 1:  # duplicate :status
+        f.insert(1, (b":status", b"200"))
+    elif kind == 2:  # missing :status: a regular field first, or no field at all
+        f = f[1:] if not trailers else f
+        if rng.random() < 0.2:
+            f = []
+    elif kind == 3:  # other pseudo-headers
+        f.insert(int(rng.integers(len(f) + 1)), [(b":path", b"/"), (b":method", b"GET"), (b":foo", b"x"),
+                                                 (b":authority", b"a.example")][int(rng.integers(4))])
+    elif kind == 4:  # :status after a regular field
+        f.append((b":status", b"200"))
+    elif kind == 5:  # the passed-through special fields
+        f.append([(b"content-length", b"123"), (b"content-length", b"abc"), (b"host", b"h.example"),
+                  (b"cache-digest", b"AfdA; complete")][int(rng.integers(4))])
+    elif kind == 6:  # the rejected ones
+        f.append([(b"connection", b"close"), (b"transfer-encoding", b"chunked"), (b"upgrade", b"h2c"),
+                  (b"http2-settings", b"AAMA"), (b"te", b"trailers"), (b"expect", b"100-continue")]
+                 [int(rng.integers(6))])
+    elif kind == 7:  # datagram-flow-id: not listed (stored for HTTP/3)
+        f.insert(max(1, int(rng.integers(len(f) + 1))), (b"datagram-flow-id", b"4"))
+    elif kind == 8:  # past H2O_MAX_HEADERS (100)
+        f += [(b"x-n%d" % (i % 7), b"%d" % i) for i in range(int(rng.integers(95, 130)))]
+    elif kind == 9:  # past the hard limit (1000)
+        f += [(b"vary", b"accept-encoding")] * int(rng.integers(990, 1010))
+    elif kind == 10:  # soft errors in values (the first one is kept in err_desc)
+        f.append((b"x-bad", [b"a\x01b", b" lead", b"trail\t"][int(rng.integers(3))]))
+    elif kind == 11:  # keep-alive / proxy-connection: listed
+        f.append([(b"keep-alive", b"timeout=5"), (b"proxy-connection", b"keep-alive")][int(rng.integers(2))])
+    else:  # only :status
+        f = f[:1]
+    return f
+
+
+def make_response_connections(nconn, blocks_per_conn=(1, 8), seed=0, table_size=4096, adversarial_frac=0.05,
+                              rule_frac=0.3, trailer_frac=0.2):
+    """-> the make_connections layout plus trailers u8[nb] (nonzero: a trailers block, status == NULL);
+    rule_frac of the blocks exercise one of h2o_hpack_parse_response's rules (_response_rules)"""
+    rng = np.random.default_rng(seed)
+    V = _vocab(rng)
+    blocks, conn_first, trailers = [], [0], []
+    for c in range(nconn):
+        table = _Table(table_size)
+        nb = int(rng.integers(blocks_per_conn[0], blocks_per_conn[1] + 1))
+        cb, ct = [], []
+        for k in range(nb):
+            su = None
+            if rng.random() < 0.05:
+                su = int(rng.integers(0, table_size + 1))
+            tr = rng.random() < trailer_frac
+            f = _trailers(rng) if tr else _response(rng, V)
+            if rng.random() < rule_frac:
+                f = _response_rules(rng, f, tr)
+            cb.append(encode_block(rng, table, f, table_size, su))
+            ct.append(1 if tr else 0)
+        if rng.random() < adversarial_frac:
+            _mutate(rng, cb, table_size)
+        blocks += cb
+        trailers += ct
+        conn_first.append(len(blocks))
+    data, off = b"".join(blocks), np.zeros(len(blocks) + 1, np.uint64)
+    off[1:] = np.cumsum([len(b) for b in blocks])
+    return dict(data=np.frombuffer(data, np.uint8).copy(), blk_off=off.astype(np.uint32),
+                conn_first=np.asarray(conn_first, np.uint32), table_size=table_size,
+                trailers=np.asarray(trailers, np.uint8))

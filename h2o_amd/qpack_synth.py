@@ -21,7 +21,7 @@ Step layout (include/hhuff.h hhuff_qpack_decode): sections packed back to back f
 import numpy as np
 
 from . import tables
-from .hpack_synth import _huffman, _vocab, _request, _request_rules, encode_int
+from .hpack_synth import _huffman, _vocab, _request, _request_rules, _response, _response_rules, encode_int
 
 QSTATIC = tables.QPACK_STATIC_TABLE
 ENTRY_OVERHEAD = 32
@@ -211,12 +211,14 @@ def _mutate_encoder(rng, ins, header_table_size):
 
 
 def make_session(nconn, steps=3, seed=0, header_table_size=4096, adversarial_frac=0.05, max_sections=(1, 4),
-                 blocked_frac=0.05, request_frac=0.0):
+                 blocked_frac=0.05, request_frac=0.0, responses=False):
     """-> list over steps of dict(data, sec_off, conn_first, enc_off, enc_len) for one decoder session.
     request_frac: the fraction of requests given one of h2o_hpack_parse_request's cases (duplicate / late /
     unknown pseudo-headers, content-length, connection-specific fields, te, host, cache-digest,
     datagram-flow-id, the 100 / 1000 field limits, ...: hpack_synth._request_rules) -- what
-    h2o_qpack_parse_request checks for HTTP/3 (qpack.c:848)"""
+    h2o_qpack_parse_request checks for HTTP/3 (qpack.c:848).  responses=True: the sections are response heads
+    (what h2o's HTTP/3 client parses, h2o_qpack_parse_response), request_frac of them given one of
+    h2o_hpack_parse_response's cases (hpack_synth._response_rules)"""
     rng = np.random.default_rng(seed)
     V = _vocab(rng)
     hosts = V[0]
@@ -232,9 +234,14 @@ def make_session(nconn, steps=3, seed=0, header_table_size=4096, adversarial_fra
         for s in range(steps):
             ins, sections = [], []
             for _ in range(int(rng.integers(max_sections[0], max_sections[1] + 1))):
-                req = _request(rng, V, host)
-                if request_frac and rng.random() < request_frac:
-                    req = _request_rules(rng, req)
+                if responses:
+                    req = _response(rng, V)
+                    if request_frac and rng.random() < request_frac:
+                        req = _response_rules(rng, req, False)
+                else:
+                    req = _request(rng, V, host)
+                    if request_frac and rng.random() < request_frac:
+                        req = _request_rules(rng, req)
                 ins += _encoder_instructions(rng, t, req, header_table_size)
                 if header_table_size == 0 or rng.random() < 0.1:
                     sections.append(encode_section(rng, _QTable(0), req, max_entries))

@@ -247,6 +247,33 @@ int hhuff_hpack_parse_requests(const uint8_t *in, uint64_t in_size, const uint32
                                uint8_t *fflags, uint32_t *nfields, int32_t *bstatus, hhuff_request_t *req,
                                void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
 
+/* (2c'') HTTP/2 response header blocks, client side: the same pass with h2o_hpack_parse_response's rules
+ *      (lib/http2/hpack.c:642-750) applied to each field as it is decoded, called as h2o's HTTP/2 client calls
+ *      it (lib/common/http2client.c:332 for a response head, :421 for trailers; no datagram flow id):
+ *        - a head block must not be empty and must start with :status -> else PROTOCOL, missing mandatory
+ *          pseudo header (:652-655, :706-709); :status once, three digits, the first 1-9 (PARSE_DIGIT: the
+ *          digits before a bad one stay added); any other pseudo-header, or any in trailers -> PROTOCOL
+ *        - more than 1000 fields -> COMPRESSION; content-length, cache-digest and host are listed as they are;
+ *          datagram-flow-id is not listed; expect, te, connection, http2-settings, transfer-encoding and
+ *          upgrade -> PROTOCOL (unexpected connection-specific header, :712-725)
+ *        - the first 100 remaining fields go to the header list, beyond that the block ends with -254
+ *      trailers[b] != 0 makes block b a trailers block (status == NULL; NULL: every block is a head; an empty
+ *      trailers block fails in decode_header with COMPRESSION, hpack.c:328-329).  Outputs as
+ *      hhuff_hpack_parse_requests with res[b] in place of req[b]; bstatus[b] is h2o_hpack_parse_response's
+ *      return value (0, -254, -1, -9) or the HHUFF_BLK_* codes. */
+#define HHUFF_HERR_MISSING_PSEUDO 9u /* h2o_hpack_err_missing_mandatory_pseudo_header */
+typedef struct hhuff_response {
+    int32_t status;           /* *status: 0 if none was parsed (trailers: always 0) */
+    uint32_t nheaders;        /* fields added to the header list */
+    uint32_t err;             /* HHUFF_HERR_*: what *err_desc points at when the call returns */
+    int32_t datagram_flow_id; /* HTTP/3: the field whose value h2o stored in *datagram_flow_id, or -1 */
+} hhuff_response_t;           /* 16 bytes */
+int hhuff_hpack_parse_responses(const uint8_t *in, uint64_t in_size, const uint32_t *blk_off, const uint32_t *conn_first,
+                                uint32_t nconn, uint32_t table_size, const uint8_t *trailers, uint8_t *arena,
+                                const uint64_t *arena_off, uint32_t *name_off, uint32_t *name_len, uint32_t *value_off,
+                                uint32_t *value_len, uint8_t *fflags, uint32_t *nfields, int32_t *bstatus,
+                                hhuff_response_t *res, void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
+
 /* (2d) QPACK decoder (QPACK half): h2o's QPACK decoder (lib/http3/qpack.c) for many
  *      connections at once.  One call is one step of every connection c:
  *        encoder stream  in[enc_off[c] .. + enc_len[c]): h2o_qpack_decoder_handle_input (qpack.c:420-485,
@@ -335,6 +362,29 @@ int hhuff_qpack_parse_requests(const uint8_t *in, uint64_t in_size, const uint32
                                int32_t *sstatus, uint64_t *req_insert_count, int32_t *enc_status, uint32_t *enc_consumed,
                                uint64_t *insert_count, const uint64_t *stream_id, hhuff_qpack_request_t *req,
                                void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
+
+/* (2e'') HTTP/3 response sections, client side: the step of hhuff_qpack_decode with h2o_qpack_parse_response
+ *      (lib/http3/qpack.c:860-882) applied to every section as h2o's HTTP/3 client calls it
+ *      (lib/common/http3client.c:542-544: a status and a datagram-flow-id out-parameter; the client has no
+ *      blocked-streams budget, so pass max_blocked = 0 to match it): h2o_hpack_parse_response's rules on the
+ *      section's fields (as hhuff_hpack_parse_responses, heads only), every hard error -- -254 excepted --
+ *      normalised to HHUFF_QPK_DECOMPRESSION_FAILED (:877-878), and the Section Acknowledgment only for a
+ *      section that parsed with status 0 and a Required Insert Count other than 0 (:880).  sstatus[k] as for
+ *      hhuff_qpack_parse_requests. */
+typedef struct hhuff_qpack_response_head {
+    hhuff_response_t res;  /* h2o_hpack_parse_response's out-parameters */
+    uint32_t ack_len;      /* *outbufsize (0: no acknowledgment) */
+    uint32_t reserved;
+    uint8_t ack[16];       /* the Section Acknowledgment instruction */
+} hhuff_qpack_response_head_t; /* 40 bytes */
+int hhuff_qpack_parse_responses(const uint8_t *in, uint64_t in_size, const uint32_t *enc_off, const uint32_t *enc_len,
+                                const uint32_t *sec_off, const uint32_t *conn_first, uint32_t nconn, uint32_t nsec,
+                                uint32_t header_table_size, uint64_t max_blocked, const uint32_t *num_blocked,
+                                uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off, uint32_t *name_len,
+                                uint32_t *value_off, uint32_t *value_len, uint8_t *fflags, uint32_t *nfields,
+                                int32_t *sstatus, uint64_t *req_insert_count, int32_t *enc_status, uint32_t *enc_consumed,
+                                uint64_t *insert_count, const uint64_t *stream_id, hhuff_qpack_response_head_t *res,
+                                void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
 
 /* (2f) HTTP/2 response header blocks, encode side (SURVEY f4 encode half): h2o_hpack_flatten_response
  *      (lib/http2/hpack.c:1137-1177) and h2o_hpack_flatten_trailers (:1179-1196) for many responses of many

@@ -14,6 +14,8 @@ Fixture sets (numpy .npz, arrays only, no pickles):
                    re-decoded by the reference, plus the plain bytes decoded as (mostly invalid) Huffman
   adversarial.npz  hand-built decode edge cases (padding, EOS, truncation, long codes, names/values)
   framing.npz      HPACK h2o_hpack_encode_string and QPACK flatten_string (prefix 3/5/7) outputs
+  resp.npz         response header blocks / sections as h2o's clients parse them (h2o_hpack_parse_response,
+                   h2o_qpack_parse_response run by the reference itself): verdicts, records, fields
   blocks.npz       header blocks (f4): the fuzz corpus's connections, the unit test's request sequences,
                    a static-table sweep and synthetic connections (h2o_amd/hpack_synth.py), decoded by
                    h2o_hpack_decode_header field after field with a table per connection (4096 bytes);
@@ -703,6 +705,92 @@ def qpack_set():
     return out
 
 
+def _resp_fields(r, blk_off, nb, nfields):
+    names, values, fl = [], [], []
+    for bi in range(nb):
+        s = int(blk_off[bi])
+        for f in range(s, s + int(nfields[bi])):
+            names.append(r["arena"][r["name_off"][f]:r["name_off"][f] + r["name_len"][f]].tobytes())
+            values.append(r["arena"][r["value_off"][f]:r["value_off"][f] + r["value_len"][f]].tobytes())
+            fl.append(r["fflags"][f])
+    nd, no = pack(names)
+    vd, vo = pack(values)
+    return dict(fld_name=nd, fld_name_off=no, fld_value=vd, fld_value_off=vo, fflags=np.asarray(fl, np.uint8))
+
+
+def resp_set():
+    """tests/golden/resp.npz: response header blocks as h2o's clients parse them, through the reference's own
+    functions (oracle/_ref): h2o_hpack_parse_response over HPACK blocks (ref_hpack_parse_responses: heads and
+    trailers, lib/common/http2client.c:332 / :421) and h2o_qpack_parse_response over QPACK sections
+    (ref_qpack_step_resp, lib/common/http3client.c:542, each section also checked against the real function).
+    Per set: the inputs, every block's verdict, record and fields (names, values, flags)."""
+    from h2o_amd import hpack_synth as HS
+    from h2o_amd import qpack_synth as QS
+
+    out = {}
+    edge = [[b""], [b"\x88"], [b"\x08\x03200"], [b"\x08\x03" + b"2x0"], [b"\x0f\x1c\x03abc"],
+            [b"\x88", b"\x0f\x1c\x03123"], [b"\x88\x88"], [b"\x82"], [b"\x88", b""]]
+    edge_tr = [0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 1]  # per block: the second block of two is trailers
+    sets = []
+    a = HS.make_response_connections(1500, seed=41, adversarial_frac=0.05, rule_frac=0.12)
+    b = HS.make_response_connections(800, blocks_per_conn=(1, 1), seed=42, adversarial_frac=0.0, rule_frac=1.0,
+                                     trailer_frac=0.25)
+    e = HS.pack_connections(edge, 4096)
+    e["trailers"] = np.asarray(edge_tr, np.uint8)
+    c = HS.make_response_connections(300, seed=43, table_size=256, adversarial_frac=0.2, rule_frac=0.2)
+    u = HS.pack_connections(UNIT_RESPONSES_256, 256)
+    u["trailers"] = np.zeros(len(u["blk_off"]) - 1, np.uint8)
+
+    def join(parts):
+        conns, tr = [], []
+        for s in parts:
+            for ci in range(len(s["conn_first"]) - 1):
+                ks = range(int(s["conn_first"][ci]), int(s["conn_first"][ci + 1]))
+                conns.append([s["data"][s["blk_off"][k]:s["blk_off"][k + 1]].tobytes() for k in ks])
+                tr += [int(s["trailers"][k]) for k in ks]
+        return conns, np.asarray(tr, np.uint8)
+
+    for name, parts, ts in (("h", [e, a, b], 4096), ("h256", [u, c], 256)):
+        conns, tr = join(parts)
+        pk = HS.pack_connections(conns, ts)
+        nb = len(pk["blk_off"]) - 1
+        r = O.ref().hpack_decode_blocks(pk["data"], pk["blk_off"], pk["conn_first"], ts, responses=True, trailers=tr)
+        p = name + "_"
+        out.update({p + "data": pk["data"], p + "blk_off": pk["blk_off"], p + "conn_first": pk["conn_first"],
+                    p + "trailers": tr, p + "table_size": np.asarray([ts], np.uint32), p + "nfields": r["nfields"][:nb],
+                    p + "bstatus": r["bstatus"][:nb], p + "res": r["res"][:nb].view(np.uint32).reshape(nb, 4)})
+        out.update({p + k: v for k, v in _resp_fields(r, pk["blk_off"], nb, r["nfields"]).items()})
+        print("resp %-5s connections %5d  blocks %6d  fields %7d  errors %d" % (
+            name, len(pk["conn_first"]) - 1, nb, int(r["nfields"][:nb].sum()), int((r["bstatus"][:nb] != 0).sum())))
+    # HTTP/3: a decoder session whose sections are response heads
+    nconn, hts, mb = 400, 4096, 4
+    steps = QS.make_session(nconn, steps=3, seed=44, header_table_size=hts, adversarial_frac=0.05, request_frac=0.35,
+                            responses=True)
+    sq = O.QpackSession(O.ref(), nconn, hts, mb)
+    nbl = (np.arange(nconn) % 6).astype(np.uint32)
+    out["q_meta"] = np.asarray([nconn, hts, mb, len(steps)], np.uint32)
+    out["q_num_blocked"] = nbl
+    for k, st in enumerate(steps):
+        ao = QS.arena_offsets(st["sec_off"], hts)
+        ns = len(st["sec_off"]) - 1
+        sid = qpack_stream_ids(ns, k)
+        q = sq.step(st["data"], st["enc_off"], st["enc_len"], st["sec_off"], st["conn_first"], ao, nbl, stream_id=sid,
+                    responses=True)
+        p = "q_%d_" % k
+        for key in ("data", "sec_off", "conn_first", "enc_off", "enc_len"):
+            out[p + key] = st[key]
+        out[p + "arena_off"] = ao
+        out[p + "stream_id"] = sid
+        for key in ("nfields", "sstatus", "req_insert_count"):
+            out[p + key] = q[key][:ns]
+        for key in ("enc_status", "enc_consumed", "insert_count"):
+            out[p + key] = q[key][:nconn]
+        out[p + "res"] = q["res"][:ns].view(np.uint32).reshape(ns, 10)
+        out.update({p + kk: v for kk, v in _resp_fields(q, st["sec_off"], ns, q["nfields"]).items()})
+    sq.close()
+    return out
+
+
 HPENC_SESSIONS = [  # name, seed, connections, steps, knobs (h2o_amd.hpenc_synth.make_session), error mutations
     ("h4096", 301, 160, 3, dict(), False),
     ("hedge", 302, 120, 3, dict(small_table_frac=0.3, trailers_frac=0.1, big_frac=0.01, notoken_frac=0.1,
@@ -808,6 +896,9 @@ def qpenc_set():
 
 
 def main():
+    if "--only-resp" in sys.argv:
+        np.savez_compressed(os.path.join(GOLDEN, "resp.npz"), **resp_set())
+        return
     if "--only-qpenc" in sys.argv:
         np.savez_compressed(os.path.join(GOLDEN, "qpenc.npz"), **qpenc_set())
         return
@@ -838,6 +929,7 @@ def main():
     sets["qpack"] = qpack_set()
     sets["hpenc"] = hpenc_set()
     sets["qpenc"] = qpenc_set()
+    sets["resp"] = resp_set()
     for name, arrays in sets.items():
         path = os.path.join(GOLDEN, name + ".npz")
         np.savez_compressed(path, **arrays)

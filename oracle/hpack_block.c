@@ -363,6 +363,75 @@ int orc_rq_field(orc_req_t *r, const uint8_t *name, uint32_t nl, const uint8_t *
     return 0;
 }
 
+void orc_rs_init(orc_resp_t *r, int trailers)
+{
+    memset(r, 0, sizeof(*r));
+    r->dfid = -1;
+    r->trailers = trailers;
+}
+
+void orc_rs_store(uint32_t *w, const orc_resp_t *r)
+{
+    w[0] = (uint32_t)r->status, w[1] = r->nheaders, w[2] = r->err, w[3] = (uint32_t)r->dfid;
+}
+
+/* h2o_hpack_parse_response (hpack.c:642-750) for field k: 0 or the hard error; *header = listed.  h3: a
+ * datagram-flow-id out-parameter (lib/common/http3client.c:542); HTTP/2's client passes NULL (http2client.c:332) */
+int orc_rs_field(orc_resp_t *r, const uint8_t *name, uint32_t nl, const uint8_t *value, uint32_t vl, unsigned soft,
+                 int32_t k, int *header, int h3)
+{
+    *header = 0;
+    if (soft && r->err == 0)
+        r->err = (soft & ORC_SOFT_NAME) ? 1 : 2;
+    if (++r->ndecoded > 1000) { /* :668-671 */
+        r->err = 3;
+        return ORC_ERR_COMPRESSION;
+    }
+    if (nl > 0 && name[0] == ':') { /* :672-704 */
+        if (r->trailers || !(nl == 7 && memcmp(name, ":status", 7) == 0) || r->status != 0 || vl != 3) {
+            r->err = 4;
+            return ORC_ERR_PROTOCOL;
+        }
+        static const int mul[3] = {100, 10, 1};
+        for (int i = 0; i < 3; ++i) { /* PARSE_DIGIT: each digit is added before the next is looked at */
+            if (value[i] < '0' + (i == 0 ? 1 : 0) || value[i] > '9') {
+                r->err = 4;
+                return ORC_ERR_PROTOCOL;
+            }
+            r->status += (value[i] - '0') * mul[i];
+        }
+        return 0;
+    }
+    if (!r->trailers && r->status == 0) { /* :706-709 */
+        r->err = 9;
+        return ORC_ERR_PROTOCOL;
+    }
+    switch (rq_kind(name, nl)) { /* the is_hpack_special tokens, :712-725 */
+    case RQ_CONTENT_LENGTH:
+    case RQ_CACHE_DIGEST:
+    case RQ_HOST:
+        break;
+    case RQ_DATAGRAM_FLOW_ID:
+        if (h3)
+            r->dfid = k;
+        return 0;
+    case RQ_EXPECT:
+    case RQ_TE:
+    case RQ_REJECT:
+        r->err = 6;
+        return ORC_ERR_PROTOCOL;
+    default:
+        break;
+    }
+    if (r->nheaders < 100) {
+        ++r->nheaders;
+        *header = 1;
+    } else if (r->err == 0) {
+        r->err = 3;
+    }
+    return 0;
+}
+
 typedef struct {
     const uint8_t *in;
     const uint32_t *blk_off, *conn_first;
@@ -373,6 +442,8 @@ typedef struct {
     uint8_t *fflags;
     int32_t *bstatus;
     uint32_t *req; /* request mode: 12 words per block, else NULL */
+    uint32_t *res; /* response mode: 4 words per block, else NULL */
+    const uint8_t *trailers; /* response mode: nonzero = a trailers block (NULL: none) */
 } orc_blk_job_t;
 
 static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
@@ -381,12 +452,16 @@ static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
     int failed = 0;
     for (uint32_t b = j->conn_first[c]; b < j->conn_first[c + 1]; ++b) {
         orc_req_t rq;
+        orc_resp_t rs;
         orc_rq_init(&rq);
+        orc_rs_init(&rs, j->trailers != NULL && j->trailers[b] != 0);
         j->nfields[b] = 0;
         if (failed) {
             j->bstatus[b] = ORC_BLK_SKIPPED;
             if (j->req)
                 orc_rq_store(j->req + 12 * (size_t)b, &rq);
+            if (j->res)
+                orc_rs_store(j->res + 4 * (size_t)b, &rs);
             continue;
         }
         const uint8_t *p = j->in + j->blk_off[b], *end = j->in + j->blk_off[b + 1];
@@ -394,18 +469,26 @@ static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
         orc_arena_t A = {j->arena, j->arena_off[b], j->arena_off[b + 1] < (1ull << 32) ? j->arena_off[b + 1] : (1ull << 32)};
         uint32_t nf = 0, slot = j->blk_off[b];
         int st = 0;
-        while (p != end) {
+        if (j->res && p == end) { /* a head needs :status (hpack.c:652-655); empty trailers: decode_header (:328-329) */
+            if (!rs.trailers)
+                rs.err = 9;
+            st = rs.trailers ? ORC_ERR_COMPRESSION : ORC_ERR_PROTOCOL;
+        }
+        while (st == 0 && p != end) {
             uint32_t no = 0, nl = 0, vo = 0, vl = 0;
             unsigned soft = 0;
             int rc = orc_block_field(&t, &p, end, &A, &no, &nl, &vo, &vl, &soft);
             if (rc != 0 && rc != ORC_ERR_INVALID_CHAR) {
                 st = rc;
-                rq.err = rc == ORC_ERR_PROTOCOL ? 7 : 0; /* *err_desc = decode_err (hpack.c:523-525) */
+                rq.err = rc == ORC_ERR_PROTOCOL ? 7 : 0; /* *err_desc = decode_err (hpack.c:523-525, :663-665) */
+                rs.err = rq.err;
                 break;
             }
             int header = 0, rr = 0;
             if (j->req)
                 rr = orc_rq_field(&rq, j->arena + no, nl, j->arena + vo, vl, soft, (int32_t)nf, &header, 0);
+            if (j->res)
+                rr = orc_rs_field(&rs, j->arena + no, nl, j->arena + vo, vl, soft, (int32_t)nf, &header, 0);
             j->name_off[slot + nf] = no;
             j->name_len[slot + nf] = nl;
             j->value_off[slot + nf] = vo;
@@ -421,6 +504,11 @@ static void orc_hpack_connection(const orc_blk_job_t *j, uint32_t c)
             if (st == 0 && rq.err != 0)
                 st = ORC_ERR_INVALID_CHAR; /* hpack.c:636-637 */
             orc_rq_store(j->req + 12 * (size_t)b, &rq);
+        }
+        if (j->res) {
+            if (st == 0 && rs.err != 0)
+                st = ORC_ERR_INVALID_CHAR; /* hpack.c:745-747 */
+            orc_rs_store(j->res + 4 * (size_t)b, &rs);
         }
         j->nfields[b] = nf;
         j->bstatus[b] = st;
@@ -440,7 +528,8 @@ static void *orc_blk_worker(void *arg)
 static int orc_hpack_blocks(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
                             uint32_t table_size, uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off,
                             uint32_t *name_len, uint32_t *value_off, uint32_t *value_len, uint8_t *fflags,
-                            uint32_t *nfields, int32_t *bstatus, uint32_t *req, int nthreads)
+                            uint32_t *nfields, int32_t *bstatus, uint32_t *req, uint32_t *res, const uint8_t *trailers,
+                            int nthreads)
 {
     if (nthreads < 1)
         nthreads = 1;
@@ -458,7 +547,7 @@ static int orc_hpack_blocks(const uint8_t *in, const uint32_t *blk_off, const ui
         j->in = in, j->blk_off = blk_off, j->conn_first = conn_first, j->table_size = table_size;
         j->arena = arena, j->arena_off = arena_off, j->name_off = name_off, j->name_len = name_len;
         j->value_off = value_off, j->value_len = value_len, j->fflags = fflags, j->nfields = nfields;
-        j->bstatus = bstatus, j->req = req;
+        j->bstatus = bstatus, j->req = req, j->res = res, j->trailers = trailers;
         j->c_begin = (uint32_t)(((uint64_t)nconn * k) / nthreads);
         j->c_end = (uint32_t)(((uint64_t)nconn * (k + 1)) / nthreads);
     }
@@ -478,7 +567,7 @@ int orc_hpack_decode_blocks(const uint8_t *in, const uint32_t *blk_off, const ui
                             uint32_t *nfields, int32_t *bstatus, int nthreads)
 {
     return orc_hpack_blocks(in, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len, value_off,
-                            value_len, fflags, nfields, bstatus, NULL, nthreads);
+                            value_len, fflags, nfields, bstatus, NULL, NULL, NULL, nthreads);
 }
 
 int orc_hpack_parse_requests(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
@@ -487,5 +576,14 @@ int orc_hpack_parse_requests(const uint8_t *in, const uint32_t *blk_off, const u
                              uint32_t *nfields, int32_t *bstatus, uint32_t *req, int nthreads)
 {
     return orc_hpack_blocks(in, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len, value_off,
-                            value_len, fflags, nfields, bstatus, req, nthreads);
+                            value_len, fflags, nfields, bstatus, req, NULL, NULL, nthreads);
+}
+
+int orc_hpack_parse_responses(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
+                              uint32_t table_size, const uint8_t *trailers, uint8_t *arena, const uint64_t *arena_off,
+                              uint32_t *name_off, uint32_t *name_len, uint32_t *value_off, uint32_t *value_len,
+                              uint8_t *fflags, uint32_t *nfields, int32_t *bstatus, uint32_t *res, int nthreads)
+{
+    return orc_hpack_blocks(in, blk_off, conn_first, nconn, table_size, arena, arena_off, name_off, name_len, value_off,
+                            value_len, fflags, nfields, bstatus, NULL, res, trailers, nthreads);
 }

@@ -25,6 +25,10 @@ QREQ_DTYPE = np.dtype([("content_length", "<u8"), ("method", "<i4"), ("scheme", 
                        ("path", "<i4"), ("protocol", "<i4"), ("expect", "<i4"), ("exists_map", "<u4"),
                        ("nheaders", "<u4"), ("err", "<u4"), ("scheme_kind", "<u4"), ("datagram_flow_id", "<i4"),
                        ("ack_len", "<u4"), ("ack", "u1", (16,))])
+# include/hhuff.h hhuff_response_t (16 bytes) and hhuff_qpack_response_head_t (40 bytes)
+RES_DTYPE = np.dtype([("status", "<i4"), ("nheaders", "<u4"), ("err", "<u4"), ("datagram_flow_id", "<i4")])
+QRES_DTYPE = np.dtype([("status", "<i4"), ("nheaders", "<u4"), ("err", "<u4"), ("datagram_flow_id", "<i4"),
+                       ("ack_len", "<u4"), ("reserved", "<u4"), ("ack", "u1", (16,))])
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
 
@@ -81,6 +85,10 @@ class _Codec:
         f = getattr(L, P + "_hpack_parse_requests")
         f.restype = ctypes.c_int
         f.argtypes = [_u8p, _u32p, _u32p, ctypes.c_uint32, ctypes.c_uint32, _u8p, ctypes.POINTER(ctypes.c_uint64),
+                      _u32p, _u32p, _u32p, _u32p, _u8p, _u32p, ctypes.POINTER(ctypes.c_int32), _u32p, ctypes.c_int]
+        f = getattr(L, P + "_hpack_parse_responses")
+        f.restype = ctypes.c_int
+        f.argtypes = [_u8p, _u32p, _u32p, ctypes.c_uint32, ctypes.c_uint32, _u8p, _u8p, ctypes.POINTER(ctypes.c_uint64),
                       _u32p, _u32p, _u32p, _u32p, _u8p, _u32p, ctypes.POINTER(ctypes.c_int32), _u32p, ctypes.c_int]
         f = getattr(L, P + "_literals_batch")
         f.restype = ctypes.c_int
@@ -190,10 +198,12 @@ class _Codec:
 
 
     def hpack_decode_blocks(self, data, blk_off, conn_first, table_size=4096, arena_off=None, nthreads=1,
-                            requests=False):
+                            requests=False, responses=False, trailers=None):
         """HPACK header blocks (include/hhuff.h hhuff_hpack_decode_blocks contract) -> dict of arrays:
         arena, name_off, name_len, value_off, value_len, fflags (per field slot), nfields, bstatus (per block);
-        requests=True: hhuff_hpack_parse_requests (h2o_hpack_parse_request per block), plus req (REQ_DTYPE)"""
+        requests=True: hhuff_hpack_parse_requests (h2o_hpack_parse_request per block), plus req (REQ_DTYPE);
+        responses=True: hhuff_hpack_parse_responses (h2o_hpack_parse_response per block; trailers = u8 per
+        block, nonzero for a trailers block), plus res (RES_DTYPE)"""
         data = np.ascontiguousarray(data, dtype=np.uint8)
         blk_off = np.ascontiguousarray(blk_off, dtype=np.uint32)
         conn_first = np.ascontiguousarray(conn_first, dtype=np.uint32)
@@ -212,7 +222,13 @@ class _Codec:
                 _ptr(r["name_off"], _u32p), _ptr(r["name_len"], _u32p), _ptr(r["value_off"], _u32p),
                 _ptr(r["value_len"], _u32p), _ptr(r["fflags"], _u8p), _ptr(r["nfields"], _u32p),
                 r["bstatus"].ctypes.data_as(ctypes.POINTER(ctypes.c_int32))]
-        if requests:
+        if responses:
+            tr = None if trailers is None else np.ascontiguousarray(trailers, dtype=np.uint8)
+            words = np.zeros((max(1, nb), 4), np.uint32)
+            rc = getattr(self.lib, self.prefix + "_hpack_parse_responses")(*args[:5], _ptr(tr, _u8p), *args[5:],
+                                                                            _ptr(words, _u32p), nthreads)
+            r["res"] = words.view(RES_DTYPE).reshape(-1)
+        elif requests:
             words = np.zeros((max(1, nb), 12), np.uint32)
             rc = getattr(self.lib, self.prefix + "_hpack_parse_requests")(*args, _ptr(words, _u32p), nthreads)
             r["req"] = words.view(REQ_DTYPE).reshape(-1)
@@ -237,6 +253,9 @@ class QpackSession:
         self._step_req = getattr(L, P + "_qpack_step_req")
         self._step_req.restype = ctypes.c_int
         self._step_req.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 21
+        self._step_resp = getattr(L, P + "_qpack_step_resp")
+        self._step_resp.restype = ctypes.c_int
+        self._step_resp.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 21
         self.nconn = nconn
         self.h = self._open(nconn, header_table_size, max_blocked)
 
@@ -247,12 +266,14 @@ class QpackSession:
 
     __del__ = close
 
-    def step(self, data, enc_off, enc_len, sec_off, conn_first, arena_off, num_blocked=None, stream_id=None):
+    def step(self, data, enc_off, enc_len, sec_off, conn_first, arena_off, num_blocked=None, stream_id=None,
+             responses=False):
         """-> dict: arena, name_off, name_len, value_off, value_len, fflags (per field slot), nfields, sstatus,
         req_insert_count (per section), enc_status, enc_consumed, insert_count (per connection).  With
         stream_id (u64 per section): h2o_qpack_parse_request per section (hhuff_qpack_parse_requests'
         contract), plus "req" (QREQ_DTYPE records); the reference harness also checks every section against
-        the real h2o_qpack_parse_request and fails on a disagreement."""
+        the real h2o_qpack_parse_request and fails on a disagreement.  responses=True (with stream_id):
+        h2o_qpack_parse_response per section instead (hhuff_qpack_parse_responses), plus "res" (QRES_DTYPE)."""
         c = lambda a, t: np.ascontiguousarray(a, dtype=t)  # noqa: E731
         data, enc_off, enc_len, sec_off, conn_first = (c(data, np.uint8), c(enc_off, np.uint32), c(enc_len, np.uint32),
                                                        c(sec_off, np.uint32), c(conn_first, np.uint32))
@@ -280,6 +301,12 @@ class QpackSession:
             assert rc == 0
             return r
         sid = c(stream_id, np.uint64)
+        if responses:
+            words = np.zeros((max(1, ns), 10), np.uint32)
+            rc = self._step_resp(*args, d(sid), d(words))
+            assert rc == 0, "%d section(s) disagree with the real h2o_qpack_parse_response" % rc
+            r["res"] = words.view(QRES_DTYPE).reshape(-1)
+            return r
         words = np.zeros((max(1, ns), 18), np.uint32)
         rc = self._step_req(*args, d(sid), d(words))
         assert rc == 0, "%d section(s) disagree with the real h2o_qpack_parse_request" % rc

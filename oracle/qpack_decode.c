@@ -528,13 +528,17 @@ static uint32_t qpk_header_ack(uint64_t stream_id, uint8_t *out)
  * blocked streams (h2o's conn->num_qpack_blocked, lib/http3/server.c:1544).  With req != NULL every section
  * goes through h2o_qpack_parse_request (qpack.c:830-858): h2o_hpack_parse_request's rules with the HTTP/3
  * arguments, normalize_error_code, send_header_ack; req = 18 u32 words per section: the hhuff_request_t
- * words, datagram_flow_id, ack_len, ack[16]. */
+ * words, datagram_flow_id, ack_len, ack[16].  With res != NULL every section goes through
+ * h2o_qpack_parse_response (qpack.c:860-882) as h2o's HTTP/3 client calls it (lib/common/http3client.c:542):
+ * h2o_hpack_parse_response's rules on a response head with a datagram-flow-id out-parameter, the same
+ * normalisation, and the acknowledgment only after a clean parse; res = 10 u32 words per section
+ * (include/hhuff.h hhuff_qpack_response_head_t: status, nheaders, err, dfid, ack_len, 0, ack[16]). */
 static int qpk_step(qpk_session_t *s, const uint8_t *in, const uint32_t *enc_off, const uint32_t *enc_len,
                     const uint32_t *sec_off, const uint32_t *conn_first, const uint32_t *num_blocked, uint8_t *arena,
                     const uint64_t *arena_off, uint32_t *name_off, uint32_t *name_len, uint32_t *value_off,
                     uint32_t *value_len, uint8_t *fflags, uint32_t *nfields, int32_t *sstatus, uint64_t *req_insert_count,
                     int32_t *enc_status, uint32_t *enc_consumed, uint64_t *insert_count, const uint64_t *stream_id,
-                    uint32_t *req)
+                    uint32_t *req, uint32_t *res)
 {
     for (uint32_t c = 0; c < s->nconn; ++c) {
         qpk_conn_t *t = &s->c[c];
@@ -555,7 +559,9 @@ static int qpk_step(qpk_session_t *s, const uint8_t *in, const uint32_t *enc_off
             nfields[k] = 0;
             req_insert_count[k] = 0;
             orc_req_t rq;
+            orc_resp_t rs;
             orc_rq_init(&rq);
+            orc_rs_init(&rs, 0);
             int st = 0;
             qpk_ctx_t ctx = {t, 0, 0};
             uint32_t nf = 0;
@@ -574,6 +580,10 @@ static int qpk_step(qpk_session_t *s, const uint8_t *in, const uint32_t *enc_off
                 }
                 uint32_t slot = sec_off[k];
                 qpk_arena_t A = {arena, arena_off[k], arena_off[k + 1] < (1ull << 32) ? arena_off[k + 1] : (1ull << 32)};
+                if (res && st == 0 && p == end) { /* no :status (hpack.c:652-655), normalised (:877-878) */
+                    rs.err = 9;
+                    st = ORC_QPK_DECOMPRESSION_FAILED;
+                }
                 while (st == 0 && p != end) {
                     uint32_t no = 0, nl = 0, vo = 0, vl = 0;
                     unsigned soft = 0;
@@ -581,11 +591,14 @@ static int qpk_step(qpk_session_t *s, const uint8_t *in, const uint32_t *enc_off
                     if (rc != 0 && rc != ORC_ERR_INVALID_CHAR) {
                         st = rc;
                         rq.err = rc == ORC_BLK_ARENA ? 0 : 8; /* HHUFF_HERR_DECODE: decode_header's own error */
+                        rs.err = rq.err;
                         break;
                     }
                     int header = 0, rr = 0;
                     if (req)
                         rr = orc_rq_field(&rq, arena + no, nl, arena + vo, vl, soft, (int32_t)nf, &header, 1);
+                    if (res)
+                        rr = orc_rs_field(&rs, arena + no, nl, arena + vo, vl, soft, (int32_t)nf, &header, 1);
                     name_off[slot + nf] = no;
                     name_len[slot + nf] = nl;
                     value_off[slot + nf] = vo;
@@ -599,6 +612,8 @@ static int qpk_step(qpk_session_t *s, const uint8_t *in, const uint32_t *enc_off
                 }
                 if (req && st == 0 && rq.err != 0)
                     st = ORC_ERR_INVALID_CHAR; /* hpack.c:636-637 */
+                if (res && st == 0 && rs.err != 0)
+                    st = ORC_ERR_INVALID_CHAR; /* hpack.c:745-747 */
             }
             nfields[k] = nf;
             sstatus[k] = st;
@@ -610,6 +625,14 @@ static int qpk_step(qpk_session_t *s, const uint8_t *in, const uint32_t *enc_off
                 w[13] = (st == 0 || st == ORC_ERR_INVALID_CHAR) && ctx.req_insert_count != 0
                             ? qpk_header_ack(stream_id[k], ack) : 0;
                 memcpy(w + 14, ack, 16);
+            }
+            if (res) {
+                uint32_t *w = res + 10 * (size_t)k;
+                orc_rs_store(w, &rs);
+                uint8_t ack[16] = {0};
+                w[4] = st == 0 && ctx.req_insert_count != 0 ? qpk_header_ack(stream_id[k], ack) : 0;
+                w[5] = 0;
+                memcpy(w + 6, ack, 16);
             }
         }
     }
@@ -624,7 +647,7 @@ int orc_qpack_step(void *h, const uint8_t *in, const uint32_t *enc_off, const ui
 {
     return qpk_step((qpk_session_t *)h, in, enc_off, enc_len, sec_off, conn_first, num_blocked, arena, arena_off, name_off,
                     name_len, value_off, value_len, fflags, nfields, sstatus, req_insert_count, enc_status, enc_consumed,
-                    insert_count, NULL, NULL);
+                    insert_count, NULL, NULL, NULL);
 }
 
 int orc_qpack_step_req(void *h, const uint8_t *in, const uint32_t *enc_off, const uint32_t *enc_len,
@@ -636,5 +659,17 @@ int orc_qpack_step_req(void *h, const uint8_t *in, const uint32_t *enc_off, cons
 {
     return qpk_step((qpk_session_t *)h, in, enc_off, enc_len, sec_off, conn_first, num_blocked, arena, arena_off, name_off,
                     name_len, value_off, value_len, fflags, nfields, sstatus, req_insert_count, enc_status, enc_consumed,
-                    insert_count, stream_id, req);
+                    insert_count, stream_id, req, NULL);
+}
+
+int orc_qpack_step_resp(void *h, const uint8_t *in, const uint32_t *enc_off, const uint32_t *enc_len,
+                        const uint32_t *sec_off, const uint32_t *conn_first, const uint32_t *num_blocked, uint8_t *arena,
+                        const uint64_t *arena_off, uint32_t *name_off, uint32_t *name_len, uint32_t *value_off,
+                        uint32_t *value_len, uint8_t *fflags, uint32_t *nfields, int32_t *sstatus,
+                        uint64_t *req_insert_count, int32_t *enc_status, uint32_t *enc_consumed, uint64_t *insert_count,
+                        const uint64_t *stream_id, uint32_t *res)
+{
+    return qpk_step((qpk_session_t *)h, in, enc_off, enc_len, sec_off, conn_first, num_blocked, arena, arena_off, name_off,
+                    name_len, value_off, value_len, fflags, nfields, sstatus, req_insert_count, enc_status, enc_consumed,
+                    insert_count, stream_id, NULL, res);
 }

@@ -16,6 +16,9 @@
  * decode_cb wrapper around h2o_hpack_decode_header copies each field to the arena and, from the
  * out-parameters' changes between calls, learns which field each one took and which fields went to the
  * header list.
+ * ref_hpack_parse_responses runs h2o_hpack_parse_response (hpack.c:642-750) over every block as h2o's HTTP/2
+ * client calls it (lib/common/http2client.c:332 with a status out-parameter, :421 with status == NULL for
+ * trailers; no datagram flow id) through the same wrapper, and records the include/hhuff.h hhuff_response_t.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -179,6 +182,8 @@ static uint32_t rq_err_code(const char *e)
         return 6;
     if (e == h2o_hpack_err_found_upper_case_in_header_name)
         return 7;
+    if (e == h2o_hpack_err_missing_mandatory_pseudo_header)
+        return 9;
     return 99;
 }
 
@@ -237,6 +242,59 @@ REF_API int ref_hpack_parse_requests(const uint8_t *in, const uint32_t *blk_off,
             w[9] = (uint32_t)headers.size;
             w[10] = rq_err_code(err_desc);
             w[11] = scheme == NULL ? 0 : scheme == &H2O_URL_SCHEME_HTTP ? 1 : scheme == &H2O_URL_SCHEME_HTTPS ? 2 : 3;
+        }
+        h2o_hpack_dispose_header_table(&table);
+    }
+    return 0;
+}
+
+/* ---- h2o_hpack_parse_response ---- */
+REF_API int ref_hpack_parse_responses(const uint8_t *in, const uint32_t *blk_off, const uint32_t *conn_first, uint32_t nconn,
+                                      uint32_t table_size, const uint8_t *trailers, uint8_t *arena, const uint64_t *arena_off,
+                                      uint32_t *name_off, uint32_t *name_len, uint32_t *value_off, uint32_t *value_len,
+                                      uint8_t *fflags, uint32_t *nfields, int32_t *bstatus, uint32_t *res, int nthreads)
+{
+    (void)nthreads;
+    for (uint32_t c = 0; c < nconn; ++c) {
+        h2o_hpack_header_table_t table;
+        memset(&table, 0, sizeof(table));
+        table.hpack_capacity = table.hpack_max_capacity = table_size;
+        int failed = 0;
+        for (uint32_t b = conn_first[c]; b < conn_first[c + 1]; ++b) {
+            uint32_t *w = res + 4 * (size_t)b;
+            nfields[b] = 0;
+            int status = 0;
+            h2o_headers_t headers = {NULL, 0, 0};
+            h2o_iovec_t unused = {NULL, 0};
+            const char *err_desc = NULL;
+            rq_ctx_t x;
+            memset(&x, 0, sizeof(x));
+            for (int i = 0; i < 6; ++i)
+                x.taken[i] = -1, x.out[i] = &unused;
+            x.scheme = (const h2o_url_scheme_t **)&x.scheme_snap; /* unchanging: rq_settle sees no scheme */
+            if (!failed) {
+                h2o_mem_pool_t pool;
+                h2o_mem_init_pool(&pool);
+                x.table = &table, x.arena = arena, x.cur = arena_off[b];
+                x.aend = arena_off[b + 1] < (1ull << 32) ? arena_off[b + 1] : (1ull << 32);
+                x.name_off = name_off, x.name_len = name_len, x.value_off = value_off, x.value_len = value_len;
+                x.fflags = fflags, x.slot = blk_off[b];
+                x.headers = &headers;
+                int is_trailers = trailers != NULL && trailers[b] != 0;
+                int ret = h2o_hpack_parse_response(&pool, rq_decode_cb, &x, is_trailers ? NULL : &status, &headers, NULL,
+                                                   in + blk_off[b], blk_off[b + 1] - blk_off[b], &err_desc);
+                rq_settle(&x);
+                h2o_mem_clear_pool(&pool);
+                nfields[b] = x.nf;
+                bstatus[b] = ret;
+                failed = ret != 0 && ret != H2O_HTTP2_ERROR_INVALID_HEADER_CHAR;
+            } else {
+                bstatus[b] = REF_BLK_SKIPPED;
+            }
+            w[0] = (uint32_t)status;
+            w[1] = (uint32_t)headers.size;
+            w[2] = rq_err_code(err_desc);
+            w[3] = (uint32_t)-1; /* no datagram flow id out-parameter (http2client.c:332) */
         }
         h2o_hpack_dispose_header_table(&table);
     }

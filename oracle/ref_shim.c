@@ -323,6 +323,8 @@ static uint32_t q3_err_code(const char *e)
         return 6;
     if (e == h2o_hpack_err_found_upper_case_in_header_name)
         return 7;
+    if (e == h2o_hpack_err_missing_mandatory_pseudo_header)
+        return 9;
     return 99;
 }
 
@@ -451,6 +453,129 @@ REF_API int ref_qpack_step_req(void *h, const uint8_t *in, const uint32_t *enc_o
             w[12] = (uint32_t)x.taken[6];
             w[13] = (uint32_t)outbufsize;
             memcpy(w + 14, outbuf, 16);
+        }
+    }
+    return mismatches;
+}
+
+/* ---- h2o_qpack_parse_response (qpack.c:860-882) as h2o's HTTP/3 client calls it ----
+ * lib/common/http3client.c:542-544: a status and a datagram-flow-id out-parameter.  Per section the record
+ * (include/hhuff.h hhuff_qpack_response_head_t, 10 u32 words) is produced by h2o_qpack_parse_response's own
+ * steps through the copying decode_cb wrapper (it learns which fields went to the header list and which one
+ * took the datagram flow id), and every section is ALSO run through the real h2o_qpack_parse_response on the
+ * same decoder (with a blocked_ref: the sessions' decoders may permit blocked sections, where the client's
+ * permits none); return value, status, header count, err_desc, datagram flow id and acknowledgment must agree
+ * (the count of disagreeing sections is the return value). */
+REF_API int ref_qpack_step_resp(void *h, const uint8_t *in, const uint32_t *enc_off, const uint32_t *enc_len,
+                                const uint32_t *sec_off, const uint32_t *conn_first, const uint32_t *num_blocked,
+                                uint8_t *arena, const uint64_t *arena_off, uint32_t *name_off, uint32_t *name_len,
+                                uint32_t *value_off, uint32_t *value_len, uint8_t *fflags, uint32_t *nfields,
+                                int32_t *sstatus, uint64_t *req_insert_count, int32_t *enc_status, uint32_t *enc_consumed,
+                                uint64_t *insert_count, const uint64_t *stream_id, uint32_t *res)
+{
+    ref_qpk_session_t *s = h;
+    int mismatches = 0;
+    for (uint32_t c = 0; c < s->nconn; ++c) {
+        h2o_qpack_decoder_t *q = s->d[c];
+        enc_status[c] = 0;
+        enc_consumed[c] = 0;
+        insert_count[c] = 0;
+        if (s->failed[c]) {
+            enc_status[c] = REF_QPK_SKIPPED;
+        } else if (enc_len[c]) {
+            const uint8_t *src = in + enc_off[c], *end = src + enc_len[c];
+            const char *err_desc = NULL;
+            int r = h2o_qpack_decoder_handle_input(q, &insert_count[c], &src, end, &err_desc);
+            enc_consumed[c] = (uint32_t)(src - (in + enc_off[c]));
+            enc_status[c] = r;
+            s->failed[c] = r != 0;
+        }
+        uint64_t nb = num_blocked ? num_blocked[c] : 0;
+        for (uint32_t k = conn_first[c]; k < conn_first[c + 1]; ++k) {
+            uint32_t *w = res + 10 * (size_t)k;
+            nfields[k] = 0;
+            req_insert_count[k] = 0;
+            int status = 0;
+            h2o_iovec_t unused = {NULL, 0}, dfid = {NULL, 0};
+            h2o_headers_t headers = {NULL, 0, 0};
+            size_t outbufsize = 0;
+            uint8_t outbuf[16] = {0};
+            const char *err_desc = NULL;
+            q3_ctx_t x;
+            memset(&x, 0, sizeof(x));
+            for (int i = 0; i < Q3_OUTS; ++i)
+                x.taken[i] = -1, x.out[i] = &unused;
+            x.out[6] = &dfid;
+            x.scheme = (const h2o_url_scheme_t **)&x.scheme_snap; /* unchanging: q3_settle sees no scheme */
+            int st;
+            h2o_mem_pool_t pool;
+            h2o_mem_init_pool(&pool);
+            const uint8_t *src0 = in + sec_off[k], *end = in + sec_off[k + 1];
+            if (s->failed[c]) {
+                st = REF_QPK_SKIPPED;
+            } else {
+                const uint8_t *src = src0;
+                struct st_h2o_qpack_decode_header_ctx_t ctx;
+                h2o_qpack_section_stats_t stats = {0};
+                uint64_t blocked_ref = 0;
+                st = parse_decode_context(q, &ctx, &src, end);
+                if (st == 0) {
+                    req_insert_count[k] = (uint64_t)ctx.req_insert_count;
+                    st = check_decode_context_blocked(q, &ctx, nb, &blocked_ref);
+                }
+                int blocked = st == 0 && blocked_ref != 0;
+                if (st == 0 && !blocked) {
+                    ctx.stats = &stats;
+                    x.dctx = &ctx, x.arena = arena, x.cur = arena_off[k];
+                    x.aend = arena_off[k + 1] < (1ull << 32) ? arena_off[k + 1] : (1ull << 32);
+                    x.name_off = name_off, x.name_len = name_len, x.value_off = value_off, x.value_len = value_len;
+                    x.fflags = fflags, x.slot = sec_off[k];
+                    x.headers = &headers;
+                    st = h2o_hpack_parse_response(&pool, q3_decode_cb, &x, &status, &headers, &dfid, src, end - src,
+                                                  &err_desc);
+                    q3_settle(&x);
+                    if (x.arena_full)
+                        st = REF_QPK_ARENA;
+                    else if (st != 0)
+                        st = normalize_error_code(st);
+                    else
+                        outbufsize = send_header_ack(q, &ctx, outbuf, (int64_t)stream_id[k]);
+                }
+                /* the real function, on the same decoder and the same blocked count */
+                int status2 = 0;
+                h2o_iovec_t d2 = {NULL, 0};
+                h2o_headers_t hd2 = {NULL, 0, 0};
+                size_t obs2 = 0;
+                uint8_t ob2[16] = {0};
+                uint64_t bref2 = 0;
+                h2o_qpack_section_stats_t st2 = {0};
+                const char *ed2 = NULL;
+                h2o_mem_pool_t pool2;
+                h2o_mem_init_pool(&pool2);
+                int ret2 = h2o_qpack_parse_response(&pool2, q, (int64_t)stream_id[k], &status2, &hd2, &d2, nb, &bref2, &st2,
+                                                    ob2, &obs2, src0, end - src0, &ed2);
+                if (!x.arena_full) {
+                    int ok = (blocked ? (ret2 == 0 && bref2 != 0) : (ret2 == st && bref2 == 0)) && obs2 == outbufsize &&
+                             memcmp(ob2, outbuf, 16) == 0 && status2 == status && hd2.size == headers.size &&
+                             ed2 == err_desc && q3_iov_eq(d2, dfid);
+                    mismatches += !ok;
+                }
+                h2o_mem_clear_pool(&pool2);
+                if (blocked) {
+                    st = REF_QPK_BLOCKED;
+                    ++nb;
+                }
+            }
+            h2o_mem_clear_pool(&pool);
+            nfields[k] = x.nf;
+            sstatus[k] = st;
+            w[0] = (uint32_t)status;
+            w[1] = (uint32_t)headers.size;
+            w[2] = x.hard ? 8u /* HHUFF_HERR_DECODE */ : q3_err_code(err_desc);
+            w[3] = (uint32_t)x.taken[6];
+            w[4] = (uint32_t)outbufsize;
+            w[5] = 0;
+            memcpy(w + 6, outbuf, 16);
         }
     }
     return mismatches;
