@@ -15,6 +15,7 @@
 // Reference semantics: lib/http2/hpack.c:117-156 (decode), :774-804 (encode); see hhuff_device.h.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <mutex>
 
 #include "hhuff_device.h"
@@ -2669,50 +2670,57 @@ __device__ __forceinline__ WaveStep wave_step(const uint8_t* in, uint32_t TB, ui
     }
     return s;
 }
+template <int NC>
 __device__ __forceinline__ DecResult wave_decode(const uint8_t* in, uint32_t len, uint8_t* out, const DecTables& T,
                                                  uint32_t lane) {
+    static_assert(NC == 1 || NC == 2, "one or two candidates per lane");
+    constexpr uint32_t kWin = 64u * NC;
     const uint32_t TB = 8u * len;
     uint32_t W = 0, opos = 0, flags = 0;
     DecResult r;
     r.ok = false;
     for (;;) {
-        const WaveStep a = wave_step(in, TB, W + lane, lane, T), b = wave_step(in, TB, W + 64u + lane, 64u + lane, T);
-        // follow the chain through this round's 128 candidates (scalar: c is wave-uniform)
-        uint64_t on0 = 0, on1 = 0;
+        WaveStep s[NC];
+#pragma unroll
+        for (int j = 0; j < NC; ++j) s[j] = wave_step(in, TB, W + 64u * j + lane, 64u * j + lane, T);
+        // follow the chain through this round's candidates (scalar: c is wave-uniform)
+        uint64_t on[NC];
+#pragma unroll
+        for (int j = 0; j < NC; ++j) on[j] = 0;
         uint32_t c = 0;
         bool end = false;
-        while (c < 128u) {
-            const uint32_t nx = c < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)a.nx, (int)c)
-                                        : (uint32_t)__builtin_amdgcn_readlane((int)b.nx, (int)(c - 64u));
+        while (c < kWin) {
+            const uint32_t nx = NC == 1 || c < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)s[0].nx, (int)(c & 63u))
+                                                   : (uint32_t)__builtin_amdgcn_readlane((int)s[NC - 1].nx, (int)(c & 63u));
             if (nx == kStop) {
                 end = true;
                 break;
             }
-            if (c < 64u) on0 |= 1ull << c;
-            else on1 |= 1ull << (c - 64u);
+            if (NC == 1 || c < 64u) on[0] |= 1ull << (c & 63u);
+            else on[NC - 1] |= 1ull << (c & 63u);
             c = nx;
         }
-        const uint32_t n0 = ((on0 >> lane) & 1u) ? a.ns : 0u, n1 = ((on1 >> lane) & 1u) ? b.ns : 0u;
-        const uint32_t i0 = wave_incl_scan(n0), i1 = wave_incl_scan(n1);
-        const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
-        if (n0) {
-            out[opos + i0 - n0] = (uint8_t)a.syms;
-            if (n0 == 2u) out[opos + i0 - 1u] = (uint8_t)(a.syms >> 8);
-            flags |= a.fl;
+        uint32_t base = opos;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            const uint32_t n = ((on[j] >> lane) & 1u) ? s[j].ns : 0u;
+            const uint32_t incl = wave_incl_scan(n);
+            if (n) {
+                out[base + incl - n] = (uint8_t)s[j].syms;
+                if (n == 2u) out[base + incl - 1u] = (uint8_t)(s[j].syms >> 8);
+                flags |= s[j].fl;
+            }
+            base += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         }
-        if (n1) {
-            out[opos + t0 + i1 - n1] = (uint8_t)b.syms;
-            if (n1 == 2u) out[opos + t0 + i1 - 1u] = (uint8_t)(b.syms >> 8);
-            flags |= b.fl;
-        }
-        opos += t0 + (uint32_t)__builtin_amdgcn_readlane((int)i1, 63);
+        opos = base;
         if (end) {
             // padding: at most 7 bits, all ones (mkhufftbl.py:374-381, hpack.c:132-133); EOS fails (hpack.c:88-89)
-            const bool lo = c < 64u;
-            const uint32_t cl = lo ? c : c - 64u;
-            const uint32_t wc = (uint32_t)__builtin_amdgcn_readlane((int)(lo ? a.w : b.w), (int)cl);
-            const uint32_t Rc = (uint32_t)__builtin_amdgcn_readlane((int)(lo ? a.R : b.R), (int)cl);
-            const uint32_t ec = (uint32_t)__builtin_amdgcn_readlane((int)((lo ? a.eos : b.eos) ? 1u : 0u), (int)cl);
+            const bool lo = NC == 1 || c < 64u;
+            const uint32_t cl = c & 63u;
+            const uint32_t wc = (uint32_t)__builtin_amdgcn_readlane((int)(lo ? s[0].w : s[NC - 1].w), (int)cl);
+            const uint32_t Rc = (uint32_t)__builtin_amdgcn_readlane((int)(lo ? s[0].R : s[NC - 1].R), (int)cl);
+            const uint32_t ec =
+                (uint32_t)__builtin_amdgcn_readlane((int)((lo ? s[0].eos : s[NC - 1].eos) ? 1u : 0u), (int)cl);
             r.ok = ec == 0u && Rc <= 7u && ((wc >> 24) | (0xFFu >> Rc)) == 0xFFu;
             break;
         }
@@ -2745,6 +2753,7 @@ __device__ __forceinline__ void sys_load16x2(const void* pa, const void* pb, uin
         : "memory");
 }
 
+template <int NC>
 __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
                                                      uint64_t idle_ticks, uint64_t max_ticks) {
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
@@ -2811,7 +2820,7 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
                 st = ol == kFailLen ? kStatusFail : 0u;
                 if (ol != kFailLen) ol = (ol + 7u) >> 3;
             } else {
-                const DecResult d = wave_decode(in, len, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane);
+                const DecResult d = wave_decode<NC>(in, len, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane);
                 wave_lds_sync();
                 ol = d.ok ? d.len : kFailLen;
                 st = d.ok ? soft_bits(is_name != 0, d.len, d.flags, d.len ? s_out[0] : 0u, d.len ? s_out[d.len - 1] : 0u)
@@ -2848,7 +2857,14 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
 }
 
 hipError_t launch_service(SvcSlot* slots, SvcCtrl* ctrl, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream) {
-    hipLaunchKernelGGL(service_kernel, dim3(1), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
+    static const int nc = [] {  // decode candidates per lane (HHUFF_SVC_NC=1 or 2; A/B knob)
+        const char* e = getenv("HHUFF_SVC_NC");
+        return e && *e == '2' ? 2 : 1;
+    }();
+    if (nc == 2)
+        hipLaunchKernelGGL(service_kernel<2>, dim3(1), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
+    else
+        hipLaunchKernelGGL(service_kernel<1>, dim3(1), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
     return hipGetLastError();
 }
 
