@@ -120,6 +120,8 @@ def lib():
         L.hhuff_grid_size.restype = ctypes.c_int
         L.hhuff_per_string_calls.restype = ctypes.c_uint64
         L.hhuff_grid_size.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.hhuff_decode_prices.restype = ctypes.c_int
+        L.hhuff_decode_prices.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
         L.hhuff_pool_trim.restype = ctypes.c_int
         L.hhuff_pool_trim.argtypes = []
         _lib = L
@@ -134,7 +136,7 @@ EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decod
             "hhuff_qpack_decode", "hhuff_qpack_parse_requests", "hhuff_qpack_parse_responses", "hhuff_qpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string", "hhuff_per_string_calls",
-            "hhuff_grid_size", "hhuff_pool_trim", "hhuff_service_stamps", "hhuff_hpack_enc_scratch_size",
+            "hhuff_grid_size", "hhuff_decode_prices", "hhuff_pool_trim", "hhuff_service_stamps", "hhuff_hpack_enc_scratch_size",
             "hhuff_hpack_flatten_responses", "hhuff_qpack_flatten_responses")
 
 
@@ -450,7 +452,7 @@ HPE_RESPONSE_DTYPE = np.dtype([("content_length", "<u8"), ("stream_id", "<u4"), 
                                ("hdr_first", "<u4"), ("nhdr", "<u4"), ("header_table_size", "<u4"),
                                ("max_frame_size", "<u4"), ("flags", "<u4"), ("reserved", "<u4")])
 HDR_DONT_COMPRESS, HDR_TOKEN = 1, 2
-RES_END_STREAM, RES_SERVER, RES_TRAILERS = 1, 2, 4
+RES_END_STREAM, RES_SERVER, RES_TRAILERS, RES_REQUEST = 1, 2, 4, 8
 ENC_CONTINUE = 1
 RES_SPACE, RES_SKIPPED, RES_EINVAL = -300, -301, -303
 
@@ -583,3 +585,11 @@ def encode_batch_host_pipelined(data, in_off, n, out=None, chunk_bytes=0, device
                                                    _hp(out_len), _hp(status), device, chunk_bytes),
            "hhuff_encode_batch_host_pipelined")
     return out, out_len[:n], status[:n]
+
+
+def decode_prices(device=0):
+    """the staged / stream prices (ps per string, per byte, each kernel) the mixed-length decode of `device`
+    uses (include/hhuff.h hhuff_decode_prices; measured at first use)"""
+    buf = (ctypes.c_float * 4)()
+    _check(lib().hhuff_decode_prices(device, buf), "hhuff_decode_prices")
+    return [float(x) for x in buf]

@@ -922,6 +922,11 @@ HHUFF_API int hhuff_pool_trim(void) {
     hipError_t e = hhuff::pool_trim();
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "pool trim");
 }
+HHUFF_API int hhuff_decode_prices(int device, float* out4) {
+    if (!out4) return arg_fail("NULL out4");
+    return hhuff::decode_prices_of(device, out4) == 0 ? HHUFF_OK : hip_fail(hipErrorInvalidDevice, "hhuff_decode_prices");
+}
+
 HHUFF_API int hhuff_grid_size(int device, int which) {
     DeviceGuard guard(device);
     if (guard.err != hipSuccess) return -1;

@@ -16,7 +16,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <algorithm>
 #include <mutex>
+#include <vector>
 
 #include "hhuff_device.h"
 #include "hhuff_launch.h"
@@ -209,10 +211,11 @@ __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t 
 constexpr uint32_t kGateStaged = 0u, kGateStream = 1u;
 
 // The staged/stream verdict from decode_select_kernel's partial sums; called by one whole wave.
-// Prices (MI355X, tools/ab.py, ms per 1M strings of fixed length 64..120 B and c3): staged ~ 40 ps per
-// string + 1.07 ps per tile-padded byte (64 x the tile's longest string); stream ~ 184 ps per string +
-// 1.15 ps per byte.
-__device__ __forceinline__ uint32_t select_verdict(const uint64_t* __restrict__ part) {
+// Prices: ps per string and per byte of each kernel (DecArgs::price) -- staged per tile-padded byte (64 x
+// the tile's longest string), stream per byte.  Measured per device at its first mixed-length decode
+// (decode_prices: both kernels timed on two fixed-length probe batches); one MI355X gave ~40 / 1.07 and
+// ~184 / 1.15.
+__device__ __forceinline__ uint32_t select_verdict(const uint64_t* __restrict__ part, const float (&price)[4]) {
     constexpr uint32_t kB = 64;  // kSelBlocks
     const uint32_t lane = threadIdx.x & 63;
     uint64_t pad = part[lane], sum = part[kB + lane], cnt = part[2 * kB + lane];
@@ -222,7 +225,8 @@ __device__ __forceinline__ uint32_t select_verdict(const uint64_t* __restrict__ 
         sum += (uint64_t)__shfl_xor((long long)sum, d);
         cnt += (uint64_t)__shfl_xor((long long)cnt, d);
     }
-    const double staged = 40.0 * (double)cnt + 1.07 * (double)pad, streamed = 184.0 * (double)cnt + 1.15 * (double)sum;
+    const double staged = (double)price[0] * (double)cnt + (double)price[1] * (double)pad,
+                 streamed = (double)price[2] * (double)cnt + (double)price[3] * (double)sum;
     return streamed < staged ? kGateStream : kGateStaged;
 }
 
@@ -327,6 +331,9 @@ struct DecArgs {
     const uint64_t* sel;   // decode_select_kernel's partial sums [3][kSelBlocks] (with gate)
     uint32_t* pk_off;      // packed mode (decode_staged_kernel<.., true>): u32[n + 1] output places
     const uint32_t* n_dev;  // NULL, or the string count in device memory (n an upper bound)
+    // with gate: the staged / stream prices select_verdict uses, ps per string and per (tile-padded) byte --
+    // measured on the device at first use (decode_prices), these fitted values until then
+    float price[4] = {40.0f, 1.07f, 184.0f, 1.15f};
 };
 
 __device__ __forceinline__ void load_dec_tables(uint32_t* s_lut, uint32_t* s_kinfo, uint32_t* s_ones, int nthreads) {
@@ -392,7 +399,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     if (A.gate) {  // mixed-length batch: price both kernels from the sampled tiles (decode_select_kernel)
         __shared__ uint32_t verdict;
         if (threadIdx.x < 64) {
-            const uint32_t g = select_verdict(A.sel);
+            const uint32_t g = select_verdict(A.sel, A.price);
             if (threadIdx.x == 0) {
                 verdict = g;
                 if (blockIdx.x == 0) *A.gate = g;  // read by edge_fix_kernel and the stream kernel, launched after
@@ -2407,6 +2414,92 @@ static int pick_encode(uint64_t in_size, uint32_t n) {
     return kEncD;
 }
 
+// Staged / stream prices of this device (select_verdict), measured once: both kernels decode two probe
+// batches of fixed-length strings (zero bytes: '0' symbols to the end, so every string is decoded whole and
+// then fails its padding), 131,072 x 48 B and 65,536 x 120 B (a 64-string tile of those still fits the
+// staged kernel's stage), timed with events on a private stream (best of 3 after a warm-up); per kernel,
+// per-string and per-byte costs solve t / n = a + b L on the two lengths.  A failed or implausible fit
+// keeps the fitted defaults.  Blocks the calling thread once per device (about 2 ms).
+static void decode_prices(int dev, float out[4]) {
+    static std::mutex mu;
+    static bool done[64] = {};
+    static float cache[64][4];
+    if (dev < 0 || dev >= 64) return;
+    std::lock_guard<std::mutex> g(mu);
+    if (!done[dev]) {
+        done[dev] = true;
+        const float def[4] = {40.0f, 1.07f, 184.0f, 1.15f};
+        for (int k = 0; k < 4; ++k) cache[dev][k] = def[k];
+        constexpr uint32_t kN[2] = {131072u, 65536u}, kL[2] = {48u, 120u};
+        const uint64_t bytes = (uint64_t)kN[1] * kL[1];
+        hipStream_t s = nullptr;
+        uint8_t *in = nullptr, *out = nullptr, *st = nullptr;
+        uint32_t *off = nullptr, *olen = nullptr;
+        unsigned long long* ctr = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+                  hipMalloc((void**)&in, bytes + 64) == hipSuccess && hipMalloc((void**)&out, (bytes * 8) / 5 + 64) == hipSuccess &&
+                  hipMalloc((void**)&st, kN[0]) == hipSuccess && hipMalloc((void**)&off, 4ull * (kN[0] + 1)) == hipSuccess &&
+                  hipMalloc((void**)&olen, 4ull * kN[0]) == hipSuccess && hipMalloc((void**)&ctr, 8) == hipSuccess &&
+                  hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
+                  hipMemsetAsync(in, 0, bytes + 64, s) == hipSuccess;
+        double u[2][2] = {};  // [kernel][probe]: ms per string
+        for (int p = 0; ok && p < 2; ++p) {
+            std::vector<uint32_t> h(kN[p] + 1);
+            for (uint32_t i = 0; i <= kN[p]; ++i) h[i] = i * kL[p];
+            ok = hipMemcpyAsync(off, h.data(), 4ull * (kN[p] + 1), hipMemcpyHostToDevice, s) == hipSuccess &&
+                 hipStreamSynchronize(s) == hipSuccess;
+            DecArgs A{in, (uint64_t)kN[p] * kL[p], off, nullptr, kN[p], nullptr, out, nullptr, olen, st,
+                      nullptr, nullptr, nullptr, nullptr, nullptr};
+            for (int k = 0; ok && k < 2; ++k) {
+                float best = 1e30f;
+                for (int r = 0; ok && r < 4; ++r) {
+                    ok = hipMemsetAsync(ctr, 0, 8, s) == hipSuccess && hipEventRecord(e0, s) == hipSuccess;
+                    if (k == 0)
+                        hipLaunchKernelGGL(DEC_L, dim3(grid_for(kDecL, dev, kN[p])), dim3(384), 0, s, A);
+                    else
+                        hipLaunchKernelGGL(DEC_T, dim3(grid_for(kDecT, dev, kN[p])), dim3(kDecTWaves * 64), 0, s, A, ctr);
+                    float ms = 0.f;
+                    ok = ok && hipGetLastError() == hipSuccess && hipEventRecord(e1, s) == hipSuccess &&
+                         hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+                    if (r > 0) best = std::min(best, ms);  // r == 0 warms up
+                }
+                u[k][p] = best / kN[p];
+            }
+        }
+        if (ok) {
+            float fit[4];
+            for (int k = 0; k < 2; ++k) {
+                const double b = (u[k][1] - u[k][0]) / (double)(kL[1] - kL[0]), a = u[k][0] - b * kL[0];
+                fit[2 * k] = (float)(a * 1e9), fit[2 * k + 1] = (float)(b * 1e9);  // ms -> ps
+            }
+            bool sane = true;
+            for (int k = 0; k < 4; ++k) sane = sane && fit[k] > -50.0f && fit[k] < 5000.0f;
+            sane = sane && fit[1] > 0.0f && fit[3] > 0.0f;
+            if (sane)
+                for (int k = 0; k < 4; ++k) cache[dev][k] = std::max(fit[k], 0.0f);
+        }
+        (void)hipGetLastError();  // a failed probe leaves the defaults and no sticky error
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        for (void* q : {(void*)in, (void*)out, (void*)st, (void*)off, (void*)olen, (void*)ctr})
+            if (q) (void)hipFree(q);
+        if (s) (void)hipStreamDestroy(s);
+    }
+    for (int k = 0; k < 4; ++k) out[k] = cache[dev][k];
+}
+
+int decode_prices_of(int device, float out[4]) {
+    const float def[4] = {40.0f, 1.07f, 184.0f, 1.15f};
+    for (int k = 0; k < 4; ++k) out[k] = def[k];
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return -1;
+    if (device != cur && hipSetDevice(device) != hipSuccess) return -1;
+    decode_prices(device, out);
+    if (device != cur) (void)hipSetDevice(cur);
+    return 0;
+}
+
 hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
                          const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
                          uint8_t* status, hipStream_t stream, uint64_t sel_bytes) {
@@ -2416,6 +2509,7 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     const int grid = grid_for(v, current_device(), n);
     const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr;
     if (v == kDecL) {  // mixed lengths: the device picks staged or stream (see below)
+        decode_prices(current_device(), A.price);
         uint64_t* sel = nullptr;  // [0, 3 kSelBlocks): partial sums; then the verdict and the work counter
         hipError_t e = pool_alloc((void**)&sel, (3 * kSelBlocks + 2) * sizeof(uint64_t), stream);
         if (e != hipSuccess) return e;

@@ -387,7 +387,8 @@ int hhuff_qpack_parse_responses(const uint8_t *in, uint64_t in_size, const uint3
                                 void *scratch, uint64_t scratch_size, unsigned flags, void *stream);
 
 /* (2f) HTTP/2 response header blocks, encode side (SURVEY f4 encode half): h2o_hpack_flatten_response
- *      (lib/http2/hpack.c:1137-1177) and h2o_hpack_flatten_trailers (:1179-1196) for many responses of many
+ *      (lib/http2/hpack.c:1137-1177) and h2o_hpack_flatten_trailers (:1179-1196) -- and, for h2o's HTTP/2
+ *      client (lib/common/http2client.c:1140), h2o_hpack_flatten_request (:1044-1096) -- for many responses of many
  *      connections, with one encoder dynamic table per connection (conn->_output_header_table; do_encode_header
  *      :858-937, at most 32 entries, initial capacity 4096 as lib/http2/connection.c:1847 sets it) kept in
  *      scratch between calls.  A call flattens the responses conn_first[c] .. conn_first[c+1]-1 of every
@@ -400,13 +401,21 @@ int hhuff_qpack_parse_responses(const uint8_t *in, uint64_t in_size, const uint3
  *                    responses must not overlap; headers outside every range are ignored); HHUFF_RES_SERVER
  *                    sends server_name (in[server_off .. + server_len), h2o's globalconf->server_name; clear
  *                    it where h2o passes NULL: informational responses); HHUFF_RES_TRAILERS makes r a trailers
- *                    block (flatten_trailers: no :status, server or content-length, END_STREAM)
+ *                    block (flatten_trailers: no :status, server or content-length, END_STREAM);
+ *                    HHUFF_RES_REQUEST makes r a request (flatten_request: no :status, server or content-length):
+ *                    its first `status` headers are flatten_request's own fields in its order -- :method,
+ *                    :scheme, :authority, :path (an old-style CONNECT, method CONNECT without :protocol, has no
+ *                    :scheme or :path), :protocol if any, "expect: 100-continue" if send_own_expect -- with
+ *                    HHUFF_HDR_TOKEN and no HHUFF_HDR_DONT_COMPRESS; :method GET / POST, :scheme https / http,
+ *                    :path / and /index.html among them, and accept-encoding "gzip, deflate" (token) among the
+ *                    others, are the one-byte static references h2o writes without its table (:950-985,
+ *                    :1083-1086; a scheme named https / http is h2o's H2O_URL_SCHEME_HTTPS / _HTTP)
  *        out         response r's frames (HEADERS, then CONTINUATIONs past max_frame_size, fixup_frame_headers
  *                    :1012-1042) at out + out_off[r]; region [out_off[r], out_off[r+1]) (u64, nres + 1 entries);
  *                    hhuff_hpack_response_bound() is enough for any table state
  *      Per response: out_len[r] = bytes written (frame headers included), headers_size[r] = the payload bytes
  *      (h2o_hpack_flatten_response's return value), rstatus[r] = 0, HHUFF_RES_SPACE (the frames do not fit
- *      the region), HHUFF_RES_EINVAL (status outside 100..999, max_frame_size outside 16384..2^24-1, a string
+ *      the region), HHUFF_RES_EINVAL (status outside 100..999 -- past nhdr for a request --, max_frame_size outside 16384..2^24-1, a string
  *      past in_size) or HHUFF_RES_SKIPPED (an earlier response of the connection failed: its table is no
  *      longer the peer's, h2o would have dropped the connection).  A failed response writes nothing.
  *      Device arrays; scratch = hhuff_hpack_enc_scratch_size(nconn) bytes (16-byte aligned) holding the
@@ -422,7 +431,7 @@ typedef struct hhuff_hpack_header {
 #define HHUFF_HDR_TOKEN 2u
 typedef struct hhuff_hpack_response {
     uint64_t content_length;    /* res.content_length: SIZE_MAX (all ones) sends none */
-    uint32_t stream_id, status; /* status: res.status (ignored for trailers) */
+    uint32_t stream_id, status; /* status: res.status (ignored for trailers; own fields of a request) */
     uint32_t hdr_first, nhdr;
     uint32_t header_table_size; /* conn->peer_settings.header_table_size (header_table_adjust_size, :839-856) */
     uint32_t max_frame_size;    /* conn->peer_settings.max_frame_size */
@@ -432,6 +441,7 @@ typedef struct hhuff_hpack_response {
 #define HHUFF_RES_END_STREAM 1u /* is_end_stream */
 #define HHUFF_RES_SERVER 2u     /* server_name != NULL */
 #define HHUFF_RES_TRAILERS 4u   /* h2o_hpack_flatten_trailers */
+#define HHUFF_RES_REQUEST 8u    /* h2o_hpack_flatten_request (status = the number of its own fields) */
 #define HHUFF_ENC_CONTINUE 1u
 #define HHUFF_RES_SPACE (-300)
 #define HHUFF_RES_SKIPPED (-301)
@@ -508,6 +518,11 @@ const char *hhuff_version(void);
 /* Text of the last HIP error seen by this thread ("" if none). */
 const char *hhuff_last_error_string(void);
 /* Number of workgroups the decode / encode launches use on `device` (grid sizing, for profiling). */
+/* The prices a mixed-length decode (mean Huffman length 41..128 B) uses to choose between the staged and the
+ * stream kernel: out4 = {staged ps per string, staged ps per tile-padded byte, stream ps per string, stream ps
+ * per byte}, measured on `device` at its first mixed-length decode (both kernels timed on two probe batches;
+ * this call runs the measurement if none has run yet, about 2 ms).  HHUFF_OK or an error code. */
+int hhuff_decode_prices(int device, float *out4);
 int hhuff_grid_size(int device, int which /* 0 decode, 1 encode */);
 /* Return the memory the library's stream-ordered pool on the caller's current device keeps between calls
  * (batch workspaces, edge records) to the driver.  Synchronises the device first.  HHUFF_OK or an error. */

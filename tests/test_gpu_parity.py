@@ -305,8 +305,10 @@ def test_streaming_decode_long_mixed(torch_cuda, oracle_codec):
     assert compact(g[0], slots, g[1]) == compact(o[0], slots, o[1])
 
 
-def _select_verdict(lens):
-    """host mirror of decode_select_kernel + select_verdict (hhuff_kernels.hip): 1 = stream kernel"""
+def _select_verdict(lens, prices=(40.0, 1.07, 184.0, 1.15)):
+    """host mirror of decode_select_kernel + select_verdict (hhuff_kernels.hip) with the device's prices
+    (hhuff_decode_prices: staged ps per string / per tile-padded byte, stream ps per string / per byte): 1 =
+    stream kernel"""
     n = len(lens)
     ntiles = (n + 63) // 64
     S = min(ntiles, 256)
@@ -317,7 +319,8 @@ def _select_verdict(lens):
         pad += 64 * int(seg.max())
         tot += int(seg.sum())
         cnt += len(seg)
-    return int(184.0 * cnt + 1.15 * tot < 40.0 * cnt + 1.07 * pad)
+    a_s, b_s, a_t, b_t = (float(x) for x in prices)
+    return int(a_t * cnt + b_t * tot < a_s * cnt + b_s * pad)
 
 
 @pytest.mark.parametrize("lengths,verdict", [(("zipf", 8, 512), 1), (("uniform", 110, 130), 0)])
@@ -335,7 +338,11 @@ def test_mixed_length_decode_select(torch_cuda, oracle_codec, lengths, verdict):
     hdata, hoff = synth.pack(huff)
     m = len(huff)
     assert 40 < hdata.size // m <= 128
-    assert _select_verdict(np.diff(hoff)) == verdict
+    from h2o_amd import codec
+
+    prices = codec.decode_prices(0)  # measured on this device (first use), not the fitted constants
+    assert prices[1] > 0 and prices[3] > 0, prices
+    assert _select_verdict(np.diff(hoff), prices) == verdict, prices
     names = synth.bits_from_bools(rng.random(m) < 0.3)
     g = gpu_decode(torch_cuda, hdata, hoff, m, is_name_bits=names)
     o = oracle_codec.decode_batch(hdata, hoff, m, is_name_bits=names, nthreads=8)

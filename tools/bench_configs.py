@@ -286,6 +286,52 @@ def hpenc_line(torch, codec, nconn=65536):
     return line
 
 
+def responses_line(torch, codec, nconn=65536):
+    """f4, client side: HTTP/2 response blocks as h2o's client receives them (h2o_amd/hpack_synth.py
+    make_response_connections: 1-8 response heads per connection, a tenth of them trailers, 1 % adversarial)
+    through h2o_hpack_parse_response's rules (hhuff_hpack_parse_responses); the CPU baseline runs 4,096 of the
+    connections through the reference's h2o_hpack_parse_response (oracle/_ref, 1 thread)"""
+    import time
+
+    from h2o_amd import hpack_synth as HS
+
+    b = HS.make_response_connections(nconn, seed=9, adversarial_frac=0.01, rule_frac=0.0, trailer_frac=0.1)
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
+    d, bo, cf, tr = dev(b["data"]), dev(b["blk_off"].view(np.int32)), dev(b["conn_first"].view(np.int32)), dev(b["trailers"])
+    L = np.diff(b["blk_off"].astype(np.int64))
+    ao = dev(np.concatenate([[0], np.cumsum(16 * L + 1024)]).astype(np.int64))
+    res = {}
+
+    def run():
+        res["r"] = codec.hpack_decode_blocks(d, bo, cf, 4096, arena_off=ao, in_size=int(b["data"].size), responses=True,
+                                             trailers=tr)
+
+    t = timed(torch, run, steps=10, warmup=2)
+    r = res["r"]
+    nblk = len(b["blk_off"]) - 1
+    nf = int(r["nfields"][:nblk].to(torch.int64).sum().item())
+    W = int(b["data"].size)
+    line = {"config": "responses", "connections": nconn, "blocks": nblk, "trailer_blocks": int(b["trailers"].sum()),
+            "fields": nf, "block_bytes": W, "ok_blocks": int((r["bstatus"][:nblk] == 0).sum().item()),
+            "parse_responses_ms": round(t, 4), "blocks_per_s": round(nblk / (t * 1e-3), 1),
+            "fields_per_s": round(nf / (t * 1e-3), 1), "block_gibps": round(W / GIB / (t * 1e-3), 3)}
+    try:
+        sys.path.insert(0, ROOT)
+        from oracle import oracle as O
+
+        if O.ref_available():
+            m = min(nconn, 4096)
+            k = int(b["conn_first"][m])
+            t0 = time.perf_counter()
+            O.ref().hpack_decode_blocks(b["data"][:int(b["blk_off"][k])], b["blk_off"][:k + 1], b["conn_first"][:m + 1],
+                                        4096, responses=True, trailers=b["trailers"][:k])
+            dt = time.perf_counter() - t0
+            line["cpu"] = {"reference_1thread_blocks_per_s": round(k / dt, 1)}
+    except Exception as e:  # the CPU baseline is a report, not a gate
+        line["cpu_error"] = str(e)
+    return line
+
+
 def main():
     import torch
 
@@ -306,6 +352,10 @@ def main():
         if cfg.startswith("hpenc"):
             n = int(cfg[5:]) if len(cfg) > 5 else 65536
             print(json.dumps(hpenc_line(torch, codec, n)), flush=True)
+            continue
+        if cfg.startswith("resp"):
+            n = int(cfg[4:]) if len(cfg) > 4 else 65536
+            print(json.dumps(responses_line(torch, codec, n)), flush=True)
             continue
         if cfg.startswith("blocks"):
             n = int(cfg[6:]) if len(cfg) > 6 else 65536
