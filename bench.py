@@ -532,12 +532,13 @@ def f4_lines(torch, codec):
     """whole header blocks (65,536 browser-like HTTP/2 connections, h2o_hpack_decode_header per field
     with one dynamic table each, and h2o_hpack_parse_request's rules), one QPACK decoder step (65,536 HTTP/3
     connections: encoder streams, then field sections) and, encode side, HTTP/2 responses of 65,536 connections
-    flattened with their encoder tables (h2o_hpack_flatten_response), and, client side, response blocks through
-    h2o_hpack_parse_response's rules, with their CPU baselines (tools/bench_configs.py)"""
+    flattened with their encoder tables (h2o_hpack_flatten_response), and, client side, requests flattened
+    (h2o_hpack_flatten_request) and response blocks through h2o_hpack_parse_response's rules, with their CPU baselines (tools/bench_configs.py)"""
     import bench_configs as BC
 
     res = {}
     for name, fn in (("blocks", BC.blocks_line), ("qpack", BC.qpack_line), ("hpenc", BC.hpenc_line),
+                     ("reqenc", lambda torch, codec, n: BC.hpenc_line(torch, codec, n, requests=True)),
                      ("responses", BC.responses_line)):
         try:
             res[name] = fn(torch, codec, 65536)

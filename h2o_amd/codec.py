@@ -466,7 +466,7 @@ def hpack_response_bound(name_value_bytes, nhdr, server_len, max_frame_size):
 
 QPE_RESPONSE_DTYPE = np.dtype([("content_length", "<u8"), ("status", "<u4"), ("hdr_first", "<u4"), ("nhdr", "<u4"),
                                ("flags", "<u4"), ("dfid_off", "<u4"), ("dfid_len", "<u4")])
-QRES_DATAGRAM = 8
+QRES_DATAGRAM, QRES_REQUEST = 8, 16
 
 
 def qpack_response_bound(name_value_bytes, nhdr, server_len, dfid_len):

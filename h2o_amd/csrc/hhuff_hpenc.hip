@@ -1,7 +1,7 @@
 // Response header encoders on the GPU (encode side).
 //
-// HTTP/2: h2o_hpack_flatten_response (lib/http2/hpack.c:1137-1177) and h2o_hpack_flatten_trailers
-// (:1179-1196) for many connections, each with its encoder dynamic table (do_encode_header :858-937,
+// HTTP/2: h2o_hpack_flatten_response (lib/http2/hpack.c:1137-1177), h2o_hpack_flatten_trailers
+// (:1179-1196) and, on the client side, h2o_hpack_flatten_request (:1044-1096) for many connections, each with its encoder dynamic table (do_encode_header :858-937,
 // header_table_add :277-317 with at most 32 entries, header_table_adjust_size :839-856).
 // What a field becomes depends on the table, and the table on every earlier field of the connection, so
 // the table work is sequential per connection -- but it needs no output bytes: only lengths and equality.
@@ -54,10 +54,13 @@ constexpr uint32_t kInfoTokDc = 1u << 8;  // token flag dont_compress (cookie, s
 constexpr uint32_t kInfoTok = 1u << 9;
 constexpr uint32_t kInfoHdrDc = 1u << 10;
 constexpr uint32_t kInfoBad = 1u << 11;  // a string past in_size
+constexpr uint32_t kInfoFastShift = 12;  // bits 12-19: h2o_hpack_flatten_request's one-byte reference, 0 = none
+constexpr uint32_t kInfoFastOwn = 1u << 20;  // ... for one of its own fields (:method, :scheme, :path)
 
 // op code of a field
 constexpr uint32_t kOpIndexed = 0, kOpIdxName = 1, kOpNever = 2, kOpNewName = 3;
 constexpr uint32_t kOpAsIs = 1u << 9;  // the value goes as it is (encode_as_is, hpack.c:806-814)
+constexpr uint32_t kOpFast = 1u << 10; // one byte (bits 11-18): flatten_request's static references
 constexpr uint32_t kOpSkip = 1u << 31;
 
 // byte sources of a table entry's name / value
@@ -223,6 +226,22 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uin
     return diff == 0;
 }
 
+// h2o_hpack_flatten_request's one-byte static references (hpack.c:950-985 for its own fields, :1083-1086 for
+// accept-encoding among the headers) as an info word; the walk applies them by the field's place
+__device__ __forceinline__ uint32_t request_fast(const uint8_t* n, uint32_t nl, const uint8_t* v, uint32_t vl) {
+    uint32_t b = 0, own = kInfoFastOwn;
+    if (nl == 7 && lit_eq(n, ":method", 7)) {
+        b = vl == 3 && lit_eq(v, "GET", 3) ? 0x82u : vl == 4 && lit_eq(v, "POST", 4) ? 0x83u : 0u;
+    } else if (nl == 7 && lit_eq(n, ":scheme", 7)) {
+        b = vl == 5 && lit_eq(v, "https", 5) ? 0x87u : vl == 4 && lit_eq(v, "http", 4) ? 0x86u : 0u;
+    } else if (nl == 5 && lit_eq(n, ":path", 5)) {
+        b = vl == 1 && v[0] == '/' ? 0x84u : vl == 11 && lit_eq(v, "/index.html", 11) ? 0x85u : 0u;
+    } else if (nl == 15 && vl == 13 && lit_eq(n, "accept-encoding", 15) && lit_eq(v, "gzip, deflate", 13)) {
+        b = 0x90u, own = 0u;
+    }
+    return b ? (b << kInfoFastShift | own) : 0u;
+}
+
 __device__ __forceinline__ void push_long_bits(const LongWork& L, uint32_t item, uint32_t which) {
     const uint32_t j = atomicAdd(L.bits, 1u);
     if (j < L.cap) L.bits[1 + j] = item << 1 | which;
@@ -256,7 +275,7 @@ __global__ __launch_bounds__(256) void hpe_prep_kernel(HpeArgs A) {
                 for (uint32_t k = 0; k < 61 && sidx == 0; ++k)
                     if (e_static_ent[4 * k + 1] == nl && bytes_eq(e_static_bytes + e_static_ent[4 * k], n, nl)) sidx = k + 1;
                 const bool dc = (nl == 6 && lit_eq(n, "cookie", 6)) || (nl == 10 && lit_eq(n, "set-cookie", 10));
-                info |= kInfoTok | sidx | (dc ? kInfoTokDc : 0u);
+                info |= kInfoTok | sidx | (dc ? kInfoTokDc : 0u) | request_fast(n, nl, v, vl);
             }
         }
         if (nl > kLongStr) {
@@ -521,12 +540,16 @@ __global__ __launch_bounds__(64) void hpe_table_kernel(HpeArgs A) {
         const hhuff_hpack_response_t Rn = A.res[rn];
         const uint64_t base_n = limit, limit_n = A.out_off[rn + 1];
         const bool trailers = (R.flags & HHUFF_RES_TRAILERS) != 0;
-        const bool server = !trailers && (R.flags & HHUFF_RES_SERVER) && A.server_len != 0;
+        const bool request = !trailers && (R.flags & HHUFF_RES_REQUEST);  // h2o_hpack_flatten_request
+        const bool head = !trailers && !request;                          // :status, server, content-length
+        const bool server = head && (R.flags & HHUFF_RES_SERVER) && A.server_len != 0;
         const uint32_t h0 = R.hdr_first, h1 = R.hdr_first + R.nhdr;
+        const uint32_t own_end = request ? h0 + R.status : h0;  // a request's own fields: method .. expect
         int32_t st = 0;
         if (failed) {
             st = HHUFF_RES_SKIPPED;
-        } else if ((!trailers && (R.status < 100 || R.status > 999)) || R.max_frame_size < 16384u ||
+        } else if ((head && (R.status < 100 || R.status > 999)) || (request && R.status > R.nhdr) ||
+                   R.max_frame_size < 16384u ||
                    R.max_frame_size > 0xFFFFFFu || (server && (srv_info & kInfoBad))) {
             st = HHUFF_RES_EINVAL;
         }
@@ -538,7 +561,7 @@ __global__ __launch_bounds__(64) void hpe_table_kernel(HpeArgs A) {
                 su = t.cap;
                 pos += int_len(su, 5);
             }
-            if (!trailers) {
+            if (head) {
                 const uint32_t s = R.status;  // encode_status (:437-466)
                 pos += (s == 200 || s == 204 || s == 206 || s == 304 || s == 400 || s == 404 || s == 500) ? 1u : 5u;
             }
@@ -556,8 +579,14 @@ __global__ __launch_bounds__(64) void hpe_table_kernel(HpeArgs A) {
                     st = HHUFF_RES_EINVAL;  // matters: the connection fails with it)
                     break;
                 }
-                uint32_t l;
-                const uint32_t code = hpe_field(A, t, cur, kSrcIn | cur.noff, kSrcIn | cur.voff, l);
+                uint32_t l, code;
+                const uint32_t fast = (cur.info >> kInfoFastShift) & 0xFFu;
+                if (request && fast && (cur.info & kInfoTok) && ((cur.info & kInfoFastOwn) != 0) == (h < own_end)) {
+                    code = kOpFast | fast << 11;  // encode_method / _scheme / _path, accept-encoding: no table
+                    l = 1;
+                } else {
+                    code = hpe_field(A, t, cur, kSrcIn | cur.noff, kSrcIn | cur.voff, l);
+                }
                 const uint64_t dst = base + 9u + pos;
 #ifndef HHUFF_HPE_NOOPST  // ablation only: what the per-field op stores cost the walk
                 A.op[h] = make_uint4((uint32_t)dst, (uint32_t)(dst >> 32), code, 0u);
@@ -565,7 +594,7 @@ __global__ __launch_bounds__(64) void hpe_table_kernel(HpeArgs A) {
                 pos += l;
                 cur = nxt;
             }
-            if (!trailers && R.content_length != ~0ull) {  // encode_content_length (:468-485)
+            if (head && R.content_length != ~0ull) {  // encode_content_length (:468-485)
                 cll = 3u + digits(R.content_length);
                 pos += cll;
             }
@@ -652,6 +681,10 @@ __device__ __forceinline__ void sink_string(RegSink& sink, const GlobalSource& s
 
 __device__ void emit_field(const GlobalSource& src, uint8_t* dst, uint32_t code, uint32_t noff, uint32_t nl, uint32_t voff,
                            uint32_t vl, uint4 rc, const uint2* enc, const LongWork& L) {
+    if (code & kOpFast) {
+        *dst = (uint8_t)(code >> 11);
+        return;
+    }
     RegSink sink;
     sink.init(dst);
     const uint32_t kind = code & 3u, idx = (code >> 2) & 0x7Fu;
@@ -717,7 +750,7 @@ __global__ __launch_bounds__(256) void hpe_emit_kernel(HpeArgs A) {
         RegSink sink;
         sink.init(base + 9);
         if (p1.x != ~0u) sink_int(sink, 0x20u, p1.x, 5);  // Dynamic Table Size Update (:852-853)
-        if (!trailers) {
+        if (!trailers && !(R.flags & HHUFF_RES_REQUEST)) {
             const uint32_t s = R.status;  // encode_status (:437-466)
             const uint32_t c = s == 200 ? 8 : s == 204 ? 9 : s == 206 ? 10 : s == 304 ? 11 : s == 400 ? 12 : s == 404 ? 13 : s == 500 ? 14 : 0;
             if (c) {
@@ -1039,20 +1072,21 @@ __global__ __launch_bounds__(256) void qpe_size_kernel(QpeArgs A) {
 __global__ __launch_bounds__(256) void qpe_layout_kernel(QpeArgs A) {
     for (uint64_t r = (uint64_t)blockIdx.x * 256u + threadIdx.x; r < A.nres; r += (uint64_t)gridDim.x * 256u) {
         const hhuff_qpack_response_t R = A.res[r];
-        const bool server = (R.flags & HHUFF_RES_SERVER) && A.server_len != 0;
+        const bool request = (R.flags & HHUFF_QRES_REQUEST) != 0;  // h2o_qpack_flatten_request: its own fields are
+        const bool server = !request && (R.flags & HHUFF_RES_SERVER) && A.server_len != 0;  // headers of the list
         const bool dfid = (R.flags & HHUFF_QRES_DATAGRAM) != 0;
         const uint4 sr = A.rec[A.nhdr];
         bool bad = (server && (sr.y & kQBad)) || (dfid && (uint64_t)R.dfid_off + R.dfid_len > A.in_size);
         uint32_t bits;
-        const uint32_t si = q_status_index(R.status);
+        const uint32_t si = request ? 0u : q_status_index(R.status);
         uint32_t st_len = si ? int_len(si, 6) : 0u;
-        if (!si) {
+        if (!si && !request) {
             const uint32_t n = q_digits((uint16_t)R.status, bits);
             st_len = q_local_len(24, n, bits);
         }
         const uint32_t sv_len = server ? q_field_len(sr.y & ~kQBad, 0, A.server_len, 0, sr.w) : 0u;
         uint32_t cl_len = 0;
-        if (R.content_length != ~0ull) {
+        if (!request && R.content_length != ~0ull) {
             if (R.content_length == 0) {
                 cl_len = 1;
             } else {
@@ -1136,10 +1170,12 @@ __global__ __launch_bounds__(256) void qpe_emit_kernel(QpeArgs A) {
         sink.put1(0u);  // Required Insert Count 0
         sink.put1(0u);  // Delta Base 0
         const uint32_t si = q_status_index(R.status);
-        if (si)
+        if (R.flags & HHUFF_QRES_REQUEST) {
+        } else if (si) {
             sink_int(sink, 0xc0u, si, 6);
-        else
+        } else {
             q_emit_local(sink, 24, (uint16_t)R.status, s_enc);
+        }
         if (p1.y) {
             const uint4 sr = A.rec[A.nhdr];
             q_emit_field(sink, src, sr.y & ~kQBad, 0u, 0u, A.server_off, A.server_len, 0u, sr.w, s_enc, A.lw);

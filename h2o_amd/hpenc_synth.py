@@ -18,7 +18,7 @@ Several steps of one session continue the same connections (HHUFF_ENC_CONTINUE).
 import numpy as np
 
 from .codec import HPE_HEADER_DTYPE, HPE_RESPONSE_DTYPE, QPE_RESPONSE_DTYPE, HDR_DONT_COMPRESS, HDR_TOKEN, \
-    QRES_DATAGRAM, RES_END_STREAM, RES_SERVER, RES_TRAILERS, hpack_response_bound, qpack_response_bound
+    QRES_DATAGRAM, QRES_REQUEST, RES_END_STREAM, RES_REQUEST, RES_SERVER, RES_TRAILERS, hpack_response_bound, qpack_response_bound
 
 SERVER = b"h2o/2.3.0-dev"
 _CTYPES = [b"text/html; charset=utf-8", b"text/css", b"application/javascript", b"image/png", b"image/jpeg",
@@ -180,6 +180,120 @@ def make_session(nconn, steps=1, resp_per_conn=(1, 8), seed=0, small_table_frac=
     return out
 
 
+# ---- the client side: h2o_hpack_flatten_request (lib/http2/hpack.c:1044-1096) as lib/common/http2client.c:1140
+# calls it for a proxied request ----
+_REQ_TOKENS = {b"user-agent", b"accept", b"accept-language", b"accept-encoding", b"cookie", b"content-type",
+               b"content-length", b"referer", b"x-forwarded-for", b"via", b"authorization", b"if-none-match",
+               b"if-modified-since", b"origin", b"range", b"cache-control", b"priority", b"forwarded", b"te"}
+_METHODS = [b"GET"] * 75 + [b"POST"] * 10 + [b"HEAD"] * 4 + [b"PUT"] * 3 + [b"DELETE"] * 2 + [b"OPTIONS"] * 2 + \
+    [b"PATCH"] + [b"CONNECT"] * 2 + [b"XCONNECT"]  # XCONNECT: an RFC 9220 extended CONNECT (:protocol)
+_UAS = [b"Mozilla/5.0 (X11; Linux x86_64) AppleWebKit/537.36 (KHTML, like Gecko) Chrome/126.0 Safari/537.36",
+        b"curl/8.5.0", b"h2o/2.3.0-dev", b"Mozilla/5.0 (Macintosh; Intel Mac OS X 14_5) Gecko/20100101 Firefox/127.0"]
+_ACCEPTS = [b"*/*", b"text/html,application/xhtml+xml,application/xml;q=0.9,*/*;q=0.8", b"application/json",
+            b"image/avif,image/webp,*/*"]
+_AES = [b"gzip, deflate"] * 5 + [b"gzip, deflate, br"] * 3 + [b"br", b"identity"]
+
+
+def _client(rng):
+    host = b"%s.example.%s" % (_rand(rng, _B64[26:52], int(rng.integers(3, 10))), [b"com", b"net", b"org"][int(rng.integers(0, 3))])
+    if rng.random() < 0.2:
+        host += b":%d" % int(rng.integers(1024, 65536))
+    return dict(host=host, ua=_UAS[int(rng.integers(0, len(_UAS)))], lang=[b"en-US,en;q=0.9", b"ja,en;q=0.5", b"de-DE"][
+        int(rng.integers(0, 3))], ae=_AES[int(rng.integers(0, len(_AES)))] if rng.random() < 0.9 else None,
+        cookie=b"sid=" + _rand(rng, _B64, int(rng.integers(8, 40))) if rng.random() < 0.4 else None,
+        scheme=b"https" if rng.random() < 0.88 else b"http" if rng.random() < 0.85 else [b"masque", b"ftp", b""][
+            int(rng.integers(0, 3))], xff=b"192.0.2.%d" % int(rng.integers(1, 255)))
+
+
+def _request(rng, cl, big_frac):
+    """-> (own fields, headers, end_stream): flatten_request's own fields in its order, then the headers"""
+    m = _METHODS[int(rng.integers(0, len(_METHODS)))]
+    extended = m == b"XCONNECT"
+    if extended:
+        m = b"CONNECT"
+    own = [(b":method", m)]
+    old_style = m == b"CONNECT" and not extended
+    if not old_style:
+        own.append((b":scheme", cl["scheme"]))
+    own.append((b":authority", cl["host"] if not old_style else b"proxy.example.net:443"))
+    if not old_style:
+        u = rng.random()
+        path = b"/" if u < 0.1 else b"/index.html" if u < 0.15 else b"/chat" if extended else \
+            b"/%s/%s" % (_rand(rng, _B64[26:52], int(rng.integers(2, 8))), _rand(rng, _B64, int(rng.integers(1, 40))))
+        if rng.random() < 0.3 and not extended:
+            path += b"?q=" + _rand(rng, _B64, int(rng.integers(1, 30)))
+        own.append((b":path", path))
+    if extended:
+        own.append((b":protocol", [b"websocket", b"connect-udp", b""][int(rng.integers(0, 3))]))
+    body = m in (b"POST", b"PUT", b"PATCH")
+    if body and rng.random() < 0.3:  # send_own_expect (http2client.c:1135-1136)
+        own.append((b"expect", b"100-continue"))
+    hs = [(b"user-agent", cl["ua"]), (b"accept", _ACCEPTS[int(rng.integers(0, len(_ACCEPTS)))])]
+    if cl["ae"] is not None:
+        hs.append((b"accept-encoding", cl["ae"]))
+    hs.append((b"accept-language", cl["lang"]))
+    if cl["cookie"] is not None:
+        hs.append((b"cookie", cl["cookie"]))
+    if rng.random() < 0.3:
+        hs.append((b"referer", b"https://%s/%s" % (cl["host"], _rand(rng, _B64, int(rng.integers(1, 20))))))
+    if rng.random() < 0.1:
+        hs.append((b"if-none-match", b'"' + _rand(rng, _HEX, 16) + b'"'))
+    if body:
+        hs.append((b"content-type", [b"application/json", b"application/x-www-form-urlencoded"][int(rng.integers(0, 2))]))
+        hs.append((b"content-length", b"%d" % int(rng.integers(0, 1 << 20))))
+    if rng.random() < 0.05:
+        hs.append((b"authorization", b"Bearer " + _rand(rng, _B64, int(rng.integers(5, 60)))))
+    hs.append((b"x-forwarded-for", cl["xff"]))
+    hs.append((b"via", b"2 h2o"))
+    hs.append((b"x-request-id", _rand(rng, _HEX, 32)))
+    if rng.random() < 0.05:  # accept-encoding "gzip, deflate" a second time, then some other value
+        hs.append((b"accept-encoding", b"gzip, deflate"))
+    if rng.random() < big_frac:  # longer than max_frame_size: CONTINUATION frames
+        hs.append((b"cookie", b"; ".join(b"k%d=%s" % (j, _rand(rng, _B64, 24)) for j in range(int(rng.integers(600, 1500))))))
+    end = not body and m != b"CONNECT"
+    return own, hs, end
+
+
+def make_request_session(nconn, steps=1, req_per_conn=(1, 8), seed=0, small_table_frac=0.05, big_frac=0.002,
+                         notoken_frac=0.01, dont_compress_frac=0.01, frame_frac=0.05):
+    """Client requests (HHUFF_RES_REQUEST records: `status` = the number of own fields), one encoder table per
+    upstream connection; same batch layout as make_session"""
+    rng = np.random.default_rng(seed)
+    clients = [_client(rng) for _ in range(nconn)]
+    caps = [4096 if rng.random() >= small_table_frac else int(rng.choice([0, 64, 256, 1024, 2048])) for _ in range(nconn)]
+    mfs = [16384 if rng.random() >= frame_frac else int(rng.choice([1 << 15, 1 << 20, (1 << 24) - 1])) for _ in range(nconn)]
+    sids = [1] * nconn
+    out = []
+    for _ in range(steps):
+        B = _Batch()
+        server_off = B.s(SERVER)
+        conn_first = [0]
+        for c in range(nconn):
+            for _k in range(int(rng.integers(req_per_conn[0], req_per_conn[1] + 1))):
+                if rng.random() < 0.02:
+                    caps[c] = int(rng.choice([0, 128, 512, 1024, 4096, 65536]))
+                own, hs, end = _request(rng, clients[c], big_frac)
+                first = len(B.hdr)
+                for name, value in own:
+                    B.header(name, value, HDR_TOKEN)
+                for name, value in hs:
+                    f = HDR_TOKEN if name in _REQ_TOKENS and rng.random() >= notoken_frac else 0
+                    if rng.random() < dont_compress_frac:
+                        f |= HDR_DONT_COMPRESS
+                    B.header(name, value, f)
+                fl = RES_REQUEST | (RES_END_STREAM if end else 0) | (RES_SERVER if rng.random() < 0.05 else 0)
+                B.res.append((np.uint64(0xFFFFFFFFFFFFFFFF) if rng.random() < 0.9 else int(rng.integers(0, 1 << 30)),
+                              sids[c], len(own), first, len(B.hdr) - first, caps[c], mfs[c], fl, 0))
+                sids[c] += 2
+            conn_first.append(len(B.res))
+        hdr = np.array(B.hdr, dtype=HPE_HEADER_DTYPE) if B.hdr else np.zeros(0, HPE_HEADER_DTYPE)
+        res = np.array(B.res, dtype=HPE_RESPONSE_DTYPE)
+        data = np.frombuffer(b"".join(B.chunks), np.uint8).copy()
+        out.append(dict(data=data, hdr=hdr, res=res, conn_first=np.array(conn_first, np.uint32), server_off=server_off,
+                        server_len=len(SERVER), out_off=out_offsets(hdr, res, len(SERVER))))
+    return out
+
+
 def out_offsets(hdr, res, server_len):
     """[nres + 1] u64 region starts: hhuff_hpack_response_bound per response, 16-byte aligned"""
     nv = (hdr["name_len"].astype(np.int64) + hdr["value_len"]) if hdr.size else np.zeros(0, np.int64)
@@ -256,6 +370,38 @@ def to_qpack(b, seed=0, dfid_frac=0.02, odd_status_frac=0.01):
         data = np.concatenate([data, np.frombuffer(b"".join(extra), np.uint8)])
     return dict(data=data, hdr=b["hdr"], res=res, server_off=b["server_off"], server_len=b["server_len"],
                 out_off=qpack_out_offsets(b["hdr"], res, b["server_len"]))
+
+
+def to_qpack_requests(b, seed=0, dfid_frac=0.05):
+    """make_request_session's requests as HTTP/3 requests (h2o_qpack_flatten_request, lib/http3/qpack.c:1312-1350,
+    as lib/common/http3client.c:792 calls it): HHUFF_QRES_REQUEST records with the same own fields, minus the
+    HTTP/2 client's own "expect" (h2o_qpack_flatten_request has no send_own_expect: it stays as a header), and a
+    datagram flow id on some (CONNECT-UDP, http3client.c:781-785) -> dict data, hdr, res, server_off, server_len,
+    out_off"""
+    rng = np.random.default_rng(seed)
+    src, hdr, data = b["res"], b["hdr"], b["data"]
+    res = np.zeros(src.size, QPE_RESPONSE_DTYPE)
+    for k in ("content_length", "status", "hdr_first", "nhdr"):
+        res[k] = src[k]
+    last = src["hdr_first"].astype(np.int64) + src["status"].astype(np.int64) - 1
+    has_own = src["status"] > 0
+    nl = np.where(has_own, hdr["name_len"][np.maximum(last, 0)], 0)
+    vo = hdr["name_off"][np.maximum(last, 0)].astype(np.int64)
+    expect = has_own & (nl == 6) & np.array([data[o:o + 6].tobytes() == b"expect" for o in vo], bool)
+    res["status"][expect] -= 1
+    res["flags"] = QRES_REQUEST | (src["flags"] & RES_SERVER)  # server: ignored for requests
+    extra = []
+    dfid = rng.random(src.size) < dfid_frac
+    for r in np.flatnonzero(dfid):
+        v = b"%d" % int(rng.integers(0, 1 << 40))
+        res["dfid_off"][r] = data.size + sum(len(e) for e in extra)
+        res["dfid_len"][r] = len(v)
+        extra.append(v)
+    res["flags"][dfid] |= QRES_DATAGRAM
+    if extra:
+        data = np.concatenate([data, np.frombuffer(b"".join(extra), np.uint8)])
+    return dict(data=data, hdr=hdr, res=res, server_off=b["server_off"], server_len=b["server_len"],
+                out_off=qpack_out_offsets(hdr, res, b["server_len"]))
 
 
 def qpack_out_offsets(hdr, res, server_len):

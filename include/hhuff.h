@@ -471,6 +471,11 @@ int hhuff_hpack_flatten_responses(const uint8_t *in, uint64_t in_size, const hhu
  *      the HEADERS frame header (type 0x01, QUIC varint length; finalize_flatten :1265-1310).
  *        header h    hdr[h] as for hhuff_hpack_flatten_responses (HHUFF_HDR_TOKEN, HHUFF_HDR_DONT_COMPRESS); the
  *                    ranges hdr_first .. + nhdr of two responses must not overlap
+ *        request     HHUFF_QRES_REQUEST: h2o_qpack_flatten_request (:1312-1350) as h2o's HTTP/3 client calls it
+ *                    (lib/common/http3client.c:792, no encoder-stream buffer): no :status, server or content-length;
+ *                    the headers start with its own fields as for HHUFF_RES_REQUEST (no expect: HTTP/3 has no
+ *                    send_own_expect), which flatten exactly as token headers do (its static-indexed http / https
+ *                    scheme, :1325-1329, is the static lookup's exact match); datagram-flow-id last as for responses
  *        out         frame r at out + out_off[r]; region [out_off[r], out_off[r+1]) (u64, nres + 1 entries):
  *                    hhuff_qpack_response_bound() always fits
  *      out_len[r] = frame bytes, header_len[r] = *serialized_header_len (the field section, frame header
@@ -479,12 +484,14 @@ int hhuff_hpack_flatten_responses(const uint8_t *in, uint64_t in_size, const hhu
  *      workspace of 24 bytes per header and 32 per response. */
 typedef struct hhuff_qpack_response {
     uint64_t content_length; /* res.content_length: SIZE_MAX (all ones) sends none */
-    uint32_t status;         /* res.status: a static entry, else the decimal of (uint16_t)status against :status */
+    uint32_t status;         /* res.status: a static entry, else the decimal of (uint16_t)status against :status;
+                                HHUFF_QRES_REQUEST: the number of own fields (the bytes do not depend on it) */
     uint32_t hdr_first, nhdr;
     uint32_t flags;          /* HHUFF_RES_SERVER, HHUFF_QRES_DATAGRAM */
     uint32_t dfid_off, dfid_len;
 } hhuff_qpack_response_t;    /* 32 bytes */
 #define HHUFF_QRES_DATAGRAM 8u
+#define HHUFF_QRES_REQUEST 16u /* h2o_qpack_flatten_request: status = the number of its own fields */
 static inline uint64_t hhuff_qpack_response_bound(uint64_t name_value_bytes, uint32_t nhdr, uint32_t server_len,
                                                   uint32_t dfid_len)
 {

@@ -26,12 +26,14 @@ Fixture sets (numpy .npz, arrays only, no pickles):
                    reference's decode_int / decode_huffman / validators / h2o_lookup_token composed as
                    decode_string and decode_header_{name,value}_literal call them (oracle/ref_shim.c)
   hpenc.npz        HTTP/2 response header blocks (f4 encode half): synthetic sessions of responses flattened by
-                   the real h2o_hpack_flatten_response / _trailers with one encoder table per connection
-                   (oracle/ref_hpenc.c), the restatement checked against them as they are written; one session
-                   with invalid arguments and short output regions
+                   the real h2o_hpack_flatten_response / _trailers, and of client requests by the real
+                   h2o_hpack_flatten_request, with one encoder table per connection (oracle/ref_hpenc.c), the
+                   restatement checked against them as they are written; sessions with invalid arguments and
+                   short output regions
   qpenc.npz        HTTP/3 response HEADERS frames (f4, QPACK encode half): synthetic responses (datagram flow ids,
                    statuses outside the static table, dont_compress, names added without their token) flattened by
-                   the real h2o_qpack_flatten_response as h2o's HTTP/3 server calls it (ref_shim.c ref_qpe_step)
+                   the real h2o_qpack_flatten_response as h2o's HTTP/3 server calls it (ref_shim.c ref_qpe_step),
+                   and client requests (CONNECT-UDP datagram flow ids) by the real h2o_qpack_flatten_request
 
 Usage:  python3 oracle/gen_golden.py            (rewrites tests/golden/)
 """
@@ -796,6 +798,11 @@ HPENC_SESSIONS = [  # name, seed, connections, steps, knobs (h2o_amd.hpenc_synth
     ("hedge", 302, 120, 3, dict(small_table_frac=0.3, trailers_frac=0.1, big_frac=0.01, notoken_frac=0.1,
                                 dont_compress_frac=0.15, frame_frac=0.3), False),
     ("herr", 303, 120, 2, dict(small_table_frac=0.1, big_frac=0.005, dont_compress_frac=0.05), True),
+    # client requests (h2o_hpack_flatten_request, hpenc_synth.make_request_session)
+    ("rq4096", 311, 160, 3, dict(requests=True), False),
+    ("rqedge", 312, 120, 3, dict(requests=True, small_table_frac=0.3, big_frac=0.02, notoken_frac=0.1,
+                                 dont_compress_frac=0.15, frame_frac=0.3), False),
+    ("rqerr", 313, 120, 2, dict(requests=True, small_table_frac=0.1, big_frac=0.01, dont_compress_frac=0.05), True),
 ]
 
 
@@ -808,7 +815,7 @@ def hpenc_errors(rng, st):
     for r in rng.choice(n, max(1, n // 40), replace=False):
         regions[r] = int(rng.integers(0, 24))
     for r in rng.choice(n, max(1, n // 80), replace=False):
-        if not res["flags"][r] & 4:
+        if not res["flags"][r] & 12:  # not trailers or requests (a request's `status` counts its own fields)
             res["status"][r] = int(rng.choice([0, 99, 1000]))
     for r in rng.choice(n, max(1, n // 150), replace=False):
         res["max_frame_size"][r] = int(rng.choice([100, 16383, 1 << 24]))
@@ -821,13 +828,16 @@ def hpenc_errors(rng, st):
 
 def hpenc_set():
     """HTTP/2 response header blocks (f4 encode half): sessions of synthetic responses flattened by the
-    real h2o_hpack_flatten_response / _trailers (oracle/ref_hpenc.c), one encoder table per connection
+    real h2o_hpack_flatten_response / _trailers, and of client requests by the real h2o_hpack_flatten_request
+    (oracle/ref_hpenc.c), one encoder table per connection
     across the steps; per step the inputs and the reference's frames (compacted), lengths and statuses"""
     from h2o_amd import hpenc_synth as HE
 
     out = {}
     for name, seed, nconn, nsteps, knobs, errors in HPENC_SESSIONS:
-        steps = HE.make_session(nconn, steps=nsteps, seed=seed, **knobs)
+        knobs = dict(knobs)
+        make = HE.make_request_session if knobs.pop("requests", False) else HE.make_session
+        steps = make(nconn, steps=nsteps, seed=seed, **knobs)
         rng = np.random.default_rng(seed + 7)
         sr, so = O.HpeSession(O.ref(), nconn), O.HpeSession(O.oracle(), nconn)
         out[name + "_meta"] = np.array([nconn, nsteps], np.uint32)
@@ -858,6 +868,9 @@ QPENC_SETS = [  # name, seed, connections, knobs (make_session), to_qpack knobs,
     ("qedge", 402, 200, dict(big_frac=0.01, notoken_frac=0.1, dont_compress_frac=0.15),
      dict(dfid_frac=0.2, odd_status_frac=0.1), False),
     ("qerr", 403, 200, dict(big_frac=0.005), dict(dfid_frac=0.05), True),
+    # client requests (h2o_qpack_flatten_request; hpenc_synth.make_request_session + to_qpack_requests)
+    ("qrq", 411, 300, dict(requests=True, notoken_frac=0.05, dont_compress_frac=0.05), dict(dfid_frac=0.1), False),
+    ("qrqerr", 412, 200, dict(requests=True, big_frac=0.01), dict(dfid_frac=0.05), True),
 ]
 
 
@@ -869,7 +882,11 @@ def qpenc_set():
 
     out = {}
     for name, seed, nconn, knobs, qknobs, errors in QPENC_SETS:
-        q = HE.to_qpack(HE.make_session(nconn, seed=seed, **knobs)[0], seed=seed, **qknobs)
+        knobs = dict(knobs)
+        if knobs.pop("requests", False):
+            q = HE.to_qpack_requests(HE.make_request_session(nconn, seed=seed, **knobs)[0], seed=seed, **qknobs)
+        else:
+            q = HE.to_qpack(HE.make_session(nconn, seed=seed, **knobs)[0], seed=seed, **qknobs)
         if errors:
             rng = np.random.default_rng(seed + 7)
             n = q["res"].size

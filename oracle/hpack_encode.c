@@ -6,7 +6,9 @@
  *                      h2o_hpack_encode_int :757-772, encode_as_is :806-814, h2o_hpack_encode_string
  *                      :816-837 (Huffman through orc_encode_huffman, huff_oracle.c), header_table_adjust_size
  *                      :839-856, do_encode_header :858-937, encode_header :939-942, encode_header_token
- *                      :944-948, fixup_frame_headers :1012-1042, h2o_hpack_flatten_response :1137-1177,
+ *                      :944-948, encode_method / encode_scheme / encode_path :950-985, fixup_frame_headers
+ *                      :1012-1042, h2o_hpack_flatten_request :1044-1096 (the client side, called by
+ *                      lib/common/http2client.c:1140), h2o_hpack_flatten_response :1137-1177,
  *                      h2o_hpack_flatten_trailers :1179-1196
  *   lib/http2/frame.c  h2o_http2_encode_frame_header :68-79
  *   lib/http2/connection.c:1847  a connection's encoder table starts with hpack_capacity 4096
@@ -149,6 +151,25 @@ static uint8_t *hpe_encode_header(hpe_table_t *t, uint8_t *dst, const uint8_t *n
     return dst;
 }
 
+/* The one-byte static references h2o_hpack_flatten_request writes without looking at the table: encode_method
+ * (:950-961), encode_scheme (:963-974; h2o compares the scheme object, whose name is "https" / "http" exactly
+ * for H2O_URL_SCHEME_HTTPS / _HTTP), encode_path (:976-985) for its own fields, and accept-encoding
+ * "gzip, deflate" among the headers (:1083-1086).  0 = none. */
+static uint8_t hpe_request_fast(const uint8_t *n, uint32_t nl, const uint8_t *v, uint32_t vl, int own)
+{
+#define HPE_IS(p, l, lit) ((l) == sizeof(lit) - 1 && memcmp((p), (lit), sizeof(lit) - 1) == 0)
+    if (!own)
+        return HPE_IS(n, nl, "accept-encoding") && HPE_IS(v, vl, "gzip, deflate") ? 0x90 : 0;
+    if (HPE_IS(n, nl, ":method"))
+        return HPE_IS(v, vl, "GET") ? 0x82 : HPE_IS(v, vl, "POST") ? 0x83 : 0;
+    if (HPE_IS(n, nl, ":scheme"))
+        return HPE_IS(v, vl, "https") ? 0x87 : HPE_IS(v, vl, "http") ? 0x86 : 0;
+    if (HPE_IS(n, nl, ":path"))
+        return HPE_IS(v, vl, "/") ? 0x84 : HPE_IS(v, vl, "/index.html") ? 0x85 : 0;
+    return 0;
+#undef HPE_IS
+}
+
 static uint8_t *hpe_frame_header(uint8_t *dst, uint32_t len, uint8_t type, uint8_t flags, uint32_t sid) /* frame.c:68-79 */
 {
     dst[0] = (uint8_t)(len >> 16), dst[1] = (uint8_t)(len >> 8), dst[2] = (uint8_t)len;
@@ -228,10 +249,12 @@ int orc_hpe_step(void *h, const uint8_t *in, uint64_t in_size, const uint32_t *h
                 rstatus[r] = -301; /* HHUFF_RES_SKIPPED */
                 continue;
             }
-            int trailers = (fl & 4u) != 0, bad = 0;
-            if ((!trailers && (status < 100 || status > 999)) || mfs < 16384 || mfs > 0xffffff)
+            /* a request (h2o_hpack_flatten_request): no :status, server or content-length; `status` = the number of
+             * leading headers that are its own fields (method, scheme, authority, path, protocol, expect) */
+            int trailers = (fl & 4u) != 0, request = (fl & 8u) && !trailers, head = !trailers && !request, bad = 0;
+            if ((head && (status < 100 || status > 999)) || (request && status > nh) || mfs < 16384 || mfs > 0xffffff)
                 bad = 1; /* encode_status asserts (:441); SETTINGS_MAX_FRAME_SIZE bounds (RFC 9113 6.5.2) */
-            if ((fl & 2u) && !trailers && (uint64_t)server_off + server_len > in_size)
+            if ((fl & 2u) && head && (uint64_t)server_off + server_len > in_size)
                 bad = 1;
             size_t need = 9 + 5 + 5 + 5 + server_len + 32;
             for (uint32_t i = 0; i < nh; ++i) {
@@ -258,7 +281,7 @@ int orc_hpe_step(void *h, const uint8_t *in, uint64_t in_size, const uint32_t *h
                     hpe_evict_one(t);
                 dst = hpe_int(dst, 0x20, t->capacity, 5);
             }
-            if (!trailers) {
+            if (head) {
                 switch (status) { /* encode_status (:437-466) */
                 case 200: *dst++ = 0x88; break;
                 case 204: *dst++ = 0x89; break;
@@ -277,9 +300,13 @@ int orc_hpe_step(void *h, const uint8_t *in, uint64_t in_size, const uint32_t *h
             }
             for (uint32_t i = 0; i < nh; ++i) {
                 const uint32_t *H = hdr + 5 * (size_t)(hfirst + i);
-                dst = hpe_encode_header(t, dst, in + H[0], H[1], (H[4] & 2u) != 0, in + H[2], H[3], (H[4] & 1u) != 0);
+                uint8_t fast = request && (H[4] & 2u) ? hpe_request_fast(in + H[0], H[1], in + H[2], H[3], i < status) : 0;
+                if (fast)
+                    *dst++ = fast;
+                else
+                    dst = hpe_encode_header(t, dst, in + H[0], H[1], (H[4] & 2u) != 0, in + H[2], H[3], (H[4] & 1u) != 0);
             }
-            if (!trailers && content_length != UINT64_MAX) { /* encode_content_length (:468-485) */
+            if (head && content_length != UINT64_MAX) { /* encode_content_length (:468-485) */
                 char d[24];
                 int l = 0;
                 uint64_t v = content_length;
@@ -297,7 +324,7 @@ int orc_hpe_step(void *h, const uint8_t *in, uint64_t in_size, const uint32_t *h
                 t->failed = 1;
                 continue;
             }
-            uint8_t flags = (trailers || (fl & 1u)) ? 0x1 : 0; /* END_STREAM (:1174-1175, :1195) */
+            uint8_t flags = (trailers || (fl & 1u)) ? 0x1 : 0; /* END_STREAM (:1094-1095, :1174-1175, :1195) */
             uint64_t got = hpe_frames(tmp, payload, 0x1, sid, mfs, flags);
             (void)got;
             memcpy(out + out_off[r], tmp, total);

@@ -2,7 +2,11 @@
  * ORACLE -- TEST INFRASTRUCTURE ONLY.  Clean-room CPU restatement of h2o's HTTP/3 response encoder (SURVEY.md 8
  * f4, QPACK encode half), the contract of include/hhuff.h hhuff_qpack_flatten_responses:
  *   lib/http3/qpack.c  h2o_qpack_flatten_response :1352-1399 as h2o's HTTP/3 server calls it
- *                      (lib/http3/server.c:1680-1683: no encoder-stream buffer), prepare_flatten :1247-1263,
+ *                      (lib/http3/server.c:1680-1683: no encoder-stream buffer), h2o_qpack_flatten_request
+ *                      :1312-1350 as h2o's HTTP/3 client calls it (lib/common/http3client.c:792, no encoder-stream
+ *                      buffer either; its own fields are token fields of the request's header list, and its
+ *                      flatten_static_indexed 22 / 23 for the http / https scheme objects equals the generic
+ *                      lookup's exact match), prepare_flatten :1247-1263,
  *                      flatten_static_indexed :1086-1094, flatten_static_nameref :1114-1120,
  *                      flatten_without_nameref :1138-1146, do_flatten_header :1148-1213, flatten_header
  *                      :1215-1228, flatten_known_header_with_static_lookup :1230-1238, finalize_flatten
@@ -119,7 +123,8 @@ int orc_qpe_step(const uint8_t *in, uint64_t in_size, const uint32_t *hdr, const
         uint64_t content_length;
         memcpy(&content_length, R, 8);
         uint32_t status = R[2], hfirst = R[3], nh = R[4], fl = R[5], doff = R[6], dlen = R[7];
-        int server = (fl & 2u) && server_len != 0, dfid = (fl & 8u) != 0;
+        int request = (fl & 16u) != 0; /* flatten_request: no :status, server or content-length */
+        int server = !request && (fl & 2u) && server_len != 0, dfid = (fl & 8u) != 0;
         out_len[r] = header_len[r] = 0;
         int bad = (server && (uint64_t)server_off + server_len > in_size) || (dfid && (uint64_t)doff + dlen > in_size);
         size_t need = 64 + server_len + dlen;
@@ -140,7 +145,8 @@ int orc_qpe_step(const uint8_t *in, uint64_t in_size, const uint32_t *hdr, const
         uint8_t *p = tmp;
         *p++ = 0, *p++ = 0; /* Required Insert Count 0, Delta Base 0 (finalize_flatten :1290-1301) */
         uint32_t si = qpe_status_index(status);
-        if (si) {
+        if (request) {
+        } else if (si) {
             p = qpe_int(p, 0xc0, si, 6);
         } else { /* :1379-1383: "%u" of (uint16_t)status against :status (24) */
             char d[8];
@@ -149,7 +155,7 @@ int orc_qpe_step(const uint8_t *in, uint64_t in_size, const uint32_t *hdr, const
         }
         if (server) /* :1387-1389, the server entry 92 */
             p = qpe_field(p, 92, 0, NULL, 0, in + server_off, server_len, 0);
-        if (content_length != UINT64_MAX) { /* :1391-1399 */
+        if (!request && content_length != UINT64_MAX) { /* :1391-1399 */
             if (content_length == 0) {
                 p = qpe_int(p, 0xc0, 4, 6);
             } else {

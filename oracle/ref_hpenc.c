@@ -11,7 +11,11 @@
  * conn->_output_header_table; a step flattens every connection's responses in order, as
  * lib/http2/stream.c:311-314 (final responses, server_name given) / :404-406 (informational, no server
  * name) and lib/http2/connection.c:1580-1582 (trailers) call them, into the caller's output slots -- the
- * contract of include/hhuff.h hhuff_hpack_flatten_responses.
+ * contract of include/hhuff.h hhuff_hpack_flatten_responses.  Request records (flag 8) go through the real
+ * h2o_hpack_flatten_request (:1044-1096) as lib/common/http2client.c:1140 calls it: their own fields (the first
+ * `status` headers) are turned back into its arguments -- method, the url's scheme object (H2O_URL_SCHEME_HTTPS /
+ * _HTTP for "https" / "http", so h2o's pointer comparison sees them), authority and path, protocol, and
+ * send_own_expect for a trailing "expect: 100-continue".
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -21,6 +25,8 @@
 #include "h2o/http2_common.h"
 #include "h2o/memory.h"
 #include "h2o/token.h"
+#include "h2o/url.h"
+#include "ref_request_args.h"
 
 #define REF_API __attribute__((visibility("default")))
 
@@ -53,6 +59,18 @@ REF_API void ref_hpe_close(void *h)
     free(s);
 }
 
+/* the HEADERS (+ CONTINUATION) frames' payload bytes */
+static size_t frames_payload(const uint8_t *p, size_t size)
+{
+    size_t off = 0, sum = 0;
+    while (off + 9 <= size) {
+        size_t len = (size_t)p[off] << 16 | (size_t)p[off + 1] << 8 | p[off + 2];
+        sum += len;
+        off += 9 + len;
+    }
+    return sum;
+}
+
 /* Returns 0, or the number of headers flagged HHUFF_HDR_TOKEN whose name is not an h2o token (a caller
  * error: nothing is flattened then). */
 REF_API int ref_hpe_step(void *h, const uint8_t *in, uint64_t in_size, const uint32_t *hdr, const uint32_t *res,
@@ -69,6 +87,15 @@ REF_API int ref_hpe_step(void *h, const uint8_t *in, uint64_t in_size, const uin
             if ((H[4] & 2u) && h2o_lookup_token((const char *)in + H[0], H[1]) == NULL)
                 ++bad_tokens;
         }
+        /* a request's own fields must be flatten_request's arguments (a string past in_size is refused later) */
+        int in_bounds = 1;
+        for (uint32_t i = 0; i < R[5]; ++i) {
+            const uint32_t *H = hdr + 5 * (size_t)(R[4] + i);
+            in_bounds &= (uint64_t)H[0] + H[1] <= in_size && (uint64_t)H[2] + H[3] <= in_size;
+        }
+        ref_req_t a;
+        if ((R[8] & 8u) && !(R[8] & 4u) && in_bounds && (R[3] > R[5] || ref_req_args(in, hdr, R[4], R[3], 1, &a) != 0))
+            ++bad_tokens;
     }
     if (bad_tokens)
         return bad_tokens;
@@ -80,15 +107,15 @@ REF_API int ref_hpe_step(void *h, const uint8_t *in, uint64_t in_size, const uin
             uint64_t content_length;
             memcpy(&content_length, R, 8);
             uint32_t sid = R[2], status = R[3], hfirst = R[4], nh = R[5], cap = R[6], mfs = R[7], fl = R[8];
-            int trailers = (fl & 4u) != 0;
+            int trailers = (fl & 4u) != 0, request = (fl & 8u) && !trailers;
             out_len[r] = 0;
             headers_size[r] = 0;
             if (s->failed[c]) {
                 rstatus[r] = -301;
                 continue;
             }
-            int bad = (!trailers && (status < 100 || status > 999)) || mfs < 16384 || mfs > 0xffffff ||
-                      ((fl & 2u) && !trailers && (uint64_t)server_off + server_len > in_size);
+            int bad = (!trailers && !request && (status < 100 || status > 999)) || mfs < 16384 || mfs > 0xffffff ||
+                      ((fl & 2u) && !trailers && !request && (uint64_t)server_off + server_len > in_size);
             h2o_iovec_t *names = calloc(nh ? nh : 1, sizeof(h2o_iovec_t));
             h2o_header_t *headers = calloc(nh ? nh : 1, sizeof(h2o_header_t));
             for (uint32_t i = 0; i < nh; ++i) {
@@ -115,7 +142,13 @@ REF_API int ref_hpe_step(void *h, const uint8_t *in, uint64_t in_size, const uin
             size_t hs = 0;
             if (trailers) {
                 h2o_hpack_flatten_trailers(&buf, t, cap, sid, mfs, headers, nh);
-                hs = buf->size - 9;
+                hs = frames_payload((const uint8_t *)buf->bytes, buf->size);
+            } else if (request) {
+                ref_req_t a;
+                ref_req_args(in, hdr, hfirst, status, 1, &a);
+                h2o_hpack_flatten_request(&buf, t, cap, sid, mfs, a.method, &a.url, a.protocol, headers + status, nh - status,
+                                          fl & 1u, a.expect);
+                hs = frames_payload((const uint8_t *)buf->bytes, buf->size);
             } else {
                 hs = h2o_hpack_flatten_response(&buf, t, cap, sid, mfs, (int)status, headers, nh,
                                                 (fl & 2u) ? &server_name : NULL,

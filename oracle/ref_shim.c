@@ -15,6 +15,7 @@
  * run h2o's own callers through it.  Built only where /root/reference exists.
  */
 #include "lib/http3/qpack.c"
+#include "ref_request_args.h"
 
 #define REF_API __attribute__((visibility("default")))
 
@@ -586,6 +587,8 @@ REF_API int ref_qpack_step_resp(void *h, const uint8_t *in, const uint32_t *enc_
  * into the encoder's table), the globalconf server name, the response's content length and datagram flow id.
  * One response after another into the caller's output slots: the include/hhuff.h hhuff_qpack_flatten_responses
  * contract (res = hhuff_qpack_response_t, 8 u32 words; hdr = hhuff_hpack_header_t, 5 words). */
+/* Request records (flag 16) go through the real h2o_qpack_flatten_request (:1312-1350) as lib/common/http3client.c:792
+ * calls it, their own fields turned back into its arguments (ref_request_args.h). */
 REF_API int ref_qpe_step(const uint8_t *in, uint64_t in_size, const uint32_t *hdr, const uint32_t *res, uint32_t nres,
                          uint32_t server_off, uint32_t server_len, uint8_t *out, const uint64_t *out_off, uint32_t *out_len,
                          uint32_t *header_len, int32_t *rstatus)
@@ -598,7 +601,8 @@ REF_API int ref_qpe_step(const uint8_t *in, uint64_t in_size, const uint32_t *hd
         uint64_t content_length;
         memcpy(&content_length, R, 8);
         uint32_t status = R[2], hfirst = R[3], nh = R[4], fl = R[5], doff = R[6], dlen = R[7];
-        int server = (fl & 2u) && server_len != 0, dfid = (fl & 8u) != 0;
+        int request = (fl & 16u) != 0;
+        int server = !request && (fl & 2u) && server_len != 0, dfid = (fl & 8u) != 0;
         out_len[r] = header_len[r] = 0;
         int bad = (server && (uint64_t)server_off + server_len > in_size) || (dfid && (uint64_t)doff + dlen > in_size);
         h2o_iovec_t *names = calloc(nh ? nh : 1, sizeof(h2o_iovec_t));
@@ -626,10 +630,23 @@ REF_API int ref_qpe_step(const uint8_t *in, uint64_t in_size, const uint32_t *hd
             h2o_iovec_t dv = dfid ? h2o_iovec_init(in + doff, dlen) : h2o_iovec_init(NULL, 0);
             if (dfid && dv.base == NULL)
                 dv.base = (char *)"";
-            h2o_iovec_t f = h2o_qpack_flatten_response(enc, &pool, 4 * (int64_t)r, NULL, (int)status, headers, nh,
-                                                       server ? &server_name : NULL,
-                                                       content_length == UINT64_MAX ? SIZE_MAX : (size_t)content_length, dv,
-                                                       &stats, &shl);
+            h2o_iovec_t f;
+            ref_req_t a;
+            if (request && (status > nh || ref_req_args(in, hdr, hfirst, status, 0, &a) != 0)) {
+                ++bad_tokens; /* not flatten_request's arguments: a caller error */
+                f = h2o_iovec_init(NULL, 0);
+            } else if (request) {
+                f = h2o_qpack_flatten_request(enc, &pool, 4 * (int64_t)r, NULL, a.method, a.url.scheme, a.url.authority,
+                                              a.url.path, a.protocol, headers + status, nh - status, dv, &stats);
+                unsigned t = (uint8_t)f.base[1] >> 6;
+                uint64_t v = t == 0 ? 1 : t == 1 ? 2 : t == 2 ? 4 : 8;
+                shl = f.len - 1 - v; /* the field section: the frame minus its type and length (finalize_flatten) */
+            } else {
+                f = h2o_qpack_flatten_response(enc, &pool, 4 * (int64_t)r, NULL, (int)status, headers, nh,
+                                               server ? &server_name : NULL,
+                                               content_length == UINT64_MAX ? SIZE_MAX : (size_t)content_length, dv,
+                                               &stats, &shl);
+            }
             if (f.len > out_off[r + 1] - out_off[r]) {
                 rstatus[r] = -300;
             } else {

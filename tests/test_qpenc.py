@@ -6,7 +6,10 @@ restatement (oracle/qpack_encode.c) against the reference's frames (tests/golden
 oracle/ref_shim.c ref_qpe_step) and against the reference directly on fresh responses, and a round trip: every
 section decoded again by the QPACK decoder restatement gives back the response's fields.
 GPU: hhuff_qpack_flatten_responses through the C-ABI against the fixtures, fresh edge-heavy responses against
-the restatement, and a bench-sized batch (about 290,000 responses) byte for byte."""
+the restatement, and a bench-sized batch (about 290,000 responses) byte for byte.
+Requests (HHUFF_QRES_REQUEST): h2o_qpack_flatten_request (:1312-1350) as h2o's HTTP/3 client calls it
+(lib/common/http3client.c:792) -- fixtures, the reference directly (incl. the request of the reference's own
+t/00unit/lib/http3/qpack.c:65-67), a round trip through the decoder restatement, the GPU against all three."""
 import numpy as np
 import pytest
 
@@ -14,7 +17,7 @@ from conftest import load_golden
 from h2o_amd import codec as C
 from h2o_amd import hpenc_synth as HE
 
-SETS = ["q1", "qedge", "qerr"]
+SETS = ["q1", "qedge", "qerr", "qrq", "qrqerr"]
 KEYS = ("out_len", "header_len", "rstatus")
 
 
@@ -82,6 +85,44 @@ def test_restatement_vs_reference(oracle_codec, seed):
     check(ostep(O.oracle(), q), q, want=ostep(O.ref(), q))
 
 
+def unit_request():
+    """t/00unit/lib/http3/qpack.c:61-67: GET https example.com /foobar, dnt: 1 and x-hoge: A added by string
+    (h2o_add_header_by_str with maybe_token 0: not tokens), no encoder stream (the enc_stream == NULL case)"""
+    TOK = C.HDR_TOKEN
+    own = [(b":method", b"GET", TOK), (b":scheme", b"https", TOK), (b":authority", b"example.com", TOK),
+           (b":path", b"/foobar", TOK)]
+    b = HE.build_batch([[dict(status=4, flags=C.RES_REQUEST, headers=own + [(b"dnt", b"1", 0), (b"x-hoge", b"A", 0)])]])
+    return HE.to_qpack_requests(b, dfid_frac=0.0)
+
+
+@pytest.mark.parametrize("seed", [33, 34])
+def test_requests_restatement_vs_reference(oracle_codec, seed):
+    from oracle import oracle as O
+
+    if not O.ref_available():
+        pytest.skip("oracle/_ref not built (needs /root/reference)")
+    b = HE.make_request_session(200, seed=seed, big_frac=0.01, notoken_frac=0.1, dont_compress_frac=0.1)[0]
+    q = HE.to_qpack_requests(b, seed=seed, dfid_frac=0.2)
+    check(ostep(O.oracle(), q), q, want=ostep(O.ref(), q))
+    u = unit_request()
+    check(ostep(O.oracle(), u), u, want=ostep(O.ref(), u))
+
+
+def test_unit_request_bytes(oracle_codec):
+    """the unit test's request: :method GET (17), :scheme https (23) static; :authority (0) and :path (1) name
+    references with Huffman values; dnt and x-hoge literals with literal names"""
+    from oracle import oracle as O
+
+    u = unit_request()
+    r = ostep(O.oracle(), u)
+    f = r["out"][:int(r["out_len"][0])].tobytes()
+    n, p = _varint(f, 1)
+    sec = f[p:]
+    assert sec[:4] == bytes([0, 0, 0xC0 | 17, 0xC0 | 23])
+    assert sec[4] == 0x50 and sec[5] & 0x80  # :authority (static 0), Huffman value
+    assert n == len(sec) == r["header_len"][0]
+
+
 def _varint(b, p):
     n = 1 << (b[p] >> 6)
     v = b[p] & 0x3F
@@ -134,6 +175,40 @@ def test_round_trip(oracle_codec):
         assert got == fl, k
 
 
+def test_requests_round_trip(oracle_codec):
+    """request sections decoded by the QPACK decoder restatement give back the own fields, the headers and the
+    datagram-flow-id, in order"""
+    from oracle import oracle as O
+
+    b = HE.make_request_session(150, seed=43, big_frac=0.0, dont_compress_frac=0.1)[0]
+    q = HE.to_qpack_requests(b, seed=43, dfid_frac=0.2)
+    r = ostep(O.oracle(), q)
+    data = q["data"].tobytes()
+    sections, want = [], []
+    for k in range(q["res"].size):
+        f = r["out"][int(q["out_off"][k]):int(q["out_off"][k]) + int(r["out_len"][k])].tobytes()
+        n, p = _varint(f, 1)
+        sections.append(f[p:])
+        R = q["res"][k]
+        fl = [(data[h["name_off"]:h["name_off"] + h["name_len"]], data[h["value_off"]:h["value_off"] + h["value_len"]])
+              for h in q["hdr"][int(R["hdr_first"]):int(R["hdr_first"]) + int(R["nhdr"])]]
+        if R["flags"] & C.QRES_DATAGRAM:
+            fl.append((b"datagram-flow-id", data[R["dfid_off"]:R["dfid_off"] + R["dfid_len"]]))
+        want.append(fl)
+    blob = b"".join(sections)
+    sec_off = np.concatenate([[0], np.cumsum([len(s) for s in sections])]).astype(np.uint32)
+    arena_off = np.concatenate([[0], np.cumsum([4 * len(x) + 256 for x in sections])]).astype(np.uint64)
+    d = O.QpackSession(O.oracle(), 1).step(np.frombuffer(blob, np.uint8), np.zeros(1, np.uint32), np.zeros(1, np.uint32),
+                                           sec_off, np.array([0, len(sections)], np.uint32), arena_off)
+    assert (d["sstatus"][:len(sections)] == 0).all()
+    a = d["arena"]
+    for k, fl in enumerate(want):
+        got = [(a[d["name_off"][f]:d["name_off"][f] + d["name_len"][f]].tobytes(),
+                a[d["value_off"][f]:d["value_off"][f] + d["value_len"][f]].tobytes())
+               for f in range(int(sec_off[k]), int(sec_off[k]) + int(d["nfields"][k]))]
+        assert got == fl, k
+
+
 # ---------------------------------------------------------------------------------------------------
 # GPU
 # ---------------------------------------------------------------------------------------------------
@@ -176,6 +251,18 @@ def test_gpu_vs_restatement(torch_cuda, oracle_codec, seed):
     q = HE.to_qpack(HE.make_session(600, seed=seed, big_frac=0.01, notoken_frac=0.1, dont_compress_frac=0.1)[0],
                     seed=seed, dfid_frac=0.2, odd_status_frac=0.1)
     check(gpu(torch_cuda, q), q, want=ostep(O.oracle(), q))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [53, 54])
+def test_gpu_requests_vs_restatement(torch_cuda, oracle_codec, seed):
+    from oracle import oracle as O
+
+    b = HE.make_request_session(600, seed=seed, big_frac=0.01, notoken_frac=0.1, dont_compress_frac=0.1)[0]
+    q = HE.to_qpack_requests(b, seed=seed, dfid_frac=0.2)
+    check(gpu(torch_cuda, q), q, want=ostep(O.oracle(), q))
+    u = unit_request()
+    check(gpu(torch_cuda, u), u, want=ostep(O.oracle(), u))
 
 
 @pytest.mark.gpu

@@ -5,6 +5,7 @@
   c5  512K QPACK values mean 512 B (cookie/URI charset), encode only with flatten_string(prefix 7) framing
   hpenc[N]   f4 encode half: HTTP/2 responses of N connections (default 65536) flattened with their encoder
              tables (hhuff_hpack_flatten_responses)
+  reqenc[N]  the same for the client's requests (h2o_hpack_flatten_request)
   blocks[N]  f4: N synthetic HPACK connections (default 65536), header blocks decoded with a dynamic
       table per connection; CPU baselines: the reference (1 thread) and the restatement (16 threads)
   lit 16M c4 strings framed as HPACK literals (h2o_hpack_encode_string), then decoded as literals
@@ -231,17 +232,18 @@ def qpack_line(torch, codec, nconn=65536):
     return line
 
 
-def hpenc_line(torch, codec, nconn=65536):
+def hpenc_line(torch, codec, nconn=65536, requests=False):
     """f4 encode half: HTTP/2 response header blocks (h2o_amd/hpenc_synth.py: 4,096 synthetic connections of 1-8
     responses tiled to nconn, 1 % edge cases) flattened as h2o_hpack_flatten_response / _trailers do, one encoder
     table per connection; the CPU baselines run the 4,096 distinct connections through the reference's
-    h2o_hpack_flatten_response (oracle/_ref, 1 thread) and the restatement (1 thread)"""
+    h2o_hpack_flatten_response (oracle/_ref, 1 thread) and the restatement (1 thread).  requests=True: the
+    client's requests instead (make_request_session, h2o_hpack_flatten_request)"""
     import time
 
     from h2o_amd import hpenc_synth as HE
 
     big = float(os.environ.get("HHUFF_HPENC_BIG", "0.001"))  # A/B knob: share of responses past max_frame_size
-    base = HE.make_session(4096, seed=13, big_frac=big)[0]
+    base = (HE.make_request_session(4096, seed=13, big_frac=big) if requests else HE.make_session(4096, seed=13, big_frac=big))[0]
     b = HE.tile(base, max(1, nconn // 4096))
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
     d, hd, rs = dev(b["data"]), dev(b["hdr"].view(np.uint8)), dev(b["res"].view(np.uint8))
@@ -259,9 +261,9 @@ def hpenc_line(torch, codec, nconn=65536):
     r = res["r"]
     frame_bytes = int(r["out_len"][:nres].to(torch.int64).sum().item())
     field_bytes = int(b["hdr"]["name_len"].astype(np.int64).sum() + b["hdr"]["value_len"].astype(np.int64).sum())
-    line = {"config": "hpenc", "connections": nc, "responses": nres, "fields": nhdr, "field_bytes": field_bytes,
+    line = {"config": "reqenc" if requests else "hpenc", "connections": nc, ("requests" if requests else "responses"): nres, "fields": nhdr, "field_bytes": field_bytes,
             "frame_bytes": frame_bytes, "ok_responses": int((r["rstatus"][:nres] == 0).sum().item()),
-            "flatten_ms": round(t, 4), "responses_per_s": round(nres / (t * 1e-3), 1),
+            "flatten_ms": round(t, 4), ("requests_per_s" if requests else "responses_per_s"): round(nres / (t * 1e-3), 1),
             "fields_per_s": round(nhdr / (t * 1e-3), 1), "field_gibps": round(field_bytes / GIB / (t * 1e-3), 3)}
     try:
         sys.path.insert(0, ROOT)
@@ -279,7 +281,7 @@ def hpenc_line(torch, codec, nconn=65536):
             s.step(*args)
             dt = time.perf_counter() - t0
             s.close()
-            cpu[kind + "_1thread_responses_per_s"] = round(n0 / dt, 1)
+            cpu[kind + ("_1thread_requests_per_s" if requests else "_1thread_responses_per_s")] = round(n0 / dt, 1)
         line["cpu"] = cpu
     except Exception as e:  # the CPU baseline is a report, not a gate
         line["cpu_error"] = str(e)
@@ -348,6 +350,10 @@ def main():
         if cfg.startswith("qpack"):
             n = int(cfg[5:]) if len(cfg) > 5 else 65536
             print(json.dumps(qpack_line(torch, codec, n)), flush=True)
+            continue
+        if cfg.startswith("reqenc"):
+            n = int(cfg[6:]) if len(cfg) > 6 else 65536
+            print(json.dumps(hpenc_line(torch, codec, n, requests=True)), flush=True)
             continue
         if cfg.startswith("hpenc"):
             n = int(cfg[5:]) if len(cfg) > 5 else 65536
