@@ -76,7 +76,7 @@ def kernel_key(name):
     if "decode_staged_kernel" in name or "decode_stream_kernel" in name or "decode_direct_kernel" in name:
         return "decode_packed" if packed else "decode"
     if ("encode_staged_kernel" in name or "encode_pl_kernel" in name or "encode_direct_kernel" in name or
-            "encode_cp_kernel" in name):
+            "encode_cp_kernel" in name or "encode_sorted_kernel" in name):
         return "encode_packed" if packed else "encode"
     if "flatten_pl_kernel" in name or "flatten_direct_kernel" in name:
         return "flatten"

@@ -1444,6 +1444,158 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
     }
 }
 
+// Length-sorted chunks (contiguous layout, deferred edges).  A staged tile of 64 consecutive strings runs
+// as long as its longest string (U[24,72]: 71 of the mean 48 bytes' steps).  Here a workgroup stages the
+// span of NS consecutive strings once (coalesced), counting-sorts their lengths in LDS and gives each of
+// its waves 64 strings of about one length, so a wave's lock-step lasts about as long as its strings (wave
+// w takes the w-th length group).  Two workgroups share a CU: while one waits at a barrier for its longest
+// group, the other's waves keep the SIMDs busy.  Every string is encoded in place in the chunk's output
+// stage (slot = input offset), which is then copied out whole.
+constexpr uint32_t kSortBins = 128;  // whole dwords 0..126, and 127+
+struct SortChunk {  // per thread: its string of a chunk and the chunk's input span
+    uint32_t s, e, lo, hi;
+};
+__device__ __forceinline__ SortChunk sort_chunk_issue(const EncArgs& A, uint64_t cb, uint32_t t, uint32_t ns) {
+    const uint64_t ic = min(cb + t, (uint64_t)A.n - 1u);  // clamped: every load issues
+    return SortChunk{A.in_off[ic], A.in_off[ic + 1], A.in_off[min(cb, (uint64_t)A.n - 1u)],
+                     A.in_off[min(cb + ns, (uint64_t)A.n)]};
+}
+// NS strings per chunk, one thread each (NS / 64 waves); CH bytes of stage
+template <int NS, int CH>
+__global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
+    constexpr uint32_t kSortStr = NS;
+    constexpr int NV = (CH + 16 * NS - 1) / (16 * NS);  // 16-B span chunks per thread
+    __shared__ __attribute__((aligned(16))) uint2 s_enc[512];  // 256..511: bytes outside a string
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[CH / 4 + 8];
+    __shared__ __attribute__((aligned(16))) uint32_t s_out[CH / 4 + 8];
+    __shared__ uint2 s_str[kSortStr];  // {offset in the span, length} of chunk string t
+    __shared__ uint16_t s_perm[kSortStr];
+    __shared__ uint32_t s_bin[kSortBins];  // strings per bin, then the bins' first places
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    for (uint32_t k = t; k < 512; k += NS) s_enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
+    const uint64_t nch = ((uint64_t)A.n + kSortStr - 1) / kSortStr;
+    const uint64_t nrec = 2 * (((uint64_t)A.n + 63) / 64);
+    uint64_t c = blockIdx.x;
+    if (c >= nch) return;
+    auto span_of = [](const SortChunk& q) { return q.hi > q.lo ? ((q.hi + 15u) & ~15u) - (q.lo & ~15u) : 0u; };
+    auto issue_span = [&](uint4 (&v)[NV], const SortChunk& q) {
+        const uint32_t a0 = q.lo & ~15u, span = span_of(q);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const uint32_t k = (uint32_t)j * (16u * NS) + t * 16u;
+            const uint64_t g = (uint64_t)a0 + k;
+            if (k < span && span <= (uint32_t)CH && g + 16 <= A.in_size) v[j] = *reinterpret_cast<const uint4*>(A.in + g);
+        }
+    };
+    auto commit_span = [&](const uint4 (&v)[NV], const SortChunk& q) {
+        const uint32_t a0 = q.lo & ~15u, span = span_of(q);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const uint32_t k = (uint32_t)j * (16u * NS) + t * 16u;
+            const uint64_t g = (uint64_t)a0 + k;
+            if (k < span) *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_in) + k) =
+                g + 16 <= A.in_size ? v[j] : load16_tail(A.in, A.in_size, g);
+        }
+    };
+    if (t < kSortBins) s_bin[t] = 0u;  // then cleared by each chunk once every wave has read it
+    __syncthreads();
+    // prepare(q): chunk q's span into the input stage, the output stage zeroed from z0 on ([0, z0) is zero
+    // already), its strings' {offset, length} and their ranks within their length bins.  Called once
+    // nothing reads those areas any more (three barriers a chunk in all).
+    uint4 pv[NV];
+    uint32_t bin = 0, rank = 0;
+    auto prepare = [&](const SortChunk& q, uint64_t qb, uint32_t z0) {
+        const uint32_t sp = span_of(q);
+        if (sp > (uint32_t)CH) return;  // workgroup-uniform: the per-thread path needs none of it
+        commit_span(pv, q);
+        for (uint32_t k = z0 + t * 16u; k < sp + 16u; k += 16u * NS)
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_out) + k) = make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t ln = qb + t < A.n ? q.e - q.s : 0u;
+        s_str[t] = make_uint2(q.s - (q.lo & ~15u), ln);
+        bin = min(ln >> 2, kSortBins - 1u);  // counting sort by whole dwords (the bulk steps)
+        rank = atomicAdd(&s_bin[bin], 1u);
+    };
+    SortChunk cur = sort_chunk_issue(A, c * kSortStr, t, NS);
+    issue_span(pv, cur);
+    prepare(cur, c * kSortStr, 0u);
+    for (;;) {
+        const uint64_t cb = c * kSortStr, i = cb + t;
+        const bool valid = i < A.n;
+        const uint32_t len = valid ? cur.e - cur.s : 0u;
+        const uint32_t lo = cur.lo, hi = cur.hi, a0 = lo & ~15u, span = span_of(cur);
+        EdgeRec* rec = A.edges + 2 * (cb >> 6);
+        const uint64_t r1 = min(2 * ((cb + kSortStr + 63) >> 6), nrec);
+        const uint64_t cn = c + gridDim.x;
+        const bool more = cn < nch;
+        SortChunk nxt = sort_chunk_issue(A, (more ? cn : c) * kSortStr, t, NS);  // in flight during this chunk
+        __syncthreads();  // the chunk's stage, strings and ranks are in
+        if (span > (uint32_t)CH) {  // (workgroup-uniform) a chunk larger than the stage: one thread per string
+            uint32_t ol = kFailLen;
+            if (valid && len <= kMaxStrLen) {
+                RegSink sink;
+                sink.init(A.out + cur.s);
+                ol = encode_core(GlobalSource{A.in, A.in_size}, cur.s, len, sink, s_enc);
+            }
+            if (valid) finish_encode(A, (uint32_t)i, len, ol);
+            for (uint64_t q = 2 * (cb >> 6) + t; q < r1; q += NS) A.edges[q].m = make_uint4(0u, 0u, 0u, 0u);
+            if (!more) break;
+            issue_span(pv, nxt);
+            prepare(nxt, cn * kSortStr, 0u);
+            cur = nxt;
+            c = cn;
+            continue;
+        }
+        {  // every wave scans the bin counts (two per lane)
+            const uint32_t x0 = s_bin[2 * lane], x1 = s_bin[2 * lane + 1];
+            const uint32_t ex = wave_excl_scan(x0 + x1, (int)lane);
+            const uint32_t eb = (uint32_t)__shfl((int)ex, (int)(bin >> 1)), xb = (uint32_t)__shfl((int)x0, (int)(bin >> 1));
+            s_perm[eb + ((bin & 1u) ? xb : 0u) + rank] = (uint16_t)t;
+        }
+        __syncthreads();
+        if (t < kSortBins) s_bin[t] = 0u;  // read by every wave above: cleared for the next chunk
+        if (more) issue_span(pv, nxt);     // the next chunk's span: in flight during the encode
+        // sorted position t = 64 wave + lane: wave w encodes the w-th length group
+        const uint32_t j = s_perm[t];
+        const uint2 sj = s_str[j];
+        const bool vj = cb + j < A.n;
+        const bool act = vj && sj.y != 0 && sj.y <= kMaxStrLen;
+        const uint32_t tb = encode_chunk_v2(s_in, span - 4u, sj.x, sj.y, act, lds_addr(s_out), 8u * sj.x, s_enc,
+                                            act ? 8 * sj.y - 7 : 0xFFFFFFFFu, true);
+        const uint32_t ol = act && tb != kFailLen ? (tb + 7) >> 3 : kFailLen;
+        __syncthreads();
+        if (vj) finish_encode(A, (uint32_t)(cb + j), sj.y, ol);
+        // the stage's MSB-first words, byte-swapped on the way out (each read chunk is zeroed for the next
+        // chunk); the chunk's first and last 16-B chunks are deferred (edge_fix_kernel), the records of its
+        // other tiles cleared
+        const uint32_t kl = (span - 1u) & ~15u;
+        for (uint32_t k = t * 16u; k < span; k += 16u * NS) {
+            const uint64_t g = (uint64_t)a0 + k;
+            uint4* sp = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_out) + k);
+            uint4 v = *sp;
+            *sp = make_uint4(0u, 0u, 0u, 0u);
+            v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+            const bool full = g >= lo && g + 16 <= hi;
+            if (full) *reinterpret_cast<uint4*>(A.out + g) = v;
+            if (k == 0 || k == kl) {
+                const uint32_t elo = lo > g ? (uint32_t)(lo - g) : 0u;
+                const uint32_t ehi = hi - g < 16 ? (uint32_t)(hi - g) : 16u;
+                EdgeRec* e = rec + (k == 0 ? 0 : 1);
+                e->v = v;
+                e->m = make_uint4((uint32_t)g, (uint32_t)(g >> 32), full ? 0u : elo, full ? 0u : ehi);
+            }
+        }
+        if (t == 0 && (kl == 0 || span == 0)) rec[1].m = make_uint4(0u, 0u, 0u, 0u);  // one chunk, or none
+        if (t == 0 && span == 0) rec[0].m = make_uint4(0u, 0u, 0u, 0u);
+        for (uint64_t q = 2 * (cb >> 6) + 2 + t; q < r1; q += NS) A.edges[q].m = make_uint4(0u, 0u, 0u, 0u);
+        if (!more) break;
+        // the stages are free (the input since the encode, the output but for this thread's chunks above):
+        // the next chunk goes in before this chunk's stores have landed
+        prepare(nxt, cn * kSortStr, span);
+        cur = nxt;
+        c = cn;
+    }
+}
+
 // Chunk-parallel encode (contiguous layout, deferred edges): tiles of 64 strings, each encoded by
 // encode_tile_cp (the per-lane encoder on tiles off its fast path).  The loop keeps little state across
 // the tile (the next tile's offsets only): encode_tile_cp holds its runs' codes in registers.
@@ -2222,7 +2374,11 @@ __global__ void literal_fix_kernel(LitArgs A) {
 // (measured shapes, kept for the record: stream kernel waves / window dwords / output bytes per lane, c3 /
 //  u400 decode ms: 12,12,96: 0.335 / 0.621; 16,8,64: 0.390 / 0.783; 8,16,112: 0.316 / 0.527.  Short-string
 //  encode waves per block, c4 ms: 16: 0.83; 12: 0.93; 20 does not launch at 118 VGPRs.)
-constexpr int kDecSWaves = 16, kDecTWaves = 8, kEncSWaves = 16;
+#ifndef HHUFF_ENCO_NS  // length-sorted encode chunks: strings per chunk, stage bytes (64 B a string: 4 per CU)
+#define HHUFF_ENCO_NS 256
+#define HHUFF_ENCO_CH 16384
+#endif
+constexpr int kDecSWaves = 16, kDecTWaves = 8, kEncSWaves = 16, kEncOStr = HHUFF_ENCO_NS;
 #define DEC_S decode_staged_kernel<kDecSWaves, 3072, 4608, false>
 #define DEC_L decode_staged_kernel<6, 8192, 12928, false>
 #define DEC_SP decode_staged_kernel<kDecSWaves, 3072, 4608, true>
@@ -2231,6 +2387,7 @@ constexpr int kDecSWaves = 16, kDecTWaves = 8, kEncSWaves = 16;
 #define DEC_T decode_stream_kernel<kDecTWaves, 16, 112>
 #define ENC_S encode_staged_kernel<kEncSWaves, 3584, false, false>
 #define ENC_C encode_cp_kernel<kEncSWaves, 3584>
+#define ENC_O encode_sorted_kernel<kEncOStr, HHUFF_ENCO_CH>
 #define ENC_L encode_staged_kernel<8, 8192, false>
 #define ENC_SP encode_staged_kernel<kEncSWaves, 3584, true>
 #define ENC_LP encode_staged_kernel<8, 8192, true>
@@ -2240,7 +2397,7 @@ constexpr int kDecSWaves = 16, kDecTWaves = 8, kEncSWaves = 16;
 #define FLAT_P flatten_pl_kernel<16, kPlStage>
 
 enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncP, kFlatP, kDecT, kDecSP, kDecLP, kEncSP, kEncLP,
-               kEncC, kNumVariants };
+               kEncC, kEncO, kNumVariants };
 
 static const void* variant_fn(int v) {
     switch (v) {
@@ -2254,6 +2411,7 @@ static const void* variant_fn(int v) {
         case kDecT: return (const void*)DEC_T;
         case kEncS: return (const void*)ENC_S;
         case kEncC: return (const void*)ENC_C;
+        case kEncO: return (const void*)ENC_O;
         case kEncL: return (const void*)ENC_L;
         case kFlatD: return (const void*)FLAT_D;
         case kEncP: return (const void*)ENC_P;
@@ -2273,6 +2431,7 @@ static int variant_threads(int v) {
         case kDecLP: return 384;
         case kEncL:
         case kEncLP: return 512;
+        case kEncO: return kEncOStr;
         case kEncP:
         case kFlatP: return 1024;
         default: return 256;
@@ -2602,6 +2761,9 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
 #ifdef HHUFF_CP  // A/B builds: chunk-parallel tiles for the contiguous layout (measured slower, DESIGN (e))
     if (v == kEncS && in_len == nullptr && out_off == nullptr) v = kEncC;
 #endif
+#ifndef HHUFF_ENC_TILES  // contiguous layout: length-sorted chunks (A/B builds -DHHUFF_ENC_TILES: 64-string tiles)
+    if (v == kEncS && in_len == nullptr && out_off == nullptr) v = kEncO;
+#endif
     const int grid = grid_for(v, current_device(), n);
     const bool defer = v != kEncD && in_len == nullptr && out_off == nullptr;
     if (defer) {
@@ -2611,6 +2773,7 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     switch (v) {
         case kEncS: hipLaunchKernelGGL(ENC_S, dim3(grid), dim3(kEncSWaves * 64), 0, stream, A); break;
         case kEncC: hipLaunchKernelGGL(ENC_C, dim3(grid), dim3(kEncSWaves * 64), 0, stream, A); break;
+        case kEncO: hipLaunchKernelGGL(ENC_O, dim3(grid), dim3(kEncOStr), 0, stream, A); break;
         case kEncL: hipLaunchKernelGGL(ENC_L, dim3(grid), dim3(512), 0, stream, A); break;
         default: hipLaunchKernelGGL(ENC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }

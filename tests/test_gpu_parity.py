@@ -120,6 +120,29 @@ def test_random_batches_vs_oracle(torch_cuda, oracle_codec, cfg, n, seed):
     assert compact(gd[0], slots, gd[1]) == compact(od[0], slots, od[1])
 
 
+@pytest.mark.gpu
+def test_contiguous_encode_sorted_chunks_and_oversized(torch_cuda, oracle_codec):
+    """contiguous layout with a mean under the staged threshold: the length-sorted chunk encoder -- empty
+    strings and whole chunks of them, a ragged last chunk, and runs of long strings whose chunks exceed the
+    stage (its per-thread path), next to staged chunks whose deferred edges share 16-B chunks with them"""
+    rng = np.random.default_rng(7)
+    n = 5037
+    lens = rng.integers(1, 40, n)
+    lens[600:900] = 220
+    lens[2000:2100] = rng.integers(100, 300, 100)
+    lens[rng.choice(n, 60, replace=False)] = 0
+    lens[3000:3600] = 0  # whole chunks with no bytes (no output region, no edges)
+    off = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint32)
+    data = rng.integers(32, 127, int(off[-1])).astype(np.uint8)
+    hi = rng.random(data.size) < 0.02
+    data[hi] = rng.integers(128, 256, int(hi.sum()))
+    o_out, o_len, o_st = oracle_codec.encode_batch(data, off, n, nthreads=8)
+    g_out, g_len, g_st = gpu_encode(torch_cuda, data, off, n)
+    np.testing.assert_array_equal(g_len, o_len)
+    np.testing.assert_array_equal(g_st, o_st)
+    assert compact(g_out, off[:n], g_len) == compact(o_out, off[:n], o_len)
+
+
 def _gather(buf, starts, lens):
     """the bytes of every successful slot, concatenated (vectorised compact())"""
     ok = lens != FAIL

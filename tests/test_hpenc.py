@@ -393,9 +393,15 @@ def test_gpu_request_roundtrip(torch_cuda):
     assert (r["rstatus"] == 0).all()
     data, blk_off = request_blocks(st, r)
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a).copy()).cuda()  # noqa: E731
-    d = C.hpack_decode_blocks(dev(data), dev(blk_off.view(np.int32)), dev(st["conn_first"].view(np.int32)), requests=True)
+    L = np.diff(blk_off.astype(np.int64))
+    ao = np.concatenate([[0], np.cumsum(16 * L + 1024)]).astype(np.int64)  # 8/5 of a block is its longest decode
+    d = C.hpack_decode_blocks(dev(data), dev(blk_off.view(np.int32)), dev(st["conn_first"].view(np.int32)),
+                              arena_off=dev(ao), requests=True)
     torch.cuda.synchronize()
-    check_request_roundtrip(st, blk_off, {k: v.cpu().numpy() for k, v in d.items() if k != "scratch"})
+    h = {k: v.cpu().numpy() for k, v in d.items() if k != "scratch"}
+    for k in ("name_off", "name_len", "value_off", "value_len", "nfields"):
+        h[k] = h[k].view(np.uint32)  # u32 bits in int32 tensors
+    check_request_roundtrip(st, blk_off, h)
 
 
 @pytest.mark.gpu

@@ -262,7 +262,7 @@ def hpenc_line(torch, codec, nconn=65536, requests=False):
     frame_bytes = int(r["out_len"][:nres].to(torch.int64).sum().item())
     field_bytes = int(b["hdr"]["name_len"].astype(np.int64).sum() + b["hdr"]["value_len"].astype(np.int64).sum())
     line = {"config": "reqenc" if requests else "hpenc", "connections": nc, ("requests" if requests else "responses"): nres, "fields": nhdr, "field_bytes": field_bytes,
-            "frame_bytes": frame_bytes, "ok_responses": int((r["rstatus"][:nres] == 0).sum().item()),
+            "frame_bytes": frame_bytes, ("ok_requests" if requests else "ok_responses"): int((r["rstatus"][:nres] == 0).sum().item()),
             "flatten_ms": round(t, 4), ("requests_per_s" if requests else "responses_per_s"): round(nres / (t * 1e-3), 1),
             "fields_per_s": round(nhdr / (t * 1e-3), 1), "field_gibps": round(field_bytes / GIB / (t * 1e-3), 3)}
     try:
