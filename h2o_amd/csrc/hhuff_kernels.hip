@@ -2927,10 +2927,13 @@ __device__ __forceinline__ WaveStep wave_step(const uint8_t* in, uint32_t TB, ui
     }
     return s;
 }
-template <int NC>
+// JUMP (NC = 1): every lane also holds the step after its own (one ds_bpermute per round), so the scalar walk
+// reads two steps per chain link and the chain is half as long.
+template <int NC, bool JUMP = false>
 __device__ __forceinline__ DecResult wave_decode(const uint8_t* in, uint32_t len, uint8_t* out, const DecTables& T,
                                                  uint32_t lane) {
     static_assert(NC == 1 || NC == 2, "one or two candidates per lane");
+    static_assert(!JUMP || NC == 1, "the jump table is for one candidate per lane");
     constexpr uint32_t kWin = 64u * NC;
     const uint32_t TB = 8u * len;
     uint32_t W = 0, opos = 0, flags = 0;
@@ -2946,7 +2949,31 @@ __device__ __forceinline__ DecResult wave_decode(const uint8_t* in, uint32_t len
         for (int j = 0; j < NC; ++j) on[j] = 0;
         uint32_t c = 0;
         bool end = false;
-        while (c < kWin) {
+        if constexpr (JUMP) {
+            const uint32_t n1 = s[0].nx;  // < 64: the next step starts in this window (kStop = 255 is not)
+            const uint32_t n2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((n1 < 64u ? n1 : lane) << 2), (int)n1);
+            while (c < 64u) {
+                const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)n1, (int)c);  // both reads hang on c only
+                const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)n2, (int)c);
+                if (a == kStop) {
+                    end = true;
+                    break;
+                }
+                on[0] |= 1ull << c;
+                if (a >= 64u) {
+                    c = a;
+                    break;
+                }
+                if (b == kStop) {
+                    c = a;
+                    end = true;
+                    break;
+                }
+                on[0] |= 1ull << a;
+                c = b;
+            }
+        }
+        while (!JUMP && c < kWin) {
             const uint32_t nx = NC == 1 || c < 64u ? (uint32_t)__builtin_amdgcn_readlane((int)s[0].nx, (int)(c & 63u))
                                                    : (uint32_t)__builtin_amdgcn_readlane((int)s[NC - 1].nx, (int)(c & 63u));
             if (nx == kStop) {
@@ -3010,7 +3037,7 @@ __device__ __forceinline__ void sys_load16x2(const void* pa, const void* pb, uin
         : "memory");
 }
 
-template <int NC>
+template <int NC, bool JUMP = false>
 __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
                                                      uint64_t idle_ticks, uint64_t max_ticks) {
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
@@ -3077,7 +3104,7 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
                 st = ol == kFailLen ? kStatusFail : 0u;
                 if (ol != kFailLen) ol = (ol + 7u) >> 3;
             } else {
-                const DecResult d = wave_decode<NC>(in, len, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane);
+                const DecResult d = wave_decode<NC, JUMP>(in, len, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane);
                 wave_lds_sync();
                 ol = d.ok ? d.len : kFailLen;
                 st = d.ok ? soft_bits(is_name != 0, d.len, d.flags, d.len ? s_out[0] : 0u, d.len ? s_out[d.len - 1] : 0u)
@@ -3114,14 +3141,18 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
 }
 
 hipError_t launch_service(SvcSlot* slots, SvcCtrl* ctrl, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream) {
-    static const int nc = [] {  // decode candidates per lane (HHUFF_SVC_NC=1 or 2; A/B knob)
+    // decode walk (A/B knob HHUFF_SVC_NC): 1 = one candidate per lane, one step per chain link; 2 = two
+    // candidates per lane; default: one candidate per lane, two steps per link (the jump table)
+    static const int nc = [] {
         const char* e = getenv("HHUFF_SVC_NC");
-        return e && *e == '2' ? 2 : 1;
+        return e && *e == '2' ? 2 : e && *e == '1' ? 1 : 3;
     }();
     if (nc == 2)
         hipLaunchKernelGGL(service_kernel<2>, dim3(1), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
-    else
+    else if (nc == 1)
         hipLaunchKernelGGL(service_kernel<1>, dim3(1), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
+    else
+        hipLaunchKernelGGL((service_kernel<1, true>), dim3(1), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
     return hipGetLastError();
 }
 
