@@ -1561,9 +1561,11 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         const bool act = vj && sj.y != 0 && sj.y <= kMaxStrLen;
         const uint32_t tb = encode_chunk_v2(s_in, span - 4u, sj.x, sj.y, act, lds_addr(s_out), 8u * sj.x, s_enc,
                                             act ? 8 * sj.y - 7 : 0xFFFFFFFFu, true);
-        const uint32_t ol = act && tb != kFailLen ? (tb + 7) >> 3 : kFailLen;
+        // the encoded length goes back to the string's own record (read by this thread only), so the lengths
+        // and statuses are stored in string order, coalesced
+        s_str[j].x = act && tb != kFailLen ? (tb + 7) >> 3 : kFailLen;
         __syncthreads();
-        if (vj) finish_encode(A, (uint32_t)(cb + j), sj.y, ol);
+        if (valid) finish_encode(A, (uint32_t)i, len, s_str[t].x);
         // the stage's MSB-first words, byte-swapped on the way out (each read chunk is zeroed for the next
         // chunk); the chunk's first and last 16-B chunks are deferred (edge_fix_kernel), the records of its
         // other tiles cleared

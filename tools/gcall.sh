@@ -1,6 +1,6 @@
 mkdir -p gpurun_out
-timeout -k 10 400 python3 -u tools/ab.py run cfg=c4 base srt7 srt9 > gpurun_out/ab_srt9_c4.log 2>&1 || exit 2
-timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/r03s3_gpu_tests.log 2>&1 || exit 3
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03s3_smoke.log 2>&1 || exit 4
-timeout -k 10 600 python3 bench.py > gpurun_out/r03s3_bench.json 2> gpurun_out/r03s3_bench.err || exit 5
-bash tools/profile.sh r03s3c4 --no-extra || exit 6
+true
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/r03s4_gpu_tests.log 2>&1 || exit 3
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03s4_smoke.log 2>&1 || exit 4
+timeout -k 10 600 python3 bench.py > gpurun_out/r03s4_bench.json 2> gpurun_out/r03s4_bench.err || exit 5
+bash tools/profile.sh r03s4c4 --no-extra || exit 6
