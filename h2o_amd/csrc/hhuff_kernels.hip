@@ -1474,7 +1474,6 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
     const uint32_t t = threadIdx.x, lane = t & 63u;
     for (uint32_t k = t; k < 512; k += NS) s_enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
     const uint64_t nch = ((uint64_t)A.n + kSortStr - 1) / kSortStr;
-    const uint64_t nrec = 2 * (((uint64_t)A.n + 63) / 64);
     uint64_t c = blockIdx.x;
     if (c >= nch) return;
     auto span_of = [](const SortChunk& q) { return q.hi > q.lo ? ((q.hi + 15u) & ~15u) - (q.lo & ~15u) : 0u; };
@@ -1523,8 +1522,7 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         const bool valid = i < A.n;
         const uint32_t len = valid ? cur.e - cur.s : 0u;
         const uint32_t lo = cur.lo, hi = cur.hi, a0 = lo & ~15u, span = span_of(cur);
-        EdgeRec* rec = A.edges + 2 * (cb >> 6);
-        const uint64_t r1 = min(2 * ((cb + kSortStr + 63) >> 6), nrec);
+        EdgeRec* rec = A.edges + 2 * c;  // two records a chunk (sorted_edge_recs)
         const uint64_t cn = c + gridDim.x;
         const bool more = cn < nch;
         SortChunk nxt = sort_chunk_issue(A, (more ? cn : c) * kSortStr, t, NS);  // in flight during this chunk
@@ -1537,7 +1535,7 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
                 ol = encode_core(GlobalSource{A.in, A.in_size}, cur.s, len, sink, s_enc);
             }
             if (valid) finish_encode(A, (uint32_t)i, len, ol);
-            for (uint64_t q = 2 * (cb >> 6) + t; q < r1; q += NS) A.edges[q].m = make_uint4(0u, 0u, 0u, 0u);
+            if (t < 2) rec[t].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges to defer
             if (!more) break;
             issue_span(pv, nxt);
             prepare(nxt, cn * kSortStr, 0u);
@@ -1567,8 +1565,7 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         __syncthreads();
         if (valid) finish_encode(A, (uint32_t)i, len, s_str[t].x);
         // the stage's MSB-first words, byte-swapped on the way out (each read chunk is zeroed for the next
-        // chunk); the chunk's first and last 16-B chunks are deferred (edge_fix_kernel), the records of its
-        // other tiles cleared
+        // chunk); the chunk's first and last 16-B chunks are deferred (edge_fix_kernel)
         const uint32_t kl = (span - 1u) & ~15u;
         for (uint32_t k = t * 16u; k < span; k += 16u * NS) {
             const uint64_t g = (uint64_t)a0 + k;
@@ -1588,7 +1585,6 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         }
         if (t == 0 && (kl == 0 || span == 0)) rec[1].m = make_uint4(0u, 0u, 0u, 0u);  // one chunk, or none
         if (t == 0 && span == 0) rec[0].m = make_uint4(0u, 0u, 0u, 0u);
-        for (uint64_t q = 2 * (cb >> 6) + 2 + t; q < r1; q += NS) A.edges[q].m = make_uint4(0u, 0u, 0u, 0u);
         if (!more) break;
         // the stages are free (the input since the encode, the output but for this thread's chunks above):
         // the next chunk goes in before this chunk's stores have landed
@@ -2552,10 +2548,10 @@ static hipError_t alloc_edges(EdgeRec** p, uint32_t n, hipStream_t stream) {
 
 // after a staged kernel launched with deferred edges: write them, release the records (stream order)
 static hipError_t finish_deferred(uint8_t* out, EdgeRec* edges, uint32_t n, hipStream_t stream,
-                                  const uint32_t* gate = nullptr) {
+                                  const uint32_t* gate = nullptr, uint64_t recs = 0) {
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) {
-        const uint64_t nrec = edge_recs(n);
+        const uint64_t nrec = recs ? recs : edge_recs(n);
         const uint32_t blocks = (uint32_t)min((4 * nrec + 255) / 256, (uint64_t)8192);
         hipLaunchKernelGGL(edge_fix_kernel, dim3(blocks), dim3(256), 0, stream, out, edges, nrec, gate);
         e = hipGetLastError();
@@ -2779,7 +2775,9 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         case kEncL: hipLaunchKernelGGL(ENC_L, dim3(grid), dim3(512), 0, stream, A); break;
         default: hipLaunchKernelGGL(ENC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }
-    return defer ? finish_deferred(out, A.edges, n, stream) : hipGetLastError();
+    // the sorted encoder writes two records per chunk of kEncOStr strings, the tile kernels two per 64
+    const uint64_t recs = v == kEncO ? 2 * (((uint64_t)n + kEncOStr - 1) / kEncOStr) : 0;
+    return defer ? finish_deferred(out, A.edges, n, stream, nullptr, recs) : hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------------
