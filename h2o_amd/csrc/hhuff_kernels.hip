@@ -1511,7 +1511,9 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
             *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_out) + k) = make_uint4(0u, 0u, 0u, 0u);
         const uint32_t ln = qb + t < A.n ? q.e - q.s : 0u;
         s_str[t] = make_uint2(q.s - (q.lo & ~15u), ln);
-        bin = min(ln >> 2, kSortBins - 1u);  // counting sort by whole dwords (the bulk steps)
+        // counting sort by the bulk loop's trip count (encode_chunk_v2: dwords from the string's first aligned
+        // dword to its end), which the wave's longest string sets
+        bin = ln ? min((q.s + ln - (q.s & ~3u)) >> 2, kSortBins - 1u) : 0u;
         rank = atomicAdd(&s_bin[bin], 1u);
     };
     SortChunk cur = sort_chunk_issue(A, c * kSortStr, t, NS);
