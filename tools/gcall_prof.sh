@@ -1,2 +1,2 @@
 mkdir -p gpurun_out
-bash tools/profile.sh r03s5c4 --no-extra || exit 6
+bash tools/profile.sh r03s6c4 --no-extra || exit 6
