@@ -70,13 +70,14 @@ def kernel_key(name):
         return None
     args = _template_args(name)
     # the PACKED template argument: decode_staged_kernel<WAVES, IN, OUT, PACKED>,
-    # encode_staged_kernel<WAVES, STAGE, PACKED, CP>
+    # encode_staged_kernel<WAVES, STAGE, PACKED>
     pos = 3 if "decode_staged_kernel" in name else 2 if "encode_staged_kernel" in name else None
     packed = pos is not None and len(args) > pos and args[pos] == "true"
-    if "decode_staged_kernel" in name or "decode_stream_kernel" in name or "decode_direct_kernel" in name:
+    if ("decode_staged_kernel" in name or "decode_stream_kernel" in name or "decode_direct_kernel" in name or
+            "decode_seg_kernel" in name):
         return "decode_packed" if packed else "decode"
     if ("encode_staged_kernel" in name or "encode_pl_kernel" in name or "encode_direct_kernel" in name or
-            "encode_cp_kernel" in name or "encode_sorted_kernel" in name):
+            "encode_sorted_kernel" in name):
         return "encode_packed" if packed else "encode"
     if "flatten_pl_kernel" in name or "flatten_direct_kernel" in name:
         return "flatten"
@@ -89,7 +90,13 @@ SQ_GROUP = ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_INSTS_S
             "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
 
 
-def pmc_passes(args, config=None, groups=None):
+def synth_n(config):
+    from h2o_amd import synth
+
+    return synth.CONFIGS[config]["n"]
+
+
+def pmc_passes(args, config=None, groups=None, n=None):
     """Per-launch PMC counters of each hhuff kernel: one rocprofv3 run per counter group (FETCH_SIZE,
     WRITE_SIZE, the SQ group, GRBM_GUI_ACTIVE) over this script as a child on `config` (default: the bench's
     own), BEFORE this process touches the GPU.  Returns {kernel key: {counter: per launch}} or {} when
@@ -105,8 +112,8 @@ def pmc_passes(args, config=None, groups=None):
         return {}
     child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "2", "--warmup", "1",
              "--no-cpu-baseline", "--no-traffic", "--no-host", "--no-extra", "--config", config or args.config]
-    if args.n and config is None:
-        child += ["--n", str(args.n)]
+    if (n or args.n) and config is None:
+        child += ["--n", str(n or args.n)]
     if config is not None:
         child += ["--no-packed"]
     vals = {}
@@ -261,9 +268,12 @@ def main():
         sys.exit(spawn_ranks(world, sys.argv[1:]))
     args.gpus = world
     pmc, pmc_cfg = {}, {}
-    if not args.pmc_child and not args.no_traffic and world == 1:
-        pmc = pmc_passes(args)  # child processes; this process has not touched the GPU yet
-        if not args.no_extra:  # HBM traffic of the other configs' kernels (two passes each)
+    rank = int(os.environ.get("RANK", "0"))
+    if not args.pmc_child and not args.no_traffic and rank == 0:
+        # child processes; this process has not touched the GPU yet.  N > 1: rank 0 profiles one shard's worth
+        # of the batch (N / world strings) on its GPU while the other ranks wait in the rendezvous
+        pmc = pmc_passes(args, n=None if world == 1 else -(-(args.n or synth_n(args.config)) // world))
+        if not args.no_extra and world == 1:  # HBM traffic of the other configs' kernels (two passes each)
             pmc_cfg = {c: pmc_passes(args, config=c, groups=(("FETCH_SIZE",), ("WRITE_SIZE",))) for c in ("c2", "c3", "c5")}
     import torch
     import torch.distributed as dist
@@ -271,7 +281,6 @@ def main():
     from h2o_amd import codec, synth
     from h2o_amd import dist as hd
 
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local % torch.cuda.device_count())
@@ -462,14 +471,16 @@ def main():
                     "traffic_over_algorithmic": round(tr[k] / B, 4) if tr.get(k) else None}
                 for k, B in (("encode_packed", B_enc_pk), ("decode_packed", B_dec_pk))}
             line["packed"] = packed
-        if world == 1 and not args.pmc_child:
-            if not args.no_extra:
+        if world > 1 and pmc:
+            line["traffic_note"] = "PMC passes of one shard's worth (%d strings) on rank 0's GPU" % -(-n_all // world)
+        if not args.pmc_child:
+            if world == 1 and not args.no_extra:
                 line["configs"] = other_configs(torch, codec, synth, pmc_cfg)
                 line["f4"] = f4_lines(torch, codec)
                 line["per_string_latency_us"] = per_string_latency(codec)
-            if not args.no_host:
+            if world == 1 and not args.no_host:
                 line["host_inclusive"] = host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch)
-            if not args.no_cpu_baseline:
+            if not args.no_cpu_baseline:  # rank 0's host cores, on a sample of its shard (N > 1 too)
                 line["cpu_baseline"] = cpu_baseline(b, args)
         print(json.dumps(line), flush=True)
     if world > 1:

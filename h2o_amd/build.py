@@ -14,8 +14,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libhhuff.so")
 ARCH = os.environ.get("HHUFF_ARCH", "gfx950")
 
-HIPCC_FLAGS = ["-O3", "--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
-               "-Wall", "-Wno-unused-function"]
+HIPCC_FLAGS = ["-O3", "--offload-arch=" + ARCH, "-std=c++17", "-fPIC", "-fvisibility=hidden", "-Wall",
+               "-Wno-unused-function"]
 
 
 def sources():
@@ -33,11 +33,28 @@ def stale():
     return any(os.path.getmtime(p) > t for p in deps())
 
 
-def build(force=False, verbose=True):
+def _compile(hipcc, src, obj, extra, verbose):
+    cmd = [hipcc] + HIPCC_FLAGS + ["-c", "-I" + os.path.join(ROOT, "include"), "-I" + CSRC] + extra + [src, "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def build(force=False, verbose=True, extra=()):
+    """One object per translation unit, compiled in parallel (the units share no device symbols), then linked."""
     if not force and not stale():
         return LIB
+    from concurrent.futures import ThreadPoolExecutor
+
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc] + HIPCC_FLAGS + ["-I" + os.path.join(ROOT, "include"), "-I" + CSRC] + sources() + ["-o", LIB + ".tmp"]
+    objdir = os.path.join(ROOT, "build", "obj")
+    os.makedirs(objdir, exist_ok=True)
+    srcs = sources()
+    objs = [os.path.join(objdir, os.path.basename(s) + ".o") for s in srcs]
+    with ThreadPoolExecutor(max_workers=min(len(srcs), os.cpu_count() or 1, 8)) as ex:
+        for f in [ex.submit(_compile, hipcc, s, o, list(extra), verbose) for s, o in zip(srcs, objs)]:
+            f.result()
+    cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC"] + objs + ["-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

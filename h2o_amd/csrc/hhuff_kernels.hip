@@ -1042,213 +1042,12 @@ __device__ __forceinline__ uint32_t count_code_bits(const GlobalSource& src, uin
     return bits;
 }
 
-// ------------------------------------------------------------------------------------------------
-// Chunk-parallel tile encode (contiguous layout; output slot = input offset).  One lane per string runs a
-// tile as long as its longest string (U[24,72]: the mean lane is busy 2/3 of the steps).  Here the tile's
-// staged span is cut into 64 runs of K = ceil(dwords / 64) dwords, one per lane, whatever the string
-// lengths, and the code is placed by stateless bit placement (place_bits: OR-ed MSB-first stage words):
-//   marks    every non-empty string sets the bit of its first byte in a bitmap (and lane 0 the tile's end
-//            when bytes follow it), so a run knows where strings start inside it;
-//   phase 1  each lane looks its run's dwords up (4 independent table reads per dword, no dependency
-//            chain), keeps each dword's four codes left-aligned in 64 bits and its four code lengths, and
-//            records the run-local code-bit prefix at every mark; a wave scan of the run totals gives every
-//            byte p its global code-bit prefix P(p);
-//   strings  string j's code bits are P(end) - P(start), hence its verdict (hpack.c:799-800) and length;
-//            its code starts at stage bit 8 (s_j - a0), so every byte p of it goes to bit P(p) + D_j with
-//            D_j = 8 (s_j - a0) - P(s_j) (D_j = dead for a failed string: nothing of it is placed);
-//            the string's lane places its first dword's bytes [s_j & 3, 4) and the EOS padding;
-//   phase 2  each lane places its run dword by dword from registers: bytes before the dword's mark with
-//            the current string's D, then the next string's D takes over.
-// Fast path only: at most kCpMarks marks per run and one per dword (strings of >= 4 bytes in general; c4's
-// 24..72 always); the caller runs the per-lane encoder on other tiles.  The scratch (bitmap, prefixes, D
-// table) lives in the output stage, which is zeroed before the placements.
-// ------------------------------------------------------------------------------------------------
-constexpr uint32_t kCpMaxK = 14;  // dwords per run: STAGE 3584 / 256
-constexpr uint32_t kCpMarks = 4;  // marks per run on the fast path
-#ifndef HHUFF_CP_U
-#define HHUFF_CP_U 4
-#endif
-constexpr uint32_t kCpU = HHUFF_CP_U;  // dwords per round: their table reads are in flight together
-constexpr int32_t kCpDead = INT32_MIN;
-constexpr uint32_t kCpBm = 0, kCpBmWords = 114, kCpSp = 116, kCpDt = 184, kCpDummy = 256;  // scratch dwords in the output stage
-
-// n <= 64 code bits, left-aligned in t, OR-ed in at stage bit tb of the MSB-first output stage at obase
-__device__ __forceinline__ void place_left(uint32_t obase, uint32_t tb, uint64_t t, uint32_t n) {
-    const uint32_t sh = tb & 31u;
-    const uint64_t u = t >> sh;
-    const uint32_t a = obase + ((tb >> 3) & ~3u);
-    lds_or32(a, (uint32_t)(u >> 32));
-    lds_or32(a + 4u, (uint32_t)u);
-    if (__builtin_amdgcn_ballot_w64(sh + n > 64u) != 0) {
-        if (sh + n > 64u) lds_or32(a + 8u, (uint32_t)t << (32u - sh));
-    }
-}
-__device__ __forceinline__ uint32_t byte_sum(uint32_t packed) { return __builtin_amdgcn_udot4(packed, 0x01010101u, 0u, false); }
-__device__ __forceinline__ uint32_t low_bytes(uint32_t k) { return (uint32_t)((1ull << (8u * k)) - 1ull); }  // k <= 4
-
-// Returns false (nothing placed, output stage holds scratch: the caller zeroes it) when the tile is not a
-// fast-path tile.  Else the stage's output is placed and `ol` holds this lane's string's result.
-template <int STAGE>
-__device__ __forceinline__ bool encode_tile_cp(const uint32_t* __restrict__ stage, uint32_t* obuf32, const uint2* s_enc,
-                                               const Tile& t, uint32_t a0, uint32_t span, int lane, uint32_t& ol) {
-    static_assert(STAGE <= 256 * kCpMaxK, "runs longer than kCpMaxK dwords");
-    uint32_t* bmw = obuf32 + kCpBm;
-    uint32_t* sP = obuf32 + kCpSp;
-    int32_t* Dt = reinterpret_cast<int32_t*>(obuf32 + kCpDt);
-    const uint32_t obase = lds_addr(obuf32);
-    const uint32_t ndw = span >> 2;
-    const uint32_t K = (uint32_t)__builtin_amdgcn_readfirstlane((int)((ndw + 63u) >> 6));  // wave-uniform
-    const uint32_t hi_rel = t.hi - a0;
-    const bool has = t.valid && t.len != 0;
-    const uint32_t rel = t.s - a0;
-    // ---- marks
-    for (uint32_t k = (uint32_t)lane; k < kCpBmWords; k += 64u) bmw[k] = 0u;
-    wave_lds_sync();
-    if (has) lds_or32(lds_addr(bmw) + 4u * (rel >> 5), 1u << (rel & 31u));
-    const bool sentinel = hi_rel < span;  // bytes after the tile's last string: a mark with no string
-    if (sentinel && lane == 0) lds_or32(lds_addr(bmw) + 4u * (hi_rel >> 5), 1u << (hi_rel & 31u));
-    wave_lds_sync();
-    const uint32_t b0 = 4u * K * (uint32_t)lane;  // the run's first span byte = its first bitmap bit
-    const uint32_t wi = b0 >> 5, bsh = b0 & 31u;
-    const uint32_t x0 = bmw[wi], x1 = bmw[wi + 1], x2 = bmw[wi + 2];
-    uint64_t bm = (uint64_t)__builtin_amdgcn_alignbit(x2, x1, bsh) << 32 | __builtin_amdgcn_alignbit(x1, x0, bsh);
-    bm &= (1ull << (4u * K)) - 1ull;  // 4K <= 56
-    const uint32_t nm = (uint32_t)__popcll(bm);
-    const uint64_t two = ((bm & (bm >> 1)) & 0x7777777777777777ull) | ((bm & (bm >> 2)) & 0x3333333333333333ull) |
-                         ((bm & (bm >> 3)) & 0x1111111111111111ull);
-    if (__builtin_amdgcn_ballot_w64(nm > kCpMarks || two != 0) != 0) return false;
-    const uint32_t rb = wave_excl_scan(nm, lane);  // rank of the run's first mark
-    const uint32_t M = (uint32_t)__builtin_amdgcn_readlane((int)(rb + nm), 63);
-    // ---- phase 1: the run's code lengths and run-local prefixes at its marks, kCpU dwords per round: the
-    // rounds carry only the prefix, so the table reads of a round are all in flight together
-    const uint32_t* run = stage + K * (uint32_t)lane;
-    const uint32_t dummy = lds_addr(obuf32 + kCpDummy + (uint32_t)lane);
-    const uint32_t sp_base = lds_addr(sP);
-    const uint32_t dlim = min(K, ndw > K * (uint32_t)lane ? ndw - K * (uint32_t)lane : 0u);  // dwords of this run in the span
-    uint32_t pre = 0, cnt = 0;
-    auto look = [&](uint32_t d, uint32_t w, uint32_t iw, uint2& e0, uint2& e1, uint2& e2, uint2& e3) {
-        iw |= d < dlim ? 0u : 0x01010101u;  // past the run or the span: zero entries
-        e0 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0400u)];
-        e1 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)];
-        e2 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)];
-        e3 = s_enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)];
-    };
-    for (uint32_t g = 0; g < K; g += kCpU) {
-        uint32_t w[kCpU];
-        uint2 e[kCpU][4];
-#pragma unroll
-        for (uint32_t u = 0; u < kCpU; ++u) w[u] = run[g + u];
-#pragma unroll
-        for (uint32_t u = 0; u < kCpU; ++u) look(g + u, w[u], 0u, e[u][0], e[u][1], e[u][2], e[u][3]);
-#pragma unroll
-        for (uint32_t u = 0; u < kCpU; ++u) {
-            const uint32_t d = g + u;
-            const uint32_t m = (uint32_t)(bm >> (4u * d)) & 0xFu;  // d < 16: bits past 4K are zero
-            const uint32_t k = (uint32_t)__builtin_ctz(m | 0x10u);
-            const uint32_t p1 = e[u][0].y, p2 = p1 + e[u][1].y, p3 = p2 + e[u][2].y, n = p3 + e[u][3].y;
-            const uint32_t part = k == 0 ? 0u : k == 1 ? p1 : k == 2 ? p2 : p3;
-            lds_st32(m != 0u ? sp_base + 4u * (rb + cnt) : dummy, (pre + part) << 6 | (uint32_t)lane);
-            cnt += m != 0u ? 1u : 0u;
-            pre += n;
-        }
-    }
-    const uint32_t B = wave_excl_scan(pre, lane);  // code bits of the span before this run
-    if (lane == 63) sP[M] = pre << 6 | 63u;        // the span's end
-    wave_lds_sync();
-    // ---- per string: code bits, verdict, displacement
-    const uint32_t r = wave_excl_scan(has ? 1u : 0u, lane);
-    const uint32_t v0 = sP[r], v1 = sP[r + 1u];
-    const uint32_t P0 = (uint32_t)__shfl((int)B, (int)(v0 & 63u)) + (v0 >> 6);
-    const uint32_t P1 = (uint32_t)__shfl((int)B, (int)(v1 & 63u)) + (v1 >> 6);
-    const uint32_t tot = P1 - P0;
-    const bool ok = has && t.len <= kMaxStrLen && tot + 8u <= 8u * t.len;
-    ol = ok ? (tot + 7u) >> 3 : kFailLen;
-    if (has) Dt[r + 1u] = ok ? (int32_t)(8u * rel - P0) : kCpDead;
-    if (lane == 0) {
-        Dt[0] = kCpDead;  // bytes before the tile's first string
-        if (sentinel) Dt[M] = kCpDead;
-    }
-    wave_lds_sync();
-    int32_t Dv[kCpMarks + 1];
-#pragma unroll
-    for (uint32_t i = 0; i <= kCpMarks; ++i) Dv[i] = Dt[rb + i];
-    // the string's first dword, read before the stage is zeroed (bytes before the string read as zero entries)
-    const uint32_t hw = stage[rel >> 2];
-    wave_lds_sync();
-    lds_zero(reinterpret_cast<uint8_t*>(obuf32), 0u, span + 16u, lane);  // what the region copy reads
-    wave_lds_sync();
-    // ---- the string's lane: its first dword's bytes [rel & 3, 4) (two pair placements: any code length) and the padding
-    if (ok) {
-        const uint32_t iw = low_bytes(rel & 3u) & 0x01010101u;
-        const uint2 e0 = s_enc[__builtin_amdgcn_perm(iw, hw, 0x0C0C0400u)];
-        const uint2 e1 = s_enc[__builtin_amdgcn_perm(iw, hw, 0x0C0C0501u)];
-        const uint2 e2 = s_enc[__builtin_amdgcn_perm(iw, hw, 0x0C0C0602u)];
-        const uint2 e3 = s_enc[__builtin_amdgcn_perm(iw, hw, 0x0C0C0703u)];
-        const uint32_t n01 = e0.y + e1.y, n23 = e2.y + e3.y;
-        place_bits(obase, 8u * rel, (uint64_t)e0.x << e1.y | e1.x, n01);
-        place_bits(obase, 8u * rel + n01, (uint64_t)e2.x << e3.y | e3.x, n23);
-        const uint32_t p = (0u - tot) & 7u;  // fill the last byte with ones (EOS prefix, hpack.c:795-798)
-        if (p) place_bits(obase, 8u * rel + tot, (1ull << p) - 1ull, p);
-    }
-    // ---- phase 2: the runs again, kCpU dwords per round (a dword that places nothing ORs zeros).  In a mark
-    // dword only bytes [0, k) are placed here (the next string's lane places the rest); its whole code
-    // length still enters the prefix.
-    int32_t Dc = Dv[0];
-    pre = 0;
-    for (uint32_t g = 0; g < K; g += kCpU) {
-        uint32_t w[kCpU];
-        uint2 e[kCpU][4];
-#pragma unroll
-        for (uint32_t u = 0; u < kCpU; ++u) w[u] = run[g + u];
-#pragma unroll
-        for (uint32_t u = 0; u < kCpU; ++u) look(g + u, w[u], 0u, e[u][0], e[u][1], e[u][2], e[u][3]);
-#pragma unroll
-        for (uint32_t u = 0; u < kCpU; ++u) {
-            const uint32_t d = g + u;
-            const uint32_t m = (uint32_t)(bm >> (4u * d)) & 0xFu;
-            const uint32_t k = (uint32_t)__builtin_ctz(m | 0x10u);  // bytes [0, k) are the current string's
-            const uint2 e0 = e[u][0], e1 = e[u][1], e2 = e[u][2], e3 = e[u][3];
-            const uint32_t p1 = e0.y, p2 = p1 + e1.y, n23 = e2.y + e3.y, n = p2 + n23;
-            const uint32_t na = k >= 4u ? n : k == 3u ? p2 + e2.y : k == 2u ? p2 : k == 1u ? p1 : 0u;
-            const uint32_t tb = B + pre + (uint32_t)Dc;
-            const bool live = Dc != kCpDead && na != 0u;
-            const bool lng = max(max(e0.y, e1.y), max(e2.y, e3.y)) > kFusedMaxBits;
-            const uint64_t c = (uint64_t)(e0.x << e1.y | e1.x) << n23 | (e2.x << e3.y | e3.x);  // codes <= 16 bits
-            const uint64_t keep = live && !lng ? ~0ull << ((64u - na) & 63u) : 0ull;  // the first na bits
-            const uint64_t t2 = (c << ((64u - n) & 63u)) & keep;
-            const uint32_t sh = tb & 31u;
-            const uint64_t uu = t2 >> sh;
-            const uint32_t a = obase + ((tb >> 3) & ~3u);
-            lds_or32(a, (uint32_t)(uu >> 32));
-            lds_or32(a + 4u, (uint32_t)uu);
-            lds_or32(a + 8u, sh ? (uint32_t)t2 << (32u - sh) : 0u);
-            if (__builtin_amdgcn_ballot_w64(live && lng) != 0) {  // a code longer than 16 bits: two pair placements
-                if (live && lng) {
-                    const uint2 z = make_uint2(0u, 0u);
-                    const uint2 f1 = k > 1u ? e1 : z, f2 = k > 2u ? e2 : z, f3 = k > 3u ? e3 : z;
-                    const uint32_t n01 = e0.y + f1.y;
-                    place_bits(obase, tb, (uint64_t)e0.x << f1.y | f1.x, n01);
-                    place_bits(obase, tb + n01, (uint64_t)f2.x << f3.y | f3.x, f2.y + f3.y);
-                }
-            }
-            pre += n;
-            if (m != 0u) {  // the next string takes over
-#pragma unroll
-                for (uint32_t i = 0; i < kCpMarks; ++i) Dv[i] = Dv[i + 1];
-            }
-            Dc = Dv[0];
-        }
-    }
-    wave_lds_sync();
-    return true;
-}
-
 // Packed output (PACKED, contiguous layout): as decode_staged_kernel's -- the tile's encoded strings back to
 // back in string order from G = in_off[first string of the tile], failed strings taking no bytes.  The
 // strings are encoded into their slots (the output stage mirrors the input) and then moved to their places
 // in the input stage, which is free once the tile is encoded (the next span is committed after the
 // stores); no two regions overlap, so one pass suffices.
-template <int WAVES, int STAGE, bool PACKED, bool CP = false>
+template <int WAVES, int STAGE, bool PACKED>
 __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
     __shared__ __attribute__((aligned(16))) uint2 s_enc[512];  // 256..511: bytes outside a string
     // + 32 B: a packed run starts up to 15 B into the stage and its last 16-B chunk may end 15 B past it
@@ -1338,15 +1137,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
         uint32_t ol = kFailLen;
         PROF_MARK(0);
         if (cur.fits) {
-            bool cp_done = false;
-            if constexpr (CP && !PACKED) {  // chunk-parallel tile (contiguous layout with deferred edges)
-                if (region && A.edges) {
-                    uint32_t r_cp = kFailLen;
-                    cp_done = encode_tile_cp<STAGE>(stage, obuf32, s_enc, t, cur.a0, cur.span, lane, r_cp);
-                    if (cp_done) ol = r_cp;
-                }
-            }
-            if (!cp_done) {
+            {
                 for (uint32_t k = (uint32_t)lane * 16u; k < cur.ospan + 16u; k += 64u * 16u)
                     *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(obuf32) + k) = make_uint4(0u, 0u, 0u, 0u);
                 wave_lds_sync();
@@ -1593,67 +1384,6 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         prepare(nxt, cn * kSortStr, span);
         cur = nxt;
         c = cn;
-    }
-}
-
-// Chunk-parallel encode (contiguous layout, deferred edges): tiles of 64 strings, each encoded by
-// encode_tile_cp (the per-lane encoder on tiles off its fast path).  The loop keeps little state across
-// the tile (the next tile's offsets only): encode_tile_cp holds its runs' codes in registers.
-template <int WAVES, int STAGE>
-__global__ __launch_bounds__(WAVES * 64) void encode_cp_kernel(EncArgs A) {
-    __shared__ __attribute__((aligned(16))) uint2 s_enc[512];  // 256..511: bytes outside a string
-    __shared__ __attribute__((aligned(16))) uint32_t s_in[WAVES][STAGE / 4 + 8];
-    __shared__ __attribute__((aligned(16))) uint32_t s_out[WAVES][STAGE / 4 + 4];
-    for (uint32_t k = threadIdx.x; k < 512; k += WAVES * 64)
-        s_enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t* stage = s_in[wave];
-    uint32_t* obuf32 = s_out[wave];
-    const uint64_t stride = (uint64_t)gridDim.x * WAVES * 64;
-    uint64_t base = ((uint64_t)blockIdx.x * WAVES + wave) * 64;
-    if (base >= A.n) return;
-    TileIn ti = issue_tile(base, lane, A.n, A.in_off, nullptr, nullptr, nullptr);
-    for (;;) {
-        const Tile t = finish_tile(base, lane, A.n, ti, false);
-        const uint64_t nbase = base + stride;
-        ti = issue_tile(nbase, lane, A.n, A.in_off, nullptr, nullptr, nullptr);  // clamped: always safe
-        const uint32_t a0 = t.lo & ~15u;
-        const uint32_t span = t.hi > t.lo ? ((t.hi + 15u) & ~15u) - a0 : 0u;
-        EdgeRec* rec = A.edges + 2 * (base >> 6);
-        uint32_t ol = kFailLen;
-        if (span <= STAGE) {
-            stage_span(stage, A.in, A.in_size, a0, span, lane);
-            wave_lds_sync();
-            uint32_t r_cp = kFailLen;
-            if (encode_tile_cp<STAGE>(stage, obuf32, s_enc, t, a0, span, lane, r_cp)) {
-                ol = r_cp;
-            } else {
-                lds_zero(reinterpret_cast<uint8_t*>(obuf32), 0u, span + 16u, lane);
-                wave_lds_sync();
-                const bool act = t.valid && t.len != 0 && t.len <= kMaxStrLen;
-                const uint32_t rel = t.len ? t.s - a0 : 0u;
-                const uint32_t tb = encode_chunk_v2(stage, span ? span - 4u : 0u, rel, t.len, act, lds_addr(obuf32),
-                                                    8u * rel, s_enc, act ? 8 * t.len - 7 : 0xFFFFFFFFu, true);
-                if (act && tb != kFailLen) ol = (tb + 7) >> 3;
-            }
-            wave_lds_sync();
-            region_copy_deferred<true>(A.out, a0, reinterpret_cast<const uint8_t*>(obuf32), span, t.lo, t.hi, lane, rec);
-            wave_lds_sync();
-        } else {
-            if (t.valid && t.len <= kMaxStrLen) {
-                RegSink sink;
-                sink.init(A.out + t.s);
-                ol = encode_core(GlobalSource{A.in, A.in_size}, t.s, t.len, sink, s_enc);
-            }
-            if (lane == 0) {  // direct path: no edges to defer
-                rec[0].m = make_uint4(0u, 0u, 0u, 0u);
-                rec[1].m = make_uint4(0u, 0u, 0u, 0u);
-            }
-        }
-        if (t.valid) finish_encode(A, t.i, t.len, ol);
-        if (nbase >= A.n) break;
-        base = nbase;
     }
 }
 
@@ -2385,8 +2115,7 @@ constexpr int kDecSWaves = 16, kDecTWaves = 8, kEncSWaves = 16, kEncOStr = HHUFF
 #define DEC_LP decode_staged_kernel<6, 8192, 12928, true>
 #define DEC_D decode_direct_kernel<4>
 #define DEC_T decode_stream_kernel<kDecTWaves, 16, 112>
-#define ENC_S encode_staged_kernel<kEncSWaves, 3584, false, false>
-#define ENC_C encode_cp_kernel<kEncSWaves, 3584>
+#define ENC_S encode_staged_kernel<kEncSWaves, 3584, false>
 #define ENC_O encode_sorted_kernel<kEncOStr, HHUFF_ENCO_CH>
 #define ENC_L encode_staged_kernel<8, 8192, false>
 #define ENC_SP encode_staged_kernel<kEncSWaves, 3584, true>
@@ -2397,7 +2126,7 @@ constexpr int kDecSWaves = 16, kDecTWaves = 8, kEncSWaves = 16, kEncOStr = HHUFF
 #define FLAT_P flatten_pl_kernel<16, kPlStage>
 
 enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncP, kFlatP, kDecT, kDecSP, kDecLP, kEncSP, kEncLP,
-               kEncC, kEncO, kNumVariants };
+               kEncO, kNumVariants };
 
 static const void* variant_fn(int v) {
     switch (v) {
@@ -2410,7 +2139,6 @@ static const void* variant_fn(int v) {
         case kDecD: return (const void*)DEC_D;
         case kDecT: return (const void*)DEC_T;
         case kEncS: return (const void*)ENC_S;
-        case kEncC: return (const void*)ENC_C;
         case kEncO: return (const void*)ENC_O;
         case kEncL: return (const void*)ENC_L;
         case kFlatD: return (const void*)FLAT_D;
@@ -2425,7 +2153,6 @@ static int variant_threads(int v) {
         case kDecSP: return kDecSWaves * 64;
         case kDecT: return kDecTWaves * 64;
         case kEncS:
-        case kEncC:
         case kEncSP: return kEncSWaves * 64;
         case kDecL:
         case kDecLP: return 384;
@@ -2758,9 +2485,6 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         return e != hipSuccess ? e : f;
     }
     int v = pick_encode(in_size, n);
-#ifdef HHUFF_CP  // A/B builds: chunk-parallel tiles for the contiguous layout (measured slower, DESIGN (e))
-    if (v == kEncS && in_len == nullptr && out_off == nullptr) v = kEncC;
-#endif
 #ifndef HHUFF_ENC_TILES  // contiguous layout: length-sorted chunks (A/B builds -DHHUFF_ENC_TILES: 64-string tiles)
     if (v == kEncS && in_len == nullptr && out_off == nullptr) v = kEncO;
 #endif
@@ -2772,7 +2496,6 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     }
     switch (v) {
         case kEncS: hipLaunchKernelGGL(ENC_S, dim3(grid), dim3(kEncSWaves * 64), 0, stream, A); break;
-        case kEncC: hipLaunchKernelGGL(ENC_C, dim3(grid), dim3(kEncSWaves * 64), 0, stream, A); break;
         case kEncO: hipLaunchKernelGGL(ENC_O, dim3(grid), dim3(kEncOStr), 0, stream, A); break;
         case kEncL: hipLaunchKernelGGL(ENC_L, dim3(grid), dim3(512), 0, stream, A); break;
         default: hipLaunchKernelGGL(ENC_D, dim3(grid), dim3(256), 0, stream, A); break;

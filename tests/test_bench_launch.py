@@ -51,3 +51,29 @@ def test_rank_command():
     assert cmd.count("--gpus") == 1
     assert bench.rank_command(2, ["--gpus", "2"], 1).count("--gpus") == 1
     assert bench.rank_command(2, ["--gpus=2"], 1)[-1] == "--gpus=2"
+
+
+@pytest.mark.gpu
+def test_bench_self_spawns_two_ranks_end_to_end():
+    """`bench.py --gpus 2` with no outside launcher, as the driver's multi-GPU run starts it: the script
+    starts its two ranks through torch.distributed.run (gloo here, both ranks on the one GPU of the box),
+    every rank runs the HIP codec on its shard, and rank 0 prints exactly one JSON line for the job."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, HHUFF_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    env.pop("LOCAL_RANK", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--n", "262144", "--steps", "2",
+           "--warmup", "1", "--no-extra", "--no-host", "--no-cpu-baseline", "--no-traffic"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-4000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "shard2"
+    assert line["config"]["global_strings"] == 262144
+    assert 0 < line["config"]["strings_rank0"] < 262144
+    assert "exchange_issue_ms" in line and "exchange_wait_ms" in line and line["dist_backend"] == "gloo"
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0
