@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c4")
-    ap.add_argument("--n", type=int, default=None, help="strings in the whole batch (default: the config's N)")
+    ap.add_argument("--strings", "--n", dest="n", type=int, default=None,
+                    help="strings in the whole batch (default: the config's N)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0, help="strings in the CPU-baseline sample (0: 4M)")
     ap.add_argument("--cpu-threads", type=int, default=None)
@@ -113,7 +114,7 @@ def pmc_passes(args, config=None, groups=None, n=None):
     child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "2", "--warmup", "1",
              "--no-cpu-baseline", "--no-traffic", "--no-host", "--no-extra", "--config", config or args.config]
     if (n or args.n) and config is None:
-        child += ["--n", str(n or args.n)]
+        child += ["--strings", str(n or args.n)]
     if config is not None:
         child += ["--no-packed"]
     vals = {}
@@ -234,7 +235,9 @@ def launch_plan(gpus, env, backend, device_count):
 def rank_command(n, argv, port):
     """the child command that starts n ranks of this script: torch.distributed.run sets RANK / LOCAL_RANK /
     WORLD_SIZE / MASTER_* for each; every rank sees the same arguments and --gpus n"""
-    args = [a for a in argv]
+    # torch.distributed.run's parser matches option prefixes even among the script's arguments, and `--n` is a
+    # prefix of several of its own options: pass the batch size under its long name
+    args = ["--strings" + a[3:] if a == "--n" or a.startswith("--n=") else a for a in argv]
     if not any(a == "--gpus" or a.startswith("--gpus=") for a in args):
         args += ["--gpus", str(n)]
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),

@@ -14,7 +14,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libhhuff.so")
+# HHUFF_AB_LIB: an A/B build of the same library (tools/ab.py build NAME -> build/ab/libhhuff_NAME.so), for
+# running the test suite against an experiment; the product path is always h2o_amd/libhhuff.so
+LIB_PATH = os.environ.get("HHUFF_AB_LIB") or os.path.join(HERE, "libhhuff.so")
 
 FAIL_LEN = 0xFFFFFFFF
 SOFT_NAME = 0x1

@@ -392,11 +392,12 @@ namespace {
 constexpr size_t kMeta = 32;
 uint64_t g_per_string_calls = 0;  // process-wide, atomic adds (hhuff_per_string_calls)
 
-// ---- the resident per-string service (service_kernel, hhuff_kernels.hip), one per device ----
+// ---- the resident per-string service (service_kernel, hhuff_kernels.hip), one grid per device ----
 // A call posts its string in its thread's mailbox (slot = thread number mod kSvcSlots, a mutex per slot for
 // more threads than slots), raises the slot's request counter and spins on the slot's done counter.  The
-// service wave exits after kSvcIdle of idleness; a call that finds its request unserved and the wave gone
-// (ctrl->alive 0, the service stream idle) launches it again.  atexit stops every service before the HIP
+// grid has service_waves() waves (default 16), wave g serving mailboxes g, g + G, ..., so calls from up to G
+// threads are coded at once.  It exits after kSvcIdle without a request to any wave; a call that finds its
+// request unserved and the grid gone (ctrl->alive 0, the service stream idle) launches it again.  atexit stops every service before the HIP
 // runtime goes away.  HHUFF_NO_SERVICE=1 in the environment keeps the launch-per-string path.
 constexpr uint64_t kSvcIdle = 200000;      // real-time counter ticks (100 MHz): 2 ms without a request
 constexpr uint64_t kSvcLife = 1000000000;  // 10 s in all, then a fresh launch
@@ -466,7 +467,12 @@ int svc_kick(Service& S, int dev) {
     const hipError_t q = hipStreamQuery(S.stream);
     if (q == hipErrorNotReady) return HHUFF_OK;  // running (or starting)
     if (q != hipSuccess) return hip_fail(q, "per-string service query");
+    // a fresh grid: no quit, no wave gone yet, alive from the launch on (the stream tells a finished grid)
+    for (uint32_t g = 0; g < hhuff::kSvcMaxWaves; ++g) S.ctrl->gone[g] = 0u;
+    S.ctrl->quit = 0u;
+    S.ctrl->waves = hhuff::service_waves();
     __atomic_store_n(&S.ctrl->stop, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(&S.ctrl->alive, 1u, __ATOMIC_RELEASE);
     const hipError_t e = hhuff::launch_service(S.d_slots, S.d_ctrl, kSvcIdle, kSvcLife, S.stream);
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "per-string service launch");
 }
@@ -503,10 +509,12 @@ int svc_call(int dev, bool encode, const uint8_t* src, size_t len, int is_name, 
         if ((spins & 63u) == 0u) {
             if (__atomic_load_n(&S.ctrl->alive, __ATOMIC_ACQUIRE) == 0u && svc_kick(S, dev) != HHUFF_OK) return -1;
             if ((spins & 4095u) == 0u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-                snprintf(t_err, sizeof(t_err), "per-string service: no answer in 5 s");
+                // a busy device (a long batch kernel ahead of the wave) is not a HIP failure: this call and
+                // the later ones take the launch path, so a valid string is still coded
+                snprintf(t_err, sizeof(t_err), "per-string service: no answer in 5 s (launch path from now on)");
                 std::lock_guard<std::mutex> gg(S.mu);
-                S.broken = true;  // later calls take the launch path
-                return -1;
+                S.broken = true;
+                return 0;
             }
         }
         __builtin_ia32_pause();
@@ -919,6 +927,17 @@ HHUFF_API int hhuff_debug_prof(unsigned long long* out16, int reset) {
 HHUFF_API const char* hhuff_version(void) { return "hhuff 0.1.0 (gfx950)"; }
 HHUFF_API const char* hhuff_last_error_string(void) { return t_err; }
 HHUFF_API int hhuff_pool_trim(void) {
+    // pool_trim synchronises the device (memory freed on any stream returns to the pool once that stream
+    // passes the free), which would also wait for the resident per-string wave: it is stopped first, with
+    // its lock held so no per-string call relaunches it meanwhile (the next call after the trim does)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hip_fail(hipErrorInvalidDevice, "pool trim");
+    Service& S = g_svc[dev];
+    std::lock_guard<std::mutex> g(S.mu);
+    if (S.ready) {
+        __atomic_store_n(&S.ctrl->stop, 1u, __ATOMIC_RELEASE);
+        (void)hipStreamSynchronize(S.stream);  // the wave polls stop: it exits within a poll
+    }
     hipError_t e = hhuff::pool_trim();
     return e == hipSuccess ? HHUFF_OK : hip_fail(e, "pool trim");
 }

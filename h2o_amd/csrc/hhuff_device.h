@@ -855,6 +855,40 @@ __device__ __forceinline__ void stage_bswap(uint32_t* obuf32, uint32_t bytes, in
     }
 }
 
+// Code bits of the stage bytes [start, start + len), as encode_chunk_v2 walks them: a masked head dword, whole
+// dwords with no byte masks (one code-length read per byte; the trip count is wave-uniform and lanes outside
+// their range add nothing), a masked tail dword (pass 1 of the proportional-lane kernels).
+__device__ __forceinline__ uint32_t chunk_code_bits_v2(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
+                                                       bool active, const uint2* __restrict__ enc) {
+    const uint32_t end = start + len;
+    const uint32_t a0 = start & ~3u;
+    const uint32_t ndw = active ? (end - a0 + 3u) >> 2 : 0u;
+    const uint32_t jf = (start & 3u) ? 1u : 0u;  // whole dwords: [jf, jl)
+    const uint32_t jl = active ? (end - a0) >> 2 : 0u;
+    const uint32_t mfirst = 0xFFFFFFFFu << (8u * (start & 3u));
+    const uint32_t mlast = (uint32_t)(0xFFFFFFFFull >> ((32u - 8u * (end & 3u)) & 31u));
+    auto masked = [&](uint32_t j, bool on) {
+        const uint32_t w = stage[min(a0 + 4u * j, last) >> 2];
+        uint32_t vm = j == 0 ? mfirst : 0xFFFFFFFFu;
+        vm &= (j + 1 == ndw) ? mlast : 0xFFFFFFFFu;
+        vm = on ? vm : 0u;
+        const uint32_t iw = ~vm & 0x01010101u;
+        return enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0400u)].y + enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)].y +
+               enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)].y + enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)].y;
+    };
+    uint32_t tb = masked(0, active && jf != 0);  // head
+    const uint32_t* sw = stage + (a0 >> 2);
+    const uint32_t jlast = (last >> 2) - (a0 >> 2);
+    const uint32_t jend = wave_max_u32(jl);
+    uint32_t bulk = 0;
+    for (uint32_t j = 0; j < jend; ++j) {
+        const uint32_t w = sw[min(j, jlast)];
+        const uint32_t n = enc[w & 0xFFu].y + enc[(w >> 8) & 0xFFu].y + enc[(w >> 16) & 0xFFu].y + enc[w >> 24].y;
+        bulk += (j >= jf && j < jl) ? n : 0u;
+    }
+    return tb + bulk + masked(jl, active && (end & 3u) != 0 && jl >= jf);  // + tail
+}
+
 // Code bits of the stage bytes [start, start + len) (pass 1 of the proportional-lane encode).
 __device__ __forceinline__ uint32_t chunk_code_bits(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
                                                     bool active, const uint2* __restrict__ enc, uint32_t jmax) {

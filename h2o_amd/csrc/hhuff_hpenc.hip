@@ -526,7 +526,8 @@ __global__ __launch_bounds__(64) void hpe_table_kernel(HpeArgs A) {
     bool failed = s0.failed != 0;
     const uint4 srv_rc = A.rec[A.nhdr];
     const uint32_t srv_info = A.info[A.nhdr];
-    const uint32_t r0 = A.conn_first[c], r1 = A.conn_first[c + 1];
+    // a malformed conn_first cannot send the walk past the response array
+    const uint32_t r1 = min(A.conn_first[c + 1], A.nres), r0 = min(A.conn_first[c], r1);
     hhuff_hpack_response_t R{};
     uint64_t base = 0, limit = 0;
     if (r0 < r1) {  // (res and out_off may be NULL when the call has no responses)
@@ -548,7 +549,8 @@ __global__ __launch_bounds__(64) void hpe_table_kernel(HpeArgs A) {
         int32_t st = 0;
         if (failed) {
             st = HHUFF_RES_SKIPPED;
-        } else if ((head && (R.status < 100 || R.status > 999)) || (request && R.status > R.nhdr) ||
+        } else if ((uint64_t)R.hdr_first + R.nhdr > A.nhdr || limit < base ||  // header range / region malformed
+                   (head && (R.status < 100 || R.status > 999)) || (request && R.status > R.nhdr) ||
                    R.max_frame_size < 16384u ||
                    R.max_frame_size > 0xFFFFFFu || (server && (srv_info & kInfoBad))) {
             st = HHUFF_RES_EINVAL;
@@ -614,7 +616,8 @@ __global__ __launch_bounds__(64) void hpe_table_kernel(HpeArgs A) {
             A.headers_size[r] = 0;
             A.plan[2 * r + 1] = make_uint4(~0u, kOpSkip, 0u, 0u);
             A.plan[2 * r] = make_uint4(0u, 0u, 0u, 0u);
-            for (uint32_t h = h0; h < h1; ++h) A.op[h] = make_uint4(0u, 0u, kOpSkip, 0u);
+            if ((uint64_t)R.hdr_first + R.nhdr <= A.nhdr)  // a malformed range is not touched
+                for (uint32_t h = h0; h < h1; ++h) A.op[h] = make_uint4(0u, 0u, kOpSkip, 0u);
             failed = true;
         }
         A.rstatus[r] = st;
@@ -1076,7 +1079,9 @@ __global__ __launch_bounds__(256) void qpe_layout_kernel(QpeArgs A) {
         const bool server = !request && (R.flags & HHUFF_RES_SERVER) && A.server_len != 0;  // headers of the list
         const bool dfid = (R.flags & HHUFF_QRES_DATAGRAM) != 0;
         const uint4 sr = A.rec[A.nhdr];
-        bool bad = (server && (sr.y & kQBad)) || (dfid && (uint64_t)R.dfid_off + R.dfid_len > A.in_size);
+        // a header range past the call's headers or a region that ends before it starts: EINVAL
+        const bool malformed = (uint64_t)R.hdr_first + R.nhdr > A.nhdr || A.out_off[r + 1] < A.out_off[r];
+        bool bad = malformed || (server && (sr.y & kQBad)) || (dfid && (uint64_t)R.dfid_off + R.dfid_len > A.in_size);
         uint32_t bits;
         const uint32_t si = request ? 0u : q_status_index(R.status);
         uint32_t st_len = si ? int_len(si, 6) : 0u;
@@ -1126,7 +1131,7 @@ __global__ __launch_bounds__(256) void qpe_layout_kernel(QpeArgs A) {
             A.out_len[r] = (uint32_t)total;
             A.header_len[r] = (uint32_t)body;
         } else {
-            for (uint32_t h = h0; h < h1; ++h) A.dst[h] = make_uint2(0u, ~0u);
+            for (uint32_t h = h0; h < h1 && !malformed; ++h) A.dst[h] = make_uint2(0u, ~0u);
             A.plan[2 * r] = make_uint4(0u, 0u, 0u, 0u);
             A.out_len[r] = 0;
             A.header_len[r] = 0;

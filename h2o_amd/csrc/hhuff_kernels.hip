@@ -1439,8 +1439,18 @@ __device__ __forceinline__ uint32_t plan_tile_strings(const uint32_t* __restrict
     return pick < K0 ? pick : K0;
 }
 
+// Edge records of the proportional-lane kernels: 2 per tile of the planned K, allocated for the smallest K the
+// plan can pick (rec_cap records); the records of tiles that K does not make are cleared here, so
+// edge_fix_kernel reads all rec_cap of them
+__device__ __forceinline__ void pl_clear_spare_edges(EdgeRec* edges, uint64_t ntiles, uint64_t rec_cap) {
+    const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t r = 2 * ntiles + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rec_cap; r += nth)
+        edges[r].m = make_uint4(0u, 0u, 0u, 0u);
+}
+
 template <int WAVES, int STAGE>
-__global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32_t K, const uint32_t* __restrict__ kplan) {
+__global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32_t K, const uint32_t* __restrict__ kplan,
+                                                               uint64_t rec_cap) {
     struct __attribute__((aligned(16))) Smem {
         uint2 enc[512];  // 256..511: bytes outside a share
         uint32_t in[WAVES][STAGE / 4];
@@ -1464,6 +1474,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
     const uint8_t* obuf = reinterpret_cast<const uint8_t*>(obuf32);
     uint32_t* lmap = sm.lmap[wave];
     const uint64_t ntiles = ((uint64_t)A.n + K - 1) / K;
+    pl_clear_spare_edges(A.edges, ntiles, rec_cap);
     const uint64_t tstride = (uint64_t)gridDim.x * WAVES;
     uint64_t t = (uint64_t)blockIdx.x * WAVES + wave;
     if (t >= ntiles) return;
@@ -1545,13 +1556,11 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
             const bool multi = gj > 1;
             const bool big = act && lj <= kMaxStrLen;
             const uint32_t last = cur.span ? cur.span - 4u : 0u;
-            const uint32_t ndw = big && clen ? (cs + clen - (cs & ~3u) + 3u) >> 2 : 0u;
-            const uint32_t jmax = wave_max_u32(ndw);
             uint32_t off = 0, tot = 0;
             bool sfail = false;
             wave_lds_sync();
             if (__any(multi && big)) {  // pass 1: code bits of every share, then starting bits and totals
-                const uint32_t b = chunk_code_bits(stage, last, cs, clen, big && multi, s_enc, jmax);
+                const uint32_t b = chunk_code_bits_v2(stage, last, cs, clen, big && multi && clen != 0, s_enc);
                 const uint32_t x = wave_excl_scan(b, lane);
                 const uint32_t xs = (uint32_t)__shfl((int)x, (int)Lj, 64);
                 const uint32_t xe = (uint32_t)__shfl((int)(x + b), (int)(Lj + gj - 1), 64);
@@ -1559,9 +1568,11 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
                 tot = xe - xs;
                 sfail = multi && ((tot + 7u) >> 3) >= lj;
             }
-            const uint32_t r = encode_chunk(stage, last, cs, clen, big && !sfail && clen != 0, obuf32,
-                                            8u * (sj - cur.a0) + off, s_enc, jmax,
-                                            multi ? 0xFFFFFFFFu : 8u * lj - 7u, c1 == lj);  // the share holding the string's end pads it
+            // pass 2: the shares' codes OR-ed into the MSB-first output stage (encode_chunk_v2); the share
+            // holding the string's end pads it
+            const uint32_t r = encode_chunk_v2(stage, last, cs, clen, big && !sfail && clen != 0, lds_addr(obuf32),
+                                               8u * (sj - cur.a0) + off, s_enc, multi ? 0xFFFFFFFFu : 8u * lj - 7u,
+                                               c1 == lj);
             uint32_t res = kFailLen;  // verdict of this lane's string, as seen by the string's first lane
             if (act && lj != 0 && lj <= kMaxStrLen) {
                 if (multi) res = sfail ? kFailLen : (tot + 7u) >> 3;
@@ -1569,12 +1580,17 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
             }
             ol = (uint32_t)__shfl((int)res, (int)L, 64);
             wave_lds_sync();
-            region_copy<(STAGE + 1023) / 1024>(A.out, cur.a0, obuf, cur.span, cur.lo, cur.hi, lane);
+            // byte-swapped on the way out; the (at most two) 16-B chunks shared with the neighbouring tiles
+            // are deferred to edge_fix_kernel
+            region_copy_deferred<true>(A.out, cur.a0, obuf, cur.span, cur.lo, cur.hi, lane, A.edges + 2 * t);
             wave_lds_sync();
-        } else if (own && len <= kMaxStrLen) {
-            RegSink sink;
-            sink.init(A.out + cur.s);
-            ol = encode_core(GlobalSource{A.in, A.in_size}, cur.s, len, sink, s_enc);
+        } else {
+            if (own && len <= kMaxStrLen) {
+                RegSink sink;
+                sink.init(A.out + cur.s);
+                ol = encode_core(GlobalSource{A.in, A.in_size}, cur.s, len, sink, s_enc);
+            }
+            if (lane < 2) A.edges[2 * t + lane].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges
         }
         if (own) finish_encode(A, (uint32_t)(cur.i0 + lane), len, ol);
         if (!have_next) break;
@@ -1624,6 +1640,7 @@ struct FlatArgs {
     uint8_t* out;
     const uint32_t* out_off;
     uint32_t* out_len;
+    EdgeRec* edges = nullptr;  // flatten_pl_kernel: 2 deferred-edge records per tile
 };
 
 // RFC 7541 5.1 prefix integer (hpack.c:757-772) OR-ed into first byte h0: up to 6 bytes for v < 2^32
@@ -1717,7 +1734,8 @@ __device__ __forceinline__ uint32_t prefix_int_bytes(uint32_t h0, uint32_t v, ui
 // (qpack.c:1052-1060); raw fallbacks copy their shares after the raw header (qpack.c:1046-1051).
 // ------------------------------------------------------------------------------------------------
 template <int WAVES, int STAGE>
-__global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint32_t K, const uint32_t* __restrict__ kplan) {
+__global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint32_t K, const uint32_t* __restrict__ kplan,
+                                                                uint64_t rec_cap) {
     constexpr uint32_t OSTAGE = STAGE + 11u * 64u + 32u;
     struct __attribute__((aligned(16))) Smem {
         uint2 enc[512];
@@ -1743,33 +1761,78 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
     uint32_t* lmap = sm.lmap[wave];
     const uint32_t p = A.prefix_bits;
     const uint64_t ntiles = ((uint64_t)A.n + K - 1) / K;
-    for (uint64_t t = (uint64_t)blockIdx.x * WAVES + wave; t < ntiles; t += (uint64_t)gridDim.x * WAVES) {
-        const uint64_t i0 = t * K;
-        const uint32_t kt = (uint32_t)min<uint64_t>(K, A.n - i0);
-        const bool own = (uint32_t)lane < kt;
-        const uint64_t i = i0 + lane;
-        uint32_t s = 0, e = 0, first = 0;
-        bool rawf = false;
-        if (own) {
-            s = A.in_off[i];
-            e = A.in_off[i + 1];
-            first = A.first_bytes ? A.first_bytes[i] : 0u;
-            rawf = A.raw_bits ? ((A.raw_bits[i >> 5] >> (i & 31)) & 1u) != 0 : false;
+    pl_clear_spare_edges(A.edges, ntiles, rec_cap);
+    const uint64_t tstride = (uint64_t)gridDim.x * WAVES;
+    uint64_t t = (uint64_t)blockIdx.x * WAVES + wave;
+    if (t >= ntiles) return;
+
+    // Software pipeline as encode_pl_kernel: the next tile's offsets, first bytes and raw bits, then its span,
+    // are in flight while the current tile is framed.  The output stage holds MSB-first words (encode_chunk_v2
+    // places code bits in them); prefix-integer headers and raw payload bytes go to their byte-swapped
+    // positions (x ^ 3), and the region is byte-swapped on the way out.
+    struct TIn {
+        uint32_t s, e, first, raww;
+    };
+    auto issue = [&](uint64_t tt) {
+        TIn r{0u, 0u, 0u, 0u};
+        const uint64_t i = tt * K + lane;
+        if ((uint32_t)lane < K && i < A.n) {
+            r.s = A.in_off[i];
+            r.e = A.in_off[i + 1];
+            r.first = A.first_bytes ? A.first_bytes[i] : 0u;
+            r.raww = A.raw_bits ? A.raw_bits[i >> 5] : 0u;
         }
-        const uint32_t len = e - s;
-        const uint32_t lo = (uint32_t)__shfl((int)s, 0, 64), hi = (uint32_t)__shfl((int)e, (int)kt - 1, 64);
-        const uint32_t a0 = lo & ~15u;
-        const uint32_t span = hi > lo ? ((hi + 15u) & ~15u) - a0 : 0u;
-        const uint64_t O = (uint64_t)s + 11u * i;  // output slot (owner lanes)
-        const uint64_t olo = (uint64_t)lo + 11u * i0, ohi = (uint64_t)hi + 11u * (i0 + kt);
-        const uint64_t ob = olo & ~15ull;
-        const uint32_t ospan = (uint32_t)(((ohi + 15u) & ~15ull) - ob);
+        return r;
+    };
+    struct Plan {
+        uint64_t i0, olo, ohi, ob;
+        uint32_t kt, lo, hi, a0, span, ospan;
+        bool fits;
+    };
+    auto plan = [&](uint64_t tt, const TIn& x) {
+        Plan P;
+        P.i0 = tt * K;
+        P.kt = (uint32_t)min<uint64_t>(K, A.n - P.i0);
+        P.lo = (uint32_t)__shfl((int)x.s, 0, 64);
+        P.hi = (uint32_t)__shfl((int)x.e, (int)P.kt - 1, 64);
+        P.a0 = P.lo & ~15u;
+        P.span = P.hi > P.lo ? ((P.hi + 15u) & ~15u) - P.a0 : 0u;
+        P.olo = (uint64_t)P.lo + 11u * P.i0;
+        P.ohi = (uint64_t)P.hi + 11u * (P.i0 + P.kt);
+        P.ob = P.olo & ~15ull;
+        P.ospan = (uint32_t)(((P.ohi + 15u) & ~15ull) - P.ob);
+        P.fits = P.span <= STAGE && P.ospan <= OSTAGE;
+        return P;
+    };
+    SpanPrefetch<(STAGE + 1023) / 1024> pf;
+    TIn nx = issue(t);
+    Plan cur = plan(t, nx);
+    TIn cx = nx;
+    if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
+    if (t + tstride < ntiles) nx = issue(t + tstride);
+    if (cur.fits) pf.commit(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+    for (;;) {
+        const uint64_t tn = t + tstride;
+        const bool have_next = tn < ntiles;
+        Plan nxt;
+        TIn nxi{0u, 0u, 0u, 0u};
+        if (have_next) {
+            nxt = plan(tn, nx);
+            nxi = nx;
+            if (nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
+            if (tn + tstride < ntiles) nx = issue(tn + tstride);
+        }
+        // ---- the current tile ----
+        const uint32_t kt = cur.kt;
+        const bool own = (uint32_t)lane < kt;
+        const uint64_t i = cur.i0 + lane;
+        const uint32_t s = cx.s, len = cx.e - cx.s, first = cx.first;
+        const bool rawf = A.raw_bits ? ((cx.raww >> (i & 31)) & 1u) != 0 : false;
         uint32_t ol = kFailLen;
-        if (span <= STAGE && ospan <= OSTAGE) {
-            stage_span(stage, A.in, A.in_size, a0, span, lane);
-            for (uint32_t k = (uint32_t)lane * 16u; k < ospan + 16u; k += 64u * 16u)
+        if (cur.fits) {
+            for (uint32_t k = (uint32_t)lane * 16u; k < cur.ospan + 16u; k += 64u * 16u)
                 *reinterpret_cast<uint4*>(obuf + k) = make_uint4(0u, 0u, 0u, 0u);
-            const uint32_t total = hi - lo;
+            const uint32_t total = cur.hi - cur.lo;
             const uint32_t g = own ? 1u + (uint32_t)(((uint64_t)(64u - kt) * len) / (total ? total : 1u)) : 0u;
             const uint32_t L = wave_excl_scan(g, lane);
             const uint32_t used = (uint32_t)__shfl((int)(L + g), (int)kt - 1, 64);
@@ -1792,14 +1855,12 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
             const uint32_t sub = (uint32_t)lane - Lj;
             const uint32_t C = gj > 1 ? (((lj + gj - 1) / gj) + 3u) & ~3u : lj;
             const uint32_t c0 = min(sub * C, lj), c1 = min(sub * C + C, lj);
-            const uint32_t cs = sj - a0 + c0, clen = c1 - c0;
+            const uint32_t cs = sj - cur.a0 + c0, clen = c1 - c0;
             const bool ok = act && lj <= kMaxStrLen;
-            const uint32_t last = span ? span - 4u : 0u;
-            const uint32_t ndw = ok && clen ? (cs + clen - (cs & ~3u) + 3u) >> 2 : 0u;
-            const uint32_t jmax = wave_max_u32(ndw);
+            const uint32_t last = cur.span ? cur.span - 4u : 0u;
             wave_lds_sync();
             // pass 1: code bits per share -> starting bit of each share, string totals, verdicts
-            const uint32_t b = chunk_code_bits(stage, last, cs, clen, ok && !rj, s_enc, jmax);
+            const uint32_t b = chunk_code_bits_v2(stage, last, cs, clen, ok && !rj && clen != 0, s_enc);
             const uint32_t x = wave_excl_scan(b, lane);
             const uint32_t xs = (uint32_t)__shfl((int)x, (int)Lj, 64);
             const uint32_t xe = (uint32_t)__shfl((int)(x + b), (int)(Lj + gj - 1), 64);
@@ -1811,46 +1872,55 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
             uint64_t hb = 0;
             const uint32_t hn = huff ? prefix_int_bytes((fj & ~((1u << p) - 1u)) | (1u << p), hlen, p, hb)
                                      : prefix_int_bytes(fj & ~((2u << p) - 1u), lj, p, hb);
-            const uint32_t orel = (uint32_t)((uint64_t)sj + 11u * (i0 + j) - ob);  // slot start in the out stage
+            const uint32_t orel = (uint32_t)((uint64_t)sj + 11u * (cur.i0 + j) - cur.ob);  // slot start in the out stage
             if (ok && sub == 0)
-                for (uint32_t k = 0; k < hn; ++k) obuf[orel + k] = (uint8_t)(hb >> (8 * k));
-            // pass 2: Huffman shares emit their bits; raw shares copy their bytes
-            encode_chunk(stage, last, cs, clen, huff && clen != 0, obuf32, 8u * (orel + hn) + (x - xs), s_enc, jmax,
-                         0xFFFFFFFFu, c1 == lj);
+                for (uint32_t k = 0; k < hn; ++k) obuf[(orel + k) ^ 3u] = (uint8_t)(hb >> (8 * k));
+            // pass 2: Huffman shares place their code bits; raw shares copy their bytes
+            encode_chunk_v2(stage, last, cs, clen, huff && clen != 0, lds_addr(obuf32), 8u * (orel + hn) + (x - xs), s_enc,
+                            0xFFFFFFFFu, c1 == lj);
             if (ok && !huff && clen) {
                 const uint8_t* in8 = reinterpret_cast<const uint8_t*>(stage);
-                for (uint32_t k = 0; k < clen; ++k) obuf[orel + hn + c0 + k] = in8[cs + k];
+                for (uint32_t k = 0; k < clen; ++k) obuf[(orel + hn + c0 + k) ^ 3u] = in8[cs + k];
             }
             const uint32_t res = ok ? hn + (huff ? hlen : lj) : kFailLen;
             ol = (uint32_t)__shfl((int)res, (int)L, 64);
             wave_lds_sync();
-            region_copy<(OSTAGE + 1023) / 1024>(A.out, ob, obuf, ospan, olo, ohi, lane);
+            region_copy_deferred<true>(A.out, cur.ob, obuf, cur.ospan, cur.olo, cur.ohi, lane, A.edges + 2 * t);
             wave_lds_sync();
-        } else if (own && len <= kMaxStrLen) {  // tile larger than the stage: one string per lane from global
-            const GlobalSource src{A.in, A.in_size};
-            RegSink sink;
-            sink.init(A.out + O);
-            const uint32_t bits = (rawf || len == 0) ? 0u : count_code_bits(src, s, len, s_enc);
-            const bool huff = !rawf && len != 0 && bits <= 8 * len - 8;
-            if (huff) {
-                push_prefix_int(sink, (first & ~((1u << p) - 1u)) | (1u << p), (bits + 7) >> 3, p);
-                encode_core(src, s, len, sink, s_enc);
-            } else {
-                push_prefix_int(sink, first & ~((2u << p) - 1u), len, p);
-                uint32_t a = s & ~3u, rem = len, skip = s & 3u;
-                while (rem) {
-                    const uint32_t w = src.word(a) >> (8 * skip);
-                    const uint32_t k = min(4u - skip, rem);
-                    sink.push(w, k);
-                    rem -= k;
-                    a += 4;
-                    skip = 0;
+        } else {
+            if (own && len <= kMaxStrLen) {  // tile larger than the stage: one string per lane from global
+                const uint64_t O = (uint64_t)s + 11u * i;  // output slot
+                const GlobalSource src{A.in, A.in_size};
+                RegSink sink;
+                sink.init(A.out + O);
+                const uint32_t bits = (rawf || len == 0) ? 0u : count_code_bits(src, s, len, s_enc);
+                const bool huff = !rawf && len != 0 && bits <= 8 * len - 8;
+                if (huff) {
+                    push_prefix_int(sink, (first & ~((1u << p) - 1u)) | (1u << p), (bits + 7) >> 3, p);
+                    encode_core(src, s, len, sink, s_enc);
+                } else {
+                    push_prefix_int(sink, first & ~((2u << p) - 1u), len, p);
+                    uint32_t a = s & ~3u, rem = len, skip = s & 3u;
+                    while (rem) {
+                        const uint32_t w = src.word(a) >> (8 * skip);
+                        const uint32_t k = min(4u - skip, rem);
+                        sink.push(w, k);
+                        rem -= k;
+                        a += 4;
+                        skip = 0;
+                    }
+                    sink.finish();
                 }
-                sink.finish();
+                ol = sink.count();
             }
-            ol = sink.count();
+            if (lane < 2) A.edges[2 * t + lane].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges
         }
         if (own) A.out_len[i] = ol;
+        if (!have_next) break;
+        if (nxt.fits) pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+        cur = nxt;
+        cx = nxi;
+        t = tn;
     }
 }
 
@@ -2108,13 +2178,18 @@ __global__ void literal_fix_kernel(LitArgs A) {
 #define HHUFF_ENCO_NS 256
 #define HHUFF_ENCO_CH 16384
 #endif
-constexpr int kDecSWaves = 16, kDecTWaves = 8, kEncSWaves = 16, kEncOStr = HHUFF_ENCO_NS;
+#ifndef HHUFF_DECT  // stream decode: waves per block, window dwords, output bytes per lane
+#define HHUFF_DECT_W 8
+#define HHUFF_DECT_NW 16
+#define HHUFF_DECT_OUT 112
+#endif
+constexpr int kDecSWaves = 16, kDecTWaves = HHUFF_DECT_W, kEncSWaves = 16, kEncOStr = HHUFF_ENCO_NS;
 #define DEC_S decode_staged_kernel<kDecSWaves, 3072, 4608, false>
 #define DEC_L decode_staged_kernel<6, 8192, 12928, false>
 #define DEC_SP decode_staged_kernel<kDecSWaves, 3072, 4608, true>
 #define DEC_LP decode_staged_kernel<6, 8192, 12928, true>
 #define DEC_D decode_direct_kernel<4>
-#define DEC_T decode_stream_kernel<kDecTWaves, 16, 112>
+#define DEC_T decode_stream_kernel<kDecTWaves, HHUFF_DECT_NW, HHUFF_DECT_OUT>
 #define ENC_S encode_staged_kernel<kEncSWaves, 3584, false>
 #define ENC_O encode_sorted_kernel<kEncOStr, HHUFF_ENCO_CH>
 #define ENC_L encode_staged_kernel<8, 8192, false>
@@ -2391,7 +2466,11 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
                          uint8_t* status, hipStream_t stream, uint64_t sel_bytes) {
     if (n == 0) return hipSuccess;
     DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr, nullptr, nullptr, nullptr, nullptr};
+#ifdef HHUFF_MIX_STREAM  // A/B builds: mixed lengths go to the stream kernel alone
+    const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n) == kDecL ? (int)kDecT : pick_decode(sel_bytes ? sel_bytes : in_size, n);
+#else
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n);
+#endif
     const int grid = grid_for(v, current_device(), n);
     const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr;
     if (v == kDecL) {  // mixed lengths: the device picks staged or stream (see below)
@@ -2467,22 +2546,33 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         const int g = grid_for(kEncP, current_device(), 0xFFFFFFFFu);
         const uint64_t want = (tiles + 15) / 16;
         const int grid = (int)(want < (uint64_t)g ? (want ? want : 1) : g);
+        const uint64_t recs = 2 * tiles;  // deferred edges: 2 per tile of the smallest K the plan can pick
+        hipError_t e = pool_alloc((void**)&A.edges, recs * sizeof(EdgeRec), stream);
+        if (e != hipSuccess) return e;
         if (!sample) {
-            hipLaunchKernelGGL(ENC_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)nullptr);
-            return hipGetLastError();
+            hipLaunchKernelGGL(ENC_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)nullptr, recs);
+            return finish_deferred(out, A.edges, n, stream, nullptr, recs);
         }
         uint32_t* part = nullptr;
-        hipError_t e = pool_alloc((void**)&part, 6 * kPlBlocks * sizeof(uint32_t), stream);
-        if (e != hipSuccess) return e;
-        // a tile fits when its 16-B aligned span does: raw span + 30 <= stage
-        hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, in_off, n, K, kPlStage - 30u, part);
-        e = hipGetLastError();
+        e = pool_alloc((void**)&part, 6 * kPlBlocks * sizeof(uint32_t), stream);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(ENC_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)part);
+            // a tile fits when its 16-B aligned span does: raw span + 30 <= stage
+            hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, in_off, n, K, kPlStage - 30u, part);
             e = hipGetLastError();
         }
-        const hipError_t f = hipFreeAsync(part, stream);
-        return e != hipSuccess ? e : f;
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(ENC_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)part, recs);
+            e = hipGetLastError();
+        }
+        if (part) {
+            const hipError_t f = hipFreeAsync(part, stream);
+            if (e == hipSuccess) e = f;
+        }
+        if (e != hipSuccess) {
+            (void)hipFreeAsync(A.edges, stream);
+            return e;
+        }
+        return finish_deferred(out, A.edges, n, stream, nullptr, recs);
     }
     int v = pick_encode(in_size, n);
 #ifndef HHUFF_ENC_TILES  // contiguous layout: length-sorted chunks (A/B builds -DHHUFF_ENC_TILES: 64-string tiles)
@@ -2772,35 +2862,48 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
     __shared__ __attribute__((aligned(16))) uint32_t s_in[kSvcMax / 4 + 8];  // [input][slack]
     __shared__ __attribute__((aligned(16))) uint8_t s_out[(kSvcMax * 8) / 5 + 64];
     const uint32_t lane = threadIdx.x;
+    const uint32_t G = gridDim.x, g = blockIdx.x;  // G divides kSvcSlots (launch_service)
+    const uint32_t M = kSvcSlots / G;              // mailboxes of this wave: lane j < M polls mailbox g + G j
+    const bool mine = lane < M;
+    SvcSlot* const my = slots + (g + G * (mine ? lane : 0u));
     load_dec_tables(s_lut, s_kinfo, s_ones, 64);
     for (uint32_t k = lane; k < 256; k += 64) s_enc[k] = make_uint2(g_enc_code[k], g_enc_nbits[k]);
     __syncthreads();
-    if (lane == 0) sys_store(&ctrl->alive, 1u);
-    uint32_t handled = sys_load(&slots[lane].done);  // lane l keeps slot l's last served request
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t last = t0;
-    uint32_t hot = 0, polls = 0;  // hot: the mailbox served last, whose chunks every poll reads too
+    if (lane == 0) {
+        sys_store(&ctrl->last[g], (uint32_t)t0);
+        if (g == 0) sys_store(&ctrl->alive, 1u);
+    }
+    uint32_t handled = sys_load(&my->done);  // lane j keeps its mailbox's last served request
+    uint32_t hot = 0, polls = 0;  // hot: the lane whose mailbox was served last; every poll reads its chunks too
     for (;;) {
-        // one round: lane l reads mailbox l's header and chunk l of the hot mailbox
+        // one round: lane j < M reads its mailbox's header, lane M the control words {stop, alive, quit, G};
+        // every lane reads its chunk of the hot mailbox
         uint4 hdr, ck;
-        sys_load16x2(&slots[lane].req, slots[hot].chunk[lane], hdr, ck);
+        const void* hp = mine ? (const void*)&my->req : (const void*)ctrl;
+        sys_load16x2(hp, slots[g + G * hot].chunk[lane], hdr, ck);
         const uint32_t req = hdr.x;
-        uint64_t pend = __builtin_amdgcn_ballot_w64(req != handled);
+        const uint32_t ctl_stop = (uint32_t)__shfl((int)hdr.x, (int)M), ctl_quit = (uint32_t)__shfl((int)hdr.z, (int)M);
+        uint64_t pend = __builtin_amdgcn_ballot_w64(mine && req != handled);
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         if (pend == 0) {
-            if ((++polls & 15u) == 0u) {  // the stop flag costs a round trip of its own: every 16th poll
-                const uint32_t stop = sys_load(&ctrl->stop);
-                if (stop != 0) break;
+            if (ctl_quit != 0 || ctl_stop != 0) break;
+            if (g == 0 && (++polls & 15u) == 0u) {
+                // wave 0: the grid's idle time is the youngest of the waves' last requests
+                const uint32_t l = lane < G ? sys_load(&ctrl->last[lane]) : (uint32_t)t0;
+                const uint32_t idle = wave_min_u32((uint32_t)now - l);
+                if (idle > (uint32_t)idle_ticks || now - t0 > max_ticks) {
+                    if (lane == 0) sys_store(&ctrl->quit, 1u);
+                    break;
+                }
             }
-            if (now - last > idle_ticks || now - t0 > max_ticks) break;
             continue;  // each poll is a PCIe round trip already: no sleep between them
         }
-        last = now;
-        int ck_slot = (int)hot;  // the mailbox whose chunks `ck` holds
+        int ck_slot = (int)hot;  // the lane whose mailbox's chunks `ck` holds
         while (pend) {
             const uint32_t s = (uint32_t)__builtin_ctzll(pend);
             pend &= pend - 1;
-            SvcSlot* sl = slots + s;
+            SvcSlot* sl = slots + (g + G * s);
             const uint32_t r = (uint32_t)__shfl((int)req, (int)s);
             const uint32_t op = (uint32_t)__shfl((int)hdr.y, (int)s);
             const uint32_t len = min((uint32_t)__shfl((int)hdr.z, (int)s), kSvcMax);
@@ -2849,6 +2952,7 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
                 sys_store(&sl->t_data, t_data);
                 sys_store(&sl->t_coded, t_coded);
                 sys_store(&sl->t_out, (uint32_t)__builtin_amdgcn_s_memrealtime());
+                sys_store(&ctrl->last[g], t_seen);
             }
             // the result before its counter: the stores above are system-scope (write-through), so waiting
             // for their completion orders them before `done` (no L2 write-back needed)
@@ -2859,9 +2963,18 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
             wave_lds_sync();
         }
     }
-    if (lane == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        sys_store(&ctrl->alive, 0u);
+    if (lane == 0) sys_store(&ctrl->gone[g], 1u);
+    if (g == 0) {  // the grid is over for the host once every wave has left (bounded: 1 s)
+        const uint64_t tq = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            const uint32_t gone = lane < G ? sys_load(&ctrl->gone[lane]) : 1u;
+            if (__builtin_amdgcn_ballot_w64(gone == 0u) == 0 || __builtin_amdgcn_s_memrealtime() - tq > 100000000ull) break;
+            __builtin_amdgcn_s_sleep(8);
+        }
+        if (lane == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            sys_store(&ctrl->alive, 0u);
+        }
     }
 }
 
@@ -2872,13 +2985,26 @@ hipError_t launch_service(SvcSlot* slots, SvcCtrl* ctrl, uint64_t idle_ticks, ui
         const char* e = getenv("HHUFF_SVC_NC");
         return e && *e == '2' ? 2 : e && *e == '1' ? 1 : 3;
     }();
+    const uint32_t G = service_waves();
     if (nc == 2)
-        hipLaunchKernelGGL(service_kernel<2>, dim3(1), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
+        hipLaunchKernelGGL(service_kernel<2>, dim3(G), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
     else if (nc == 1)
-        hipLaunchKernelGGL(service_kernel<1>, dim3(1), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
+        hipLaunchKernelGGL(service_kernel<1>, dim3(G), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
     else
-        hipLaunchKernelGGL((service_kernel<1, true>), dim3(1), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
+        hipLaunchKernelGGL((service_kernel<1, true>), dim3(G), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
     return hipGetLastError();
+}
+
+// waves of the per-string service (HHUFF_SVC_WAVES, a divisor of kSvcSlots from 2 on -- a wave's lane M reads
+// the control words --; default 16): caller threads are spread over the mailboxes (thread number mod
+// kSvcSlots), mailbox m over wave m mod G, so up to G threads' strings are coded at once
+uint32_t service_waves() {
+    static const uint32_t G = [] {
+        const char* e = getenv("HHUFF_SVC_WAVES");
+        const uint32_t w = e && *e ? (uint32_t)atoi(e) : 16u;
+        return (w >= 2 && w <= kSvcSlots && kSvcSlots % w == 0) ? w : 16u;
+    }();
+    return G;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2990,21 +3116,32 @@ hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* i
         const int g = grid_for(kFlatP, current_device(), 0xFFFFFFFFu);
         const uint64_t want = (tiles + 15) / 16;
         const int grid = (int)(want < (uint64_t)g ? (want ? want : 1) : g);
+        const uint64_t recs = 2 * tiles;  // deferred edges (see encode_pl_kernel)
+        hipError_t e = pool_alloc((void**)&A.edges, recs * sizeof(EdgeRec), stream);
+        if (e != hipSuccess) return e;
         if (!sample) {
-            hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)nullptr);
-            return hipGetLastError();
+            hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)nullptr, recs);
+            return finish_deferred(out, A.edges, n, stream, nullptr, recs);
         }
         uint32_t* part = nullptr;
-        hipError_t e = pool_alloc((void**)&part, 6 * kPlBlocks * sizeof(uint32_t), stream);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, in_off, n, K, kPlStage - 30u, part);
-        e = hipGetLastError();
+        e = pool_alloc((void**)&part, 6 * kPlBlocks * sizeof(uint32_t), stream);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)part);
+            hipLaunchKernelGGL(encode_plan_kernel, dim3(kPlBlocks), dim3(64), 0, stream, in_off, n, K, kPlStage - 30u, part);
             e = hipGetLastError();
         }
-        const hipError_t f = hipFreeAsync(part, stream);
-        return e != hipSuccess ? e : f;
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)part, recs);
+            e = hipGetLastError();
+        }
+        if (part) {
+            const hipError_t f = hipFreeAsync(part, stream);
+            if (e == hipSuccess) e = f;
+        }
+        if (e != hipSuccess) {
+            (void)hipFreeAsync(A.edges, stream);
+            return e;
+        }
+        return finish_deferred(out, A.edges, n, stream, nullptr, recs);
     }
     const int grid = grid_for(kFlatD, current_device(), n);
     hipLaunchKernelGGL(FLAT_D, dim3(grid), dim3(256), 0, stream, A);

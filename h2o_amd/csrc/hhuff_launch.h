@@ -37,10 +37,18 @@ struct alignas(16) SvcSlot {
 };
 static_assert(sizeof(SvcSlot) % 16 == 0 && sizeof(SvcSlot) == 64 + 1024 + 1600, "mailbox layout");
 static_assert(12 * 64 == kSvcMax && (kSvcMax * 8) / 5 + 60 <= 1600, "mailbox sizes");
+// Several service waves (one per block, launch_service's grid): wave g serves mailboxes g, g + G, g + 2G, ...
+// Wave 0 decides when the grid ends (no request to any wave for idle_ticks, max_ticks in all, or `stop`) and
+// raises `quit`; every wave polls it with its mailboxes, stores gone[g] as it leaves, and wave 0 clears
+// `alive` once all have left, so the host relaunches only a finished grid.
+constexpr uint32_t kSvcMaxWaves = 64;
 struct SvcCtrl {
-    uint32_t stop, alive, pad[2];
+    uint32_t stop, alive, quit, waves;  // host: stop; wave 0: alive, quit; waves = G (read by the host)
+    uint32_t last[kSvcMaxWaves];        // wave g: low 32 bits of the real-time counter at its last request
+    uint32_t gone[kSvcMaxWaves];        // wave g: 1 once it has left its loop
 };
 hipError_t launch_service(SvcSlot* slots, SvcCtrl* ctrl, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream);
+uint32_t service_waves();
 // Packed output (include/hhuff.h hhuff_{de,en}code_batch_packed): contiguous layout, pk_off u32[n + 1]
 hipError_t launch_decode_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
                                 const uint32_t* is_name_bits, uint8_t* out, uint32_t* pk_off, uint32_t* out_len,

@@ -51,6 +51,20 @@ def test_rank_command():
     assert cmd.count("--gpus") == 1
     assert bench.rank_command(2, ["--gpus", "2"], 1).count("--gpus") == 1
     assert bench.rank_command(2, ["--gpus=2"], 1)[-1] == "--gpus=2"
+    # `--n` is a prefix of torch.distributed.run's own options (its parser refuses it as ambiguous): renamed
+    c = bench.rank_command(2, ["--n", "64", "--n=32", "--no-extra"], 1)
+    assert "--n" not in c and c[-6:-2] == ["--strings", "64", "--strings=32", "--no-extra"]
+
+
+def test_rank_command_parses_under_torchrun():
+    """torch.distributed.run's own parser accepts the generated command (it rejected `--n` as ambiguous)"""
+    from torch.distributed.run import get_args_parser
+
+    cmd = bench.rank_command(2, ["--n", "262144", "--steps", "2", "--warmup", "1", "--no-extra", "--no-host",
+                                 "--no-cpu-baseline", "--no-traffic"], 29500)
+    a = get_args_parser().parse_args(cmd[cmd.index("torch.distributed.run") + 1:])
+    assert a.nproc_per_node == "2" and a.training_script.endswith("bench.py")
+    assert a.training_script_args[:2] == ["--strings", "262144"]
 
 
 @pytest.mark.gpu

@@ -417,3 +417,24 @@ def test_gpu_bench_size(torch_cuda, oracle_codec):
         np.testing.assert_array_equal(r[key], q[key], err_msg=key)
     assert (r["rstatus"] == 0).all()
     assert frames_of(r["out"], b["out_off"], r["out_len"]) == frames_of(q["out"], b["out_off"], q["out_len"])
+
+
+@pytest.mark.gpu
+def test_gpu_malformed_ranges(torch_cuda):
+    """a response whose header range runs past the call's headers, or whose output region ends before it
+    starts, is refused with HHUFF_RES_EINVAL (the connection's later responses SKIPPED), and nothing is
+    read or written outside the arrays; the other connections are unaffected"""
+    conns = [[dict(status=200, headers=[(b"date", b"now", TOK)]), dict(status=200, headers=[(b"x-a", b"1", 0)]),
+              dict(status=204)],
+             [dict(status=200, headers=[(b"server", b"h2o", TOK)])],
+             [dict(status=301, headers=[(b"location", b"/a", TOK)]), dict(status=200)]]
+    b = HE.build_batch(conns)
+    good = host(gpu_step(torch_cuda, b))
+    assert (good["rstatus"] == 0).all()
+    bad = {k: (v.copy() if isinstance(v, np.ndarray) else v) for k, v in b.items()}
+    bad["res"]["hdr_first"][1] = np.uint32(b["hdr"].size + 1000)  # past nhdr
+    bad["res"]["hdr_first"][3] = np.uint32(0xFFFFFFF0)  # wraps u32 with its nhdr
+    bad["out_off"][5] = bad["out_off"][4] - 1  # connection 2's first region ends before it starts
+    r = host(gpu_step(torch_cuda, bad))
+    assert list(r["rstatus"]) == [0, C.RES_EINVAL, C.RES_SKIPPED, C.RES_EINVAL, C.RES_EINVAL, C.RES_SKIPPED]
+    assert r["out_len"][0] == good["out_len"][0]

@@ -293,3 +293,21 @@ def test_gpu_bench_size(torch_cuda, oracle_codec):
     r = gpu(torch_cuda, q)
     assert (r["rstatus"][:q["res"].size] == 0).all()
     check(r, q, want=ostep(O.oracle(), q))
+
+
+@pytest.mark.gpu
+def test_gpu_malformed_ranges(torch_cuda):
+    """a response whose header range runs past the call's headers, or whose output region ends before it
+    starts, is refused with HHUFF_RES_EINVAL; its neighbours are encoded as before"""
+    T = C.HDR_TOKEN
+    conns = [[dict(status=200, headers=[(b"date", b"now", T)])], [dict(status=404, headers=[(b"x-a", b"1", 0)])],
+             [dict(status=200, headers=[(b"server", b"h2o", T)])], [dict(status=204)]]
+    q = HE.to_qpack(HE.build_batch(conns), seed=1, dfid_frac=0.0, odd_status_frac=0.0)
+    good = gpu(torch_cuda, q)
+    assert (good["rstatus"] == 0).all()
+    q["res"]["hdr_first"][1] = np.uint32(q["hdr"].size + 7)
+    q["res"]["hdr_first"][2] = np.uint32(0xFFFFFFFF)
+    q["out_off"][4] = q["out_off"][3] - 1  # response 3's region ends before it starts
+    r = gpu(torch_cuda, q)
+    assert list(r["rstatus"]) == [0, C.RES_EINVAL, C.RES_EINVAL, C.RES_EINVAL]
+    assert r["out_len"][0] == good["out_len"][0] and r["header_len"][0] == good["header_len"][0]

@@ -20,7 +20,7 @@ def build(name, flags):
 
     os.makedirs(ABDIR, exist_ok=True)
     out = os.path.join(ABDIR, "libhhuff_%s.so" % name)
-    cmd = ["/opt/rocm/bin/hipcc"] + hb.HIPCC_FLAGS + flags + ["-I" + os.path.join(ROOT, "include"), "-I" + hb.CSRC] + \
+    cmd = ["/opt/rocm/bin/hipcc", "-shared"] + hb.HIPCC_FLAGS + flags + ["-I" + os.path.join(ROOT, "include"), "-I" + hb.CSRC] + \
         hb.sources() + ["-o", out]
     subprocess.run(cmd, check=True)
     print(out)

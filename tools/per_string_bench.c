@@ -1,5 +1,11 @@
-/* C-level latency of h2o's per-string symbols through libhhuff.so (as h2o calls them), and the resident
- * service's own stamps: cc -O2 tools/per_string_bench.c -Iinclude -Lh2o_amd -lhhuff -Wl,-rpath,$PWD/h2o_amd */
+/* C-level latency and throughput of h2o's per-string symbols through libhhuff.so, called the way h2o calls them:
+ * concurrently from every event-loop thread (src/main.c:5512 starts one per core).  For each thread count T given
+ * on the command line (default 1 8 16 64) T pthreads each make N encode calls, then N decode calls, of one 48-B
+ * header string; the line reports the aggregate strings/s (all threads' calls over the wall time of the phase)
+ * and the per-call median / p99 over all calls.  The T = 1 line also carries the resident service's own stamps.
+ *   cc -O2 -pthread tools/per_string_bench.c -Iinclude -Lh2o_amd -lhhuff -Wl,-rpath,$PWD/h2o_amd -o tools/per_string_bench
+ */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -21,46 +27,117 @@ static int cmp(const void *a, const void *b)
     return x < y ? -1 : x > y;
 }
 
-#define N 4000
-int main(void)
+static const char *S = "accept-encoding: gzip, deflate, br, zstd, accept-";
+enum { LEN = 48, WARM = 200 };
+static uint8_t H[64];
+static size_t HL;
+static int N = 2000;
+
+struct job {
+    int encode;
+    double *lat;
+    int bad;
+    pthread_barrier_t *bar;
+};
+
+static void *run(void *p)
 {
-    const char *s = "accept-encoding: gzip, deflate, br, zstd, accept-";
-    size_t len = 48;
-    uint8_t h[64], d[128];
-    size_t hl = h2o_hpack_encode_huffman(h, (const uint8_t *)s, len);
-    if (hl == SIZE_MAX) {
+    struct job *j = p;
+    uint8_t h[64];
+    char d[128];
+    for (int i = 0; i < WARM + N; ++i) {
+        if (i == WARM)
+            pthread_barrier_wait(j->bar);
+        double t0 = now_us();
+        if (j->encode) {
+            size_t r = h2o_hpack_encode_huffman(h, (const uint8_t *)S, LEN);
+            if (r != HL || memcmp(h, H, HL) != 0)
+                j->bad = 1;
+        } else {
+            unsigned soft = 0;
+            const char *err = NULL;
+            size_t r = h2o_hpack_decode_huffman(d, &soft, H, HL, 0, &err);
+            if (r != LEN || memcmp(d, S, LEN) != 0)
+                j->bad = 1;
+        }
+        if (i >= WARM)
+            j->lat[i - WARM] = now_us() - t0;
+    }
+    pthread_barrier_wait(j->bar);
+    return NULL;
+}
+
+/* one phase: T threads x N calls; returns strings/s, fills median / p99 (us) */
+static double phase(int T, int encode, double *med, double *p99, int *bad)
+{
+    pthread_t *th = calloc(T, sizeof(*th));
+    struct job *jb = calloc(T, sizeof(*jb));
+    double *lat = calloc((size_t)T * N, sizeof(double));
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, T + 1);
+    for (int t = 0; t < T; ++t) {
+        jb[t] = (struct job){encode, lat + (size_t)t * N, 0, &bar};
+        pthread_create(&th[t], NULL, run, &jb[t]);
+    }
+    pthread_barrier_wait(&bar); /* every thread warmed up */
+    double t0 = now_us();
+    pthread_barrier_wait(&bar); /* every thread done */
+    double wall = now_us() - t0;
+    for (int t = 0; t < T; ++t) {
+        pthread_join(th[t], NULL);
+        *bad |= jb[t].bad;
+    }
+    qsort(lat, (size_t)T * N, sizeof(double), cmp);
+    *med = lat[(size_t)T * N / 2];
+    *p99 = lat[(size_t)T * N * 99 / 100];
+    pthread_barrier_destroy(&bar);
+    free(lat), free(jb), free(th);
+    return (double)T * N / (wall * 1e-6);
+}
+
+int main(int argc, char **argv)
+{
+    HL = h2o_hpack_encode_huffman(H, (const uint8_t *)S, LEN);
+    if (HL == SIZE_MAX) {
         printf("{\"error\": \"%s\"}\n", hhuff_last_error_string());
         return 1;
     }
-    static double te[N], td[N], st[4][N];
-    for (int i = 0; i < 200; ++i)
-        h2o_hpack_encode_huffman(h, (const uint8_t *)s, len);
-    for (int i = 0; i < N; ++i) {
-        double t0 = now_us();
-        h2o_hpack_encode_huffman(h, (const uint8_t *)s, len);
-        te[i] = now_us() - t0;
+    if (getenv("PS_CALLS"))
+        N = atoi(getenv("PS_CALLS"));
+    int counts[16] = {1, 8, 16, 64}, nc = 4;
+    if (argc > 1) {
+        nc = 0;
+        for (int a = 1; a < argc && nc < 16; ++a)
+            counts[nc++] = atoi(argv[a]);
     }
-    for (int i = 0; i < N; ++i) {
-        unsigned soft = 0;
-        const char *err = NULL;
-        double t0 = now_us();
-        size_t r = h2o_hpack_decode_huffman((char *)d, &soft, h, hl, 0, &err);
-        td[i] = now_us() - t0;
-        if (r != len || memcmp(d, s, len) != 0) {
-            printf("{\"error\": \"decode mismatch\"}\n");
+    for (int c = 0; c < nc; ++c) {
+        const int T = counts[c];
+        double em, e99, dm, d99;
+        int bad = 0;
+        double er = phase(T, 1, &em, &e99, &bad);
+        double dr = phase(T, 0, &dm, &d99, &bad);
+        if (bad) {
+            printf("{\"threads\": %d, \"error\": \"result mismatch: %s\"}\n", T, hhuff_last_error_string());
             return 1;
         }
-        uint32_t t4[4];
-        if (hhuff_service_stamps(t4) == 0) {
-            st[0][i] = (t4[1] - t4[0]) * 0.01, st[1][i] = (t4[2] - t4[1]) * 0.01, st[2][i] = (t4[3] - t4[2]) * 0.01;
+        printf("{\"threads\": %d, \"calls_per_thread\": %d, \"string_bytes\": %d, "
+               "\"encode\": {\"strings_per_s\": %.0f, \"median_us\": %.2f, \"p99_us\": %.2f}, "
+               "\"decode\": {\"strings_per_s\": %.0f, \"median_us\": %.2f, \"p99_us\": %.2f}",
+               T, N, LEN, er, em, e99, dr, dm, d99);
+        if (T == 1) {
+            /* the service wave's stamps of one more decode: poll -> input, input -> coded, coded -> written */
+            unsigned soft = 0;
+            const char *err = NULL;
+            char d[128];
+            uint32_t t4[4];
+            h2o_hpack_decode_huffman(d, &soft, H, HL, 0, &err);
+            if (hhuff_service_stamps(t4) == 0)
+                printf(", \"service_decode_us\": {\"seen_to_input\": %.2f, \"input_to_coded\": %.2f, "
+                       "\"coded_to_written\": %.2f}",
+                       (t4[1] - t4[0]) * 0.01, (t4[2] - t4[1]) * 0.01, (t4[3] - t4[2]) * 0.01);
         }
+        printf("}\n");
+        fflush(stdout);
     }
-    qsort(te, N, sizeof(double), cmp);
-    qsort(td, N, sizeof(double), cmp);
-    for (int k = 0; k < 3; ++k)
-        qsort(st[k], N, sizeof(double), cmp);
-    printf("{\"encode_us\": {\"median\": %.2f, \"p99\": %.2f}, \"decode_us\": {\"median\": %.2f, \"p99\": %.2f}, "
-           "\"service_decode_us\": {\"seen_to_input\": %.2f, \"input_to_coded\": %.2f, \"coded_to_written\": %.2f}}\n",
-           te[N / 2], te[N * 99 / 100], td[N / 2], td[N * 99 / 100], st[0][N / 2], st[1][N / 2], st[2][N / 2]);
     return 0;
 }
