@@ -300,6 +300,9 @@ __device__ __forceinline__ uint32_t sel_bits(uint32_t m, uint32_t a, uint32_t b)
 __device__ __forceinline__ void lds_or32(uint32_t addr, uint32_t v) {
     __hip_atomic_fetch_or((lds_u32*)(size_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// an unaligned 2-byte LDS store (ds_write_b16 at any byte address: gfx950 runs LDS in unaligned mode)
+typedef __attribute__((address_space(3))) uint16_t lds_u16u __attribute__((aligned(1)));
+__device__ __forceinline__ void lds_st16u(uint32_t addr, uint32_t v) { *(lds_u16u*)(size_t)addr = (uint16_t)v; }
 __device__ __forceinline__ uint32_t lds_ld8(uint32_t addr) { return *(const lds_u8*)(size_t)addr; }
 __device__ __forceinline__ uint32_t lds_ld32(uint32_t addr) { return *(const lds_u32*)(size_t)addr; }
 __device__ __forceinline__ void lds_st32(uint32_t addr, uint32_t v) { *(lds_u32*)(size_t)addr = v; }
@@ -456,12 +459,13 @@ __device__ __forceinline__ DecResult decode_staged_lane_v7(const uint32_t* stage
     };
     auto bstep = [&](bool longchk) {
         if (pm < lim) {
+            // Both symbol bytes go out as one unaligned 16-bit store at o, whatever the entry holds: with >= 27
+            // string bits left the bytes past the symbols taken are rewritten by the lane's next symbols (or
+            // lie past its decoded length, inside its slot: 5 symbols' room), so no trash redirection
             const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
             const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
-            const uint32_t sl = (uint32_t)((int32_t)e >> 31);         // LONG: nothing taken from the window
-            const uint32_t h2 = (uint32_t)((int32_t)(e << 1) >> 31);  // HAS2
-            lds_st8(sel_bits(sl, trash, o), e);
-            lds_st8(sel_bits(h2, o, trash - 1u) + 1u, e >> 8);
+            const uint32_t sl = (uint32_t)((int32_t)e >> 31);  // LONG: nothing taken from the window
+            lds_st16u(o, e);
             o += (e >> 28) & 3u;
             accb |= e;
             uint32_t cons = ((e >> 20) & 15u) & ~sl;
@@ -469,9 +473,7 @@ __device__ __forceinline__ DecResult decode_staged_lane_v7(const uint32_t* stage
                 const uint32_t wb = w << cons;
                 const uint32_t eb = T.lut[wb >> (32 - HHUFF_LUT_BITS)];
                 const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
-                const uint32_t h2b = (uint32_t)((int32_t)(eb << 1) >> 31);
-                lds_st8(sel_bits(slb, trash, o), eb);
-                lds_st8(sel_bits(h2b, o, trash - 1u) + 1u, eb >> 8);
+                lds_st16u(o, eb);
                 o += (eb >> 28) & 3u;
                 accb |= eb;
                 cons += ((eb >> 20) & 15u) & ~slb;
@@ -769,10 +771,18 @@ struct EncV2 {
         const uint32_t n01 = e0.y + e1.y, n23 = e2.y + e3.y, n = n01 + n23;
         const uint32_t mx = max(max(e0.y, e1.y), max(e2.y, e3.y));
         const uint32_t lngm = (uint32_t)((int32_t)(16u - mx) >> 31);                 // a code > 16 bits
+#ifdef HHUFF_ENC_MONO
+        // the running bit count grows with every byte of the lane, placed or not: once a dword would reach
+        // tlim every later one does too, so "tb + n < tlim" alone says whether this dword is placed (the
+        // verdict is tb >= tlim after the loop)
+        const uint32_t nm = n & onm;
+        const uint32_t putm = onm & (uint32_t)((int32_t)(tb + nm - tlim) >> 31);
+#else
         const uint32_t overm = onm & livem & ~(uint32_t)((int32_t)(tb + n - tlim) >> 31);  // tb + n >= tlim
         failm |= overm;
         livem &= ~overm;
         const uint32_t putm = onm & livem;
+#endif
         if (__builtin_amdgcn_ballot_w64((putm & lngm) != 0u) != 0) {
             if (putm & lngm) {
                 place_bits(obase, tb, (uint64_t)e0.x << e1.y | e1.x, n01);
@@ -792,7 +802,11 @@ struct EncV2 {
         if (__builtin_amdgcn_ballot_w64(sh + nf > 64u) != 0) {
             if (sh + nf > 64u) lds_or32(a + 8u, (uint32_t)t << (32u - sh));
         }
+#ifdef HHUFF_ENC_MONO
+        tb += nm;
+#else
         tb += n & putm;
+#endif
     }
 };
 
@@ -825,22 +839,29 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
     const uint32_t jlast = (last >> 2) - (a0 >> 2);  // stage reads are clamped to the span
     E.livem = E.live ? 0xFFFFFFFFu : 0u;
     {
-        const uint32_t jend = wave_max_u32(E.live ? jl : 0u);  // uniform trip count: no vote per step
+        const uint32_t jlv = E.live ? jl : 0u;  // a lane that failed in its head places nothing more
+        const uint32_t jend = wave_max_u32(jlv);  // uniform trip count: no vote per step
         uint32_t wn = sw[min(0u, jlast)];
         for (uint32_t j = 0; j < jend; ++j) {  // bulk
             const uint32_t w = wn;
             wn = sw[min(j + 1u, jlast)];
-            const uint32_t onm = ~(uint32_t)((int32_t)((j - jf) | (jl - 1u - j)) >> 31);  // jf <= j < jl
+            const uint32_t onm = ~(uint32_t)((int32_t)((j - jf) | (jlv - 1u - j)) >> 31);  // jf <= j < jlv
             E.put4m(enc[w & 0xFFu], enc[(w >> 8) & 0xFFu], enc[(w >> 16) & 0xFFu], enc[w >> 24], onm);
         }
     }
+#ifdef HHUFF_ENC_MONO
+    E.fail = E.fail || (E.live && E.tb >= E.tlim);
+    E.live = E.live && !E.fail;
+#else
     E.live = E.livem != 0u;
     E.fail = E.fail || E.failm != 0u;
+#endif
     masked(jl, active && (end & 3u) != 0 && jl >= jf);  // tail
     if (E.fail || !active) return kFailLen;
     const uint32_t tbits = E.tb - startbit;
-    if (pad) {  // fill the last byte with ones (EOS prefix, hpack.c:795-798)
-        const uint32_t p = (0u - tbits) & 7u;
+    if (pad) {  // fill the last byte with ones (EOS prefix, hpack.c:795-798); strings start on a byte, so the
+                // padding is the absolute stage bit's (a share of a longer string starts mid-byte)
+        const uint32_t p = (0u - E.tb) & 7u;
         place_bits(obase, E.tb, (1ull << p) - 1ull, p);
     }
     return tbits;

@@ -844,12 +844,12 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
         // ---- 3a. bulk (decode_staged_lane_v7's step) ----
         auto bstep = [&](bool longchk) {
             if (pm < lim) {
+                // one unaligned 16-bit store per lookup, as decode_staged_lane_v7's bulk (bytes past the symbols
+                // taken are rewritten later or lie past the round's output, inside the buffer)
                 const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
                 const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
                 const uint32_t sl = (uint32_t)((int32_t)e >> 31);
-                const uint32_t h2 = (uint32_t)((int32_t)(e << 1) >> 31);
-                lds_st8(sel_bits(sl, trash, o), e);
-                lds_st8(sel_bits(h2, o, trash - 1u) + 1u, e >> 8);
+                lds_st16u(o, e);
                 o += (e >> 28) & 3u;
                 accb |= e;
                 uint32_t cons = ((e >> 20) & 15u) & ~sl;
@@ -857,9 +857,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                     const uint32_t wb2 = w << cons;
                     const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
                     const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
-                    const uint32_t h2b = (uint32_t)((int32_t)(eb << 1) >> 31);
-                    lds_st8(sel_bits(slb, trash, o), eb);
-                    lds_st8(sel_bits(h2b, o, trash - 1u) + 1u, eb >> 8);
+                    lds_st16u(o, eb);
                     o += (eb >> 28) & 3u;
                     accb |= eb;
                     cons += ((eb >> 20) & 15u) & ~slb;
