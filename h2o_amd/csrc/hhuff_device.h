@@ -300,9 +300,6 @@ __device__ __forceinline__ uint32_t sel_bits(uint32_t m, uint32_t a, uint32_t b)
 __device__ __forceinline__ void lds_or32(uint32_t addr, uint32_t v) {
     __hip_atomic_fetch_or((lds_u32*)(size_t)addr, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// an unaligned 2-byte LDS store (ds_write_b16 at any byte address: gfx950 runs LDS in unaligned mode)
-typedef __attribute__((address_space(3))) uint16_t lds_u16u __attribute__((aligned(1)));
-__device__ __forceinline__ void lds_st16u(uint32_t addr, uint32_t v) { *(lds_u16u*)(size_t)addr = (uint16_t)v; }
 __device__ __forceinline__ uint32_t lds_ld8(uint32_t addr) { return *(const lds_u8*)(size_t)addr; }
 __device__ __forceinline__ uint32_t lds_ld32(uint32_t addr) { return *(const lds_u32*)(size_t)addr; }
 __device__ __forceinline__ void lds_st32(uint32_t addr, uint32_t v) { *(lds_u32*)(size_t)addr = v; }
@@ -459,13 +456,12 @@ __device__ __forceinline__ DecResult decode_staged_lane_v7(const uint32_t* stage
     };
     auto bstep = [&](bool longchk) {
         if (pm < lim) {
-            // Both symbol bytes go out as one unaligned 16-bit store at o, whatever the entry holds: with >= 27
-            // string bits left the bytes past the symbols taken are rewritten by the lane's next symbols (or
-            // lie past its decoded length, inside its slot: 5 symbols' room), so no trash redirection
             const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
             const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
-            const uint32_t sl = (uint32_t)((int32_t)e >> 31);  // LONG: nothing taken from the window
-            lds_st16u(o, e);
+            const uint32_t sl = (uint32_t)((int32_t)e >> 31);         // LONG: nothing taken from the window
+            const uint32_t h2 = (uint32_t)((int32_t)(e << 1) >> 31);  // HAS2
+            lds_st8(sel_bits(sl, trash, o), e);
+            lds_st8(sel_bits(h2, o, trash - 1u) + 1u, e >> 8);
             o += (e >> 28) & 3u;
             accb |= e;
             uint32_t cons = ((e >> 20) & 15u) & ~sl;
@@ -473,7 +469,9 @@ __device__ __forceinline__ DecResult decode_staged_lane_v7(const uint32_t* stage
                 const uint32_t wb = w << cons;
                 const uint32_t eb = T.lut[wb >> (32 - HHUFF_LUT_BITS)];
                 const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
-                lds_st16u(o, eb);
+                const uint32_t h2b = (uint32_t)((int32_t)(eb << 1) >> 31);
+                lds_st8(sel_bits(slb, trash, o), eb);
+                lds_st8(sel_bits(h2b, o, trash - 1u) + 1u, eb >> 8);
                 o += (eb >> 28) & 3u;
                 accb |= eb;
                 cons += ((eb >> 20) & 15u) & ~slb;

@@ -844,12 +844,12 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
         // ---- 3a. bulk (decode_staged_lane_v7's step) ----
         auto bstep = [&](bool longchk) {
             if (pm < lim) {
-                // one unaligned 16-bit store per lookup, as decode_staged_lane_v7's bulk (bytes past the symbols
-                // taken are rewritten later or lie past the round's output, inside the buffer)
                 const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
                 const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
                 const uint32_t sl = (uint32_t)((int32_t)e >> 31);
-                lds_st16u(o, e);
+                const uint32_t h2 = (uint32_t)((int32_t)(e << 1) >> 31);
+                lds_st8(sel_bits(sl, trash, o), e);
+                lds_st8(sel_bits(h2, o, trash - 1u) + 1u, e >> 8);
                 o += (e >> 28) & 3u;
                 accb |= e;
                 uint32_t cons = ((e >> 20) & 15u) & ~sl;
@@ -857,7 +857,9 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                     const uint32_t wb2 = w << cons;
                     const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
                     const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
-                    lds_st16u(o, eb);
+                    const uint32_t h2b = (uint32_t)((int32_t)(eb << 1) >> 31);
+                    lds_st8(sel_bits(slb, trash, o), eb);
+                    lds_st8(sel_bits(h2b, o, trash - 1u) + 1u, eb >> 8);
                     o += (eb >> 28) & 3u;
                     accb |= eb;
                     cons += ((eb >> 20) & 15u) & ~slb;
@@ -1802,24 +1804,15 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
         P.fits = P.span <= STAGE && P.ospan <= OSTAGE;
         return P;
     };
-    SpanPrefetch<(STAGE + 1023) / 1024> pf;
-    TIn nx = issue(t);
-    Plan cur = plan(t, nx);
-    TIn cx = nx;
-    if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
-    if (t + tstride < ntiles) nx = issue(t + tstride);
-    if (cur.fits) pf.commit(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+    // (the span is staged when its tile comes up: a register prefetch of it, as encode_pl_kernel does, took
+    // this kernel past 128 VGPRs into scratch -- twice the HBM traffic)
+    TIn cx = issue(t);
     for (;;) {
         const uint64_t tn = t + tstride;
         const bool have_next = tn < ntiles;
-        Plan nxt;
-        TIn nxi{0u, 0u, 0u, 0u};
-        if (have_next) {
-            nxt = plan(tn, nx);
-            nxi = nx;
-            if (nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
-            if (tn + tstride < ntiles) nx = issue(tn + tstride);
-        }
+        const Plan cur = plan(t, cx);
+        const TIn nxi = issue(have_next ? tn : t);  // the next tile's offsets: in flight during this tile
+        if (cur.fits) stage_span(stage, A.in, A.in_size, cur.a0, cur.span, lane);
         // ---- the current tile ----
         const uint32_t kt = cur.kt;
         const bool own = (uint32_t)lane < kt;
@@ -1915,8 +1908,6 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
         }
         if (own) A.out_len[i] = ol;
         if (!have_next) break;
-        if (nxt.fits) pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
-        cur = nxt;
         cx = nxi;
         t = tn;
     }

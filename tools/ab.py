@@ -43,6 +43,8 @@ def run(names, cfg="c4", rounds=5, steps=10):
         L = ctypes.CDLL(os.path.join(ABDIR, "libhhuff_%s.so" % nm))
         L.hhuff_decode_batch.argtypes = [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp, vp]
         L.hhuff_encode_batch.argtypes = [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp]
+        L.hhuff_flatten_batch.argtypes = [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint32, vp, ctypes.c_uint32, vp, vp, vp,
+                                          vp, vp]
         libs[nm] = L
     b = synth.make_batch_torch(cfg, seed=5)
     n, P = b["n"], int(b["total"])
@@ -72,7 +74,10 @@ def run(names, cfg="c4", rounds=5, steps=10):
     d_len = torch.empty(n_ok, dtype=torch.int32, device="cuda")
     d_st = torch.empty(n_ok, dtype=torch.uint8, device="cuda")
     ref = None
-    res = {nm: {"enc": [], "dec": []} for nm in names}
+    res = {nm: {"enc": [], "dec": [], "flat": []} for nm in names}
+    f_out = torch.empty(P + 11 * n + 16, dtype=torch.uint8, device="cuda")
+    f_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    kinds = ("enc", "dec", "flat") if os.environ.get("AB_FLAT") else ("enc", "dec")
 
     def positions(starts, lens_):  # byte positions covered by [start, start + len) slots
         lens_ = lens_.to(torch.int64)
@@ -87,12 +92,15 @@ def run(names, cfg="c4", rounds=5, steps=10):
     for r in range(rounds):
         for nm in names:
             L = libs[nm]
-            for kind in ("enc", "dec"):
+            for kind in kinds:
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                 for i in range(steps + 2):
                     if i == 2:
                         ev[0].record()
-                    if kind == "enc":
+                    if kind == "flat":  # QPACK flatten_string framing (prefix 7), c5's own operation
+                        rc = L.hhuff_flatten_batch(b["data"].data_ptr(), P, off32.data_ptr(), None, n, None, 7, None,
+                                                   f_out.data_ptr(), None, f_len.data_ptr(), s)
+                    elif kind == "enc":
                         rc = L.hhuff_encode_batch(b["data"].data_ptr(), P, off32.data_ptr(), None, n, e_out.data_ptr(),
                                                   None, e_len.data_ptr(), e_st.data_ptr(), s)
                     else:
@@ -113,6 +121,9 @@ def run(names, cfg="c4", rounds=5, steps=10):
             ok_d = d_len != -1
             d_pos = positions((hoff[:-1].to(torch.int64) * 8 // 5)[ok_d], d_len[ok_d])
             chk = chk + (content_sum(e_out, e_pos), content_sum(d_out, d_pos))
+            if "flat" in kinds:  # framed literals at in_off[i] + 11 i, f_len bytes each
+                f_pos = positions(b["off"][:-1] + 11 * torch.arange(n, device="cuda"), f_len)
+                chk = chk + (int(f_len.to(torch.int64).sum().item()), content_sum(f_out, f_pos))
             if ref is None:
                 ref = chk
             assert chk == ref or nm.startswith("x_"), (nm, chk, ref)  # x_*: ablation builds, output not checked
@@ -140,8 +151,12 @@ def run(names, cfg="c4", rounds=5, steps=10):
     for nm in names:
         e = sorted(res[nm]["enc"])
         d = sorted(res[nm]["dec"])
-        print(json.dumps({"build": nm, "cfg": cfg, "enc_ms_median": round(e[len(e) // 2], 4), "enc_ms_min": round(e[0], 4),
-                          "dec_ms_median": round(d[len(d) // 2], 4), "dec_ms_min": round(d[0], 4)}))
+        line = {"build": nm, "cfg": cfg, "enc_ms_median": round(e[len(e) // 2], 4), "enc_ms_min": round(e[0], 4),
+                "dec_ms_median": round(d[len(d) // 2], 4), "dec_ms_min": round(d[0], 4)}
+        if res[nm]["flat"]:
+            f = sorted(res[nm]["flat"])
+            line.update(flat_ms_median=round(f[len(f) // 2], 4), flat_ms_min=round(f[0], 4))
+        print(json.dumps(line))
 
 
 if __name__ == "__main__":
