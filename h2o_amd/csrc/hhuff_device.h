@@ -763,24 +763,16 @@ struct EncV2 {
         tb += put ? n : 0u;
     }
     // Same with every per-lane predicate an all-ones / zero mask in a VGPR (no exec-mask juggling on
-    // the SALU): `onm` = this lane has these four bytes; `livem` mirrors `live`.
-    uint32_t livem, failm;
+    // the SALU): `onm` = this lane has these four bytes.
     __device__ __forceinline__ void put4m(uint2 e0, uint2 e1, uint2 e2, uint2 e3, uint32_t onm) {
         const uint32_t n01 = e0.y + e1.y, n23 = e2.y + e3.y, n = n01 + n23;
         const uint32_t mx = max(max(e0.y, e1.y), max(e2.y, e3.y));
         const uint32_t lngm = (uint32_t)((int32_t)(16u - mx) >> 31);                 // a code > 16 bits
-#ifdef HHUFF_ENC_MONO
         // the running bit count grows with every byte of the lane, placed or not: once a dword would reach
         // tlim every later one does too, so "tb + n < tlim" alone says whether this dword is placed (the
-        // verdict is tb >= tlim after the loop)
+        // verdict is tb >= tlim after the loop; -4 % c4 encode against masks carried from dword to dword)
         const uint32_t nm = n & onm;
         const uint32_t putm = onm & (uint32_t)((int32_t)(tb + nm - tlim) >> 31);
-#else
-        const uint32_t overm = onm & livem & ~(uint32_t)((int32_t)(tb + n - tlim) >> 31);  // tb + n >= tlim
-        failm |= overm;
-        livem &= ~overm;
-        const uint32_t putm = onm & livem;
-#endif
         if (__builtin_amdgcn_ballot_w64((putm & lngm) != 0u) != 0) {
             if (putm & lngm) {
                 place_bits(obase, tb, (uint64_t)e0.x << e1.y | e1.x, n01);
@@ -800,11 +792,7 @@ struct EncV2 {
         if (__builtin_amdgcn_ballot_w64(sh + nf > 64u) != 0) {
             if (sh + nf > 64u) lds_or32(a + 8u, (uint32_t)t << (32u - sh));
         }
-#ifdef HHUFF_ENC_MONO
         tb += nm;
-#else
-        tb += n & putm;
-#endif
     }
 };
 
@@ -821,8 +809,7 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
     const uint32_t mfirst = 0xFFFFFFFFu << (8u * (start & 3u));
     const uint32_t mlast = (uint32_t)(0xFFFFFFFFull >> ((32u - 8u * (end & 3u)) & 31u));
     // tlim < 2^31 keeps tb + n - tlim a signed quantity (stage bits are < 2^20)
-    EncV2 E{enc, obase, startbit, limit >= 0x40000000u ? 0x7FFFFFFFu : startbit + limit, active, false,
-            active ? 0xFFFFFFFFu : 0u, 0u};
+    EncV2 E{enc, obase, startbit, limit >= 0x40000000u ? 0x7FFFFFFFu : startbit + limit, active, false};
     auto masked = [&](uint32_t j, bool on) {  // one dword with byte masks (head / tail)
         const uint32_t w = stage[min(a0 + 4u * j, last) >> 2];
         uint32_t vm = j == 0 ? mfirst : 0xFFFFFFFFu;
@@ -835,7 +822,6 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
     masked(0, active && jf != 0);  // head
     const uint32_t* sw = stage + (a0 >> 2);
     const uint32_t jlast = (last >> 2) - (a0 >> 2);  // stage reads are clamped to the span
-    E.livem = E.live ? 0xFFFFFFFFu : 0u;
     {
         const uint32_t jlv = E.live ? jl : 0u;  // a lane that failed in its head places nothing more
         const uint32_t jend = wave_max_u32(jlv);  // uniform trip count: no vote per step
@@ -847,13 +833,8 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
             E.put4m(enc[w & 0xFFu], enc[(w >> 8) & 0xFFu], enc[(w >> 16) & 0xFFu], enc[w >> 24], onm);
         }
     }
-#ifdef HHUFF_ENC_MONO
     E.fail = E.fail || (E.live && E.tb >= E.tlim);
     E.live = E.live && !E.fail;
-#else
-    E.live = E.livem != 0u;
-    E.fail = E.fail || E.failm != 0u;
-#endif
     masked(jl, active && (end & 3u) != 0 && jl >= jf);  // tail
     if (E.fail || !active) return kFailLen;
     const uint32_t tbits = E.tb - startbit;

@@ -1002,6 +1002,386 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
 }
 
 // ------------------------------------------------------------------------------------------------
+// Streaming decode v2 (mixed and long lengths; same results as decode_stream_kernel / decode_core).  The
+// rounds of decode_stream_kernel, with no global-memory round trip on a lane's way from one string to the
+// next -- there every string start cost a dependent chain (the work counter, the string's offsets, its first
+// window) that stalled the whole wave once per round in which any lane took a string:
+//   * a wave claims batches of 64 strings from the counter one batch ahead and keeps each batch's fields in
+//     registers (lane l holds string b + l: offset, length, is-name bit, destination); a lane takes its next
+//     string by ds_bpermute from them;
+//   * a lane whose string ends inside this round's window reserves its next string at the start of the
+//     round and prefetches that string's first window (in place of its own continuation) for the next round;
+//   * one per-lane LDS buffer of BW dwords (odd: lanes at the same position hit distinct banks) holds the
+//     output from its start and the window at its end; a round's output grows at most 1.6x as fast as the
+//     window is consumed and starts 0.6 of a window below it, so it never overtakes unread window bytes.
+// ------------------------------------------------------------------------------------------------
+// 16 bytes of LDS at a 4-aligned address (the odd-stride buffers are not 16-aligned)
+__device__ __forceinline__ uint4 lds_ld16(const uint8_t* p) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+    return make_uint4(q[0], q[1], q[2], q[3]);
+}
+__device__ __forceinline__ void lds_st16(uint8_t* p, uint4 v) {
+    uint32_t* q = reinterpret_cast<uint32_t*>(p);
+    q[0] = v.x, q[1] = v.y, q[2] = v.z, q[3] = v.w;
+}
+// store_range16 with the chunk in registers
+__device__ __forceinline__ void store_range16v(uint8_t* __restrict__ g, uint4 v, uint32_t lo, uint32_t hi) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        if (lo <= 4u * k && 4u * k + 4u <= hi) *reinterpret_cast<uint32_t*>(g + 4u * k) = w[k];
+    const uint64_t q0 = (uint64_t)v.y << 32 | v.x, q1 = (uint64_t)v.w << 32 | v.z;
+    auto byte_at = [&](uint32_t a) { return (uint32_t)((a < 8u ? q0 : q1) >> (8u * (a & 7u))); };
+    const uint32_t e0 = min(hi, (lo + 3u) & ~3u);
+    const uint32_t s1 = max(max(lo, hi & ~3u), e0);
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) {
+        if (lo + j < e0) g[lo + j] = (uint8_t)byte_at(lo + j);
+        if (s1 + j < hi) g[s1 + j] = (uint8_t)byte_at(s1 + j);
+    }
+}
+
+struct StreamBatch {  // lane l: string b + l of a claimed batch of 64 (cnt of them exist)
+    uint64_t b;
+    uint32_t cnt;
+    uint32_t s, lw;  // offset; length (clamped to kMaxStrLen + 1) | is-name << 31
+    uint32_t dst;    // explicit destination (out_off) or 0
+};
+
+template <int WAVES, int NW, int BW>
+__global__ __launch_bounds__(WAVES * 64) void decode_stream2_kernel(DecArgs A, unsigned long long* __restrict__ counter) {
+    static_assert(NW >= 8 && NW % 4 == 0 && (BW & 1) == 1, "window shape; odd buffer stride");
+    // in place: output [0, ...) below the window at WOFF (dwords [WOFF/4 - 1, WOFF/4 + NW) with the dword read
+    // before it), then a trash dword.  Output after c window bytes <= 15 + 1.6 c + 3 bytes, unread window >=
+    // WOFF + c: WOFF >= 15 + 0.6 (4 NW) + 3
+    constexpr uint32_t WOFF = ((15u + (12u * NW + 4u) / 5u + 3u + 4u) + 3u) & ~3u;
+    static_assert(WOFF + 4u * NW + 4u <= 4u * BW, "buffer too small for the window");
+    static_assert(15 + (32 * (NW - 2)) / 5 + 2 < WOFF + 4 * NW, "output past the window's end");
+    struct __attribute__((aligned(16))) Smem {
+        uint32_t lut[1u << HHUFF_LUT_BITS];
+        uint32_t kinfo[32];
+        uint32_t ones[(HHUFF_ONES_NENT + 3) & ~3];
+        uint32_t buf[WAVES * 64][BW];
+    };
+    if (A.gate && *A.gate != kGateStream) return;  // block-uniform: decode_select_kernel chose the staged kernel
+    __shared__ Smem sm;
+    load_dec_tables(sm.lut, sm.kinfo, sm.ones, WAVES * 64);
+    __syncthreads();
+    const DecTables T{sm.lut, sm.kinfo, sm.ones};
+    const int lane = threadIdx.x & 63;
+    uint8_t* obuf = reinterpret_cast<uint8_t*>(sm.buf[threadIdx.x]);
+    uint32_t* win = reinterpret_cast<uint32_t*>(obuf + WOFF);
+    const lds_u32* st = (const lds_u32*)win;
+    const uint32_t ob = lds_addr(obuf), trash = ob + WOFF + 4u * NW + 3u;
+    constexpr int32_t kLimW = 32 * (NW - 2) - 30;  // bulk steps start below this window bit
+    constexpr int32_t kFinal = 32 * (NW - 2);      // a string ending at or before this bit ends in the window
+
+    const uint64_t nwork = A.n_dev ? (uint64_t)*A.n_dev : (uint64_t)A.n;
+    if (nwork == 0) return;
+    auto claim = [&](StreamBatch& X) {
+        uint64_t b = 0;
+        if (lane == 0) b = atomicAdd(counter, 64ull);
+        b = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+        X.b = b;
+        X.cnt = b < nwork ? (uint32_t)min(nwork - b, (uint64_t)64) : 0u;
+        const uint64_t i = min(b + (uint64_t)lane, nwork - 1u);  // clamped: every load issues
+        X.s = A.in_off[i];
+        const uint32_t len = A.in_len ? A.in_len[i] : A.in_off[i + 1] - X.s;
+        const uint32_t nm = A.is_name_bits ? (A.is_name_bits[i >> 5] >> (i & 31)) & 1u : 0u;
+        X.lw = min(len, kMaxStrLen + 1u) | nm << 31;
+        X.dst = A.out_off ? A.out_off[i] : 0u;
+    };
+    StreamBatch QA, QB;
+    claim(QA);
+    claim(QB);
+    uint32_t qpos = 0;  // wave-uniform: strings of QA taken so far
+    // hand the queue's next strings to the lanes in `need` (in lane order); false where the queue is dry
+    auto take = [&](uint64_t need, uint32_t& i, uint32_t& s, uint32_t& lw, uint64_t& dst) {
+        const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        const uint32_t k = qpos + rank;
+        const bool inA = k < 64u;
+        const uint32_t src = (k & 63u) << 2;
+        const uint32_t sa = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)QA.s);
+        const uint32_t la = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)QA.lw);
+        const uint32_t da = A.out_off ? (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)QA.dst) : 0u;
+        // QB only when the takers run past QA (wave-uniform): its loads, issued at its claim, are waited
+        // for only here
+        uint32_t sb = 0, lb = 0, db = 0;
+        if (qpos + (uint32_t)__builtin_popcountll(need) > 64u) {
+            sb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)QB.s);
+            lb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)QB.lw);
+            if (A.out_off) db = (uint32_t)__builtin_amdgcn_ds_bpermute((int)src, (int)QB.dst);
+        }
+        const bool ok = ((need >> lane) & 1u) && (inA ? k < QA.cnt : (QA.cnt == 64u && k - 64u < QB.cnt));
+        i = (uint32_t)((inA ? QA.b : QB.b) + (k & 63u));
+        s = inA ? sa : sb;
+        lw = inA ? la : lb;
+        dst = A.out_off ? (uint64_t)(inA ? da : db) : dec_slot(s);
+        qpos += (uint32_t)__builtin_popcountll(need);
+        if (qpos >= 64u) {  // QA is used up: QB moves up, the next batch is claimed behind it
+            QA = QB;
+            qpos -= 64u;
+            claim(QB);
+        }
+        return ok;
+    };
+    auto dry = [&]() { return qpos >= QA.cnt && (QA.cnt < 64u || QB.cnt == 0u); };  // wave-uniform
+
+    // per-lane string state; the reserved next string; the prefetched window (its input address: pfa)
+    bool busy = false, head = false, is_name = false, rv = false;
+    uint32_t i = 0, s = 0, len = 0, P = 0, ocnt = 0, flags = 0, first = 0, lastb = 0, fail = 0;
+    uint64_t dst = 0;
+    uint32_t ri = 0, rs = 0, rlw = 0;
+    uint64_t rdst = 0;
+    uint4 pfv[NW / 4];
+    uint64_t pfa = ~0ull;
+    PROF_DECL
+
+    for (;;) {
+        // ---- 1. lanes without a string start their reserved one (or take one now: the first round, or after
+        //      a string that failed early) ----
+        {
+            const uint64_t need = __builtin_amdgcn_ballot_w64(!busy && !rv);
+            if (need != 0 && !dry()) rv = take(need, ri, rs, rlw, rdst) || rv;
+        }
+        if (!busy && rv) {
+            rv = false;
+            i = ri, s = rs, len = rlw & 0x7FFFFFFFu, is_name = (rlw >> 31) != 0, dst = rdst;
+            if (len > kMaxStrLen) {
+                A.out_len[i] = kFailLen;
+                A.status[i] = kStatusTooLong;
+            } else {
+                busy = true;
+                head = (dst & 15u) != 0;
+                P = ocnt = flags = first = lastb = fail = 0;
+            }
+        }
+        if (!__any(busy)) {
+            if (dry() && !__any(rv)) {
+                PROF_FLUSH(0);
+                break;
+            }
+            continue;
+        }
+        PROF_MARK(0);
+
+        // ---- 2. the lane's window: NW dwords from its current byte (dword-aligned), prefetched last round
+        //      unless the string started unannounced ----
+        const uint64_t cur = (uint64_t)s + (P >> 3);
+        const uint64_t wb = cur & ~3ull;
+        const uint64_t rem = (uint64_t)len * 8u - P;  // string bits left
+        if (busy) {
+            if (wb != pfa) {
+#pragma unroll
+                for (int j = 0; j < NW / 4; ++j) pfv[j] = load16_bounded(A.in, A.in_size, wb + 16u * j);
+            }
+#pragma unroll
+            for (int j = 0; j < NW / 4; ++j) {
+                win[4 * j + 0] = bswap32(pfv[j].x);
+                win[4 * j + 1] = bswap32(pfv[j].y);
+                win[4 * j + 2] = bswap32(pfv[j].z);
+                win[4 * j + 3] = bswap32(pfv[j].w);
+            }
+        }
+        int32_t pm = busy ? (int32_t)(8u * (uint32_t)(cur - wb) + (P & 7u)) - 1 : -1;
+        const int32_t pm0 = pm;
+        const int32_t end = busy ? (int32_t)min((uint64_t)(pm + 1) + rem, (uint64_t)0x40000000u) : 0;
+        const bool fin = busy && end <= kFinal;
+        // ---- 3. a lane whose string ends in this window reserves its next one and prefetches that string's
+        //      first window; the others prefetch their continuation ----
+        {
+            const uint64_t need = __builtin_amdgcn_ballot_w64(fin && !rv);
+            if (need != 0 && !dry()) rv = take(need, ri, rs, rlw, rdst) || rv;
+        }
+        {
+            const bool cont = busy && !fin;  // the string goes on past this window
+            pfa = cont ? wb + 4u * (NW - 3) : (fin && rv && (rlw & 0x7FFFFFFFu) <= kMaxStrLen) ? (uint64_t)(rs & ~3u) : ~0ull;
+            if (pfa != ~0ull) {
+#pragma unroll
+                for (int j = 0; j < NW / 4; ++j) pfv[j] = load16_bounded(A.in, A.in_size, pfa + 16u * j);
+            }
+        }
+        PROF_MARK(1);
+        const uint32_t h0 = (uint32_t)((dst + ocnt) & 15u);  // buffer offset of this round's first byte
+        uint32_t o = ob + h0;
+        int32_t q = pm >> 5;
+        uint32_t x0 = st[q], x1 = st[q + 1], x2 = st[q + 2];
+        uint32_t accb = 0, acc1 = 0, acc2 = 0, accl = 0, parked = busy ? 0u : 1u;
+        int32_t lim = busy ? min(end - 26, kLimW) : (int32_t)0x80000000;
+        auto advance = [&](int32_t cons) {
+            pm += cons;
+            const int32_t qn = pm >> 5;
+            const bool adv = qn != q;
+            x0 = adv ? x1 : x0;
+            x1 = adv ? x2 : x1;
+            q = qn;
+            x2 = st[q + 2];
+        };
+
+        // ---- 4a. bulk (decode_staged_lane_v7's step) ----
+        auto bstep = [&](bool longchk) {
+            if (pm < lim) {
+                const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+                const uint32_t sl = (uint32_t)((int32_t)e >> 31);
+                const uint32_t h2 = (uint32_t)((int32_t)(e << 1) >> 31);
+                lds_st8(sel_bits(sl, trash, o), e);
+                lds_st8(sel_bits(h2, o, trash - 1u) + 1u, e >> 8);
+                o += (e >> 28) & 3u;
+                accb |= e;
+                uint32_t cons = ((e >> 20) & 15u) & ~sl;
+                {
+                    const uint32_t wb2 = w << cons;
+                    const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
+                    const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
+                    const uint32_t h2b = (uint32_t)((int32_t)(eb << 1) >> 31);
+                    lds_st8(sel_bits(slb, trash, o), eb);
+                    lds_st8(sel_bits(h2b, o, trash - 1u) + 1u, eb >> 8);
+                    o += (eb >> 28) & 3u;
+                    accb |= eb;
+                    cons += ((eb >> 20) & 15u) & ~slb;
+                }
+                if (longchk && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
+                    if (sl) {
+                        const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                        const uint32_t ki = T.kinfo[k];
+                        const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                        const int32_t L = (le >> 9) & 31u;
+                        const uint32_t fits = (uint32_t)((L + pm - end) >> 31);
+                        const uint32_t eos = (le & 0x1FFu) == kEos ? 0xFFFFFFFFu : 0u;
+                        const uint32_t okm = fits & ~eos;
+                        fail |= fits & eos & 1u;  // EOS inside the string (hpack.c:88-89)
+                        lds_st8(sel_bits(okm, o, trash), le);
+                        o -= okm;
+                        accl |= le & okm;
+                        cons = okm & (uint32_t)L;
+                        parked |= ~okm & 1u;
+                        lim = (int32_t)sel_bits(okm, (uint32_t)lim, 0x80000000u);
+                    }
+                }
+                advance((int32_t)cons);
+            }
+        };
+        for (;;) {
+            bstep(false);
+            bstep(true);
+            if (!__any(pm < lim)) break;
+        }
+        PROF_MARK(2);
+
+        // ---- 4b. tail: lanes whose string ends in this window ----
+        int32_t c = (fin && !parked) ? pm - end : 0x40000000;
+        if (__any(fin)) {
+            int32_t prog = 0;
+            auto step = [&](bool longchk) {
+                const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+                const int32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+                const int32_t s1 = L1 + c, s2 = L12 + c;
+                const uint32_t m1 = (uint32_t)((s1 & ~(int32_t)e) >> 31);
+                const uint32_t m2 = (uint32_t)((s2 & (int32_t)(e << 1)) >> 31);
+                int32_t cons = (int32_t)sel_bits(m2, (uint32_t)L12, m1 & (uint32_t)L1);
+                lds_st8(sel_bits(m1, o - m2, trash), e >> 8);
+                lds_st8(sel_bits(m1, o, trash), e);
+                o = o - m1 - m2;
+                acc1 |= e & m1;
+                acc2 |= e & m2;
+                {
+                    const uint32_t wb2 = w << cons;
+                    const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
+                    const int32_t cb = c + cons;
+                    const int32_t L1b = (eb >> 16) & 15u, L12b = (eb >> 20) & 15u;
+                    const uint32_t m1b = (uint32_t)(((L1b + cb) & ~(int32_t)eb) >> 31);
+                    const uint32_t m2b = (uint32_t)(((L12b + cb) & (int32_t)(eb << 1)) >> 31);
+                    lds_st8(sel_bits(m1b, o - m2b, trash), eb >> 8);
+                    lds_st8(sel_bits(m1b, o, trash), eb);
+                    o = o - m1b - m2b;
+                    acc1 |= eb & m1b;
+                    acc2 |= eb & m2b;
+                    cons += (int32_t)sel_bits(m2b, (uint32_t)L12b, m1b & (uint32_t)L1b);
+                }
+                const bool lact = (s1 & (int32_t)e) < 0;
+                uint32_t consl = 0;
+                if (longchk && __builtin_amdgcn_ballot_w64(lact) != 0) {
+                    if (lact) {
+                        const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                        const uint32_t ki = T.kinfo[k];
+                        const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                        const int32_t L = (le >> 9) & 31u;
+                        const uint32_t fits = (uint32_t)((L + c) >> 31);
+                        const uint32_t eos = (le & 0x1FFu) == kEos ? 0xFFFFFFFFu : 0u;
+                        const uint32_t okm = fits & ~eos;
+                        fail |= fits & eos & 1u;
+                        lds_st8(sel_bits(okm, o, trash), le);
+                        o -= okm;
+                        accl |= le & okm;
+                        consl = okm & (uint32_t)L;
+                        c = (int32_t)sel_bits(okm, (uint32_t)c, 0x40000000u);
+                    }
+                }
+                cons |= (int32_t)consl;
+                c += cons;
+                advance(cons);
+                prog = cons;
+            };
+            step(true);
+            for (;;) {
+                step(false);
+                step(true);
+                if (!__any(prog != 0)) break;
+            }
+        }
+        PROF_MARK(3);
+
+        // ---- 5. flush whole chunks, carry the partial one; finish strings ----
+        if (busy) {
+            flags |= ((accb >> 24) | (accb >> 26) | (acc1 >> 24) | (acc2 >> 26) | (accl >> 14)) & 3u;
+            const uint32_t nb = o - ob;  // buffer bytes: h0 carried (or, at a string's start, foreign) + produced
+            const uint32_t made = nb - h0;
+            if (made) {
+                if (ocnt == 0) first = obuf[h0];
+                lastb = obuf[nb - 1u];
+            }
+            const bool done = parked || fin;
+            const bool ok = fin && !parked && !fail && [&] {
+                const uint32_t R = ~(uint32_t)c;
+                const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                return R <= 7 && (w | (0xFFFFFFFFu >> (R & 31u))) == 0xFFFFFFFFu;
+            }();
+            uint8_t* gchunk = A.out + ((dst + ocnt) & ~15ull);
+            const uint32_t hs = (uint32_t)(dst & 15u);  // head chunk: the string's bytes start here
+            if (!done || ok) {  // a failed string's output is unspecified: skip its last stores
+                const uint32_t nfull = nb >> 4;
+                for (uint32_t k = 0; k < nfull; ++k) {
+                    const uint4 v = lds_ld16(obuf + 16u * k);
+                    if (head && k == 0)
+                        store_range16v(gchunk, v, hs, 16u);
+                    else
+                        *reinterpret_cast<uint4*>(gchunk + 16u * k) = v;
+                }
+                head = head && nfull == 0;
+                const uint32_t part = nb & 15u;
+                if (done) {
+                    if (part > (head ? hs : 0u))
+                        store_range16v(gchunk + 16u * nfull, lds_ld16(obuf + 16u * nfull), head ? hs : 0u, part);
+                } else if (nfull) {
+                    lds_st16(obuf, lds_ld16(obuf + 16u * nfull));
+                }
+            }
+            ocnt += made;
+            P += (uint32_t)(pm - pm0);
+            if (done) {
+                A.out_len[i] = ok ? ocnt : kFailLen;
+                A.status[i] = ok ? soft_bits(is_name, ocnt, flags, first, lastb) : kStatusFail;
+                busy = false;
+            }
+        }
+        PROF_MARK(4);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // encode
 // ------------------------------------------------------------------------------------------------
 struct EncArgs {
@@ -2178,7 +2558,11 @@ constexpr int kDecSWaves = 16, kDecTWaves = HHUFF_DECT_W, kEncSWaves = 16, kEncO
 #define DEC_SP decode_staged_kernel<kDecSWaves, 3072, 4608, true>
 #define DEC_LP decode_staged_kernel<6, 8192, 12928, true>
 #define DEC_D decode_direct_kernel<4>
+#ifdef HHUFF_STREAM2  // A/B: the stream kernel with prefetched next strings, window in place (HHUFF_DECT_OUT: dwords)
+#define DEC_T decode_stream2_kernel<kDecTWaves, HHUFF_DECT_NW, HHUFF_DECT_OUT>
+#else
 #define DEC_T decode_stream_kernel<kDecTWaves, HHUFF_DECT_NW, HHUFF_DECT_OUT>
+#endif
 #define ENC_S encode_staged_kernel<kEncSWaves, 3584, false>
 #define ENC_O encode_sorted_kernel<kEncOStr, HHUFF_ENCO_CH>
 #define ENC_L encode_staged_kernel<8, 8192, false>
@@ -2841,6 +3225,10 @@ __device__ __forceinline__ void sys_load16x2(const void* pa, const void* pb, uin
         : "memory");
 }
 
+// Lanes with nothing to read in a poll read this device-memory line instead of host memory, so an idle poll
+// moves only the headers, the control words and the chunks the hot mailbox is expected to need over PCIe
+__device__ uint4 g_svc_dummy[64];
+
 template <int NC, bool JUMP = false>
 __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
                                                      uint64_t idle_ticks, uint64_t max_ticks) {
@@ -2864,13 +3252,16 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
         if (g == 0) sys_store(&ctrl->alive, 1u);
     }
     uint32_t handled = sys_load(&my->done);  // lane j keeps its mailbox's last served request
-    uint32_t hot = 0, polls = 0;  // hot: the lane whose mailbox was served last; every poll reads its chunks too
+    // hot: the lane whose mailbox was served last; every poll reads its chunks too, as many as its last
+    // request needed plus one (hot_ck)
+    uint32_t hot = 0, hot_ck = 1, polls = 0;
+    const void* const dummy = &g_svc_dummy[lane];
     for (;;) {
-        // one round: lane j < M reads its mailbox's header, lane M the control words {stop, alive, quit, G};
-        // every lane reads its chunk of the hot mailbox
+        // one round: lane j < M reads its mailbox's header, lane M the control words {stop, alive, quit, G},
+        // lane l < hot_ck chunk l of the hot mailbox; the other lanes read device memory
         uint4 hdr, ck;
-        const void* hp = mine ? (const void*)&my->req : (const void*)ctrl;
-        sys_load16x2(hp, slots[g + G * hot].chunk[lane], hdr, ck);
+        const void* hp = mine ? (const void*)&my->req : lane == M ? (const void*)ctrl : dummy;
+        sys_load16x2(hp, lane < hot_ck ? (const void*)slots[g + G * hot].chunk[lane] : dummy, hdr, ck);
         const uint32_t req = hdr.x;
         const uint32_t ctl_stop = (uint32_t)__shfl((int)hdr.x, (int)M), ctl_quit = (uint32_t)__shfl((int)hdr.z, (int)M);
         uint64_t pend = __builtin_amdgcn_ballot_w64(mine && req != handled);
@@ -2949,6 +3340,7 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
             if (lane == 0) sys_store(&sl->done, r);
             if (lane == s) handled = r;
             hot = s;
+            hot_ck = min(len / 12u + 2u, 64u);
             wave_lds_sync();
         }
     }
