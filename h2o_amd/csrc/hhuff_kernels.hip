@@ -847,9 +847,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                 const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
                 const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
                 const uint32_t sl = (uint32_t)((int32_t)e >> 31);
-                const uint32_t h2 = (uint32_t)((int32_t)(e << 1) >> 31);
-                lds_st8(sel_bits(sl, trash, o), e);
-                lds_st8(sel_bits(h2, o, trash - 1u) + 1u, e >> 8);
+                bulk_put2(o, e, trash);
                 o += (e >> 28) & 3u;
                 accb |= e;
                 uint32_t cons = ((e >> 20) & 15u) & ~sl;
@@ -857,9 +855,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                     const uint32_t wb2 = w << cons;
                     const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
                     const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
-                    const uint32_t h2b = (uint32_t)((int32_t)(eb << 1) >> 31);
-                    lds_st8(sel_bits(slb, trash, o), eb);
-                    lds_st8(sel_bits(h2b, o, trash - 1u) + 1u, eb >> 8);
+                    bulk_put2(o, eb, trash);
                     o += (eb >> 28) & 3u;
                     accb |= eb;
                     cons += ((eb >> 20) & 15u) & ~slb;
@@ -1225,9 +1221,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream2_kernel(DecArgs A, u
                 const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
                 const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
                 const uint32_t sl = (uint32_t)((int32_t)e >> 31);
-                const uint32_t h2 = (uint32_t)((int32_t)(e << 1) >> 31);
-                lds_st8(sel_bits(sl, trash, o), e);
-                lds_st8(sel_bits(h2, o, trash - 1u) + 1u, e >> 8);
+                bulk_put2(o, e, trash);
                 o += (e >> 28) & 3u;
                 accb |= e;
                 uint32_t cons = ((e >> 20) & 15u) & ~sl;
@@ -1235,9 +1229,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream2_kernel(DecArgs A, u
                     const uint32_t wb2 = w << cons;
                     const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
                     const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
-                    const uint32_t h2b = (uint32_t)((int32_t)(eb << 1) >> 31);
-                    lds_st8(sel_bits(slb, trash, o), eb);
-                    lds_st8(sel_bits(h2b, o, trash - 1u) + 1u, eb >> 8);
+                    bulk_put2(o, eb, trash);
                     o += (eb >> 28) & 3u;
                     accb |= eb;
                     cons += ((eb >> 20) & 15u) & ~slb;

@@ -543,27 +543,34 @@ def test_c5_full_size_framing_vs_oracle(torch_cuda, oracle_codec):
     assert _slot_bytes_equal(torch, f_out, torch.from_numpy(o_out).cuda(), slot_off, slot_len, f_len[:n])
 
 
-@pytest.mark.parametrize("pinned", [False, True])
-def test_pipelined_host_path(torch_cuda, pinned):
-    """chunked pageable/pinned -> device -> host path == the device-resident path, over many chunks"""
+@pytest.mark.parametrize("pinned", ["pageable", "pinned", "zero_copy", "pinned_dma"])
+def test_pipelined_host_path(torch_cuda, pinned, monkeypatch):
+    """host -> device -> host path == the device-resident path: pageable caller buffers (chunked, staged), pinned
+    data with pageable offsets (chunked DMA), everything pinned (zero copy: the kernels read and write host
+    memory), everything pinned with HHUFF_HOST_COPY=1 (the chunked DMA pipeline on pinned buffers)"""
     from h2o_amd import codec
 
     torch = torch_cuda
+    if pinned == "pinned_dma":
+        monkeypatch.setenv("HHUFF_HOST_COPY", "1")
     b = synth.make_batch_torch("c4", n=1 << 20, seed=23)
     n, P = b["n"], int(b["total"])
     off32 = b["off"].to(torch.int32)
     e_out, e_len, e_st = codec.encode_batch(b["data"], off32, n, in_size=P)
     torch.cuda.synchronize()
 
-    def host_buf(nbytes):
-        if pinned:
-            return torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True).numpy()
-        return np.zeros(nbytes, np.uint8)
+    def host_buf(nbytes, dt=torch.uint8, meta=False):
+        if pinned != "pageable" and (not meta or pinned != "pinned"):
+            return torch.zeros(nbytes, dtype=dt, pin_memory=True).numpy()
+        return np.zeros(nbytes, {torch.uint8: np.uint8, torch.int32: np.int32}[dt])
 
+    meta = dict(out_len=host_buf(n, torch.int32, True).view(np.uint32), status=host_buf(n, meta=True))
     data = host_buf(P)
     data[:] = b["data"].cpu().numpy()
-    off = off32.cpu().numpy().view(np.uint32).copy()
-    h_out, h_len, h_st = codec.encode_batch_host_pipelined(data, off, n, out=host_buf(P + 16), chunk_bytes=3 << 20)
+    off = host_buf(n + 1, torch.int32, True).view(np.uint32)
+    off[:] = off32.cpu().numpy().view(np.uint32)
+    h_out, h_len, h_st = codec.encode_batch_host_pipelined(data, off, n, out=host_buf(P + 16), chunk_bytes=3 << 20,
+                                                           **meta)
     g_len = e_len.cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(h_len, g_len)
     np.testing.assert_array_equal(h_st, e_st.cpu().numpy())
@@ -575,8 +582,12 @@ def test_pipelined_host_path(torch_cuda, pinned):
     torch.cuda.synchronize()
     src = host_buf(P)
     src[:] = g_out[:P]
-    h_out, h_len, h_st = codec.decode_batch_host_pipelined(src, off, n, is_name_bits=names.cpu().numpy().view(np.uint32),
-                                                          out=host_buf(codec.decode_slot_size(P)), chunk_bytes=5 << 20)
+    h_names = host_buf(names.numel(), torch.int32, True).view(np.uint32)
+    h_names[:] = names.cpu().numpy().view(np.uint32)
+    meta = dict(out_len=host_buf(n, torch.int32, True).view(np.uint32), status=host_buf(n, meta=True))
+    h_out, h_len, h_st = codec.decode_batch_host_pipelined(src, off, n, is_name_bits=h_names,
+                                                          out=host_buf(codec.decode_slot_size(P)), chunk_bytes=5 << 20,
+                                                          **meta)
     g_len = d_len.cpu().numpy().view(np.uint32)
     np.testing.assert_array_equal(h_len, g_len)
     np.testing.assert_array_equal(h_st, d_st.cpu().numpy())
