@@ -422,22 +422,15 @@ __device__ __forceinline__ void lds_zero(uint8_t* base, uint32_t a, uint32_t b, 
         *reinterpret_cast<uint4*>(base + k) = make_uint4(0u, 0u, 0u, 0u);
 }
 
-// A bulk step's two symbol bytes (decode_staged_lane_v7, the stream kernels).  HHUFF_DEC_B8 (A/B): both bytes
-// at o and o + 1 as they are, whatever the entry holds -- with >= 27 string bits left the bytes past the
-// symbols taken are rewritten by the lane's next symbols or lie past its decoded length inside its slot (5
-// symbols' room) -- so the stores need no trash redirection.  Default: bytes a step does not take go to the
-// lane's trash byte.  (One unaligned ds_write_b16 for both was measured: c4 decode 0.66 -> 0.98 ms.)
+// A bulk step's two symbol bytes (decode_staged_lane_v7, the stream kernels): both bytes at o and o + 1 as they
+// are, whatever the entry holds -- with >= 27 string bits left the bytes past the symbols taken are rewritten by
+// the lane's next symbols or lie past its decoded length inside its slot (5 symbols' room), so the stores need
+// no redirection of untaken bytes to a trash byte (c4 decode -7 % against that; one unaligned ds_write_b16 for
+// both bytes was measured too: 0.66 -> 0.98 ms).
 __device__ __forceinline__ void bulk_put2(uint32_t o, uint32_t e, uint32_t trash) {
-#ifdef HHUFF_DEC_B8
     (void)trash;
     lds_st8(o, e);
     lds_st8(o + 1u, e >> 8);
-#else
-    const uint32_t sl = (uint32_t)((int32_t)e >> 31);         // LONG: nothing taken from the window
-    const uint32_t h2 = (uint32_t)((int32_t)(e << 1) >> 31);  // HAS2
-    lds_st8(sel_bits(sl, trash, o), e);
-    lds_st8(sel_bits(h2, o, trash - 1u) + 1u, e >> 8);
-#endif
 }
 
 // ---------------------------------------------------------------------------------------------------

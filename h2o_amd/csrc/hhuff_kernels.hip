@@ -3217,9 +3217,30 @@ __device__ __forceinline__ void sys_load16x2(const void* pa, const void* pb, uin
         : "memory");
 }
 
-// Lanes with nothing to read in a poll read this device-memory line instead of host memory, so an idle poll
-// moves only the headers, the control words and the chunks the hot mailbox is expected to need over PCIe
-__device__ uint4 g_svc_dummy[64];
+// A poll's two 16-B system-scope loads on the lanes of two masks only (exec narrowed inside the asm and
+// restored before the wait), so an idle poll moves only the headers, the control words and the chunks the hot
+// mailbox is expected to need over PCIe -- not 2 KiB per wave per poll.  Lanes outside a mask read zeros (a
+// chunk numbered 0 never matches a request: mailbox request numbers start at 1).  (Pointing those lanes at one
+// device-memory line instead made every poll slower: 16 waves' uncached reads of the same line.)
+__device__ __forceinline__ void sys_poll(const void* pa, uint64_t ma, const void* pb, uint64_t mb, uint4& ra, uint4& rb) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    uint64_t save;
+    u32x4 a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
+    __asm__ volatile(
+        "s_mov_b64 %2, exec\n\t"
+        "s_and_b64 exec, exec, %5\n\t"
+        "global_load_dwordx4 %0, %3, off sc0 sc1\n\t"
+        "s_mov_b64 exec, %2\n\t"
+        "s_and_b64 exec, exec, %6\n\t"
+        "global_load_dwordx4 %1, %4, off sc0 sc1\n\t"
+        "s_mov_b64 exec, %2\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "+&v"(a), "+&v"(b), "=&s"(save)
+        : "v"(pa), "v"(pb), "s"(ma), "s"(mb)
+        : "memory", "scc");
+    ra = make_uint4(a.x, a.y, a.z, a.w);
+    rb = make_uint4(b.x, b.y, b.z, b.w);
+}
 
 template <int NC, bool JUMP = false>
 __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
@@ -3247,13 +3268,14 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
     // hot: the lane whose mailbox was served last; every poll reads its chunks too, as many as its last
     // request needed plus one (hot_ck)
     uint32_t hot = 0, hot_ck = 1, polls = 0;
-    const void* const dummy = &g_svc_dummy[lane];
+    const uint64_t mhdr = (2ull << M) - 1ull;  // lanes 0 .. M
+    uint4 hdr = make_uint4(0u, 0u, 0u, 0u), ck = make_uint4(0u, 0u, 0u, 0u);
     for (;;) {
         // one round: lane j < M reads its mailbox's header, lane M the control words {stop, alive, quit, G},
-        // lane l < hot_ck chunk l of the hot mailbox; the other lanes read device memory
-        uint4 hdr, ck;
-        const void* hp = mine ? (const void*)&my->req : lane == M ? (const void*)ctrl : dummy;
-        sys_load16x2(hp, lane < hot_ck ? (const void*)slots[g + G * hot].chunk[lane] : dummy, hdr, ck);
+        // lane l < hot_ck chunk l of the hot mailbox; the other lanes read nothing
+        const void* hp = mine ? (const void*)&my->req : (const void*)ctrl;
+        const uint32_t hk = (uint32_t)__builtin_amdgcn_readfirstlane((int)hot_ck);  // wave-uniform
+        sys_poll(hp, mhdr, slots[g + G * hot].chunk[lane], hk >= 64u ? ~0ull : (1ull << hk) - 1ull, hdr, ck);
         const uint32_t req = hdr.x;
         const uint32_t ctl_stop = (uint32_t)__shfl((int)hdr.x, (int)M), ctl_quit = (uint32_t)__shfl((int)hdr.z, (int)M);
         uint64_t pend = __builtin_amdgcn_ballot_w64(mine && req != handled);
