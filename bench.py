@@ -32,7 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
-HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); measured copy peak ~6300
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); the line also carries the measured copy peak
 N_SIMD, N_CU = 1024, 256
 GIB = float(1 << 30)
 METRIC = "GiB/s device-resident Huffman decode+encode, 16M header strings mean 48B"
@@ -429,6 +429,10 @@ def main():
         sec = secondary(pmc.get(dominant, {}))
         if sec:
             roof["secondary"] = sec
+        cp = copy_peak(torch)
+        if cp:
+            roof["measured_copy_peak"] = cp
+            roof["frac_of_measured"] = round(ach / cp, 4)
         line = {
             "metric": METRIC,
             "value": round(P_all / GIB / (ms_step * 1e-3), 3),
@@ -488,6 +492,29 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def copy_peak(torch, nbytes=1 << 30, reps=5):
+    """the device-to-device copy rate this GPU sustains (GB/s, bytes read + written, best of `reps`): what
+    an HBM-bound kernel can reach here, beside the 8 TB/s spec in `peak`"""
+    try:
+        src = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+        dst = torch.empty_like(src)
+    except RuntimeError:
+        return None
+    dst.copy_(src)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        dst.copy_(src)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del src, dst
+    torch.cuda.empty_cache()
+    return round(2 * nbytes / (best * 1e-3) / 1e9, 1)
 
 
 def kernel_roofline(B, t_ms, pmc, key):
@@ -627,6 +654,7 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, re
     os.environ.pop("HHUFF_HOST_COPY", None)
     t = res["pinned"]
     return {"value": round(P / GIB / t, 3), "unit": "GiB/s", "ms_per_step": round(t * 1e3, 3),
+            "pcie": pcie_rates(torch),
             "pinned_dma_value": round(P / GIB / res["pinned_dma"], 3),
             "pinned_dma_ms_per_step": round(res["pinned_dma"] * 1e3, 3),
             "pageable_value": round(P / GIB / res["pageable"], 3),
@@ -635,6 +663,37 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, re
                     "buffers are read and written by the kernels in place (zero copy), pinned_dma is the chunked DMA "
                     "pipeline on the same buffers (64 MiB chunks, 3 streams), pageable buffers go through it with "
                     "host staging; best of %d" % reps}
+
+
+def pcie_rates(torch, nbytes=256 << 20, reps=3):
+    """DMA rates of this box's link (GB/s, best of `reps`): pinned host -> device, device -> pinned host, and
+    both at once on two streams (the ceiling the host paths share)"""
+    h1 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    h2 = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    d1 = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    d2 = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+
+    def run(h2d, d2h):
+        best = None
+        for _ in range(reps + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            if h2d:
+                with torch.cuda.stream(s1):
+                    d1.copy_(h1, non_blocking=True)
+            if d2h:
+                with torch.cuda.stream(s2):
+                    h2.copy_(d2, non_blocking=True)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        return round((h2d + d2h) * nbytes / best / 1e9, 1)
+
+    out = {"h2d_gbps": run(1, 0), "d2h_gbps": run(0, 1), "bidirectional_gbps": run(1, 1)}
+    del h1, h2, d1, d2
+    torch.cuda.empty_cache()
+    return out
 
 
 def cpu_baseline(b, args):

@@ -124,6 +124,10 @@ def lib():
         L.hhuff_grid_size.argtypes = [ctypes.c_int, ctypes.c_int]
         L.hhuff_decode_prices.restype = ctypes.c_int
         L.hhuff_decode_prices.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+        L.hhuff_calibrate_decode_prices.restype = ctypes.c_int
+        L.hhuff_calibrate_decode_prices.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
+        L.hhuff_set_decode_prices.restype = ctypes.c_int
+        L.hhuff_set_decode_prices.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
         L.hhuff_pool_trim.restype = ctypes.c_int
         L.hhuff_pool_trim.argtypes = []
         _lib = L
@@ -138,7 +142,8 @@ EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decod
             "hhuff_qpack_decode", "hhuff_qpack_parse_requests", "hhuff_qpack_parse_responses", "hhuff_qpack_scratch_size",
             "hhuff_decode_batch_host", "hhuff_encode_batch_host", "hhuff_decode_batch_host_pipelined",
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string", "hhuff_per_string_calls",
-            "hhuff_grid_size", "hhuff_decode_prices", "hhuff_pool_trim", "hhuff_service_stamps", "hhuff_hpack_enc_scratch_size",
+            "hhuff_grid_size", "hhuff_decode_prices", "hhuff_calibrate_decode_prices", "hhuff_set_decode_prices",
+            "hhuff_pool_trim", "hhuff_service_stamps", "hhuff_hpack_enc_scratch_size",
             "hhuff_hpack_flatten_responses", "hhuff_qpack_flatten_responses")
 
 
@@ -591,7 +596,20 @@ def encode_batch_host_pipelined(data, in_off, n, out=None, chunk_bytes=0, device
 
 def decode_prices(device=0):
     """the staged / stream prices (ps per string, per byte, each kernel) the mixed-length decode of `device`
-    uses (include/hhuff.h hhuff_decode_prices; measured at first use)"""
+    uses (include/hhuff.h hhuff_decode_prices: fitted defaults until calibrated or pinned; no GPU work)"""
     buf = (ctypes.c_float * 4)()
     _check(lib().hhuff_decode_prices(device, buf), "hhuff_decode_prices")
     return [float(x) for x in buf]
+
+
+def calibrate_decode_prices(device=0):
+    """measure `device`'s prices now and use them from then on (hhuff_calibrate_decode_prices; synchronous)"""
+    buf = (ctypes.c_float * 4)()
+    _check(lib().hhuff_calibrate_decode_prices(device, buf), "hhuff_calibrate_decode_prices")
+    return [float(x) for x in buf]
+
+
+def set_decode_prices(prices, device=0):
+    """pin `device`'s prices (4 floats), or restore the fitted defaults with None (hhuff_set_decode_prices)"""
+    buf = None if prices is None else (ctypes.c_float * 4)(*[float(x) for x in prices])
+    _check(lib().hhuff_set_decode_prices(device, buf), "hhuff_set_decode_prices")

@@ -972,7 +972,18 @@ HHUFF_API int hhuff_pool_trim(void) {
 }
 HHUFF_API int hhuff_decode_prices(int device, float* out4) {
     if (!out4) return arg_fail("NULL out4");
-    return hhuff::decode_prices_of(device, out4) == 0 ? HHUFF_OK : hip_fail(hipErrorInvalidDevice, "hhuff_decode_prices");
+    return hhuff::decode_prices_of(device, out4, 0) == 0 ? HHUFF_OK : hip_fail(hipErrorInvalidDevice, "hhuff_decode_prices");
+}
+HHUFF_API int hhuff_calibrate_decode_prices(int device, float* out4) {
+    float tmp[4];
+    return hhuff::decode_prices_of(device, out4 ? out4 : tmp, 1) == 0
+               ? HHUFF_OK
+               : hip_fail(hipErrorInvalidDevice, "hhuff_calibrate_decode_prices");
+}
+HHUFF_API int hhuff_set_decode_prices(int device, const float* in4) {
+    const int r = hhuff::set_decode_prices(device, in4);
+    if (r == -2) return arg_fail("decode prices must be finite and >= 0");
+    return r == 0 ? HHUFF_OK : hip_fail(hipErrorInvalidDevice, "hhuff_set_decode_prices");
 }
 
 HHUFF_API int hhuff_grid_size(int device, int which) {

@@ -23,6 +23,12 @@ namespace hhuff {
 
 constexpr uint32_t kLong = 1u << 31;  // window LUT bits: tools/gen_tables.py:window_lut
 constexpr uint32_t kHas2 = 1u << 30;
+// window LUT entry fields: [7:0] sym1, [11:8] L1, [15:12] L12, [23:16] sym2 (stored by a byte store of the
+// entry's high half, no shift), [27:24] validity flags, [29:28] symbol count
+__host__ __device__ __forceinline__ uint32_t lut_l1(uint32_t e) { return (e >> 8) & 15u; }
+__host__ __device__ __forceinline__ uint32_t lut_l12(uint32_t e) { return (e >> 12) & 15u; }
+__host__ __device__ __forceinline__ uint32_t lut_sym2(uint32_t e) { return e >> 16; }  // low byte: the symbol
+__host__ __device__ __forceinline__ uint32_t lut_pair(uint32_t e) { return (e & 0xFFu) | ((e >> 8) & 0xFF00u); }
 constexpr uint32_t kEos = 256;
 constexpr uint32_t kFailLen = 0xFFFFFFFFu;
 constexpr uint8_t kStatusFail = 0x80;
@@ -271,12 +277,12 @@ __device__ __forceinline__ DecResult decode_core(const Src& src, uint32_t start,
             R -= L;
             br.consume(L, src);
         } else {
-            const uint32_t L1 = (e >> 16) & 15u;
+            const uint32_t L1 = lut_l1(e);
             if (L1 > R) break;  // fewer bits left than the next code: padding
-            const uint32_t L12 = (e >> 20) & 15u;
+            const uint32_t L12 = lut_l12(e);
             const bool two = (e & kHas2) && L12 <= R;
             const uint32_t cons = two ? L12 : L1;
-            sink.put12(e, two);
+            sink.put12(lut_pair(e), two);
             flags |= (e >> 24) & (two ? 15u : 3u);
             R -= cons;
             br.consume(cons, src);
@@ -430,7 +436,7 @@ __device__ __forceinline__ void lds_zero(uint8_t* base, uint32_t a, uint32_t b, 
 __device__ __forceinline__ void bulk_put2(uint32_t o, uint32_t e, uint32_t trash) {
     (void)trash;
     lds_st8(o, e);
-    lds_st8(o + 1u, e >> 8);
+    lds_st8(o + 1u, lut_sym2(e));
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -473,15 +479,14 @@ __device__ __forceinline__ DecResult decode_staged_lane_v7(const uint32_t* stage
             bulk_put2(o, e, trash);
             o += (e >> 28) & 3u;
             accb |= e;
-            uint32_t cons = ((e >> 20) & 15u) & ~sl;
+            uint32_t cons = lut_l12(e);  // LONG entries carry L12 = 0
             {
                 const uint32_t wb = w << cons;
                 const uint32_t eb = T.lut[wb >> (32 - HHUFF_LUT_BITS)];
-                const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
                 bulk_put2(o, eb, trash);
                 o += (eb >> 28) & 3u;
                 accb |= eb;
-                cons += ((eb >> 20) & 15u) & ~slb;
+                cons += lut_l12(eb);
             }
             if (longchk && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
                 if (sl) {
@@ -519,12 +524,12 @@ __device__ __forceinline__ DecResult decode_staged_lane_v7(const uint32_t* stage
     auto step = [&](bool longchk) {
         const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
         const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
-        const int32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+        const int32_t L1 = lut_l1(e), L12 = lut_l12(e);
         const int32_t s1 = L1 + c, s2 = L12 + c;
         const uint32_t m1 = (uint32_t)((s1 & ~(int32_t)e) >> 31);
         const uint32_t m2 = (uint32_t)((s2 & (int32_t)(e << 1)) >> 31);
         int32_t cons = (int32_t)sel_bits(m2, (uint32_t)L12, m1 & (uint32_t)L1);
-        lds_st8(sel_bits(m1, o - m2, trash), e >> 8);
+        lds_st8(sel_bits(m1, o - m2, trash), lut_sym2(e));
         lds_st8(sel_bits(m1, o, trash), e);
         o = o - m1 - m2;
         acc1 |= e & m1;
@@ -533,10 +538,10 @@ __device__ __forceinline__ DecResult decode_staged_lane_v7(const uint32_t* stage
             const uint32_t wb = w << cons;
             const uint32_t eb = T.lut[wb >> (32 - HHUFF_LUT_BITS)];
             const int32_t cb = c + cons;
-            const int32_t L1b = (eb >> 16) & 15u, L12b = (eb >> 20) & 15u;
+            const int32_t L1b = lut_l1(eb), L12b = lut_l12(eb);
             const uint32_t m1b = (uint32_t)(((L1b + cb) & ~(int32_t)eb) >> 31);
             const uint32_t m2b = (uint32_t)(((L12b + cb) & (int32_t)(eb << 1)) >> 31);
-            lds_st8(sel_bits(m1b, o - m2b, trash), eb >> 8);
+            lds_st8(sel_bits(m1b, o - m2b, trash), lut_sym2(eb));
             lds_st8(sel_bits(m1b, o, trash), eb);
             o = o - m1b - m2b;
             acc1 |= eb & m1b;

@@ -59,18 +59,30 @@ __device__ __forceinline__ uint4 load16_tail(const uint8_t* __restrict__ in, uin
     return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
 
-// Stage [a0, a0 + span) of `in` into LDS (16-byte loads; bytes past in_size read as 0).
-__device__ __forceinline__ void stage_span(uint32_t* stage, const uint8_t* __restrict__ in, uint64_t in_size, uint32_t a0,
-                                           uint32_t span, int lane) {
-    for (uint32_t k = (uint32_t)lane * 16u; k < span; k += 64u * 16u) {
-        const uint64_t g = (uint64_t)a0 + k;
-        uint4 v;
-        if (g + 16 <= in_size) {
-            v = *reinterpret_cast<const uint4*>(in + g);
-        } else {
-            v = load16_tail(in, in_size, g);
-        }
-        *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(stage) + k) = v;
+constexpr int kVmWait0 = 0x0F70;  // s_waitcnt vmcnt(0) (expcnt, lgkmcnt untouched)
+
+// Stage [a0, a0 + span) of `in` into a wave's LDS stage with LDS-DMA (global_load_lds_dwordx4: 16 B a lane to
+// the wave-uniform base + 16 lane, no VGPRs), every 1-KiB chunk in flight at once, then one wait; the chunk
+// holding the input's end goes through registers (bytes past in_size read as 0).  (A loop of load / wait /
+// ds_write paid one memory latency per KiB; register staging of all chunks spilled in flatten_pl_kernel.)
+template <int NCH>
+__device__ __forceinline__ void stage_span_dma(uint32_t* stage, const uint8_t* __restrict__ in, uint64_t in_size,
+                                               uint32_t a0, uint32_t span, int lane) {
+    const uint64_t av = in_size > (uint64_t)a0 ? in_size - a0 : 0u;
+    const uint32_t avail = av > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)av;
+    const uint32_t sb = lds_addr(stage);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const uint32_t k = (uint32_t)c * 1024u + (uint32_t)lane * 16u;
+        if (k < span && k + 16u <= avail)
+            __builtin_amdgcn_global_load_lds((const void*)(in + a0 + k), (lds_u8*)(size_t)(sb + (uint32_t)c * 1024u), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(kVmWait0);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const uint32_t k = (uint32_t)c * 1024u + (uint32_t)lane * 16u;
+        if (k < span && k + 16u > avail)
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(stage) + k) = load16_tail(in, in_size, (uint64_t)a0 + k);
     }
 }
 
@@ -332,7 +344,7 @@ struct DecArgs {
     uint32_t* pk_off;      // packed mode (decode_staged_kernel<.., true>): u32[n + 1] output places
     const uint32_t* n_dev;  // NULL, or the string count in device memory (n an upper bound)
     // with gate: the staged / stream prices select_verdict uses, ps per string and per (tile-padded) byte --
-    // measured on the device at first use (decode_prices), these fitted values until then
+    // the fitted defaults, or the device's calibration (calibrate_prices)
     float price[4] = {40.0f, 1.07f, 184.0f, 1.15f};
 };
 
@@ -850,15 +862,14 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                 bulk_put2(o, e, trash);
                 o += (e >> 28) & 3u;
                 accb |= e;
-                uint32_t cons = ((e >> 20) & 15u) & ~sl;
+                uint32_t cons = lut_l12(e);  // LONG entries carry L12 = 0
                 {
                     const uint32_t wb2 = w << cons;
                     const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
-                    const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
                     bulk_put2(o, eb, trash);
                     o += (eb >> 28) & 3u;
                     accb |= eb;
-                    cons += ((eb >> 20) & 15u) & ~slb;
+                    cons += lut_l12(eb);
                 }
                 if (longchk && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
                     if (sl) {
@@ -895,12 +906,12 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
             auto step = [&](bool longchk) {
                 const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
                 const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
-                const int32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+                const int32_t L1 = lut_l1(e), L12 = lut_l12(e);
                 const int32_t s1 = L1 + c, s2 = L12 + c;
                 const uint32_t m1 = (uint32_t)((s1 & ~(int32_t)e) >> 31);
                 const uint32_t m2 = (uint32_t)((s2 & (int32_t)(e << 1)) >> 31);
                 int32_t cons = (int32_t)sel_bits(m2, (uint32_t)L12, m1 & (uint32_t)L1);
-                lds_st8(sel_bits(m1, o - m2, trash), e >> 8);
+                lds_st8(sel_bits(m1, o - m2, trash), lut_sym2(e));
                 lds_st8(sel_bits(m1, o, trash), e);
                 o = o - m1 - m2;
                 acc1 |= e & m1;
@@ -909,10 +920,10 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                     const uint32_t wb2 = w << cons;
                     const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
                     const int32_t cb = c + cons;
-                    const int32_t L1b = (eb >> 16) & 15u, L12b = (eb >> 20) & 15u;
+                    const int32_t L1b = lut_l1(eb), L12b = lut_l12(eb);
                     const uint32_t m1b = (uint32_t)(((L1b + cb) & ~(int32_t)eb) >> 31);
                     const uint32_t m2b = (uint32_t)(((L12b + cb) & (int32_t)(eb << 1)) >> 31);
-                    lds_st8(sel_bits(m1b, o - m2b, trash), eb >> 8);
+                    lds_st8(sel_bits(m1b, o - m2b, trash), lut_sym2(eb));
                     lds_st8(sel_bits(m1b, o, trash), eb);
                     o = o - m1b - m2b;
                     acc1 |= eb & m1b;
@@ -1224,15 +1235,14 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream2_kernel(DecArgs A, u
                 bulk_put2(o, e, trash);
                 o += (e >> 28) & 3u;
                 accb |= e;
-                uint32_t cons = ((e >> 20) & 15u) & ~sl;
+                uint32_t cons = lut_l12(e);  // LONG entries carry L12 = 0
                 {
                     const uint32_t wb2 = w << cons;
                     const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
-                    const uint32_t slb = (uint32_t)((int32_t)eb >> 31);
                     bulk_put2(o, eb, trash);
                     o += (eb >> 28) & 3u;
                     accb |= eb;
-                    cons += ((eb >> 20) & 15u) & ~slb;
+                    cons += lut_l12(eb);
                 }
                 if (longchk && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
                     if (sl) {
@@ -1269,12 +1279,12 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream2_kernel(DecArgs A, u
             auto step = [&](bool longchk) {
                 const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
                 const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
-                const int32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+                const int32_t L1 = lut_l1(e), L12 = lut_l12(e);
                 const int32_t s1 = L1 + c, s2 = L12 + c;
                 const uint32_t m1 = (uint32_t)((s1 & ~(int32_t)e) >> 31);
                 const uint32_t m2 = (uint32_t)((s2 & (int32_t)(e << 1)) >> 31);
                 int32_t cons = (int32_t)sel_bits(m2, (uint32_t)L12, m1 & (uint32_t)L1);
-                lds_st8(sel_bits(m1, o - m2, trash), e >> 8);
+                lds_st8(sel_bits(m1, o - m2, trash), lut_sym2(e));
                 lds_st8(sel_bits(m1, o, trash), e);
                 o = o - m1 - m2;
                 acc1 |= e & m1;
@@ -1283,10 +1293,10 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream2_kernel(DecArgs A, u
                     const uint32_t wb2 = w << cons;
                     const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
                     const int32_t cb = c + cons;
-                    const int32_t L1b = (eb >> 16) & 15u, L12b = (eb >> 20) & 15u;
+                    const int32_t L1b = lut_l1(eb), L12b = lut_l12(eb);
                     const uint32_t m1b = (uint32_t)(((L1b + cb) & ~(int32_t)eb) >> 31);
                     const uint32_t m2b = (uint32_t)(((L12b + cb) & (int32_t)(eb << 1)) >> 31);
-                    lds_st8(sel_bits(m1b, o - m2b, trash), eb >> 8);
+                    lds_st8(sel_bits(m1b, o - m2b, trash), lut_sym2(eb));
                     lds_st8(sel_bits(m1b, o, trash), eb);
                     o = o - m1b - m2b;
                     acc1 |= eb & m1b;
@@ -2176,15 +2186,15 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
         P.fits = P.span <= STAGE && P.ospan <= OSTAGE;
         return P;
     };
-    // (the span is staged when its tile comes up: a register prefetch of it, as encode_pl_kernel does, took
-    // this kernel past 128 VGPRs into scratch -- twice the HBM traffic)
+    // (the span is staged when its tile comes up: a register prefetch of it across the tile, as encode_pl_kernel
+    // does, took this kernel past 128 VGPRs into scratch -- twice the HBM traffic)
     TIn cx = issue(t);
     for (;;) {
         const uint64_t tn = t + tstride;
         const bool have_next = tn < ntiles;
         const Plan cur = plan(t, cx);
         const TIn nxi = issue(have_next ? tn : t);  // the next tile's offsets: in flight during this tile
-        if (cur.fits) stage_span(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+        if (cur.fits) stage_span_dma<(STAGE + 1023) / 1024>(stage, A.in, A.in_size, cur.a0, cur.span, lane);
         // ---- the current tile ----
         const uint32_t kt = cur.kt;
         const bool own = (uint32_t)lane < kt;
@@ -2740,89 +2750,110 @@ static int pick_encode(uint64_t in_size, uint32_t n) {
     return kEncD;
 }
 
-// Staged / stream prices of this device (select_verdict), measured once: both kernels decode two probe
-// batches of fixed-length strings (zero bytes: '0' symbols to the end, so every string is decoded whole and
-// then fails its padding), 131,072 x 48 B and 65,536 x 120 B (a 64-string tile of those still fits the
-// staged kernel's stage), timed with events on a private stream (best of 3 after a warm-up); per kernel,
-// per-string and per-byte costs solve t / n = a + b L on the two lengths.  A failed or implausible fit
-// keeps the fitted defaults.  Blocks the calling thread once per device (about 2 ms).
-static void decode_prices(int dev, float out[4]) {
-    static std::mutex mu;
-    static bool done[64] = {};
-    static float cache[64][4];
-    if (dev < 0 || dev >= 64) return;
-    std::lock_guard<std::mutex> g(mu);
-    if (!done[dev]) {
-        done[dev] = true;
-        const float def[4] = {40.0f, 1.07f, 184.0f, 1.15f};
-        for (int k = 0; k < 4; ++k) cache[dev][k] = def[k];
-        constexpr uint32_t kN[2] = {131072u, 65536u}, kL[2] = {48u, 120u};
-        const uint64_t bytes = (uint64_t)kN[1] * kL[1];
-        hipStream_t s = nullptr;
-        uint8_t *in = nullptr, *out = nullptr, *st = nullptr;
-        uint32_t *off = nullptr, *olen = nullptr;
-        unsigned long long* ctr = nullptr;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
-                  hipMalloc((void**)&in, bytes + 64) == hipSuccess && hipMalloc((void**)&out, (bytes * 8) / 5 + 64) == hipSuccess &&
-                  hipMalloc((void**)&st, kN[0]) == hipSuccess && hipMalloc((void**)&off, 4ull * (kN[0] + 1)) == hipSuccess &&
-                  hipMalloc((void**)&olen, 4ull * kN[0]) == hipSuccess && hipMalloc((void**)&ctr, 8) == hipSuccess &&
-                  hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
-                  hipMemsetAsync(in, 0, bytes + 64, s) == hipSuccess;
-        double u[2][2] = {};  // [kernel][probe]: ms per string
-        for (int p = 0; ok && p < 2; ++p) {
-            std::vector<uint32_t> h(kN[p] + 1);
-            for (uint32_t i = 0; i <= kN[p]; ++i) h[i] = i * kL[p];
-            ok = hipMemcpyAsync(off, h.data(), 4ull * (kN[p] + 1), hipMemcpyHostToDevice, s) == hipSuccess &&
-                 hipStreamSynchronize(s) == hipSuccess;
-            DecArgs A{in, (uint64_t)kN[p] * kL[p], off, nullptr, kN[p], nullptr, out, nullptr, olen, st,
-                      nullptr, nullptr, nullptr, nullptr, nullptr};
-            for (int k = 0; ok && k < 2; ++k) {
-                float best = 1e30f;
-                for (int r = 0; ok && r < 4; ++r) {
-                    ok = hipMemsetAsync(ctr, 0, 8, s) == hipSuccess && hipEventRecord(e0, s) == hipSuccess;
-                    if (k == 0)
-                        hipLaunchKernelGGL(DEC_L, dim3(grid_for(kDecL, dev, kN[p])), dim3(384), 0, s, A);
-                    else
-                        hipLaunchKernelGGL(DEC_T, dim3(grid_for(kDecT, dev, kN[p])), dim3(kDecTWaves * 64), 0, s, A, ctr);
-                    float ms = 0.f;
-                    ok = ok && hipGetLastError() == hipSuccess && hipEventRecord(e1, s) == hipSuccess &&
-                         hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
-                    if (r > 0) best = std::min(best, ms);  // r == 0 warms up
-                }
-                u[k][p] = best / kN[p];
-            }
-        }
-        if (ok) {
-            float fit[4];
-            for (int k = 0; k < 2; ++k) {
-                const double b = (u[k][1] - u[k][0]) / (double)(kL[1] - kL[0]), a = u[k][0] - b * kL[0];
-                fit[2 * k] = (float)(a * 1e9), fit[2 * k + 1] = (float)(b * 1e9);  // ms -> ps
-            }
-            bool sane = true;
-            for (int k = 0; k < 4; ++k) sane = sane && fit[k] > -50.0f && fit[k] < 5000.0f;
-            sane = sane && fit[1] > 0.0f && fit[3] > 0.0f;
-            if (sane)
-                for (int k = 0; k < 4; ++k) cache[dev][k] = std::max(fit[k], 0.0f);
-        }
-        (void)hipGetLastError();  // a failed probe leaves the defaults and no sticky error
-        if (e0) (void)hipEventDestroy(e0);
-        if (e1) (void)hipEventDestroy(e1);
-        for (void* q : {(void*)in, (void*)out, (void*)st, (void*)off, (void*)olen, (void*)ctr})
-            if (q) (void)hipFree(q);
-        if (s) (void)hipStreamDestroy(s);
-    }
-    for (int k = 0; k < 4; ++k) out[k] = cache[dev][k];
+// Staged / stream prices of each device (select_verdict).  The launch path only reads them: the fitted
+// defaults until hhuff_calibrate_decode_prices measures this device or hhuff_set_decode_prices pins values,
+// so a decode never runs the probe (its allocations, frees and syncs) inside an asynchronous launch.
+// The calibration decodes two probe batches of fixed-length strings with both kernels (zero bytes: '0'
+// symbols to the end, so every string is decoded whole and then fails its padding), 131,072 x 48 B and
+// 65,536 x 120 B (a 64-string tile of those still fits the staged kernel's stage), timed with events on a
+// private stream (best of 3 after a warm-up); per kernel, per-string and per-byte costs solve
+// t / n = a + b L on the two lengths.  A failed or implausible fit keeps the prices in effect.
+constexpr float kDefPrices[4] = {40.0f, 1.07f, 184.0f, 1.15f};
+static std::mutex g_price_mu;
+static float g_prices[64][4];
+static bool g_price_set[64];
+
+static void prices_in_effect(int dev, float out[4]) {
+    std::lock_guard<std::mutex> g(g_price_mu);
+    const bool set = dev >= 0 && dev < 64 && g_price_set[dev];
+    for (int k = 0; k < 4; ++k) out[k] = set ? g_prices[dev][k] : kDefPrices[k];
 }
 
-int decode_prices_of(int device, float out[4]) {
-    const float def[4] = {40.0f, 1.07f, 184.0f, 1.15f};
-    for (int k = 0; k < 4; ++k) out[k] = def[k];
-    int cur = 0;
-    if (hipGetDevice(&cur) != hipSuccess) return -1;
-    if (device != cur && hipSetDevice(device) != hipSuccess) return -1;
-    decode_prices(device, out);
-    if (device != cur) (void)hipSetDevice(cur);
+static void calibrate_prices(int dev) {
+    float fit[4];
+    constexpr uint32_t kN[2] = {131072u, 65536u}, kL[2] = {48u, 120u};
+    const uint64_t bytes = (uint64_t)kN[1] * kL[1];
+    hipStream_t s = nullptr;
+    uint8_t *in = nullptr, *out = nullptr, *st = nullptr;
+    uint32_t *off = nullptr, *olen = nullptr;
+    unsigned long long* ctr = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    bool ok = hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc((void**)&in, bytes + 64) == hipSuccess && hipMalloc((void**)&out, (bytes * 8) / 5 + 64) == hipSuccess &&
+              hipMalloc((void**)&st, kN[0]) == hipSuccess && hipMalloc((void**)&off, 4ull * (kN[0] + 1)) == hipSuccess &&
+              hipMalloc((void**)&olen, 4ull * kN[0]) == hipSuccess && hipMalloc((void**)&ctr, 8) == hipSuccess &&
+              hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess &&
+              hipMemsetAsync(in, 0, bytes + 64, s) == hipSuccess;
+    double u[2][2] = {};  // [kernel][probe]: ms per string
+    for (int p = 0; ok && p < 2; ++p) {
+        std::vector<uint32_t> h(kN[p] + 1);
+        for (uint32_t i = 0; i <= kN[p]; ++i) h[i] = i * kL[p];
+        ok = hipMemcpyAsync(off, h.data(), 4ull * (kN[p] + 1), hipMemcpyHostToDevice, s) == hipSuccess &&
+             hipStreamSynchronize(s) == hipSuccess;
+        DecArgs A{in, (uint64_t)kN[p] * kL[p], off, nullptr, kN[p], nullptr, out, nullptr, olen, st,
+                  nullptr, nullptr, nullptr, nullptr, nullptr};
+        for (int k = 0; ok && k < 2; ++k) {
+            float best = 1e30f;
+            for (int r = 0; ok && r < 4; ++r) {
+                ok = hipMemsetAsync(ctr, 0, 8, s) == hipSuccess && hipEventRecord(e0, s) == hipSuccess;
+                if (k == 0)
+                    hipLaunchKernelGGL(DEC_L, dim3(grid_for(kDecL, dev, kN[p])), dim3(384), 0, s, A);
+                else
+                    hipLaunchKernelGGL(DEC_T, dim3(grid_for(kDecT, dev, kN[p])), dim3(kDecTWaves * 64), 0, s, A, ctr);
+                float ms = 0.f;
+                ok = ok && hipGetLastError() == hipSuccess && hipEventRecord(e1, s) == hipSuccess &&
+                     hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+                if (r > 0) best = std::min(best, ms);  // r == 0 warms up
+            }
+            u[k][p] = best / kN[p];
+        }
+    }
+    bool sane = ok;
+    if (ok) {
+        for (int k = 0; k < 2; ++k) {
+            const double b = (u[k][1] - u[k][0]) / (double)(kL[1] - kL[0]), a = u[k][0] - b * kL[0];
+            fit[2 * k] = (float)(a * 1e9), fit[2 * k + 1] = (float)(b * 1e9);  // ms -> ps
+        }
+        for (int k = 0; k < 4; ++k) sane = sane && fit[k] > -50.0f && fit[k] < 5000.0f;
+        sane = sane && fit[1] > 0.0f && fit[3] > 0.0f;
+    }
+    (void)hipGetLastError();  // a failed probe keeps the prices in effect and leaves no sticky error
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    for (void* q : {(void*)in, (void*)out, (void*)st, (void*)off, (void*)olen, (void*)ctr})
+        if (q) (void)hipFree(q);
+    if (s) (void)hipStreamDestroy(s);
+    if (sane) {
+        std::lock_guard<std::mutex> g(g_price_mu);
+        for (int k = 0; k < 4; ++k) g_prices[dev][k] = std::max(fit[k], 0.0f);
+        g_price_set[dev] = true;
+    }
+}
+
+int decode_prices_of(int device, float out[4], int calibrate) {
+    for (int k = 0; k < 4; ++k) out[k] = kDefPrices[k];
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev || device >= 64) return -1;
+    if (calibrate) {
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess) return -1;
+        if (device != cur && hipSetDevice(device) != hipSuccess) return -1;
+        calibrate_prices(device);
+        if (device != cur) (void)hipSetDevice(cur);
+    }
+    prices_in_effect(device, out);
+    return 0;
+}
+
+int set_decode_prices(int device, const float* in4) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev || device >= 64) return -1;
+    if (in4)
+        for (int k = 0; k < 4; ++k)
+            if (!(in4[k] >= 0.0f && in4[k] < 1e6f)) return -2;
+    std::lock_guard<std::mutex> g(g_price_mu);
+    for (int k = 0; k < 4; ++k) g_prices[device][k] = in4 ? in4[k] : kDefPrices[k];
+    g_price_set[device] = in4 != nullptr;
     return 0;
 }
 
@@ -2839,7 +2870,7 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     const int grid = grid_for(v, current_device(), n);
     const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr;
     if (v == kDecL) {  // mixed lengths: the device picks staged or stream (see below)
-        decode_prices(current_device(), A.price);
+        prices_in_effect(current_device(), A.price);  // no GPU work: see calibrate_prices
         uint64_t* sel = nullptr;  // [0, 3 kSelBlocks): partial sums; then the verdict and the work counter
         hipError_t e = pool_alloc((void**)&sel, (3 * kSelBlocks + 2) * sizeof(uint64_t), stream);
         if (e != hipSuccess) return e;
@@ -3097,12 +3128,12 @@ __device__ __forceinline__ WaveStep wave_step(const uint8_t* in, uint32_t TB, ui
         s.syms = sym;
         s.fl = (le >> 14) & 3u;
     } else {
-        const uint32_t L1 = (e >> 16) & 15u, L12 = (e >> 20) & 15u;
+        const uint32_t L1 = lut_l1(e), L12 = lut_l12(e);
         const bool two = (e & kHas2) && L12 <= s.R;
         const bool stop = L1 > s.R;
         s.nx = stop ? kStop : off + (two ? L12 : L1);
         s.ns = stop ? 0u : (two ? 2u : 1u);
-        s.syms = e & 0xFFFFu;
+        s.syms = lut_pair(e);
         s.fl = (e >> 24) & (two ? 15u : 3u);
     }
     return s;
@@ -3217,13 +3248,13 @@ __device__ __forceinline__ void sys_load16x2(const void* pa, const void* pb, uin
         : "memory");
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // A poll's two 16-B system-scope loads on the lanes of two masks only (exec narrowed inside the asm and
 // restored before the wait), so an idle poll moves only the headers, the control words and the chunks the hot
 // mailbox is expected to need over PCIe -- not 2 KiB per wave per poll.  Lanes outside a mask read zeros (a
 // chunk numbered 0 never matches a request: mailbox request numbers start at 1).  (Pointing those lanes at one
 // device-memory line instead made every poll slower: 16 waves' uncached reads of the same line.)
 __device__ __forceinline__ void sys_poll(const void* pa, uint64_t ma, const void* pb, uint64_t mb, uint4& ra, uint4& rb) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     uint64_t save;
     u32x4 a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
     __asm__ volatile(
@@ -3241,6 +3272,30 @@ __device__ __forceinline__ void sys_poll(const void* pa, uint64_t ma, const void
     ra = make_uint4(a.x, a.y, a.z, a.w);
     rb = make_uint4(b.x, b.y, b.z, b.w);
 }
+
+#ifdef HHUFF_SVC_PIPE
+// sys_poll's loads without the wait: the registers fill later (sys_poll_wait_older)
+__device__ __forceinline__ void sys_poll_issue(const void* pa, uint64_t ma, const void* pb, uint64_t mb, u32x4& a, u32x4& b) {
+    uint64_t save;
+    a = u32x4{0u, 0u, 0u, 0u};
+    b = u32x4{0u, 0u, 0u, 0u};
+    __asm__ volatile(
+        "s_mov_b64 %2, exec\n\t"
+        "s_and_b64 exec, exec, %5\n\t"
+        "global_load_dwordx4 %0, %3, off sc0 sc1\n\t"
+        "s_mov_b64 exec, %2\n\t"
+        "s_and_b64 exec, exec, %6\n\t"
+        "global_load_dwordx4 %1, %4, off sc0 sc1\n\t"
+        "s_mov_b64 exec, %2"
+        : "+&v"(a), "+&v"(b), "=&s"(save)
+        : "v"(pa), "v"(pb), "s"(ma), "s"(mb)
+        : "memory", "scc");
+}
+// the older of two polls in flight is in (each poll is two loads); the newer one's registers stay bound
+__device__ __forceinline__ void sys_poll_wait_older(u32x4& a0, u32x4& b0, u32x4& a1, u32x4& b1) {
+    __asm__ volatile("s_waitcnt vmcnt(2)" : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1) : : "memory");
+}
+#endif
 
 template <int NC, bool JUMP = false>
 __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
@@ -3265,33 +3320,32 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
         if (g == 0) sys_store(&ctrl->alive, 1u);
     }
     uint32_t handled = sys_load(&my->done);  // lane j keeps its mailbox's last served request
+    __builtin_amdgcn_s_waitcnt(kVmWait0);  // (so no compiler wait inside the poll loop covers the polls in flight)
     // hot: the lane whose mailbox was served last; every poll reads its chunks too, as many as its last
     // request needed plus one (hot_ck)
     uint32_t hot = 0, hot_ck = 1, polls = 0;
     const uint64_t mhdr = (2ull << M) - 1ull;  // lanes 0 .. M
-    uint4 hdr = make_uint4(0u, 0u, 0u, 0u), ck = make_uint4(0u, 0u, 0u, 0u);
-    for (;;) {
-        // one round: lane j < M reads its mailbox's header, lane M the control words {stop, alive, quit, G},
-        // lane l < hot_ck chunk l of the hot mailbox; the other lanes read nothing
-        const void* hp = mine ? (const void*)&my->req : (const void*)ctrl;
-        const uint32_t hk = (uint32_t)__builtin_amdgcn_readfirstlane((int)hot_ck);  // wave-uniform
-        sys_poll(hp, mhdr, slots[g + G * hot].chunk[lane], hk >= 64u ? ~0ull : (1ull << hk) - 1ull, hdr, ck);
+    // one round: lane j < M reads its mailbox's header, lane M the control words {stop, alive, quit, G},
+    // lane l < hot_ck chunk l of the hot mailbox; the other lanes read nothing.  step() handles one round's
+    // reads: true when the wave is to exit.
+    auto step = [&](uint4 hdr, uint4 ck) -> bool {
         const uint32_t req = hdr.x;
         const uint32_t ctl_stop = (uint32_t)__shfl((int)hdr.x, (int)M), ctl_quit = (uint32_t)__shfl((int)hdr.z, (int)M);
-        uint64_t pend = __builtin_amdgcn_ballot_w64(mine && req != handled);
+        // newer than the last served (a poll that left before that request was served may still show it)
+        uint64_t pend = __builtin_amdgcn_ballot_w64(mine && (int32_t)(req - handled) > 0);
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         if (pend == 0) {
-            if (ctl_quit != 0 || ctl_stop != 0) break;
+            if (ctl_quit != 0 || ctl_stop != 0) return true;
             if (g == 0 && (++polls & 15u) == 0u) {
                 // wave 0: the grid's idle time is the youngest of the waves' last requests
                 const uint32_t l = lane < G ? sys_load(&ctrl->last[lane]) : (uint32_t)t0;
                 const uint32_t idle = wave_min_u32((uint32_t)now - l);
                 if (idle > (uint32_t)idle_ticks || now - t0 > max_ticks) {
                     if (lane == 0) sys_store(&ctrl->quit, 1u);
-                    break;
+                    return true;
                 }
             }
-            continue;  // each poll is a PCIe round trip already: no sleep between them
+            return false;  // each poll is a PCIe round trip already: no sleep between them
         }
         int ck_slot = (int)hot;  // the lane whose mailbox's chunks `ck` holds
         while (pend) {
@@ -3357,7 +3411,35 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
             hot_ck = min(len / 12u + 2u, 64u);
             wave_lds_sync();
         }
+            return false;
+    };
+    const void* hp = mine ? (const void*)&my->req : (const void*)ctrl;
+    auto ck_mask = [&]() {
+        const uint32_t hk = (uint32_t)__builtin_amdgcn_readfirstlane((int)hot_ck);  // wave-uniform
+        return hk >= 64u ? ~0ull : (1ull << hk) - 1ull;
+    };
+#ifdef HHUFF_SVC_PIPE
+    // A/B: two polls in flight, a new one issued before the older one is waited for, so a request is seen
+    // about half a PCIe round trip sooner.  The loop is unrolled by two so that no register of a poll in
+    // flight is ever copied (a VGPR read does not wait for its load).
+    u32x4 pa0, pb0, pa1, pb1;
+    sys_poll_issue(hp, mhdr, slots[g + G * hot].chunk[lane], ck_mask(), pa0, pb0);
+    for (;;) {
+        sys_poll_issue(hp, mhdr, slots[g + G * hot].chunk[lane], ck_mask(), pa1, pb1);
+        sys_poll_wait_older(pa0, pb0, pa1, pb1);
+        if (step(make_uint4(pa0.x, pa0.y, pa0.z, pa0.w), make_uint4(pb0.x, pb0.y, pb0.z, pb0.w))) break;
+        sys_poll_issue(hp, mhdr, slots[g + G * hot].chunk[lane], ck_mask(), pa0, pb0);
+        sys_poll_wait_older(pa1, pb1, pa0, pb0);
+        if (step(make_uint4(pa1.x, pa1.y, pa1.z, pa1.w), make_uint4(pb1.x, pb1.y, pb1.z, pb1.w))) break;
     }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no poll in flight at the exit
+#else
+    for (;;) {
+        uint4 hdr, ck;
+        sys_poll(hp, mhdr, slots[g + G * hot].chunk[lane], ck_mask(), hdr, ck);
+        if (step(hdr, ck)) break;
+    }
+#endif
     if (lane == 0) sys_store(&ctrl->gone[g], 1u);
     if (g == 0) {  // the grid is over for the host once every wave has left (bounded: 1 s)
         const uint64_t tq = __builtin_amdgcn_s_memrealtime();

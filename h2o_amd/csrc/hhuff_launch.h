@@ -122,7 +122,10 @@ hipError_t launch_qpack(const uint8_t* in, uint64_t in_size, const uint32_t* enc
                         uint8_t* scratch, uint32_t flags, hipStream_t stream, const uint64_t* stream_id = nullptr,
                         hhuff_qpack_request_t* qreq = nullptr, hhuff_qpack_response_head_t* qres = nullptr);
 int grid_size(int device, int which);
-// the staged / stream prices (ps per string, per byte) a mixed-length decode on `device` uses (measured at
-// first use, hhuff_kernels.hip decode_prices); 0, or -1 when the device cannot be selected
-int decode_prices_of(int device, float out[4]);
+// the staged / stream prices (ps per string, per byte) a mixed-length decode on `device` uses: the fitted
+// defaults, pinned values, or (calibrate != 0: measured now, synchronously) this device's own
+// (hhuff_kernels.hip calibrate_prices); 0, or -1 when the device cannot be selected
+int decode_prices_of(int device, float out[4], int calibrate);
+// pin the prices of `device` (in4 NULL: back to the fitted defaults); 0, -1 bad device, -2 bad value
+int set_decode_prices(int device, const float* in4);
 }  // namespace hhuff

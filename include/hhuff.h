@@ -527,9 +527,17 @@ const char *hhuff_last_error_string(void);
 /* Number of workgroups the decode / encode launches use on `device` (grid sizing, for profiling). */
 /* The prices a mixed-length decode (mean Huffman length 41..128 B) uses to choose between the staged and the
  * stream kernel: out4 = {staged ps per string, staged ps per tile-padded byte, stream ps per string, stream ps
- * per byte}, measured on `device` at its first mixed-length decode (both kernels timed on two probe batches;
- * this call runs the measurement if none has run yet, about 2 ms).  HHUFF_OK or an error code. */
+ * per byte}.  A decode never measures them itself: they are fitted MI355X defaults until
+ * hhuff_calibrate_decode_prices or hhuff_set_decode_prices runs for the device.  No GPU work.  HHUFF_OK or an
+ * error code. */
 int hhuff_decode_prices(int device, float *out4);
+/* Measure this device's prices now (both kernels timed on two probe batches, about 2 ms; synchronous: it
+ * allocates and frees device memory, so call it at start-up, not beside in-flight work) and use them from
+ * then on; out4 (may be NULL) receives them.  A failed or implausible fit keeps the prices in effect. */
+int hhuff_calibrate_decode_prices(int device, float *out4);
+/* Pin the prices of `device` (e.g. a previous calibration's, so every process chooses alike); in4 NULL
+ * restores the fitted defaults.  HHUFF_EINVAL for a negative or non-finite value. */
+int hhuff_set_decode_prices(int device, const float *in4);
 int hhuff_grid_size(int device, int which /* 0 decode, 1 encode */);
 /* Return the memory the library's stream-ordered pool on the caller's current device keeps between calls
  * (batch workspaces, edge records) to the driver.  Synchronises the device first.  HHUFF_OK or an error. */

@@ -363,8 +363,9 @@ def test_mixed_length_decode_select(torch_cuda, oracle_codec, lengths, verdict):
     assert 40 < hdata.size // m <= 128
     from h2o_amd import codec
 
-    prices = codec.decode_prices(0)  # measured on this device (first use), not the fitted constants
-    assert prices[1] > 0 and prices[3] > 0, prices
+    prices = (40.0, 1.07, 184.0, 1.15)  # pinned (the fitted MI355X defaults): the verdict is fixed
+    codec.set_decode_prices(prices, 0)
+    assert codec.decode_prices(0) == pytest.approx(prices)
     assert _select_verdict(np.diff(hoff), prices) == verdict, prices
     names = synth.bits_from_bools(rng.random(m) < 0.3)
     g = gpu_decode(torch_cuda, hdata, hoff, m, is_name_bits=names)
@@ -384,6 +385,24 @@ def test_mixed_length_decode_select(torch_cuda, oracle_codec, lengths, verdict):
     np.testing.assert_array_equal(g[2], o[2])
     sl = (starts.astype(np.uint64) * 8) // 5
     assert compact(g[0], out_off, g[1]) == compact(o[0], sl, o[1])
+
+
+def test_decode_price_calibration(torch_cuda):
+    """the launch path never measures prices: defaults until hhuff_calibrate_decode_prices, which installs
+    this device's fit; hhuff_set_decode_prices pins values and NULL restores the defaults"""
+    from h2o_amd import codec
+
+    defaults = [40.0, 1.07, 184.0, 1.15]
+    codec.set_decode_prices(None, 0)
+    assert codec.decode_prices(0) == pytest.approx(defaults)
+    fit = codec.calibrate_decode_prices(0)
+    assert fit[1] > 0 and fit[3] > 0 and all(0 <= x < 5000 for x in fit), fit
+    assert codec.decode_prices(0) == pytest.approx(fit)
+    with pytest.raises(codec.HhuffError):
+        codec.set_decode_prices([1.0, -1.0, 1.0, 1.0], 0)
+    assert codec.decode_prices(0) == pytest.approx(fit)  # a rejected value changes nothing
+    codec.set_decode_prices(None, 0)
+    assert codec.decode_prices(0) == pytest.approx(defaults)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -50,20 +50,20 @@ def test_window_lut_matches_tree():
         e = lut[w]
         syms = _tree_decode(format(w, "0%db" % G.LUT_BITS), root)
         if not syms:
-            assert e >> 31 and (e >> 16) & 15 == G.LUT_BITS + 1 and (e >> 20) & 15 == G.LUT_BITS + 1
+            assert e >> 31 and (e >> 8) & 15 == G.LUT_BITS + 1 and (e >> 12) & 15 == 0
             assert (e >> 28) & 3 == 0
             continue
         assert not e >> 31
         assert (e >> 28) & 3 == min(len(syms), 2)
         s1, l1 = syms[0]
-        assert e & 0xFF == s1 and (e >> 16) & 15 == l1
+        assert e & 0xFF == s1 and (e >> 8) & 15 == l1
         assert (e >> 24) & 1 == (s1 not in G.NAME_VALID) and (e >> 25) & 1 == (s1 not in G.VALUE_VALID)
         if len(syms) > 1:
             s2, l2 = syms[1]
-            assert (e >> 30) & 1 and (e >> 8) & 0xFF == s2 and (e >> 20) & 15 == l1 + l2
+            assert (e >> 30) & 1 and (e >> 16) & 0xFF == s2 and (e >> 12) & 15 == l1 + l2
             assert (e >> 26) & 1 == (s2 not in G.NAME_VALID) and (e >> 27) & 1 == (s2 not in G.VALUE_VALID)
         else:
-            assert not (e >> 30) & 1 and (e >> 20) & 15 == l1 and not (e >> 26) & 3
+            assert not (e >> 30) & 1 and (e >> 12) & 15 == l1 and not (e >> 26) & 3
 
 
 def test_long_code_tables_decode_every_symbol():

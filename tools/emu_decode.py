@@ -83,17 +83,17 @@ def decode_v7(T, data, start, length, fill=0):
         if not e >> 31:
             out.append(e & 0xFF)
             if (e >> 30) & 1:
-                out.append((e >> 8) & 0xFF)
+                out.append((e >> 16) & 0xFF)
             flags |= e
-            cons = (e >> 20) & 15
+            cons = (e >> 12) & 15
             wb = (w << cons) & M32
             eb = lut[wb >> 19]
             if not eb >> 31:
                 out.append(eb & 0xFF)
                 if (eb >> 30) & 1:
-                    out.append((eb >> 8) & 0xFF)
+                    out.append((eb >> 16) & 0xFF)
                 flags |= eb
-                cons += (eb >> 20) & 15
+                cons += (eb >> 12) & 15
         elif longchk:
             le = long_entry(T, w)
             L = (le >> 9) & 31
@@ -118,7 +118,7 @@ def decode_v7(T, data, start, length, fill=0):
         q = pm >> 5
         w = alignbit(ln.word(q), ln.word(q + 1), ~pm)
         e = lut[w >> 19]
-        L1, L12 = (e >> 16) & 15, (e >> 20) & 15
+        L1, L12 = (e >> 8) & 15, (e >> 12) & 15
         m1 = (not e >> 31) and L1 + c < 0
         m2 = bool((e >> 30) & 1) and L12 + c < 0
         cons = L12 if m2 else (L1 if m1 else 0)
@@ -126,19 +126,19 @@ def decode_v7(T, data, start, length, fill=0):
             out.append(e & 0xFF)
             flags |= e & (3 << 24)
         if m2:
-            out.append((e >> 8) & 0xFF)
+            out.append((e >> 16) & 0xFF)
             flags |= e & (3 << 26)
         wb = (w << cons) & M32
         eb = lut[wb >> 19]
         cb = c + cons
-        L1b, L12b = (eb >> 16) & 15, (eb >> 20) & 15
+        L1b, L12b = (eb >> 8) & 15, (eb >> 12) & 15
         m1b = (not eb >> 31) and L1b + cb < 0
         m2b = bool((eb >> 30) & 1) and L12b + cb < 0
         if m1b:
             out.append(eb & 0xFF)
             flags |= eb & (3 << 24)
         if m2b:
-            out.append((eb >> 8) & 0xFF)
+            out.append((eb >> 16) & 0xFF)
             flags |= eb & (3 << 26)
         cons += L12b if m2b else (L1b if m1b else 0)
         lact = (e >> 31) and L1 + c < 0

@@ -237,23 +237,26 @@ def decode_prefix(root, bits, nbits):
 def window_lut(root):
     """GPU decode LUT indexed by the next LUT_BITS (13) bits of the stream.
 
-    u32 entry: [7:0] sym1 | [15:8] sym2 | [19:16] L1 | [23:20] L12 = L1 + L2 (= L1 without a second
-               symbol) | [24] sym1 name-invalid | [25] sym1 value-invalid | [26] sym2 name-invalid |
+    u32 entry: [7:0] sym1 | [11:8] L1 | [15:12] L12 = L1 + L2 (= L1 without a second symbol) |
+               [23:16] sym2 | [24] sym1 name-invalid | [25] sym1 value-invalid | [26] sym2 name-invalid |
                [27] sym2 value-invalid | [29:28] symbols in the entry (0 LONG, 1, 2) | [30] HAS2 |
                [31] LONG (first code longer than the window).
-    LONG entries carry L1 = L12 = LUT_BITS + 1, the shortest code they can stand for, so "L1 fits in
-    the bits left" tells the kernel whether a long code can still fit.  HAS2 and LONG sit in the top
-    bits so that a sign-bit AND with (L + c) yields the take/skip masks directly.
+    sym2 sits in bits 16..23 so the kernels store it with a byte store of the entry's high half
+    (ds_write_b8_d16_hi), no shift.  LONG entries carry L1 = LUT_BITS + 1, the shortest code they can
+    stand for, so "L1 fits in the bits left" tells the kernel whether a long code can still fit, and
+    L12 = 0, so the unchecked bulk step consumes nothing for them without masking (the long-code path
+    takes over).  HAS2 and LONG sit in the top bits so that a sign-bit AND with (L + c) yields the
+    take/skip masks directly.
     EOS (30 bits) never fits a window, so LONG covers it."""
     lut = []
     W = LUT_BITS
     for w in range(1 << W):
         r1 = decode_prefix(root, w, W)
         if r1 is None:
-            lut.append(1 << 31 | (W + 1) << 16 | (W + 1) << 20)
+            lut.append(1 << 31 | (W + 1) << 8)
             continue
         s1, l1 = r1
-        e = s1 | l1 << 16 | l1 << 20 | 1 << 28
+        e = s1 | l1 << 8 | l1 << 12 | 1 << 28
         if s1 not in NAME_VALID:
             e |= 1 << 24
         if s1 not in VALUE_VALID:
@@ -263,7 +266,7 @@ def window_lut(root):
             r2 = decode_prefix(root, w & ((1 << rest) - 1), rest)
             if r2 is not None:
                 s2, l2 = r2
-                e = (e & ~(0xF << 20) & ~(3 << 28)) | s2 << 8 | (l1 + l2) << 20 | 2 << 28 | 1 << 30
+                e = (e & ~(0xF << 12) & ~(3 << 28)) | s2 << 16 | (l1 + l2) << 12 | 2 << 28 | 1 << 30
                 if s2 not in NAME_VALID:
                     e |= 1 << 26
                 if s2 not in VALUE_VALID:
