@@ -2550,9 +2550,11 @@ __global__ void literal_fix_kernel(LitArgs A) {
 #define HHUFF_ENCO_CH 16384
 #endif
 #ifndef HHUFF_DECT  // stream decode: waves per block, window dwords, output bytes per lane
-#define HHUFF_DECT_W 8
-#define HHUFF_DECT_NW 16
-#define HHUFF_DECT_OUT 112
+// (6 waves of 24-dword windows: c3 -2.2 %, c5 -1.3 % against 8 x 16; 6 x 16 and 4 x 32 lose on c5 or c3,
+// 12 and 16 waves lose on both: profiles/r04k_stream_shapes.log, profiles/r04_ab_runs.log t12 / t16b)
+#define HHUFF_DECT_W 6
+#define HHUFF_DECT_NW 24
+#define HHUFF_DECT_OUT 160
 #endif
 constexpr int kDecSWaves = 16, kDecTWaves = HHUFF_DECT_W, kEncSWaves = 16, kEncOStr = HHUFF_ENCO_NS;
 #define DEC_S decode_staged_kernel<kDecSWaves, 3072, 4608, false>
@@ -3273,30 +3275,6 @@ __device__ __forceinline__ void sys_poll(const void* pa, uint64_t ma, const void
     rb = make_uint4(b.x, b.y, b.z, b.w);
 }
 
-#ifdef HHUFF_SVC_PIPE
-// sys_poll's loads without the wait: the registers fill later (sys_poll_wait_older)
-__device__ __forceinline__ void sys_poll_issue(const void* pa, uint64_t ma, const void* pb, uint64_t mb, u32x4& a, u32x4& b) {
-    uint64_t save;
-    a = u32x4{0u, 0u, 0u, 0u};
-    b = u32x4{0u, 0u, 0u, 0u};
-    __asm__ volatile(
-        "s_mov_b64 %2, exec\n\t"
-        "s_and_b64 exec, exec, %5\n\t"
-        "global_load_dwordx4 %0, %3, off sc0 sc1\n\t"
-        "s_mov_b64 exec, %2\n\t"
-        "s_and_b64 exec, exec, %6\n\t"
-        "global_load_dwordx4 %1, %4, off sc0 sc1\n\t"
-        "s_mov_b64 exec, %2"
-        : "+&v"(a), "+&v"(b), "=&s"(save)
-        : "v"(pa), "v"(pb), "s"(ma), "s"(mb)
-        : "memory", "scc");
-}
-// the older of two polls in flight is in (each poll is two loads); the newer one's registers stay bound
-__device__ __forceinline__ void sys_poll_wait_older(u32x4& a0, u32x4& b0, u32x4& a1, u32x4& b1) {
-    __asm__ volatile("s_waitcnt vmcnt(2)" : "+v"(a0), "+v"(b0), "+v"(a1), "+v"(b1) : : "memory");
-}
-#endif
-
 template <int NC, bool JUMP = false>
 __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
                                                      uint64_t idle_ticks, uint64_t max_ticks) {
@@ -3320,7 +3298,6 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
         if (g == 0) sys_store(&ctrl->alive, 1u);
     }
     uint32_t handled = sys_load(&my->done);  // lane j keeps its mailbox's last served request
-    __builtin_amdgcn_s_waitcnt(kVmWait0);  // (so no compiler wait inside the poll loop covers the polls in flight)
     // hot: the lane whose mailbox was served last; every poll reads its chunks too, as many as its last
     // request needed plus one (hot_ck)
     uint32_t hot = 0, hot_ck = 1, polls = 0;
@@ -3418,28 +3395,11 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
         const uint32_t hk = (uint32_t)__builtin_amdgcn_readfirstlane((int)hot_ck);  // wave-uniform
         return hk >= 64u ? ~0ull : (1ull << hk) - 1ull;
     };
-#ifdef HHUFF_SVC_PIPE
-    // A/B: two polls in flight, a new one issued before the older one is waited for, so a request is seen
-    // about half a PCIe round trip sooner.  The loop is unrolled by two so that no register of a poll in
-    // flight is ever copied (a VGPR read does not wait for its load).
-    u32x4 pa0, pb0, pa1, pb1;
-    sys_poll_issue(hp, mhdr, slots[g + G * hot].chunk[lane], ck_mask(), pa0, pb0);
-    for (;;) {
-        sys_poll_issue(hp, mhdr, slots[g + G * hot].chunk[lane], ck_mask(), pa1, pb1);
-        sys_poll_wait_older(pa0, pb0, pa1, pb1);
-        if (step(make_uint4(pa0.x, pa0.y, pa0.z, pa0.w), make_uint4(pb0.x, pb0.y, pb0.z, pb0.w))) break;
-        sys_poll_issue(hp, mhdr, slots[g + G * hot].chunk[lane], ck_mask(), pa0, pb0);
-        sys_poll_wait_older(pa1, pb1, pa0, pb0);
-        if (step(make_uint4(pa1.x, pa1.y, pa1.z, pa1.w), make_uint4(pb1.x, pb1.y, pb1.z, pb1.w))) break;
-    }
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no poll in flight at the exit
-#else
     for (;;) {
         uint4 hdr, ck;
         sys_poll(hp, mhdr, slots[g + G * hot].chunk[lane], ck_mask(), hdr, ck);
         if (step(hdr, ck)) break;
     }
-#endif
     if (lane == 0) sys_store(&ctrl->gone[g], 1u);
     if (g == 0) {  // the grid is over for the host once every wave has left (bounded: 1 s)
         const uint64_t tq = __builtin_amdgcn_s_memrealtime();
