@@ -1692,6 +1692,7 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
     SortChunk cur = sort_chunk_issue(A, c * kSortStr, t, NS);
     issue_span(pv, cur);
     prepare(cur, c * kSortStr, 0u);
+    PROF_DECL  // profile builds: barrier 1 / ranks + barrier 2 / encode / barrier 3 + lengths / copy out / prepare
     for (;;) {
         const uint64_t cb = c * kSortStr, i = cb + t;
         const bool valid = i < A.n;
@@ -1702,6 +1703,7 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         const bool more = cn < nch;
         SortChunk nxt = sort_chunk_issue(A, (more ? cn : c) * kSortStr, t, NS);  // in flight during this chunk
         __syncthreads();  // the chunk's stage, strings and ranks are in
+        PROF_MARK(0);
         if (span > (uint32_t)CH) {  // (workgroup-uniform) a chunk larger than the stage: one thread per string
             uint32_t ol = kFailLen;
             if (valid && len <= kMaxStrLen) {
@@ -1725,6 +1727,7 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
             s_perm[eb + ((bin & 1u) ? xb : 0u) + rank] = (uint16_t)t;
         }
         __syncthreads();
+        PROF_MARK(1);
         if (t < kSortBins) s_bin[t] = 0u;  // read by every wave above: cleared for the next chunk
         if (more) issue_span(pv, nxt);     // the next chunk's span: in flight during the encode
         // sorted position t = 64 wave + lane: wave w encodes the w-th length group
@@ -1737,8 +1740,10 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         // the encoded length goes back to the string's own record (read by this thread only), so the lengths
         // and statuses are stored in string order, coalesced
         s_str[j].x = act && tb != kFailLen ? (tb + 7) >> 3 : kFailLen;
+        PROF_MARK(2);
         __syncthreads();
         if (valid) finish_encode(A, (uint32_t)i, len, s_str[t].x);
+        PROF_MARK(3);
         // the stage's MSB-first words, byte-swapped on the way out (each read chunk is zeroed for the next
         // chunk); the chunk's first and last 16-B chunks are deferred (edge_fix_kernel)
         const uint32_t kl = (span - 1u) & ~15u;
@@ -1760,10 +1765,15 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         }
         if (t == 0 && (kl == 0 || span == 0)) rec[1].m = make_uint4(0u, 0u, 0u, 0u);  // one chunk, or none
         if (t == 0 && span == 0) rec[0].m = make_uint4(0u, 0u, 0u, 0u);
-        if (!more) break;
+        PROF_MARK(4);
+        if (!more) {
+            PROF_FLUSH(1);
+            break;
+        }
         // the stages are free (the input since the encode, the output but for this thread's chunks above):
         // the next chunk goes in before this chunk's stores have landed
         prepare(nxt, cn * kSortStr, span);
+        PROF_MARK(5);
         cur = nxt;
         c = cn;
     }

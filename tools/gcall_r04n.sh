@@ -1,0 +1,6 @@
+#!/bin/bash
+# round 4: sorted-encoder chunk sizes (A/B)
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T=${T:-r04n}
+timeout -k 10 600 bash tools/gcall_ab.sh ${T}_enco c4,c2 base4 e192 e320 || exit 7
