@@ -504,7 +504,13 @@ int svc_call(int dev, bool encode, const uint8_t* src, size_t len, int is_name, 
     if (__atomic_load_n(&S.ctrl->alive, __ATOMIC_ACQUIRE) == 0u && svc_kick(S, dev) != HHUFF_OK) return -1;
     uint64_t spins = 0;
     const auto t0 = std::chrono::steady_clock::now();
-    while (__atomic_load_n(&sl->done, __ATOMIC_ACQUIRE) != n) {
+    // {done, result, status} arrive as one 16-B store: one 16-B load sees them together
+    auto load16 = [](const void* q, uint32_t (&w)[4]) {
+        __asm__ volatile("" ::: "memory");  // re-read the device-written line on every try
+        _mm_storeu_si128(reinterpret_cast<__m128i*>(w), _mm_load_si128(reinterpret_cast<const __m128i*>(q)));
+    };
+    uint32_t res4[4];
+    for (load16(&sl->done, res4); res4[0] != n; load16(&sl->done, res4)) {
         ++spins;
         if ((spins & 63u) == 0u) {
             if (__atomic_load_n(&S.ctrl->alive, __ATOMIC_ACQUIRE) == 0u && svc_kick(S, dev) != HHUFF_OK) return -1;
@@ -519,10 +525,16 @@ int svc_call(int dev, bool encode, const uint8_t* src, size_t len, int is_name, 
         }
         __builtin_ia32_pause();
     }
-    const uint32_t r = sl->result;
+    const uint32_t r = res4[1];
     *res = r;
-    *status = sl->status;
-    if (r != HHUFF_FAIL_LEN) memcpy(dst, sl->out, r);
+    *status = res4[2];
+    if (r != HHUFF_FAIL_LEN) {
+        for (uint32_t i = 0; 12u * i < r; ++i) {  // each chunk once it carries this request's number
+            uint32_t c4[4];
+            for (load16(sl->outc[i], c4); c4[0] != n; load16(sl->outc[i], c4)) __builtin_ia32_pause();
+            memcpy(dst + 12u * i, &c4[1], r - 12u * i < 12u ? r - 12u * i : 12u);
+        }
+    }
     return 1;
 }
 

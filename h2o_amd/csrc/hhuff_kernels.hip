@@ -721,12 +721,14 @@ __device__ __forceinline__ void store_range16(uint8_t* __restrict__ g, const uin
     }
 }
 
-template <int WAVES, int NW, int OUT>
+// SEG: flush granularity -- whole SEG-byte aligned output segments leave before a string's end
+template <int WAVES, int NW, int OUT, int SEG = 16>
 __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, unsigned long long* __restrict__ counter) {
     static_assert(NW >= 8 && NW % 4 == 0 && OUT % 16 == 0, "window shape");
     // per round a lane consumes <= 32 (NW - 2) bits: <= 32 (NW - 2) / 5 symbols after <= 15 carried bytes,
     // plus the byte the second-symbol store may touch; the last byte of the buffer is the trash byte
-    static_assert(15 + (32 * (NW - 2)) / 5 + 2 < OUT, "output buffer too small for a window");
+    static_assert(SEG >= 16 && (SEG & (SEG - 1)) == 0 && SEG - 1 + (32 * (NW - 2)) / 5 + 2 < OUT,
+                  "output buffer too small for a window");
     constexpr uint32_t kWS = NW + 1;  // odd dword stride: lanes at the same q hit distinct banks
     struct __attribute__((aligned(16))) Smem {
         uint32_t lut[1u << HHUFF_LUT_BITS];
@@ -791,7 +793,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                     A.status[i] = kStatusTooLong;
                 } else {
                     busy = true;
-                    head = (dst & 15u) != 0;
+                    head = (dst & (SEG - 1u)) != 0;
                     P = ocnt = flags = first = lastb = fail = 0;
                 }
             }
@@ -837,7 +839,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
         PROF_MARK(1);
         const int32_t end = busy ? (int32_t)min((uint64_t)(pm + 1) + rem, (uint64_t)0x40000000u) : 0;
         const bool fin = busy && end <= kFinal;
-        const uint32_t h0 = (uint32_t)((dst + ocnt) & 15u);  // buffer offset of this round's first byte
+        const uint32_t h0 = (uint32_t)((dst + ocnt) & (SEG - 1u));  // buffer offset of this round's first byte
         uint32_t o = ob + h0;
         int32_t q = pm >> 5;
         uint32_t x0 = st[q], x1 = st[q + 1], x2 = st[q + 2];
@@ -978,22 +980,27 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                 const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
                 return R <= 7 && (w | (0xFFFFFFFFu >> (R & 31u))) == 0xFFFFFFFFu;
             }();
-            uint8_t* gchunk = A.out + ((dst + ocnt) & ~15ull);
-            const uint32_t hs = (uint32_t)(dst & 15u);  // head chunk: the string's bytes start here
+            uint8_t* gchunk = A.out + ((dst + ocnt) & ~(uint64_t)(SEG - 1));
+            const uint32_t hs = head ? (uint32_t)(dst & (SEG - 1u)) : 0u;  // head segment: the string starts here
             if (!done || ok) {  // a failed string's output is unspecified: skip its last stores
-                const uint32_t nfull = nb >> 4;
+                // whole 16-B chunks now: all of them at the string's end, else those of whole segments
+                const uint32_t nfull = done ? nb >> 4 : (nb / SEG) * (SEG / 16u);
                 for (uint32_t k = 0; k < nfull; ++k) {
-                    if (head && k == 0)
-                        store_range16(gchunk, obuf, hs, 16u);
+                    const uint32_t c0 = 16u * k;
+                    if (c0 + 16u <= hs) continue;  // foreign bytes before the string
+                    if (c0 < hs)
+                        store_range16(gchunk + c0, obuf + c0, hs - c0, 16u);
                     else
-                        *reinterpret_cast<uint4*>(gchunk + 16u * k) = *reinterpret_cast<const uint4*>(obuf + 16u * k);
+                        *reinterpret_cast<uint4*>(gchunk + c0) = *reinterpret_cast<const uint4*>(obuf + c0);
                 }
-                head = head && nfull == 0;
-                const uint32_t part = nb & 15u;
+                const uint32_t c0 = 16u * nfull;
                 if (done) {
-                    if (part > (head ? hs : 0u)) store_range16(gchunk + 16u * nfull, obuf + 16u * nfull, head ? hs : 0u, part);
-                } else if (nfull) {
-                    *reinterpret_cast<uint4*>(obuf) = *reinterpret_cast<const uint4*>(obuf + 16u * nfull);
+                    const uint32_t lo = hs > c0 ? hs - c0 : 0u;
+                    if (nb - c0 > lo) store_range16(gchunk + c0, obuf + c0, lo, nb - c0);
+                } else if (nfull) {  // carry the partial segment to the buffer's start
+                    head = false;
+                    for (uint32_t r = 0; c0 + 16u * r < nb; ++r)
+                        *reinterpret_cast<uint4*>(obuf + 16u * r) = *reinterpret_cast<const uint4*>(obuf + c0 + 16u * r);
                 }
             }
             ocnt += made;
@@ -2575,7 +2582,10 @@ constexpr int kDecSWaves = 16, kDecTWaves = HHUFF_DECT_W, kEncSWaves = 16, kEncO
 #ifdef HHUFF_STREAM2  // A/B: the stream kernel with prefetched next strings, window in place (HHUFF_DECT_OUT: dwords)
 #define DEC_T decode_stream2_kernel<kDecTWaves, HHUFF_DECT_NW, HHUFF_DECT_OUT>
 #else
-#define DEC_T decode_stream_kernel<kDecTWaves, HHUFF_DECT_NW, HHUFF_DECT_OUT>
+#ifndef HHUFF_DECT_SEG
+#define HHUFF_DECT_SEG 16
+#endif
+#define DEC_T decode_stream_kernel<kDecTWaves, HHUFF_DECT_NW, HHUFF_DECT_OUT, HHUFF_DECT_SEG>
 #endif
 #define ENC_S encode_staged_kernel<kEncSWaves, 3584, false>
 #define ENC_O encode_sorted_kernel<kEncOStr, HHUFF_ENCO_CH>
@@ -3249,6 +3259,13 @@ __device__ __forceinline__ void sys_store(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// one 16-B system-scope store (seen whole by the host: old or new, see SvcSlot)
+__device__ __forceinline__ void sys_store16(void* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+    const v4 v = {a, b, c, d};
+    __asm__ volatile("global_store_dwordx4 %0, %1, off sc0 sc1" : : "v"(p), "v"(v) : "memory");
+}
+
 // two 16-B system-scope loads (each is seen whole: old or new, see SvcSlot), waited for here
 __device__ __forceinline__ void sys_load16x2(const void* pa, const void* pb, uint4& a, uint4& b) {
     __asm__ volatile(
@@ -3375,24 +3392,19 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
             }
             const uint32_t t_coded = (uint32_t)__builtin_amdgcn_s_memrealtime();
             const uint32_t n = ol == kFailLen ? 0u : ol;
-            uint32_t* dst = reinterpret_cast<uint32_t*>(sl->out);
-            for (uint32_t k = lane; 4u * k < n; k += 64u) {  // encode's stage holds MSB-first words
-                const uint32_t wv = reinterpret_cast<const uint32_t*>(s_out)[k];
-                sys_store(dst + k, op == 1u ? bswap32(wv) : wv);
+            // the output as tagged 16-B chunks and then the result chunk, no wait between them (SvcSlot)
+            for (uint32_t k = lane; 12u * k < n; k += 64u) {  // encode's stage holds MSB-first words
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(s_out) + 3u * k;
+                const uint32_t a = w[0], b = w[1], c = w[2];
+                sys_store16(sl->outc[k], r, op == 1u ? bswap32(a) : a, op == 1u ? bswap32(b) : b,
+                            op == 1u ? bswap32(c) : c);
             }
             if (lane == 0) {
-                sys_store(&sl->result, ol);
-                sys_store(&sl->status, st);
-                sys_store(&sl->t_seen, t_seen);
-                sys_store(&sl->t_data, t_data);
-                sys_store(&sl->t_coded, t_coded);
-                sys_store(&sl->t_out, (uint32_t)__builtin_amdgcn_s_memrealtime());
+                sys_store16(&sl->t_seen, t_seen, t_data, t_coded, (uint32_t)__builtin_amdgcn_s_memrealtime());
                 sys_store(&ctrl->last[g], t_seen);
+                sys_store16(&sl->done, r, ol, st, 0u);
             }
-            // the result before its counter: the stores above are system-scope (write-through), so waiting
-            // for their completion orders them before `done` (no L2 write-back needed)
-            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) sys_store(&sl->done, r);
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of this request left in flight
             if (lane == s) handled = r;
             hot = s;
             hot_ck = min(len / 12u + 2u, 64u);

@@ -33,10 +33,13 @@ struct alignas(16) SvcSlot {
     uint32_t t_seen, t_data, t_coded, t_out;  // the wave's real-time stamps (100 MHz, low 32 bits): profiling
     uint32_t pad2[4];
     uint32_t chunk[64][4];                // {req, input bytes [12 i, 12 i + 12)}
-    uint8_t out[1600];                    // >= floor(8 kSvcMax / 5) + 60
+    uint32_t outc[104][4];                // device: {req, output bytes [12 i, 12 i + 12)}, each one 16-B store
 };
-static_assert(sizeof(SvcSlot) % 16 == 0 && sizeof(SvcSlot) == 64 + 1024 + 1600, "mailbox layout");
-static_assert(12 * 64 == kSvcMax && (kSvcMax * 8) / 5 + 60 <= 1600, "mailbox sizes");
+// The device writes the output chunks and then {done, result, status} with single 16-B system-scope stores and
+// no wait between them: the host takes a chunk when it carries the request number, as the device does with
+// the input chunks.
+static_assert(sizeof(SvcSlot) % 16 == 0 && sizeof(SvcSlot) == 64 + 1024 + 1664, "mailbox layout");
+static_assert(12 * 64 == kSvcMax && (kSvcMax * 8) / 5 <= 12 * 104, "mailbox sizes");
 // Several service waves (one per block, launch_service's grid): wave g serves mailboxes g, g + G, g + 2G, ...
 // Wave 0 decides when the grid ends (no request to any wave for idle_ticks, max_ticks in all, or `stop`) and
 // raises `quit`; every wave polls it with its mailboxes, stores gone[g] as it leaves, and wave 0 clears
