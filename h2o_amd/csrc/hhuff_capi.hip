@@ -531,7 +531,15 @@ int svc_call(int dev, bool encode, const uint8_t* src, size_t len, int is_name, 
     if (r != HHUFF_FAIL_LEN) {
         for (uint32_t i = 0; 12u * i < r; ++i) {  // each chunk once it carries this request's number
             uint32_t c4[4];
-            for (load16(sl->outc[i], c4); c4[0] != n; load16(sl->outc[i], c4)) __builtin_ia32_pause();
+            for (uint64_t k = 0;; ++k) {  // stored with the result: here within microseconds
+                load16(sl->outc[i], c4);
+                if (c4[0] == n) break;
+                if ((k & 4095u) == 4095u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+                    snprintf(t_err, sizeof(t_err), "per-string service: output chunk %u never arrived", i);
+                    return -1;
+                }
+                __builtin_ia32_pause();
+            }
             memcpy(dst + 12u * i, &c4[1], r - 12u * i < 12u ? r - 12u * i : 12u);
         }
     }

@@ -12,4 +12,4 @@ for r in 1 2; do
   LD_LIBRARY_PATH=/tmp/ps_tag timeout -k 10 200 ./tools/per_string_bench 1 4 16 > gpurun_out/${T}_ps_tag_$r.jsonl 2>&1 || exit 8
 done
 timeout -k 10 600 bash tools/gcall_ab.sh ${T}_enco c4,c2 base4 e192 e320 || exit 7
-timeout -k 10 600 bash tools/gcall_ab.sh ${T}_seg c3,c5 base5 seg64 || exit 7
+timeout -k 10 600 bash tools/gcall_ab.sh ${T}_seg c3,c5 base5 seg64 seg32 || exit 7
