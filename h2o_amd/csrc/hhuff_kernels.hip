@@ -343,6 +343,11 @@ struct DecArgs {
     const uint64_t* sel;   // decode_select_kernel's partial sums [3][kSelBlocks] (with gate)
     uint32_t* pk_off;      // packed mode (decode_staged_kernel<.., true>): u32[n + 1] output places
     const uint32_t* n_dev;  // NULL, or the string count in device memory (n an upper bound)
+    // strings of kSplitMin bytes or more are listed here for split_decode_kernel instead of decoded by one lane
+    // (NULL: every string decoded where it is met)
+    uint32_t* split_list = nullptr;
+    uint32_t* split_n = nullptr;
+    uint32_t split_cap = 0;
     // with gate: the staged / stream prices select_verdict uses, ps per string and per (tile-padded) byte --
     // the fitted defaults, or the device's calibration (calibrate_prices)
     float price[4] = {40.0f, 1.07f, 184.0f, 1.15f};
@@ -353,6 +358,17 @@ __device__ __forceinline__ void load_dec_tables(uint32_t* s_lut, uint32_t* s_kin
         reinterpret_cast<uint4*>(s_lut)[k] = reinterpret_cast<const uint4*>(g_dec_lut)[k];
     for (uint32_t k = threadIdx.x; k < HHUFF_ONES_NENT; k += nthreads) s_ones[k] = g_ones[k];
     if (threadIdx.x < 31) s_kinfo[threadIdx.x] = g_kinfo[threadIdx.x];
+}
+
+// a string long enough for split_decode_kernel goes to its list (when the launch has one) instead of being
+// decoded by this lane; a full list leaves it here
+constexpr uint32_t kSplitMinBytes = 4096;  // = kSplitMin (split_decode_kernel)
+__device__ __forceinline__ bool split_push(const DecArgs& A, uint32_t i, uint32_t len) {
+    if (A.split_list == nullptr || len < kSplitMinBytes || len > kMaxStrLen) return false;
+    const uint32_t k = atomicAdd(A.split_n, 1u);
+    if (k >= A.split_cap) return false;
+    A.split_list[k] = i;
+    return true;
 }
 
 // direct variant for one lane: global input, register sink straight to `dst`
@@ -509,6 +525,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         uint8_t st = 0;
         uint64_t G = 0;        // packed: the tile's run start in `out`
         uint32_t place = 0, T_run = 0, c0 = 0;
+        bool listed = false;
         PROF_MARK(0);
         if (cur.fits) {
             wave_lds_sync();
@@ -566,8 +583,12 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
             wave_lds_sync();
             PROF_MARK(2);  // verdicts
         } else if (!PACKED && t.valid) {
-            const uint64_t d = A.out_off ? cur.dst_g : dec_slot(t.s);
-            decode_direct(A, t.s, t.len, is_name, A.out + d, T, ol, st);
+            if (split_push(A, ti_i, t.len)) {
+                listed = true;  // split_decode_kernel writes its results
+            } else {
+                const uint64_t d = A.out_off ? cur.dst_g : dec_slot(t.s);
+                decode_direct(A, t.s, t.len, is_name, A.out + d, T, ol, st);
+            }
             PROF_MARK(6);  // direct path
         } else if (PACKED) {
             // a tile larger than the stages: count first (lengths fix the places), then decode into place
@@ -629,7 +650,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
             A.edges[2 * (base >> 6)].m = make_uint4(0u, 0u, 0u, 0u);
             A.edges[2 * (base >> 6) + 1].m = make_uint4(0u, 0u, 0u, 0u);
         }
-        if (t.valid) {
+        if (t.valid && !listed) {
             A.out_len[ti_i] = ol;
             A.status[ti_i] = st;
             if (PACKED) {
@@ -666,11 +687,179 @@ __global__ __launch_bounds__(WAVES * 64) void decode_direct_kernel(DecArgs A) {
         const uint32_t len = A.in_len ? A.in_len[i] : A.in_off[i + 1] - s;
         const bool is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) : false;
         const uint64_t d = A.out_off ? (uint64_t)A.out_off[i] : dec_slot(s);
+        if (split_push(A, (uint32_t)i, len)) continue;
         uint32_t ol;
         uint8_t st;
         decode_direct(A, s, len, is_name, A.out + d, T, ol, st);
         A.out_len[i] = ol;
         A.status[i] = st;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Split decode of long strings (SURVEY §7 hard part 2: h2o takes header values up to H2O_MAX_REQLEN).  A
+// string of kSplitMin bytes or more would keep one lane busy for its whole length; here one wave decodes it.
+// The string's bits are cut into 64 segments of `seg` bits (a dword multiple).  Huffman codes self-
+// synchronise: a lane that starts decoding `kSplitLead` bits before its segment at an arbitrary bit is, with
+// overwhelming probability, on the true symbol boundaries by the time it reaches its segment.
+//   pass A: lane k decodes from max(k seg - kSplitLead, 0) to the first symbol boundary at or after
+//           (k + 1) seg (the last active lane: to the string's end, with the padding rule, hpack.c:132-133),
+//           and counts the symbols that start at or after k seg: f_k = the first of them, e_k = where it stops;
+//   check:  lane k agrees with lane k - 1 iff f_k == e_{k-1}; a lane that does not decodes again from
+//           e_{k-1}, a true boundary (lane 0 starts at bit 0), until no lane changes;
+//   pass B: a wave prefix sum of the counts places each lane's symbols; lane k decodes [f_k, e_k) again and
+//           writes them (register sink, any alignment).
+// Same results as decode_core (hpack.c:117-156): EOS on the true path fails the string (hpack.c:88-89), the
+// soft bits come from all symbols' flags and the first and last byte.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kSplitMin = kSplitMinBytes;  // Huffman bytes: strings this long go to split_decode_kernel
+constexpr uint32_t kSplitLead = 256;  // bits decoded before a segment (synchronisation lag: mean 37, p99 193)
+
+struct SegWalk {
+    uint32_t f, e;        // first counted symbol's start, stop position (bits from the string's start)
+    uint32_t cnt, flags;  // counted symbols, their invalid-char flags (decode_core's encoding)
+    uint32_t first, last; // first / last counted symbol
+    bool eos, end_ok;     // an EOS among the counted symbols; (last segment) the padding rule held
+};
+
+// Decode the string's bits from p0; count (and with EMIT write) the symbols starting in [kstart, pstop);
+// stop at the first boundary >= pstop, or at the string's end when pstop >= TB.
+template <bool EMIT>
+__device__ __forceinline__ SegWalk seg_walk(const GlobalSource& src, uint32_t s, uint32_t TB, uint32_t p0,
+                                            uint32_t kstart, uint32_t pstop, RegSink& sink, const DecTables& T) {
+    SegWalk r{0xFFFFFFFFu, 0u, 0u, 0u, 0u, 0u, false, false};
+    // bit reader at absolute bit 8 s + p0 (MSB-first dwords)
+    const uint64_t abs = 8ull * s + p0;
+    uint32_t a = (uint32_t)((abs >> 5) << 2);
+    const uint32_t skip = (uint32_t)(abs & 31u);
+    uint64_t buf = ((uint64_t)bswap32(src.word(a)) << 32 | bswap32(src.word(a + 4u))) << skip;
+    uint32_t nb = 64u - skip;
+    a += 8u;
+    auto consume = [&](uint32_t n) {
+        buf <<= n;
+        nb -= n;
+        if (nb <= 32u) {
+            buf |= (uint64_t)bswap32(src.word(a)) << (32u - nb);
+            nb += 32u;
+            a += 4u;
+        }
+    };
+    auto take = [&](uint32_t p, uint32_t sym, uint32_t fl) {  // a symbol starting at p
+        if (p < kstart) return;
+        r.f = min(r.f, p);
+        r.first = r.cnt == 0 ? sym : r.first;
+        r.last = sym;
+        r.cnt += 1;
+        r.flags |= fl;
+        if (EMIT) sink.put1(sym);
+    };
+    uint32_t p = p0;
+    for (;;) {
+        if (p >= pstop) break;
+        const uint32_t R = TB - p;
+        const uint32_t w = (uint32_t)(buf >> 32);
+        const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+        if (e & kLong) {
+            const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+            const uint32_t ki = T.kinfo[k];
+            const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+            const uint32_t L = (le >> 9) & 31u;
+            if (L > R) break;  // the string's end: padding
+            const uint32_t sym = le & 0x1FFu;
+            if (sym == kEos && p >= kstart) {  // EOS inside the string (hpack.c:88-89)
+                r.eos = true;
+                break;
+            }
+            if (sym != kEos) take(p, sym, (le >> 14) & 3u);
+            p += L;
+            consume(L);
+        } else {
+            const uint32_t L1 = lut_l1(e);
+            if (L1 > R) break;  // fewer bits left than the next code: padding
+            const uint32_t L12 = lut_l12(e);
+            take(p, e & 0xFFu, (e >> 24) & 3u);
+            // the second symbol only when it starts before the stop and fits the string
+            const bool two = (e & kHas2) && L12 <= R && p + L1 < pstop;
+            if (two) take(p + L1, lut_sym2(e) & 0xFFu, (e >> 26) & 3u);
+            const uint32_t cons = two ? L12 : L1;
+            p += cons;
+            consume(cons);
+        }
+    }
+    r.e = p;
+    if (r.f == 0xFFFFFFFFu) r.f = p;  // no symbol starts in the segment
+    if (pstop >= TB) {  // the string's end: at most 7 bits of padding, all ones (mkhufftbl.py:374-381)
+        const uint32_t R = TB - p;
+        r.end_ok = !r.eos && R <= 7u && (((uint32_t)(buf >> 56)) | (0xFFu >> R)) == 0xFFu;
+    }
+    return r;
+}
+
+template <int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void split_decode_kernel(DecArgs A) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
+    __shared__ uint32_t s_kinfo[32];
+    __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
+    if (blockIdx.x * WAVES >= min(*A.split_n, A.split_cap)) return;  // (block-uniform) nothing listed for it
+    load_dec_tables(s_lut, s_kinfo, s_ones, WAVES * 64);
+    __syncthreads();
+    const DecTables T{s_lut, s_kinfo, s_ones};
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t nl = min(*A.split_n, A.split_cap);
+    const GlobalSource src{A.in, A.in_size};
+    for (uint32_t j = blockIdx.x * WAVES + wave; j < nl; j += gridDim.x * WAVES) {
+        const uint32_t i = A.split_list[j];
+        const uint32_t s = A.in_off[i];
+        const uint32_t len = A.in_len ? A.in_len[i] : A.in_off[i + 1] - s;  // kSplitMin <= len <= kMaxStrLen
+        const bool is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) : false;
+        const uint64_t d = A.out_off ? (uint64_t)A.out_off[i] : dec_slot(s);
+        const uint32_t TB = 8u * len;
+        const uint32_t seg = (uint32_t)(((uint64_t)TB + 64u * 32u - 1u) / (64u * 32u)) * 32u;  // bits, dword multiple
+        const uint32_t ks = lane * seg;
+        const bool act = ks < TB;
+        const bool lastl = act && ks + seg >= TB;
+        const uint32_t pstop = lastl ? TB : ks + seg;
+        RegSink none;
+        none.init(nullptr);
+        SegWalk w{};
+        if (act) w = seg_walk<false>(src, s, TB, ks > kSplitLead ? ks - kSplitLead : 0u, ks, pstop, none, T);
+        // agree with the lane before: lane k starts where lane k - 1 stopped
+        for (int it = 0; it < 64; ++it) {
+            const uint32_t pe = (uint32_t)__shfl_up((int)w.e, 1, 64);
+            const bool bad = act && lane > 0 && w.f != pe;
+            if (__builtin_amdgcn_ballot_w64(bad) == 0) break;
+            if (bad) w = seg_walk<false>(src, s, TB, pe, pe, pstop, none, T);
+        }
+        const uint32_t cnt = act ? w.cnt : 0u;
+        const uint32_t place = wave_excl_scan(cnt, (int)lane);
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(place + cnt), 63);
+        const bool eos = __builtin_amdgcn_ballot_w64(act && w.eos) != 0;
+        const bool end_ok = __builtin_amdgcn_ballot_w64(lastl && w.end_ok) != 0;
+        const bool ok = !eos && end_ok;
+        uint32_t fl = act ? w.flags : 0u;
+        fl |= (uint32_t)__shfl_xor((int)fl, 1, 64);
+        fl |= (uint32_t)__shfl_xor((int)fl, 2, 64);
+        fl |= (uint32_t)__shfl_xor((int)fl, 4, 64);
+        fl |= (uint32_t)__shfl_xor((int)fl, 8, 64);
+        fl |= (uint32_t)__shfl_xor((int)fl, 16, 64);
+        fl |= (uint32_t)__shfl_xor((int)fl, 32, 64);
+        // first byte: the first lane with symbols; last byte: the last one
+        const uint64_t has = __builtin_amdgcn_ballot_w64(cnt != 0);
+        uint32_t first = 0, last = 0;
+        if (has) {
+            first = (uint32_t)__shfl((int)w.first, (int)__builtin_ctzll(has), 64);
+            last = (uint32_t)__shfl((int)w.last, 63 - (int)__builtin_clzll(has), 64);
+        }
+        if (ok && act && cnt) {
+            RegSink sink;
+            sink.init(A.out + d + place);
+            (void)seg_walk<true>(src, s, TB, w.f, w.f, pstop, sink, T);
+            sink.finish();
+        }
+        if (lane == 0) {
+            A.out_len[i] = ok ? total : kFailLen;
+            A.status[i] = ok ? soft_bits(is_name, total, fl & 3u, first, last) : kStatusFail;
+        }
     }
 }
 
@@ -791,7 +980,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                 if (len > kMaxStrLen) {
                     A.out_len[i] = kFailLen;
                     A.status[i] = kStatusTooLong;
-                } else {
+                } else if (!split_push(A, i, len)) {
                     busy = true;
                     head = (dst & (SEG - 1u)) != 0;
                     P = ocnt = flags = first = lastb = fail = 0;
@@ -2879,11 +3068,8 @@ int set_decode_prices(int device, const float* in4) {
     return 0;
 }
 
-hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
-                         const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
-                         uint8_t* status, hipStream_t stream, uint64_t sel_bytes) {
-    if (n == 0) return hipSuccess;
-    DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr, nullptr, nullptr, nullptr, nullptr};
+static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint32_t* in_len, uint32_t n, uint8_t* out,
+                                        const uint32_t* out_off, hipStream_t stream, uint64_t sel_bytes) {
 #ifdef HHUFF_MIX_STREAM  // A/B builds: mixed lengths go to the stream kernel alone
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n) == kDecL ? (int)kDecT : pick_decode(sel_bytes ? sel_bytes : in_size, n);
 #else
@@ -2944,6 +3130,44 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         default: hipLaunchKernelGGL(DEC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }
     return defer ? finish_deferred(out, A.edges, n, stream) : hipGetLastError();
+}
+
+// Long strings (kSplitMin Huffman bytes or more) are listed by the decode kernels and decoded afterwards, one
+// wave each, by split_decode_kernel -- in batches whose mean string is long (>= 128 B: QPACK values, cookies)
+// and in tiny batches (the per-string launch path for strings over the service's 768 B).  Elsewhere the list
+// would cost a memset and a launch on every call for strings that are almost never there, and a rare long
+// string is decoded by one lane.
+#ifndef HHUFF_SPLIT
+#define HHUFF_SPLIT 1  // 0: no list (A/B builds: every long string decoded by one lane)
+#endif
+constexpr int kSplitWaves = 4;
+hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
+                         const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
+                         uint8_t* status, hipStream_t stream, uint64_t sel_bytes) {
+    if (n == 0) return hipSuccess;
+    DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr, nullptr, nullptr, nullptr, nullptr};
+    const uint64_t bytes = sel_bytes ? sel_bytes : in_size;
+    const bool split = HHUFF_SPLIT && bytes >= kSplitMin && (bytes / n >= 128u || n <= 16u);
+    uint32_t* sp = nullptr;
+    if (split) {
+        A.split_cap = (uint32_t)std::min<uint64_t>(n, bytes / kSplitMin + 1);
+        hipError_t e = pool_alloc((void**)&sp, 4ull * (A.split_cap + 1), stream);
+        if (e == hipSuccess) e = hipMemsetAsync(sp, 0, 4, stream);
+        if (e != hipSuccess) return e;
+        A.split_n = sp;
+        A.split_list = sp + 1;
+    }
+    hipError_t e = launch_decode_kernels(A, in_size, in_len, n, out, out_off, stream, sel_bytes);
+    if (split) {
+        if (e == hipSuccess) {
+            const int grid = (int)std::min<uint32_t>((A.split_cap + kSplitWaves - 1) / kSplitWaves, 512u);
+            hipLaunchKernelGGL(split_decode_kernel<kSplitWaves>, dim3(grid), dim3(kSplitWaves * 64), 0, stream, A);
+            e = hipGetLastError();
+        }
+        const hipError_t f = hipFreeAsync(sp, stream);
+        if (e == hipSuccess) e = f;
+    }
+    return e;
 }
 
 hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,

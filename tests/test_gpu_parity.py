@@ -405,6 +405,106 @@ def test_decode_price_calibration(torch_cuda):
     assert codec.decode_prices(0) == pytest.approx(defaults)
 
 
+def _long_huffman_strings(oracle_codec, rng, lengths):
+    """Huffman strings of about the given plain lengths: header text, long codes only, periodic text
+    (a wrong start may never resynchronise on it) and corruptions (an EOS or long-code run in the middle,
+    a flipped bit, truncation, bad padding)"""
+    syms, p = synth.header_alphabet()
+    plain = []
+    for k, L in enumerate(lengths):
+        kind = k % 6
+        if kind == 0:
+            s = bytes(rng.choice(syms, L, p=p))
+        elif kind == 1:  # every 10th symbol a long code (8..28 bits): still shorter than the plain text
+            t = rng.choice(syms, L, p=p)
+            sel = rng.random(L) < 0.1
+            t[sel] = rng.choice(np.frombuffer(b"{}~^|<>\\\x00\x7f", np.uint8), int(sel.sum()))
+            s = bytes(t.astype(np.uint8))
+        elif kind == 2:
+            s = (b"a" * L)
+        elif kind == 3:
+            s = (b"0e" * (L // 2 + 1))[:L]
+        else:
+            s = bytes(rng.choice(syms, L, p=p))
+        plain.append(s)
+    data, off = synth.pack(plain)
+    o_out, o_len, _ = oracle_codec.encode_batch(data, off, len(plain), nthreads=8)
+    huff = []
+    for i in range(len(plain)):
+        if o_len[i] == FAIL:  # not shorter than the plain text: the plain bytes (mostly invalid Huffman)
+            h = bytearray(plain[i])
+        else:
+            h = bytearray(o_out[int(off[i]):int(off[i]) + int(o_len[i])].tobytes())
+        if i % 6 == 5 and len(h) > 8:
+            k = (i // 6) % 4
+            j = int(rng.integers(1, len(h) - 5))
+            if k == 0:
+                h[j:j + 4] = b"\xff\xff\xff\xff"
+            elif k == 1:
+                h[j] ^= 1 << int(rng.integers(8))
+            elif k == 2:
+                h = h[:j]
+            else:
+                h += b"\x00"
+        huff.append(bytes(h))
+    return huff
+
+
+def test_split_decode_long_strings(torch_cuda, oracle_codec):
+    """strings of 4 KiB and more (one wave each, self-synchronising segments, split_decode_kernel) against
+    the oracle: implicit slots, pairs with explicit unaligned destinations, a list mixed with short strings,
+    and the per-string symbol (one string: the launch path); lengths up to 300 KB"""
+    from h2o_amd import codec
+
+    rng = np.random.default_rng(33)
+    lengths = [5200, 6000, 6500, 8000, 9000, 12000, 20000, 40000, 70000, 150000, 370000, 7000]
+    lengths += [int(x) for x in rng.integers(5200, 30000, 36)]
+    huff = _long_huffman_strings(oracle_codec, rng, lengths)
+    assert sum(len(h) >= 4096 for h in huff) > 30
+    hdata, hoff = synth.pack(huff)
+    m = len(huff)
+    names = synth.bits_from_bools(rng.random(m) < 0.3)
+    g = gpu_decode(torch_cuda, hdata, hoff, m, is_name_bits=names)
+    o = oracle_codec.decode_batch(hdata, hoff, m, is_name_bits=names, nthreads=8)
+    np.testing.assert_array_equal(g[1], o[1])
+    np.testing.assert_array_equal(g[2], o[2])
+    slots = (hoff[:m].astype(np.uint64) * 8) // 5
+    assert compact(g[0], slots, g[1]) == compact(o[0], slots, o[1])
+    good = np.nonzero(g[1] != FAIL)[0]
+    assert len(good) > m // 2
+    # pairs in reverse order, explicit destinations at odd offsets
+    idx = np.arange(m)[::-1].copy()
+    starts, lens = hoff[idx].astype(np.uint32), np.diff(hoff)[idx].astype(np.uint32)
+    dst = np.zeros(m, np.uint32)
+    pos = 3
+    for k in range(m):
+        dst[k] = pos
+        pos += int(lens[k]) * 8 // 5 + 1 + (k % 7)
+    g = gpu_decode(torch_cuda, hdata, starts, m, in_len=lens, out_off=dst, out_size=pos + 16)
+    o = oracle_codec.decode_batch(hdata, starts, m, in_len=lens, nthreads=8)
+    np.testing.assert_array_equal(g[1], o[1])
+    np.testing.assert_array_equal(g[2], o[2])
+    osl = (starts.astype(np.uint64) * 8) // 5
+    for k in np.nonzero(g[1] != FAIL)[0]:
+        assert g[0][int(dst[k]):int(dst[k]) + int(g[1][k])].tobytes() == \
+            o[0][int(osl[k]):int(osl[k]) + int(o[1][k])].tobytes()
+    # long strings among short ones (mean still above 128 B: listed from the streaming kernel)
+    short = [bytes(rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8)) for _ in range(400)]
+    mix = short[:200] + huff[:20] + short[200:]
+    mdata, moff = synth.pack(mix)
+    mm = len(mix)
+    g = gpu_decode(torch_cuda, mdata, moff, mm)
+    o = oracle_codec.decode_batch(mdata, moff, mm, nthreads=8)
+    np.testing.assert_array_equal(g[1], o[1])
+    np.testing.assert_array_equal(g[2], o[2])
+    ms = (moff[:mm].astype(np.uint64) * 8) // 5
+    assert compact(g[0], ms, g[1]) == compact(o[0], ms, o[1])
+    # one string at a time (the per-string symbol's launch path)
+    for h in huff[:12]:
+        for nm in (False, True):
+            assert codec.decode_huffman(h, nm) == oracle_codec.decode(h, nm)
+
+
 # ------------------------------------------------------------------------------------------------
 # per-string h2o symbols and the host batch API
 # ------------------------------------------------------------------------------------------------
