@@ -348,6 +348,7 @@ struct DecArgs {
     uint32_t* split_list = nullptr;
     uint32_t* split_n = nullptr;
     uint32_t split_cap = 0;
+    uint32_t split_min = 0xFFFFFFFFu;  // Huffman bytes from which a string is listed
     // with gate: the staged / stream prices select_verdict uses, ps per string and per (tile-padded) byte --
     // the fitted defaults, or the device's calibration (calibrate_prices)
     float price[4] = {40.0f, 1.07f, 184.0f, 1.15f};
@@ -362,9 +363,8 @@ __device__ __forceinline__ void load_dec_tables(uint32_t* s_lut, uint32_t* s_kin
 
 // a string long enough for split_decode_kernel goes to its list (when the launch has one) instead of being
 // decoded by this lane; a full list leaves it here
-constexpr uint32_t kSplitMinBytes = 4096;  // = kSplitMin (split_decode_kernel)
 __device__ __forceinline__ bool split_push(const DecArgs& A, uint32_t i, uint32_t len) {
-    if (A.split_list == nullptr || len < kSplitMinBytes || len > kMaxStrLen) return false;
+    if (A.split_list == nullptr || len < A.split_min || len > kMaxStrLen) return false;
     const uint32_t k = atomicAdd(A.split_n, 1u);
     if (k >= A.split_cap) return false;
     A.split_list[k] = i;
@@ -712,7 +712,8 @@ __global__ __launch_bounds__(WAVES * 64) void decode_direct_kernel(DecArgs A) {
 // Same results as decode_core (hpack.c:117-156): EOS on the true path fails the string (hpack.c:88-89), the
 // soft bits come from all symbols' flags and the first and last byte.
 // ------------------------------------------------------------------------------------------------
-constexpr uint32_t kSplitMin = kSplitMinBytes;  // Huffman bytes: strings this long go to split_decode_kernel
+constexpr uint32_t kSplitMin = 4096;     // Huffman bytes: strings this long go to split_decode_kernel
+constexpr uint32_t kSplitMinFew = 512;   // the same in batches of <= 16 strings (latency: one lane would take them)
 constexpr uint32_t kSplitLead = 256;  // bits decoded before a segment (synchronisation lag: mean 37, p99 193)
 
 struct SegWalk {
@@ -810,11 +811,11 @@ __global__ __launch_bounds__(WAVES * 64) void split_decode_kernel(DecArgs A) {
     for (uint32_t j = blockIdx.x * WAVES + wave; j < nl; j += gridDim.x * WAVES) {
         const uint32_t i = A.split_list[j];
         const uint32_t s = A.in_off[i];
-        const uint32_t len = A.in_len ? A.in_len[i] : A.in_off[i + 1] - s;  // kSplitMin <= len <= kMaxStrLen
+        const uint32_t len = A.in_len ? A.in_len[i] : A.in_off[i + 1] - s;  // split_min <= len <= kMaxStrLen
         const bool is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) : false;
         const uint64_t d = A.out_off ? (uint64_t)A.out_off[i] : dec_slot(s);
         const uint32_t TB = 8u * len;
-        const uint32_t seg = (uint32_t)(((uint64_t)TB + 64u * 32u - 1u) / (64u * 32u)) * 32u;  // bits, dword multiple
+        const uint32_t seg = (uint32_t)(((uint64_t)TB + 64u * 32u - 1u) / (64u * 32u)) * 32u;  // bits, a dword multiple
         const uint32_t ks = lane * seg;
         const bool act = ks < TB;
         const bool lastl = act && ks + seg >= TB;
@@ -3134,7 +3135,8 @@ static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint3
 
 // Long strings (kSplitMin Huffman bytes or more) are listed by the decode kernels and decoded afterwards, one
 // wave each, by split_decode_kernel -- in batches whose mean string is long (>= 128 B: QPACK values, cookies)
-// and in tiny batches (the per-string launch path for strings over the service's 768 B).  Elsewhere the list
+// and in tiny batches (kSplitMinFew: the per-string launch path for strings over the service's 768 B, where a
+// lane would take the whole string's bits one after another).  Elsewhere the list
 // would cost a memset and a launch on every call for strings that are almost never there, and a rare long
 // string is decoded by one lane.
 #ifndef HHUFF_SPLIT
@@ -3147,10 +3149,12 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     if (n == 0) return hipSuccess;
     DecArgs A{in, in_size, in_off, in_len, n, is_name_bits, out, out_off, out_len, status, nullptr, nullptr, nullptr, nullptr, nullptr};
     const uint64_t bytes = sel_bytes ? sel_bytes : in_size;
-    const bool split = HHUFF_SPLIT && bytes >= kSplitMin && (bytes / n >= 128u || n <= 16u);
+    const uint32_t smin = n <= 16u ? kSplitMinFew : kSplitMin;
+    const bool split = HHUFF_SPLIT && bytes >= smin && (bytes / n >= 128u || n <= 16u);
     uint32_t* sp = nullptr;
     if (split) {
-        A.split_cap = (uint32_t)std::min<uint64_t>(n, bytes / kSplitMin + 1);
+        A.split_min = smin;
+        A.split_cap = (uint32_t)std::min<uint64_t>(n, bytes / smin + 1);
         hipError_t e = pool_alloc((void**)&sp, 4ull * (A.split_cap + 1), stream);
         if (e == hipSuccess) e = hipMemsetAsync(sp, 0, 4, stream);
         if (e != hipSuccess) return e;

@@ -453,7 +453,7 @@ def _long_huffman_strings(oracle_codec, rng, lengths):
 def test_split_decode_long_strings(torch_cuda, oracle_codec):
     """strings of 4 KiB and more (one wave each, self-synchronising segments, split_decode_kernel) against
     the oracle: implicit slots, pairs with explicit unaligned destinations, a list mixed with short strings,
-    and the per-string symbol (one string: the launch path); lengths up to 300 KB"""
+    the per-string symbol (one string: the launch path) and tiny batches (512 B and more); lengths up to 370 KB"""
     from h2o_amd import codec
 
     rng = np.random.default_rng(33)
@@ -499,10 +499,19 @@ def test_split_decode_long_strings(torch_cuda, oracle_codec):
     np.testing.assert_array_equal(g[2], o[2])
     ms = (moff[:mm].astype(np.uint64) * 8) // 5
     assert compact(g[0], ms, g[1]) == compact(o[0], ms, o[1])
-    # one string at a time (the per-string symbol's launch path)
-    for h in huff[:12]:
+    # one string at a time (the per-string symbol's launch path) and tiny batches: split from 512 B on
+    mid = _long_huffman_strings(oracle_codec, rng, [int(x) for x in rng.integers(700, 5200, 24)])
+    for h in huff[:12] + mid:
         for nm in (False, True):
             assert codec.decode_huffman(h, nm) == oracle_codec.decode(h, nm)
+    for k in range(0, 24, 6):
+        tdata, toff = synth.pack(mid[k:k + 6])
+        g = gpu_decode(torch_cuda, tdata, toff, 6)
+        o = oracle_codec.decode_batch(tdata, toff, 6, nthreads=8)
+        np.testing.assert_array_equal(g[1], o[1])
+        np.testing.assert_array_equal(g[2], o[2])
+        ts = (toff[:6].astype(np.uint64) * 8) // 5
+        assert compact(g[0], ts, g[1]) == compact(o[0], ts, o[1])
 
 
 # ------------------------------------------------------------------------------------------------

@@ -3,7 +3,7 @@
 segment / synchronisation logic on the CPU against the oracle.  Mirrors seg_walk over the same tables
 (13-bit window LUT, long-code tables) and the kernel's agree-with-the-lane-before loop.
 
-    python tools/emu_split.py [n] [seed]
+    python tools/emu_split.py [n] [seed] [min_len] [max_len]   (plain lengths)
 """
 import os
 import sys
@@ -128,7 +128,9 @@ def main():
     T = tables()
     o = O.oracle()
     rng = np.random.default_rng(seed)
-    huff = _long_huffman_strings(o, rng, [int(x) for x in rng.integers(5200, 12000, n)])
+    lo = int(sys.argv[3]) if len(sys.argv) > 3 else 5200
+    hi = int(sys.argv[4]) if len(sys.argv) > 4 else 12000
+    huff = _long_huffman_strings(o, rng, [int(x) for x in rng.integers(lo, hi, n)])
     bad = 0
     for i, h in enumerate(huff):
         ref, _ = o.decode(h)
