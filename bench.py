@@ -606,6 +606,27 @@ def per_string_latency(codec, calls=2000):
         t.sort()
         out[name] = {"median": round(t[len(t) // 2] * 1e6, 2), "p99": round(t[int(len(t) * 0.99)] * 1e6, 2)}
     out["string_bytes"] = len(s)
+    # long values (cookies, URIs): past the service's 768 B a call is one launch; decode splits the string over
+    # a wave from 512 Huffman bytes (split_decode_kernel)
+    text = (b"session=eyJhbGciOiJIUzI1NiJ9.dXNlcj0xMjM0NTY3ODkw; theme=dark; lang=en-US; " * 300)
+    longs = {}
+    for L in (1024, 4096, 16384):
+        ls = text[:L]
+        lh = codec.encode_huffman(ls)
+        assert codec.decode_huffman(lh, False)[0] == ls
+        r = {}
+        for name, fn in (("encode", lambda: codec.encode_huffman(ls)), ("decode", lambda: codec.decode_huffman(lh, False))):
+            for _ in range(10):
+                fn()
+            t = []
+            for _ in range(200):
+                t0 = time.perf_counter()
+                fn()
+                t.append(time.perf_counter() - t0)
+            t.sort()
+            r[name] = round(t[len(t) // 2] * 1e6, 2)
+        longs[str(L)] = r
+    out["long_strings_median_us"] = longs
     return out
 
 

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Long-string decode: libhhuff builds interleaved in one process (split_decode_kernel against one lane per
-string).  Batches of long header values: 512 x 4-64 KB, 64 x 256 KB, and one string of 100 KB / 1 MB.
+string).  Batches of long header values: 512 x 4-64 KB, 64 x 256 KB, one string of 100 KB / 1 MB / 2 KB, 8 x 3 KB.
 
     python tools/split_bench.py NAME1 NAME2 ...   (libraries from build/ab)
 """
@@ -32,7 +32,7 @@ def main(names, rounds=5, steps=10):
     rng = np.random.default_rng(9)
     syms, p = synth.header_alphabet()
     cases = {"512x4-64K": [int(x) for x in rng.integers(4096, 65536, 512)], "64x256K": [262144] * 64,
-             "1x100K": [100000], "1x1M": [1 << 20]}
+             "1x100K": [100000], "1x1M": [1 << 20], "1x2K": [2000], "8x3K": [3000] * 8}
     s = torch.cuda.current_stream().cuda_stream
     res = {}
     for cname, lens in cases.items():
