@@ -700,9 +700,9 @@ __global__ __launch_bounds__(WAVES * 64) void decode_direct_kernel(DecArgs A) {
 // Split decode of long strings (SURVEY §7 hard part 2: h2o takes header values up to H2O_MAX_REQLEN).  A
 // string of kSplitMin bytes or more would keep one lane busy for its whole length; here one wave decodes it.
 // The string's bits are cut into 64 segments of `seg` bits (a dword multiple).  Huffman codes self-
-// synchronise: a lane that starts decoding `kSplitLead` bits before its segment at an arbitrary bit is, with
-// overwhelming probability, on the true symbol boundaries by the time it reaches its segment.
-//   pass A: lane k decodes from max(k seg - kSplitLead, 0) to the first symbol boundary at or after
+// synchronise: a lane that starts decoding a lead of 64..kSplitLead bits before its segment at an arbitrary bit
+// is, with high probability, on the true symbol boundaries by the time it reaches its segment.
+//   pass A: lane k decodes from max(k seg - lead, 0) to the first symbol boundary at or after
 //           (k + 1) seg (the last active lane: to the string's end, with the padding rule, hpack.c:132-133),
 //           and counts the symbols that start at or after k seg: f_k = the first of them, e_k = where it stops;
 //   check:  lane k agrees with lane k - 1 iff f_k == e_{k-1}; a lane that does not decodes again from
@@ -714,7 +714,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_direct_kernel(DecArgs A) {
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t kSplitMin = 4096;     // Huffman bytes: strings this long go to split_decode_kernel
 constexpr uint32_t kSplitMinFew = 512;   // the same in batches of <= 16 strings (latency: one lane would take them)
-constexpr uint32_t kSplitLead = 256;  // bits decoded before a segment (synchronisation lag: mean 37, p99 193)
+constexpr uint32_t kSplitLead = 256;  // bits decoded before a long segment (synchronisation lag: mean 37, p99 193)
 
 struct SegWalk {
     uint32_t f, e;        // first counted symbol's start, stop position (bits from the string's start)
@@ -725,8 +725,8 @@ struct SegWalk {
 
 // Decode the string's bits from p0; count (and with EMIT write) the symbols starting in [kstart, pstop);
 // stop at the first boundary >= pstop, or at the string's end when pstop >= TB.
-template <bool EMIT>
-__device__ __forceinline__ SegWalk seg_walk(const GlobalSource& src, uint32_t s, uint32_t TB, uint32_t p0,
+template <bool EMIT, class Src>
+__device__ __forceinline__ SegWalk seg_walk(const Src& src, uint32_t s, uint32_t TB, uint32_t p0,
                                             uint32_t kstart, uint32_t pstop, RegSink& sink, const DecTables& T) {
     SegWalk r{0xFFFFFFFFu, 0u, 0u, 0u, 0u, 0u, false, false};
     // bit reader at absolute bit 8 s + p0 (MSB-first dwords)
@@ -796,6 +796,67 @@ __device__ __forceinline__ SegWalk seg_walk(const GlobalSource& src, uint32_t s,
     return r;
 }
 
+// One wave decodes the string at src bytes [s, s + len) into dst (any alignment, global or LDS); every lane
+// returns the output length (kFailLen on failure) and the status byte.
+template <class Src>
+__device__ __forceinline__ void split_decode_wave(const Src& src, uint32_t s, uint32_t len, bool is_name, uint8_t* dst,
+                                                  const DecTables& T, uint32_t lane, uint32_t& ol, uint8_t& st) {
+    const uint32_t TB = 8u * len;
+    if (TB == 0) {  // an empty string decodes to nothing (hpack.c:117-156 with no bits)
+        ol = 0;
+        st = soft_bits(is_name, 0u, 0u, 0u, 0u);
+        return;
+    }
+    const uint32_t seg = (uint32_t)(((uint64_t)TB + 64u * 32u - 1u) / (64u * 32u)) * 32u;  // bits, a dword multiple
+    // lead: the bits a lane decodes before its segment.  Longer leads fail to synchronise less often (header
+    // text: 17 % of starts at 64 bits, 3.6 % at 128, ~0.2 % at 256), and every failure costs a sequential
+    // re-walk of a segment; short segments (per-string calls) take short leads
+    const uint32_t lead = seg <= 64u ? 64u : (seg <= 256u ? 128u : kSplitLead);
+    const uint32_t ks = lane * seg;
+    const bool act = ks < TB;
+    const bool lastl = act && ks + seg >= TB;
+    const uint32_t pstop = lastl ? TB : ks + seg;
+    RegSink none;
+    none.init(nullptr);
+    SegWalk w{};
+    if (act) w = seg_walk<false>(src, s, TB, ks > lead ? ks - lead : 0u, ks, pstop, none, T);
+    // agree with the lane before: lane k starts where lane k - 1 stopped
+    for (int it = 0; it < 64; ++it) {
+        const uint32_t pe = (uint32_t)__shfl_up((int)w.e, 1, 64);
+        const bool bad = act && lane > 0 && w.f != pe;
+        if (__builtin_amdgcn_ballot_w64(bad) == 0) break;
+        if (bad) w = seg_walk<false>(src, s, TB, pe, pe, pstop, none, T);
+    }
+    const uint32_t cnt = act ? w.cnt : 0u;
+    const uint32_t place = wave_excl_scan(cnt, (int)lane);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(place + cnt), 63);
+    const bool eos = __builtin_amdgcn_ballot_w64(act && w.eos) != 0;
+    const bool end_ok = __builtin_amdgcn_ballot_w64(lastl && w.end_ok) != 0;
+    const bool ok = !eos && end_ok;
+    uint32_t fl = act ? w.flags : 0u;
+    fl |= (uint32_t)__shfl_xor((int)fl, 1, 64);
+    fl |= (uint32_t)__shfl_xor((int)fl, 2, 64);
+    fl |= (uint32_t)__shfl_xor((int)fl, 4, 64);
+    fl |= (uint32_t)__shfl_xor((int)fl, 8, 64);
+    fl |= (uint32_t)__shfl_xor((int)fl, 16, 64);
+    fl |= (uint32_t)__shfl_xor((int)fl, 32, 64);
+    // first byte: the first lane with symbols; last byte: the last one
+    const uint64_t has = __builtin_amdgcn_ballot_w64(cnt != 0);
+    uint32_t first = 0, last = 0;
+    if (has) {
+        first = (uint32_t)__shfl((int)w.first, (int)__builtin_ctzll(has), 64);
+        last = (uint32_t)__shfl((int)w.last, 63 - (int)__builtin_clzll(has), 64);
+    }
+    if (ok && act && cnt) {
+        RegSink sink;
+        sink.init(dst + place);
+        (void)seg_walk<true>(src, s, TB, w.f, w.f, pstop, sink, T);
+        sink.finish();
+    }
+    ol = ok ? total : kFailLen;
+    st = ok ? soft_bits(is_name, total, fl & 3u, first, last) : kStatusFail;
+}
+
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void split_decode_kernel(DecArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
@@ -814,52 +875,12 @@ __global__ __launch_bounds__(WAVES * 64) void split_decode_kernel(DecArgs A) {
         const uint32_t len = A.in_len ? A.in_len[i] : A.in_off[i + 1] - s;  // split_min <= len <= kMaxStrLen
         const bool is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) : false;
         const uint64_t d = A.out_off ? (uint64_t)A.out_off[i] : dec_slot(s);
-        const uint32_t TB = 8u * len;
-        const uint32_t seg = (uint32_t)(((uint64_t)TB + 64u * 32u - 1u) / (64u * 32u)) * 32u;  // bits, a dword multiple
-        const uint32_t ks = lane * seg;
-        const bool act = ks < TB;
-        const bool lastl = act && ks + seg >= TB;
-        const uint32_t pstop = lastl ? TB : ks + seg;
-        RegSink none;
-        none.init(nullptr);
-        SegWalk w{};
-        if (act) w = seg_walk<false>(src, s, TB, ks > kSplitLead ? ks - kSplitLead : 0u, ks, pstop, none, T);
-        // agree with the lane before: lane k starts where lane k - 1 stopped
-        for (int it = 0; it < 64; ++it) {
-            const uint32_t pe = (uint32_t)__shfl_up((int)w.e, 1, 64);
-            const bool bad = act && lane > 0 && w.f != pe;
-            if (__builtin_amdgcn_ballot_w64(bad) == 0) break;
-            if (bad) w = seg_walk<false>(src, s, TB, pe, pe, pstop, none, T);
-        }
-        const uint32_t cnt = act ? w.cnt : 0u;
-        const uint32_t place = wave_excl_scan(cnt, (int)lane);
-        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)(place + cnt), 63);
-        const bool eos = __builtin_amdgcn_ballot_w64(act && w.eos) != 0;
-        const bool end_ok = __builtin_amdgcn_ballot_w64(lastl && w.end_ok) != 0;
-        const bool ok = !eos && end_ok;
-        uint32_t fl = act ? w.flags : 0u;
-        fl |= (uint32_t)__shfl_xor((int)fl, 1, 64);
-        fl |= (uint32_t)__shfl_xor((int)fl, 2, 64);
-        fl |= (uint32_t)__shfl_xor((int)fl, 4, 64);
-        fl |= (uint32_t)__shfl_xor((int)fl, 8, 64);
-        fl |= (uint32_t)__shfl_xor((int)fl, 16, 64);
-        fl |= (uint32_t)__shfl_xor((int)fl, 32, 64);
-        // first byte: the first lane with symbols; last byte: the last one
-        const uint64_t has = __builtin_amdgcn_ballot_w64(cnt != 0);
-        uint32_t first = 0, last = 0;
-        if (has) {
-            first = (uint32_t)__shfl((int)w.first, (int)__builtin_ctzll(has), 64);
-            last = (uint32_t)__shfl((int)w.last, 63 - (int)__builtin_clzll(has), 64);
-        }
-        if (ok && act && cnt) {
-            RegSink sink;
-            sink.init(A.out + d + place);
-            (void)seg_walk<true>(src, s, TB, w.f, w.f, pstop, sink, T);
-            sink.finish();
-        }
+        uint32_t ol;
+        uint8_t st;
+        split_decode_wave(src, s, len, is_name, A.out + d, T, lane, ol, st);
         if (lane == 0) {
-            A.out_len[i] = ok ? total : kFailLen;
-            A.status[i] = ok ? soft_bits(is_name, total, fl & 3u, first, last) : kStatusFail;
+            A.out_len[i] = ol;
+            A.status[i] = st;
         }
     }
 }
@@ -3241,61 +3262,6 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     return defer ? finish_deferred(out, A.edges, n, stream, nullptr, recs) : hipGetLastError();
 }
 
-// ------------------------------------------------------------------------------------------------
-// One string per launch: the h2o per-string symbols (h2o_hpack_{de,en}code_huffman).  The string sits in
-// pinned, device-visible host memory, [meta 16 B][input][output]: one launch reads it across PCIe (the
-// block's 16-B loads in one round trip) into LDS, lane 0 runs the codec from LDS into an LDS output buffer,
-// and the wave writes the result and the meta words back -- no copies, one launch, one synchronisation.
-// ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void one_string_kernel(uint8_t* __restrict__ h, uint32_t len, uint32_t in_cap,
-                                                         uint32_t is_name, uint32_t encode) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
-    __shared__ uint32_t s_kinfo[32];
-    __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
-    __shared__ __attribute__((aligned(16))) uint32_t s_in[kOneMax / 4 + 4];
-    __shared__ __attribute__((aligned(16))) uint8_t s_out[(kOneMax * 8) / 5 + 64];
-    uint2* s_enc = reinterpret_cast<uint2*>(s_lut);  // encode: the table takes the LUT's place
-    if (encode) {
-        for (uint32_t k = threadIdx.x; k < 256; k += 256) s_enc[k] = make_uint2(g_enc_code[k], g_enc_nbits[k]);
-    } else {
-        load_dec_tables(s_lut, s_kinfo, s_ones, 256);
-    }
-    for (uint32_t k = 16u * threadIdx.x; k < len; k += 16u * 256u)
-        *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_in) + k) = *reinterpret_cast<const uint4*>(h + 16 + k);
-    __syncthreads();
-    __shared__ uint32_t s_res[2];
-    if (threadIdx.x == 0) {
-        const LdsSource src{s_in, len ? ((len + 3u) & ~3u) - 4u : 0u};
-        LdsSink sink{s_out, 0u, 0u, (kOneMax * 8) / 5 + 60};
-        uint32_t ol, st = 0;
-        if (encode) {
-            ol = encode_core(src, 0u, len, sink, s_enc);
-            st = ol == kFailLen ? kStatusFail : 0u;
-        } else {
-            const DecResult r = decode_core(src, 0u, len, sink, DecTables{s_lut, s_kinfo, s_ones});
-            ol = r.ok ? r.len : kFailLen;
-            st = r.ok ? soft_bits(is_name != 0, r.len, r.flags, r.len ? s_out[0] : 0u, r.len ? s_out[r.len - 1] : 0u)
-                      : kStatusFail;
-        }
-        s_res[0] = ol;
-        s_res[1] = st;
-    }
-    __syncthreads();
-    const uint32_t ol = s_res[0];
-    const uint32_t n = ol == kFailLen ? 0u : ol;
-    for (uint32_t k = 4u * threadIdx.x; k < n; k += 4u * 256u)
-        *reinterpret_cast<uint32_t*>(h + 16 + in_cap + k) = *reinterpret_cast<const uint32_t*>(s_out + k);
-    if (threadIdx.x == 0) {
-        reinterpret_cast<uint32_t*>(h)[2] = ol;
-        reinterpret_cast<uint32_t*>(h)[3] = s_res[1];
-    }
-}
-
-hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, bool encode, hipStream_t stream) {
-    hipLaunchKernelGGL(one_string_kernel, dim3(1), dim3(256), 0, stream, h, len, in_cap, is_name ? 1u : 0u,
-                       encode ? 1u : 0u);
-    return hipGetLastError();
-}
 
 // ------------------------------------------------------------------------------------------------
 // Resident per-string service.  A launch per string costs ~18 us (launch + stream synchronisation); here
@@ -3321,13 +3287,13 @@ hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, b
 // ------------------------------------------------------------------------------------------------
 // encode s_in bytes [0, len) into out32 (LDS, MSB-first words); returns the code bits or kFailLen
 __device__ __forceinline__ uint32_t wave_encode(const uint8_t* in, uint32_t len, uint32_t* out32, const uint2* s_enc,
-                                                uint32_t lane) {
+                                                uint32_t lane, uint32_t cap = kSvcMax) {
     for (uint32_t k = lane; k < len / 4u + 4u; k += 64u) out32[k] = 0u;
     wave_lds_sync();
     const uint32_t obase = lds_addr(out32);
     const uint32_t lim = len ? 8u * len - 8u : 0u;  // hpack.c:799-800: ceil(bits / 8) < len
     uint32_t bits = 0;                               // wave-uniform
-    bool fail = len == 0 || len > kSvcMax;
+    bool fail = len == 0 || len > cap;
     for (uint32_t j0 = 0; j0 < len && !fail; j0 += 64u) {
         const uint32_t j = j0 + lane;
         const uint2 e = j < len ? s_enc[in[j]] : make_uint2(0u, 0u);
@@ -3480,6 +3446,69 @@ __device__ __forceinline__ DecResult wave_decode(const uint8_t* in, uint32_t len
     return r;
 }
 
+// ------------------------------------------------------------------------------------------------
+// One string per launch: the h2o per-string symbols (h2o_hpack_{de,en}code_huffman).  The string sits in
+// pinned, device-visible host memory, [meta 16 B][input][output]: one launch reads it across PCIe (the
+// block's 16-B loads in one round trip) into LDS, wave 0 codes it from LDS into an LDS output buffer (encode:
+// the service's 64-bytes-a-round wave encoder; decode: split_decode_wave, 64 self-synchronising segments --
+// a lone lane took ~100 us for 1 KB), and the block writes the result and the meta words back -- no copies,
+// one launch, one synchronisation.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void one_string_kernel(uint8_t* __restrict__ h, uint32_t len, uint32_t in_cap,
+                                                         uint32_t is_name, uint32_t encode) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
+    __shared__ uint32_t s_kinfo[32];
+    __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[kOneMax / 4 + 4];
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[(kOneMax * 8) / 5 + 64];
+    uint2* s_enc = reinterpret_cast<uint2*>(s_lut);  // encode: the table takes the LUT's place
+    if (encode) {
+        for (uint32_t k = threadIdx.x; k < 256; k += 256) s_enc[k] = make_uint2(g_enc_code[k], g_enc_nbits[k]);
+    } else {
+        load_dec_tables(s_lut, s_kinfo, s_ones, 256);
+    }
+    for (uint32_t k = 16u * threadIdx.x; k < len; k += 16u * 256u)
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_in) + k) = *reinterpret_cast<const uint4*>(h + 16 + k);
+    __syncthreads();
+    __shared__ uint32_t s_res[2];
+    if (threadIdx.x < 64) {  // wave 0: the service's wave encoder, the split decoder over the staged string
+        const uint32_t lane = threadIdx.x;
+        uint32_t ol, st = 0;
+        if (encode) {
+            ol = wave_encode(reinterpret_cast<const uint8_t*>(s_in), len, reinterpret_cast<uint32_t*>(s_out), s_enc,
+                             lane, kOneMax);
+            st = ol == kFailLen ? kStatusFail : 0u;
+            if (ol != kFailLen) ol = (ol + 7u) >> 3;
+        } else {
+            const LdsSource src{s_in, len ? ((len + 3u) & ~3u) - 4u : 0u};
+            uint8_t st8;
+            split_decode_wave(src, 0u, len, is_name != 0, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane, ol, st8);
+            st = st8;
+        }
+        if (lane == 0) {
+            s_res[0] = ol;
+            s_res[1] = st;
+        }
+    }
+    __syncthreads();
+    const uint32_t ol = s_res[0];
+    const uint32_t n = ol == kFailLen ? 0u : ol;
+    for (uint32_t k = 4u * threadIdx.x; k < n; k += 4u * 256u) {  // encode's stage holds MSB-first words
+        const uint32_t v = *reinterpret_cast<const uint32_t*>(s_out + k);
+        *reinterpret_cast<uint32_t*>(h + 16 + in_cap + k) = encode ? bswap32(v) : v;
+    }
+    if (threadIdx.x == 0) {
+        reinterpret_cast<uint32_t*>(h)[2] = ol;
+        reinterpret_cast<uint32_t*>(h)[3] = s_res[1];
+    }
+}
+
+hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, bool encode, hipStream_t stream) {
+    hipLaunchKernelGGL(one_string_kernel, dim3(1), dim3(256), 0, stream, h, len, in_cap, is_name ? 1u : 0u,
+                       encode ? 1u : 0u);
+    return hipGetLastError();
+}
+
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -3530,6 +3559,9 @@ __device__ __forceinline__ void sys_poll(const void* pa, uint64_t ma, const void
     rb = make_uint4(b.x, b.y, b.z, b.w);
 }
 
+#ifndef HHUFF_SVC_SPLIT
+#define HHUFF_SVC_SPLIT 1  // 0: the candidate-chain wave decoder (A/B builds)
+#endif
 template <int NC, bool JUMP = false>
 __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
                                                      uint64_t idle_ticks, uint64_t max_ticks) {
@@ -3612,11 +3644,22 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
                 st = ol == kFailLen ? kStatusFail : 0u;
                 if (ol != kFailLen) ol = (ol + 7u) >> 3;
             } else {
+#if HHUFF_SVC_SPLIT
+                // 64 self-synchronising segments (split_decode_wave): a lane walks a 64-128-bit lead and a segment
+                // of at most 96 bits, where the candidate-chain decoder took a LUT round trip per 64 string bits
+                uint8_t st8;
+                split_decode_wave(LdsSource{s_in, len ? ((len + 3u) & ~3u) - 4u : 0u}, 0u, len, is_name != 0, s_out,
+                                  DecTables{s_lut, s_kinfo, s_ones}, lane, ol, st8);
+                st = st8;
+                __builtin_amdgcn_s_waitcnt(0);  // the output went out as flat stores: landed before other lanes read it
+                wave_lds_sync();
+#else
                 const DecResult d = wave_decode<NC, JUMP>(in, len, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane);
                 wave_lds_sync();
                 ol = d.ok ? d.len : kFailLen;
                 st = d.ok ? soft_bits(is_name != 0, d.len, d.flags, d.len ? s_out[0] : 0u, d.len ? s_out[d.len - 1] : 0u)
                           : kStatusFail;
+#endif
             }
             const uint32_t t_coded = (uint32_t)__builtin_amdgcn_s_memrealtime();
             const uint32_t n = ol == kFailLen ? 0u : ol;

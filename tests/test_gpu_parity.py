@@ -535,6 +535,52 @@ def test_per_string_symbols(torch_cuda, oracle_codec):
         assert codec.encode_huffman(s) == oracle_codec.encode(s)
 
 
+_LAUNCH_PATH_CHECK = r"""
+import sys, numpy as np
+sys.path.insert(0, ".")
+sys.path.insert(0, "tests")
+import torch  # noqa: F401  (one HIP runtime: torch's)
+from h2o_amd import codec, synth
+from oracle import oracle as O
+from conftest import load_golden
+o = O.oracle()
+g = load_golden("kat")
+cases = [(s, bool(nm)) for s, nm in zip(synth.unpack(g["dec_in"], g["dec_in_off"]),
+         np.unpackbits(g["is_name_bits"].view(np.uint8), bitorder="little"))]
+rng = np.random.default_rng(5)
+syms, p = synth.header_alphabet()
+plain = [bytes(rng.choice(syms, int(L), p=p)) for L in rng.integers(0, 9000, 60)]
+plain += [b"a" * 3000, b"0e" * 1500, bytes(rng.integers(0, 256, 2000, dtype=np.uint8))]
+for s in plain:
+    h = o.encode(s)
+    assert codec.encode_huffman(s) == h, len(s)
+    if h is not None:
+        cases.append((h, False))
+        cases.append((h[:-1] + b"\x00", True))
+    cases.append((s[:8192], False))
+n = 0
+for s, nm in cases:
+    assert codec.decode_huffman(s, nm) == o.decode(s, nm), (len(s), nm)
+    n += 1
+print("ok", n)
+"""
+
+
+def test_per_string_launch_path(torch_cuda):
+    """the launch-per-string path (HHUFF_NO_SERVICE=1: one_string_kernel up to 8 KB, the batch kernels beyond):
+    wave encoder and split decoder against the oracle on the KAT strings, header text of 0-9000 B, periodic
+    text, random bytes and corrupted padding"""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, HHUFF_NO_SERVICE="1")
+    r = subprocess.run([sys.executable, "-c", _LAUNCH_PATH_CHECK], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout[-2000:] + r.stderr[-4000:]
+
+
 def test_host_batch_api(torch_cuda, oracle_codec):
     from h2o_amd import codec
 

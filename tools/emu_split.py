@@ -86,7 +86,8 @@ def split_decode(T, data, s, length):
         ks = lane * seg
         act = ks < TB
         pstop = TB if (act and ks + seg >= TB) else ks + seg
-        W.append(seg_walk(T, data, s, TB, max(ks - LEAD, 0), ks, pstop, False) if act else None)
+        lead = 64 if seg <= 64 else (128 if seg <= 256 else LEAD)
+        W.append(seg_walk(T, data, s, TB, max(ks - lead, 0), ks, pstop, False) if act else None)
     rewalks = 0
     for _ in range(64):
         bad = [lane for lane in range(1, 64) if W[lane] is not None and W[lane]["f"] != W[lane - 1]["e"]]
