@@ -3560,7 +3560,9 @@ __device__ __forceinline__ void sys_poll(const void* pa, uint64_t ma, const void
 }
 
 #ifndef HHUFF_SVC_SPLIT
-#define HHUFF_SVC_SPLIT 1  // 0: the candidate-chain wave decoder (A/B builds)
+// 1: the service decodes with split_decode_wave.  Measured slower for the service's short strings (48 B: 7.6 us
+// from input to coded against 3.0 us for the candidate chain, r04q_ps_*), so the chain decoder stays.
+#define HHUFF_SVC_SPLIT 0
 #endif
 template <int NC, bool JUMP = false>
 __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
@@ -3645,8 +3647,6 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
                 if (ol != kFailLen) ol = (ol + 7u) >> 3;
             } else {
 #if HHUFF_SVC_SPLIT
-                // 64 self-synchronising segments (split_decode_wave): a lane walks a 64-128-bit lead and a segment
-                // of at most 96 bits, where the candidate-chain decoder took a LUT round trip per 64 string bits
                 uint8_t st8;
                 split_decode_wave(LdsSource{s_in, len ? ((len + 3u) & ~3u) - 4u : 0u}, 0u, len, is_name != 0, s_out,
                                   DecTables{s_lut, s_kinfo, s_ones}, lane, ol, st8);

@@ -14,7 +14,7 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
                          uint64_t sel_bytes = 0);
 // One string per launch (the per-string h2o symbols): h = device-visible pinned host buffer
 // [u32 len, is_name, result len, status][input, in_cap bytes (16-aligned)][output]; len <= kOneMax
-constexpr uint32_t kOneMax = 8192;
+constexpr uint32_t kOneMax = 32768;  // LDS: 32 KB input + 52 KB output beside the 32-KB table
 hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, bool encode, hipStream_t stream);
 // Resident per-string service (hhuff_capi.hip per_string): one wave polls kSvcSlots mailboxes in pinned,
 // device-visible, coherent host memory and codes each posted string in place; it exits when `stop` is set,
