@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <algorithm>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "hhuff_device.h"
@@ -796,11 +797,132 @@ __device__ __forceinline__ SegWalk seg_walk(const Src& src, uint32_t s, uint32_t
     return r;
 }
 
+// seg_walk over global memory in rounds: a lane's next kSplitNW input dwords go into its LDS window `win`
+// (kSplitNW + 1 dwords, odd stride) with one 16-B load round trip for the wave, then every lane steps until its
+// window runs out; the window after it was prefetched into registers during the round.  seg_walk itself
+// waits for a dependent global load every 32 bits.
+// a dword-aligned 16-B load; at the end of the input, the bytes that exist
+__device__ __forceinline__ uint4 load16_bounded(const uint8_t* __restrict__ in, uint64_t in_size, uint64_t a) {
+    if (a + 16 <= in_size) {
+        typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-B load
+        const u32x4a v = *reinterpret_cast<const u32x4a*>(in + a);
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return load16_tail(in, in_size, a);
+}
+constexpr int kSplitNW = 16;
+template <bool EMIT>
+__device__ __forceinline__ SegWalk seg_walk_win(const GlobalSource& src, uint32_t s, uint32_t TB, uint32_t p0,
+                                                uint32_t kstart, uint32_t pstop, bool act, uint32_t* win,
+                                                RegSink& sink, const DecTables& T) {
+    constexpr uint32_t NW = kSplitNW;
+    SegWalk r{0xFFFFFFFFu, 0u, 0u, 0u, 0u, 0u, false, false};
+    auto take = [&](uint32_t p, uint32_t sym, uint32_t fl) {  // a symbol starting at p
+        if (p < kstart) return;
+        r.f = min(r.f, p);
+        r.first = r.cnt == 0 ? sym : r.first;
+        r.last = sym;
+        r.cnt += 1;
+        r.flags |= fl;
+        if (EMIT) sink.put1(sym);
+    };
+    const lds_u32* wl = (const lds_u32*)win;
+    uint4 pf[NW / 4];
+    uint64_t pfa = ~0ull;
+    uint32_t p = p0;
+    bool live = act;
+    for (;;) {
+        if (!__any(live)) break;
+        const uint64_t abit = 8ull * s + p;
+        const uint64_t wa = (abit >> 5) << 2;
+        if (live) {
+            if (wa != pfa) {
+#pragma unroll
+                for (int j = 0; j < (int)NW / 4; ++j) pf[j] = load16_bounded(src.in, src.in_size, wa + 16u * j);
+            }
+#pragma unroll
+            for (int j = 0; j < (int)NW / 4; ++j) {
+                win[4 * j + 0] = bswap32(pf[j].x);
+                win[4 * j + 1] = bswap32(pf[j].y);
+                win[4 * j + 2] = bswap32(pf[j].z);
+                win[4 * j + 3] = bswap32(pf[j].w);
+            }
+            // a lane leaves the round with its next bit in dword NW - 1: that window comes next
+            pfa = wa + 4u * (NW - 1);
+#pragma unroll
+            for (int j = 0; j < (int)NW / 4; ++j) pf[j] = load16_bounded(src.in, src.in_size, pfa + 16u * j);
+        }
+        uint32_t q = (uint32_t)(abit & 31u);
+        while (live) {
+            if (p >= pstop) {  // (pstop >= TB: p == TB, no bits left, the padding rule holds)
+                live = false;
+                r.end_ok = !r.eos;
+                break;
+            }
+            if (q >= 32u * (NW - 1)) break;  // the window runs out: next round
+            const uint32_t jq = q >> 5;
+            const uint32_t w = (uint32_t)((((uint64_t)wl[jq] << 32) | wl[jq + 1]) << (q & 31u) >> 32);
+            const uint32_t R = TB - p;
+            const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+            uint32_t cons;
+            bool stop = false;
+            if (e & kLong) {
+                const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                const uint32_t ki = T.kinfo[k];
+                const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                const uint32_t L = (le >> 9) & 31u;
+                const uint32_t sym = le & 0x1FFu;
+                stop = L > R;  // the string's end: padding
+                if (!stop && sym == kEos && p >= kstart) {  // EOS inside the string (hpack.c:88-89)
+                    r.eos = true;
+                    stop = true;
+                }
+                if (!stop && sym != kEos) take(p, sym, (le >> 14) & 3u);
+                cons = L;
+            } else {
+                const uint32_t L1 = lut_l1(e);
+                stop = L1 > R;  // fewer bits left than the next code: padding
+                const uint32_t L12 = lut_l12(e);
+                if (!stop) take(p, e & 0xFFu, (e >> 24) & 3u);
+                // the second symbol only when it starts before the stop and fits the string
+                const bool two = (e & kHas2) && L12 <= R && p + L1 < pstop;
+                if (!stop && two) take(p + L1, lut_sym2(e) & 0xFFu, (e >> 26) & 3u);
+                cons = two ? L12 : L1;
+            }
+            if (stop) {  // at most 7 bits of padding, all ones (mkhufftbl.py:374-381)
+                live = false;
+                r.end_ok = !r.eos && R <= 7u && ((w >> 24) | (0xFFu >> R)) == 0xFFu;
+                break;
+            }
+            p += cons;
+            q += cons;
+        }
+    }
+    r.e = p;
+    if (r.f == 0xFFFFFFFFu) r.f = p;  // no symbol starts in the segment
+    if (pstop < TB) r.end_ok = false;
+    return r;
+}
+
 // One wave decodes the string at src bytes [s, s + len) into dst (any alignment, global or LDS); every lane
 // returns the output length (kFailLen on failure) and the status byte.
 template <class Src>
 __device__ __forceinline__ void split_decode_wave(const Src& src, uint32_t s, uint32_t len, bool is_name, uint8_t* dst,
-                                                  const DecTables& T, uint32_t lane, uint32_t& ol, uint8_t& st) {
+                                                  const DecTables& T, uint32_t lane, uint32_t& ol, uint8_t& st,
+                                                  uint32_t* win = nullptr) {
+    // global strings walk in LDS windows (win: this lane's kSplitNW + 1 dwords), LDS strings directly
+    auto walk = [&](auto emit, uint32_t p0, uint32_t kstart, uint32_t pstop, bool act, RegSink& sink) {
+        constexpr bool E = decltype(emit)::value;
+        if constexpr (__is_same(Src, GlobalSource)) {
+            return seg_walk_win<E>(src, s, 8u * len, p0, kstart, pstop, act, win, sink, T);
+        } else {
+            SegWalk r{};
+            if (act) r = seg_walk<E>(src, s, 8u * len, p0, kstart, pstop, sink, T);
+            return r;
+        }
+    };
+    using NoEmit = std::integral_constant<bool, false>;
+    using Emit = std::integral_constant<bool, true>;
     const uint32_t TB = 8u * len;
     if (TB == 0) {  // an empty string decodes to nothing (hpack.c:117-156 with no bits)
         ol = 0;
@@ -818,14 +940,14 @@ __device__ __forceinline__ void split_decode_wave(const Src& src, uint32_t s, ui
     const uint32_t pstop = lastl ? TB : ks + seg;
     RegSink none;
     none.init(nullptr);
-    SegWalk w{};
-    if (act) w = seg_walk<false>(src, s, TB, ks > lead ? ks - lead : 0u, ks, pstop, none, T);
+    SegWalk w = walk(NoEmit{}, ks > lead ? ks - lead : 0u, ks, pstop, act, none);
     // agree with the lane before: lane k starts where lane k - 1 stopped
     for (int it = 0; it < 64; ++it) {
         const uint32_t pe = (uint32_t)__shfl_up((int)w.e, 1, 64);
         const bool bad = act && lane > 0 && w.f != pe;
         if (__builtin_amdgcn_ballot_w64(bad) == 0) break;
-        if (bad) w = seg_walk<false>(src, s, TB, pe, pe, pstop, none, T);
+        const SegWalk w2 = walk(NoEmit{}, pe, pe, pstop, bad, none);
+        if (bad) w = w2;
     }
     const uint32_t cnt = act ? w.cnt : 0u;
     const uint32_t place = wave_excl_scan(cnt, (int)lane);
@@ -847,11 +969,12 @@ __device__ __forceinline__ void split_decode_wave(const Src& src, uint32_t s, ui
         first = (uint32_t)__shfl((int)w.first, (int)__builtin_ctzll(has), 64);
         last = (uint32_t)__shfl((int)w.last, 63 - (int)__builtin_clzll(has), 64);
     }
-    if (ok && act && cnt) {
+    {
+        const bool em = ok && act && cnt != 0;
         RegSink sink;
         sink.init(dst + place);
-        (void)seg_walk<true>(src, s, TB, w.f, w.f, pstop, sink, T);
-        sink.finish();
+        (void)walk(Emit{}, w.f, w.f, pstop, em, sink);
+        if (em) sink.finish();
     }
     ol = ok ? total : kFailLen;
     st = ok ? soft_bits(is_name, total, fl & 3u, first, last) : kStatusFail;
@@ -862,6 +985,7 @@ __global__ __launch_bounds__(WAVES * 64) void split_decode_kernel(DecArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
     __shared__ uint32_t s_kinfo[32];
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
+    __shared__ uint32_t s_win[WAVES * 64][kSplitNW + 1];
     if (blockIdx.x * WAVES >= min(*A.split_n, A.split_cap)) return;  // (block-uniform) nothing listed for it
     load_dec_tables(s_lut, s_kinfo, s_ones, WAVES * 64);
     __syncthreads();
@@ -877,7 +1001,7 @@ __global__ __launch_bounds__(WAVES * 64) void split_decode_kernel(DecArgs A) {
         const uint64_t d = A.out_off ? (uint64_t)A.out_off[i] : dec_slot(s);
         uint32_t ol;
         uint8_t st;
-        split_decode_wave(src, s, len, is_name, A.out + d, T, lane, ol, st);
+        split_decode_wave(src, s, len, is_name, A.out + d, T, lane, ol, st, s_win[threadIdx.x]);
         if (lane == 0) {
             A.out_len[i] = ol;
             A.status[i] = st;
@@ -903,14 +1027,6 @@ __global__ __launch_bounds__(WAVES * 64) void split_decode_kernel(DecArgs A) {
 // Lanes share nothing but the tables: no barriers, and a lane never waits for another lane's string.
 // Same results as decode_core (hpack.c:117-156) for every layout (implicit slots, pairs, explicit dst).
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint4 load16_bounded(const uint8_t* __restrict__ in, uint64_t in_size, uint64_t a) {
-    if (a + 16 <= in_size) {
-        typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-B load
-        const u32x4a v = *reinterpret_cast<const u32x4a*>(in + a);
-        return make_uint4(v.x, v.y, v.z, v.w);
-    }
-    return load16_tail(in, in_size, a);
-}
 
 // bytes [lo, hi) of the 16-B LDS chunk `c` to global `g` (16-B aligned): whole dwords as dword stores, the
 // partial dword at each end (at most 3 bytes each) as byte stores -- a fixed set of at most 10 predicated
