@@ -724,83 +724,7 @@ struct SegWalk {
     bool eos, end_ok;     // an EOS among the counted symbols; (last segment) the padding rule held
 };
 
-// Decode the string's bits from p0; count (and with EMIT write) the symbols starting in [kstart, pstop);
-// stop at the first boundary >= pstop, or at the string's end when pstop >= TB.
-template <bool EMIT, class Src>
-__device__ __forceinline__ SegWalk seg_walk(const Src& src, uint32_t s, uint32_t TB, uint32_t p0,
-                                            uint32_t kstart, uint32_t pstop, RegSink& sink, const DecTables& T) {
-    SegWalk r{0xFFFFFFFFu, 0u, 0u, 0u, 0u, 0u, false, false};
-    // bit reader at absolute bit 8 s + p0 (MSB-first dwords)
-    const uint64_t abs = 8ull * s + p0;
-    uint32_t a = (uint32_t)((abs >> 5) << 2);
-    const uint32_t skip = (uint32_t)(abs & 31u);
-    uint64_t buf = ((uint64_t)bswap32(src.word(a)) << 32 | bswap32(src.word(a + 4u))) << skip;
-    uint32_t nb = 64u - skip;
-    a += 8u;
-    auto consume = [&](uint32_t n) {
-        buf <<= n;
-        nb -= n;
-        if (nb <= 32u) {
-            buf |= (uint64_t)bswap32(src.word(a)) << (32u - nb);
-            nb += 32u;
-            a += 4u;
-        }
-    };
-    auto take = [&](uint32_t p, uint32_t sym, uint32_t fl) {  // a symbol starting at p
-        if (p < kstart) return;
-        r.f = min(r.f, p);
-        r.first = r.cnt == 0 ? sym : r.first;
-        r.last = sym;
-        r.cnt += 1;
-        r.flags |= fl;
-        if (EMIT) sink.put1(sym);
-    };
-    uint32_t p = p0;
-    for (;;) {
-        if (p >= pstop) break;
-        const uint32_t R = TB - p;
-        const uint32_t w = (uint32_t)(buf >> 32);
-        const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
-        if (e & kLong) {
-            const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
-            const uint32_t ki = T.kinfo[k];
-            const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
-            const uint32_t L = (le >> 9) & 31u;
-            if (L > R) break;  // the string's end: padding
-            const uint32_t sym = le & 0x1FFu;
-            if (sym == kEos && p >= kstart) {  // EOS inside the string (hpack.c:88-89)
-                r.eos = true;
-                break;
-            }
-            if (sym != kEos) take(p, sym, (le >> 14) & 3u);
-            p += L;
-            consume(L);
-        } else {
-            const uint32_t L1 = lut_l1(e);
-            if (L1 > R) break;  // fewer bits left than the next code: padding
-            const uint32_t L12 = lut_l12(e);
-            take(p, e & 0xFFu, (e >> 24) & 3u);
-            // the second symbol only when it starts before the stop and fits the string
-            const bool two = (e & kHas2) && L12 <= R && p + L1 < pstop;
-            if (two) take(p + L1, lut_sym2(e) & 0xFFu, (e >> 26) & 3u);
-            const uint32_t cons = two ? L12 : L1;
-            p += cons;
-            consume(cons);
-        }
-    }
-    r.e = p;
-    if (r.f == 0xFFFFFFFFu) r.f = p;  // no symbol starts in the segment
-    if (pstop >= TB) {  // the string's end: at most 7 bits of padding, all ones (mkhufftbl.py:374-381)
-        const uint32_t R = TB - p;
-        r.end_ok = !r.eos && R <= 7u && (((uint32_t)(buf >> 56)) | (0xFFu >> R)) == 0xFFu;
-    }
-    return r;
-}
-
-// seg_walk over global memory in rounds: a lane's next kSplitNW input dwords go into its LDS window `win`
-// (kSplitNW + 1 dwords, odd stride) with one 16-B load round trip for the wave, then every lane steps until its
-// window runs out; the window after it was prefetched into registers during the round.  seg_walk itself
-// waits for a dependent global load every 32 bits.
+constexpr int kSplitNW = 16;  // window dwords per lane (split_decode_kernel, one_string_kernel)
 // a dword-aligned 16-B load; at the end of the input, the bytes that exist
 __device__ __forceinline__ uint4 load16_bounded(const uint8_t* __restrict__ in, uint64_t in_size, uint64_t a) {
     if (a + 16 <= in_size) {
@@ -810,14 +734,30 @@ __device__ __forceinline__ uint4 load16_bounded(const uint8_t* __restrict__ in, 
     }
     return load16_tail(in, in_size, a);
 }
-constexpr int kSplitNW = 16;
-template <bool EMIT>
-__device__ __forceinline__ SegWalk seg_walk_win(const GlobalSource& src, uint32_t s, uint32_t TB, uint32_t p0,
-                                                uint32_t kstart, uint32_t pstop, bool act, uint32_t* win,
-                                                RegSink& sink, const DecTables& T) {
+// A dword-aligned 16-B window piece of a split string: from global memory (bounded at the input's end) or from
+// a string staged in LDS (one_string_kernel; reads clamped to its last dword).
+__device__ __forceinline__ uint4 split_piece(const GlobalSource& src, uint64_t a) {
+    return load16_bounded(src.in, src.in_size, a);
+}
+__device__ __forceinline__ uint4 split_piece(const LdsSource& src, uint64_t a) {
+    const uint32_t b = (uint32_t)a;
+    return make_uint4(src.word(b), src.word(b + 4u), src.word(b + 8u), src.word(b + 12u));
+}
+
+// Decode the string's bits (string at byte s, TB bits) from p0; count (and with EMIT write) the symbols that
+// start in [kstart, pstop); stop at the first boundary >= pstop, or at the string's end when pstop >= TB.
+// A lane's next kSplitNW input dwords go into its LDS window `win` (kSplitNW + 1 dwords, odd stride) in
+// rounds -- one 16-B load round trip for the wave per window, the next window prefetched into registers
+// during the round -- and the lane steps until its window runs out.  Away from kstart and pstop a step is
+// decode_staged_lane_v7's bulk step (two LUT lookups, 1-4 symbols, no per-symbol checks); within 26 bits of
+// either, and for codes longer than the window LUT, it is the checked single-lookup step.
+template <bool EMIT, class Src>
+__device__ __forceinline__ SegWalk seg_walk(const Src& src, uint32_t s, uint32_t TB, uint32_t p0, uint32_t kstart,
+                                            uint32_t pstop, bool act, uint32_t* win, RegSink& sink,
+                                            const DecTables& T) {
     constexpr uint32_t NW = kSplitNW;
     SegWalk r{0xFFFFFFFFu, 0u, 0u, 0u, 0u, 0u, false, false};
-    auto take = [&](uint32_t p, uint32_t sym, uint32_t fl) {  // a symbol starting at p
+    auto take = [&](uint32_t p, uint32_t sym, uint32_t fl) {  // one symbol starting at p
         if (p < kstart) return;
         r.f = min(r.f, p);
         r.first = r.cnt == 0 ? sym : r.first;
@@ -838,7 +778,7 @@ __device__ __forceinline__ SegWalk seg_walk_win(const GlobalSource& src, uint32_
         if (live) {
             if (wa != pfa) {
 #pragma unroll
-                for (int j = 0; j < (int)NW / 4; ++j) pf[j] = load16_bounded(src.in, src.in_size, wa + 16u * j);
+                for (int j = 0; j < (int)NW / 4; ++j) pf[j] = split_piece(src, wa + 16u * j);
             }
 #pragma unroll
             for (int j = 0; j < (int)NW / 4; ++j) {
@@ -850,7 +790,7 @@ __device__ __forceinline__ SegWalk seg_walk_win(const GlobalSource& src, uint32_
             // a lane leaves the round with its next bit in dword NW - 1: that window comes next
             pfa = wa + 4u * (NW - 1);
 #pragma unroll
-            for (int j = 0; j < (int)NW / 4; ++j) pf[j] = load16_bounded(src.in, src.in_size, pfa + 16u * j);
+            for (int j = 0; j < (int)NW / 4; ++j) pf[j] = split_piece(src, pfa + 16u * j);
         }
         uint32_t q = (uint32_t)(abit & 31u);
         while (live) {
@@ -862,8 +802,34 @@ __device__ __forceinline__ SegWalk seg_walk_win(const GlobalSource& src, uint32_
             if (q >= 32u * (NW - 1)) break;  // the window runs out: next round
             const uint32_t jq = q >> 5;
             const uint32_t w = (uint32_t)((((uint64_t)wl[jq] << 32) | wl[jq + 1]) << (q & 31u) >> 32);
-            const uint32_t R = TB - p;
             const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+            // bulk: every symbol of both lookups starts before pstop (hence inside the string) and either all
+            // of them are counted (p >= kstart) or none is (p + 26 < kstart)
+            const bool counted = p >= kstart;
+            if ((counted ? p + 26u < pstop : p + 26u < kstart) && !(e & kLong)) {
+                uint32_t cons = lut_l12(e);
+                const uint32_t eb = T.lut[(w << cons) >> (32 - HHUFF_LUT_BITS)];
+                const bool useb = !(eb & kLong);
+                cons += useb ? lut_l12(eb) : 0u;
+                if (counted) {
+                    const uint32_t ne = (e >> 28) & 3u, nb = useb ? (eb >> 28) & 3u : 0u;
+                    r.f = min(r.f, p);
+                    r.first = r.cnt == 0 ? (e & 0xFFu) : r.first;
+                    const uint32_t lb = nb == 2u ? lut_sym2(eb) : eb;
+                    const uint32_t le = ne == 2u ? lut_sym2(e) : e;
+                    r.last = (nb ? lb : le) & 0xFFu;
+                    r.cnt += ne + nb;
+                    r.flags |= ((e >> 24) | (e >> 26) | (useb ? (eb >> 24) | (eb >> 26) : 0u)) & 3u;
+                    if (EMIT) {
+                        sink.put12(lut_pair(e), ne == 2u);
+                        if (nb) sink.put12(lut_pair(eb), nb == 2u);
+                    }
+                }
+                p += cons;
+                q += cons;
+                continue;
+            }
+            const uint32_t R = TB - p;
             uint32_t cons;
             bool stop = false;
             if (e & kLong) {
@@ -909,17 +875,10 @@ __device__ __forceinline__ SegWalk seg_walk_win(const GlobalSource& src, uint32_
 template <class Src>
 __device__ __forceinline__ void split_decode_wave(const Src& src, uint32_t s, uint32_t len, bool is_name, uint8_t* dst,
                                                   const DecTables& T, uint32_t lane, uint32_t& ol, uint8_t& st,
-                                                  uint32_t* win = nullptr) {
-    // global strings walk in LDS windows (win: this lane's kSplitNW + 1 dwords), LDS strings directly
+                                                  uint32_t* win) {
+    // every lane walks its string bits through its LDS window (win: kSplitNW + 1 dwords)
     auto walk = [&](auto emit, uint32_t p0, uint32_t kstart, uint32_t pstop, bool act, RegSink& sink) {
-        constexpr bool E = decltype(emit)::value;
-        if constexpr (__is_same(Src, GlobalSource)) {
-            return seg_walk_win<E>(src, s, 8u * len, p0, kstart, pstop, act, win, sink, T);
-        } else {
-            SegWalk r{};
-            if (act) r = seg_walk<E>(src, s, 8u * len, p0, kstart, pstop, sink, T);
-            return r;
-        }
+        return seg_walk<decltype(emit)::value>(src, s, 8u * len, p0, kstart, pstop, act, win, sink, T);
     };
     using NoEmit = std::integral_constant<bool, false>;
     using Emit = std::integral_constant<bool, true>;
@@ -3577,6 +3536,7 @@ __global__ __launch_bounds__(256) void one_string_kernel(uint8_t* __restrict__ h
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
     __shared__ __attribute__((aligned(16))) uint32_t s_in[kOneMax / 4 + 4];
     __shared__ __attribute__((aligned(16))) uint8_t s_out[(kOneMax * 8) / 5 + 64];
+    __shared__ uint32_t s_win[64][kSplitNW + 1];     // decode: wave 0's split windows
     uint2* s_enc = reinterpret_cast<uint2*>(s_lut);  // encode: the table takes the LUT's place
     if (encode) {
         for (uint32_t k = threadIdx.x; k < 256; k += 256) s_enc[k] = make_uint2(g_enc_code[k], g_enc_nbits[k]);
@@ -3598,7 +3558,8 @@ __global__ __launch_bounds__(256) void one_string_kernel(uint8_t* __restrict__ h
         } else {
             const LdsSource src{s_in, len ? ((len + 3u) & ~3u) - 4u : 0u};
             uint8_t st8;
-            split_decode_wave(src, 0u, len, is_name != 0, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane, ol, st8);
+            split_decode_wave(src, 0u, len, is_name != 0, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane, ol, st8,
+                              s_win[lane]);
             st = st8;
         }
         if (lane == 0) {
@@ -3675,11 +3636,8 @@ __device__ __forceinline__ void sys_poll(const void* pa, uint64_t ma, const void
     rb = make_uint4(b.x, b.y, b.z, b.w);
 }
 
-#ifndef HHUFF_SVC_SPLIT
-// 1: the service decodes with split_decode_wave.  Measured slower for the service's short strings (48 B: 7.6 us
-// from input to coded against 3.0 us for the candidate chain, r04q_ps_*), so the chain decoder stays.
-#define HHUFF_SVC_SPLIT 0
-#endif
+// (The service's strings measured faster on the candidate chain than on split_decode_wave: 48 B, 3.0 against
+// 7.6 us from input to coded, profiles/r04pq_per_string_ab.jsonl.)
 template <int NC, bool JUMP = false>
 __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
                                                      uint64_t idle_ticks, uint64_t max_ticks) {
@@ -3762,20 +3720,11 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
                 st = ol == kFailLen ? kStatusFail : 0u;
                 if (ol != kFailLen) ol = (ol + 7u) >> 3;
             } else {
-#if HHUFF_SVC_SPLIT
-                uint8_t st8;
-                split_decode_wave(LdsSource{s_in, len ? ((len + 3u) & ~3u) - 4u : 0u}, 0u, len, is_name != 0, s_out,
-                                  DecTables{s_lut, s_kinfo, s_ones}, lane, ol, st8);
-                st = st8;
-                __builtin_amdgcn_s_waitcnt(0);  // the output went out as flat stores: landed before other lanes read it
-                wave_lds_sync();
-#else
                 const DecResult d = wave_decode<NC, JUMP>(in, len, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane);
                 wave_lds_sync();
                 ol = d.ok ? d.len : kFailLen;
                 st = d.ok ? soft_bits(is_name != 0, d.len, d.flags, d.len ? s_out[0] : 0u, d.len ? s_out[d.len - 1] : 0u)
                           : kStatusFail;
-#endif
             }
             const uint32_t t_coded = (uint32_t)__builtin_amdgcn_s_memrealtime();
             const uint32_t n = ol == kFailLen ? 0u : ol;
