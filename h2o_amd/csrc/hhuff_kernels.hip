@@ -792,43 +792,55 @@ __device__ __forceinline__ SegWalk seg_walk(const Src& src, uint32_t s, uint32_t
 #pragma unroll
             for (int j = 0; j < (int)NW / 4; ++j) pf[j] = split_piece(src, pfa + 16u * j);
         }
-        uint32_t q = (uint32_t)(abit & 31u);
+        uint32_t q = (uint32_t)(abit & 31u);  // bit of the window; x0..x2 hold dwords qd..qd + 2
+        uint32_t qd = 0, x0 = wl[0], x1 = wl[1], x2 = wl[2];
+        auto advance = [&](uint32_t cons) {  // cons <= 30: at most one dword boundary crossed
+            q += cons;
+            p += cons;
+            const bool adv = (q >> 5) != qd;
+            x0 = adv ? x1 : x0;
+            x1 = adv ? x2 : x1;
+            qd = q >> 5;
+            x2 = wl[qd + 2];  // (qd <= NW - 2 while the lane steps: inside the NW + 1 dwords)
+        };
         while (live) {
             if (p >= pstop) {  // (pstop >= TB: p == TB, no bits left, the padding rule holds)
                 live = false;
                 r.end_ok = !r.eos;
                 break;
             }
-            if (q >= 32u * (NW - 1)) break;  // the window runs out: next round
-            const uint32_t jq = q >> 5;
-            const uint32_t w = (uint32_t)((((uint64_t)wl[jq] << 32) | wl[jq + 1]) << (q & 31u) >> 32);
-            const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
-            // bulk: every symbol of both lookups starts before pstop (hence inside the string) and either all
-            // of them are counted (p >= kstart) or none is (p + 26 < kstart)
-            const bool counted = p >= kstart;
-            if ((counted ? p + 26u < pstop : p + 26u < kstart) && !(e & kLong)) {
+            // bulk run: every symbol of a step's two lookups starts before pstop (hence inside the string),
+            // and either all of them are counted (p >= kstart) or none is (p + 26 < kstart)
+            for (;;) {
+                const uint32_t cm = p >= kstart ? 0xFFFFFFFFu : 0u;
+                const uint32_t lim = cm ? pstop : kstart;
+                if (p + 26u >= lim || q >= 32u * (NW - 1)) break;
+                const uint32_t wz = (q & 31u) ? __builtin_amdgcn_alignbit(x0, x1, 32u - (q & 31u)) : x0;
+                const uint32_t e = T.lut[wz >> (32 - HHUFF_LUT_BITS)];
+                if (e & kLong) break;
                 uint32_t cons = lut_l12(e);
-                const uint32_t eb = T.lut[(w << cons) >> (32 - HHUFF_LUT_BITS)];
-                const bool useb = !(eb & kLong);
-                cons += useb ? lut_l12(eb) : 0u;
-                if (counted) {
-                    const uint32_t ne = (e >> 28) & 3u, nb = useb ? (eb >> 28) & 3u : 0u;
-                    r.f = min(r.f, p);
-                    r.first = r.cnt == 0 ? (e & 0xFFu) : r.first;
-                    const uint32_t lb = nb == 2u ? lut_sym2(eb) : eb;
-                    const uint32_t le = ne == 2u ? lut_sym2(e) : e;
-                    r.last = (nb ? lb : le) & 0xFFu;
-                    r.cnt += ne + nb;
-                    r.flags |= ((e >> 24) | (e >> 26) | (useb ? (eb >> 24) | (eb >> 26) : 0u)) & 3u;
-                    if (EMIT) {
-                        sink.put12(lut_pair(e), ne == 2u);
-                        if (nb) sink.put12(lut_pair(eb), nb == 2u);
-                    }
+                const uint32_t eb = T.lut[(wz << cons) >> (32 - HHUFF_LUT_BITS)];
+                const uint32_t bm = (eb & kLong) ? 0u : 0xFFFFFFFFu;
+                cons += lut_l12(eb) & bm;
+                const uint32_t ne = (e >> 28) & 3u, nb = (eb >> 28) & 3u & bm;
+                const uint32_t lb = nb == 2u ? lut_sym2(eb) : eb;
+                const uint32_t le = ne == 2u ? lut_sym2(e) : e;
+                r.f = min(r.f, p | ~cm);
+                r.first = (cm && r.cnt == 0) ? (e & 0xFFu) : r.first;
+                r.last = cm ? (nb ? lb : le) & 0xFFu : r.last;
+                r.cnt += (ne + nb) & cm;
+                r.flags |= ((e >> 24) | (e >> 26) | (((eb >> 24) | (eb >> 26)) & bm)) & 3u & cm;
+                if (EMIT) {  // pass B starts at kstart: every bulk step is counted
+                    sink.put12(lut_pair(e), ne == 2u);
+                    if (nb) sink.put12(lut_pair(eb), nb == 2u);
                 }
-                p += cons;
-                q += cons;
-                continue;
+                advance(cons);
             }
+            if (p >= pstop) continue;
+            if (q >= 32u * (NW - 1)) break;  // the window runs out: next round
+            // one checked step
+            const uint32_t w = (q & 31u) ? __builtin_amdgcn_alignbit(x0, x1, 32u - (q & 31u)) : x0;
+            const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
             const uint32_t R = TB - p;
             uint32_t cons;
             bool stop = false;
@@ -860,8 +872,7 @@ __device__ __forceinline__ SegWalk seg_walk(const Src& src, uint32_t s, uint32_t
                 r.end_ok = !r.eos && R <= 7u && ((w >> 24) | (0xFFu >> R)) == 0xFFu;
                 break;
             }
-            p += cons;
-            q += cons;
+            advance(cons);
         }
     }
     r.e = p;
