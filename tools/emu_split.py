@@ -80,6 +80,8 @@ def seg_walk(T, data, s, TB, p0, kstart, pstop, emit):
 def split_decode(T, data, s, length):
     """-> (decoded bytes or None, rewalks)"""
     TB = 8 * length
+    if TB == 0:  # an empty string decodes to nothing
+        return b"", 0
     seg = ((TB + 64 * 32 - 1) // (64 * 32)) * 32
     W = []
     for lane in range(64):
