@@ -1937,6 +1937,12 @@ __device__ __forceinline__ SortChunk sort_chunk_issue(const EncArgs& A, uint64_t
     return SortChunk{A.in_off[ic], A.in_off[ic + 1], A.in_off[min(cb, (uint64_t)A.n - 1u)],
                      A.in_off[min(cb + ns, (uint64_t)A.n)]};
 }
+#ifndef HHUFF_ENC_EARLY
+// 1: the next chunk's offsets are loaded a chunk ahead and both they and the next span are waited for after
+// barrier 3, before the chunk's stores (c4 encode 0.680 -> 0.655 ms, profiles/r04aa_encode_early_ab.log);
+// 0: the round-3 order, where the compiler's vmcnt waits for those loads also waited for the stores
+#define HHUFF_ENC_EARLY 1
+#endif
 // NS strings per chunk, one thread each (NS / 64 waves); CH bytes of stage
 template <int NS, int CH>
 __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
@@ -1996,6 +2002,12 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
     SortChunk cur = sort_chunk_issue(A, c * kSortStr, t, NS);
     issue_span(pv, cur);
     prepare(cur, c * kSortStr, 0u);
+#if HHUFF_ENC_EARLY
+    // the next chunk's offsets are loaded a chunk ahead (after barrier 2) and waited for after barrier 3,
+    // before the chunk's stores: no load is then waited for behind a data-dependent number of stores
+    SortChunk nxt = sort_chunk_issue(A, (c + gridDim.x < nch ? c + gridDim.x : c) * kSortStr, t, NS);
+    __asm__ volatile("" : "+v"(nxt.s), "+v"(nxt.e), "+v"(nxt.lo), "+v"(nxt.hi) : : "memory");  // (once)
+#endif
     PROF_DECL  // profile builds: barrier 1 / ranks + barrier 2 / encode / barrier 3 + lengths / copy out / prepare
     for (;;) {
         const uint64_t cb = c * kSortStr, i = cb + t;
@@ -2005,7 +2017,11 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         EdgeRec* rec = A.edges + 2 * c;  // two records a chunk (sorted_edge_recs)
         const uint64_t cn = c + gridDim.x;
         const bool more = cn < nch;
+#if !HHUFF_ENC_EARLY
         SortChunk nxt = sort_chunk_issue(A, (more ? cn : c) * kSortStr, t, NS);  // in flight during this chunk
+#endif
+        const uint64_t cn2 = cn + gridDim.x;  // (HHUFF_ENC_EARLY) the chunk after next
+        (void)cn2;
         __syncthreads();  // the chunk's stage, strings and ranks are in
         PROF_MARK(0);
         if (span > (uint32_t)CH) {  // (workgroup-uniform) a chunk larger than the stage: one thread per string
@@ -2020,7 +2036,16 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
             if (!more) break;
             issue_span(pv, nxt);
             prepare(nxt, cn * kSortStr, 0u);
+#if HHUFF_ENC_EARLY
+            {
+                SortChunk nn = sort_chunk_issue(A, (cn2 < nch ? cn2 : cn) * kSortStr, t, NS);
+                __asm__ volatile("" : "+v"(nn.s), "+v"(nn.e), "+v"(nn.lo), "+v"(nn.hi) : : "memory");
+                cur = nxt;
+                nxt = nn;
+            }
+#else
             cur = nxt;
+#endif
             c = cn;
             continue;
         }
@@ -2034,6 +2059,9 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         PROF_MARK(1);
         if (t < kSortBins) s_bin[t] = 0u;  // read by every wave above: cleared for the next chunk
         if (more) issue_span(pv, nxt);     // the next chunk's span: in flight during the encode
+#if HHUFF_ENC_EARLY
+        SortChunk nn = sort_chunk_issue(A, (cn2 < nch ? cn2 : (more ? cn : c)) * kSortStr, t, NS);
+#endif
         // sorted position t = 64 wave + lane: wave w encodes the w-th length group
         const uint32_t j = s_perm[t];
         const uint2 sj = s_str[j];
@@ -2046,7 +2074,19 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         s_str[j].x = act && tb != kFailLen ? (tb + 7) >> 3 : kFailLen;
         PROF_MARK(2);
         __syncthreads();
+#if HHUFF_ENC_EARLY
+        // the next chunk goes in now, before this chunk's stores: its span loads (in flight since the encode
+        // began) are then waited for with no store ahead of them in the memory counter
+        const uint32_t olen = s_str[t].x;  // (prepare overwrites this thread's record)
+        if (more) prepare(nxt, cn * kSortStr, span);
+        // the chunk after next's offsets are waited for here too, on every path: `nxt = nn` below then copies
+        // registers with no load pending, not behind this chunk's stores
+        __asm__ volatile("" : "+v"(nn.s), "+v"(nn.e), "+v"(nn.lo), "+v"(nn.hi) : : "memory");
+        PROF_MARK(5);
+        if (valid) finish_encode(A, (uint32_t)i, len, olen);
+#else
         if (valid) finish_encode(A, (uint32_t)i, len, s_str[t].x);
+#endif
         PROF_MARK(3);
         // the stage's MSB-first words, byte-swapped on the way out (each read chunk is zeroed for the next
         // chunk); the chunk's first and last 16-B chunks are deferred (edge_fix_kernel)
@@ -2074,11 +2114,16 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
             PROF_FLUSH(1);
             break;
         }
+#if !HHUFF_ENC_EARLY
         // the stages are free (the input since the encode, the output but for this thread's chunks above):
         // the next chunk goes in before this chunk's stores have landed
         prepare(nxt, cn * kSortStr, span);
         PROF_MARK(5);
+#endif
         cur = nxt;
+#if HHUFF_ENC_EARLY
+        nxt = nn;
+#endif
         c = cn;
     }
 }
