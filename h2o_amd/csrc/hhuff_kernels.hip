@@ -2189,6 +2189,11 @@ __device__ __forceinline__ void pl_clear_spare_edges(EdgeRec* edges, uint64_t nt
         edges[r].m = make_uint4(0u, 0u, 0u, 0u);
 }
 
+#ifndef HHUFF_PL_EARLY
+// 1: the next span committed and the next offsets waited for before the tile's stores (with the clamped,
+// unconditional offset loads: c5 encode 0.331 -> 0.320 ms, c3 0.226 -> 0.222, profiles/r04ac_pl_ab.log)
+#define HHUFF_PL_EARLY 1
+#endif
 template <int WAVES, int STAGE>
 __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32_t K, const uint32_t* __restrict__ kplan,
                                                                uint64_t rec_cap) {
@@ -2225,13 +2230,12 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
         uint32_t kt, s, e, lo, hi, a0, span;
         bool fits;
     };
+    // every lane loads (index clamped; lanes past the tile's strings are never read): a load under a condition
+    // with a zero default compiled to a register copy of the pending load, i.e. a wait right behind it
     auto issue = [&](uint64_t tt, uint32_t& s0, uint32_t& e0) {
-        const uint64_t i = tt * K + lane;
-        s0 = e0 = 0;
-        if ((uint32_t)lane < K && i < A.n) {
-            s0 = A.in_off[i];
-            e0 = A.in_off[i + 1];
-        }
+        const uint64_t i = min(tt * K + min((uint32_t)lane, K - 1u), (uint64_t)A.n - 1u);
+        s0 = A.in_off[i];
+        e0 = A.in_off[i + 1];
     };
     auto plan = [&](uint64_t tt, uint32_t s0, uint32_t e0) {
         Plan P;
@@ -2252,8 +2256,11 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
     issue(t, ns, ne);
     Plan cur = plan(t, ns, ne);
     if (cur.fits) pf.issue(A.in, A.in_size, cur.a0, cur.span, lane);
-    if (t + tstride < ntiles) issue(t + tstride, ns, ne);
+    issue(min(t + tstride, ntiles - 1u), ns, ne);  // (unconditional: see issue)
     if (cur.fits) pf.commit(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+#if HHUFF_PL_EARLY
+    __asm__ volatile("" : "+v"(ns), "+v"(ne) : : "memory");  // (once: no load pending at the loop head)
+#endif
     for (;;) {
         const uint64_t tn = t + tstride;
         const bool have_next = tn < ntiles;
@@ -2261,8 +2268,8 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
         if (have_next) {
             nxt = plan(tn, ns, ne);
             if (nxt.fits) pf.issue(A.in, A.in_size, nxt.a0, nxt.span, lane);
-            if (tn + tstride < ntiles) issue(tn + tstride, ns, ne);
         }
+        issue(min(tn + tstride, ntiles - 1u), ns, ne);  // (unconditional: see issue)
         // ---- the current tile ----
         const bool own = (uint32_t)lane < cur.kt;
         const uint32_t len = own ? cur.e - cur.s : 0u;
@@ -2321,11 +2328,30 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
             }
             ol = (uint32_t)__shfl((int)res, (int)L, 64);
             wave_lds_sync();
+#if HHUFF_PL_EARLY
+            // the stage is free (pass 2 is done): the next span goes in now, and the offsets of the tile after
+            // next are waited for here, before this tile's stores -- a load waited for behind a data-dependent
+            // number of stores waits for the stores too (vmcnt counts both, in order)
+            if (have_next && nxt.fits) pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+            __asm__ volatile("" : "+v"(ns), "+v"(ne) : : "memory");
+#endif
             // byte-swapped on the way out; the (at most two) 16-B chunks shared with the neighbouring tiles
             // are deferred to edge_fix_kernel
             region_copy_deferred<true>(A.out, cur.a0, obuf, cur.span, cur.lo, cur.hi, lane, A.edges + 2 * t);
+#if HHUFF_PL_EARLY
+            // (the prefetch registers stay allocated across the copy: were they reused as its store data, the
+            // next tile's loads into them would wait for those stores -- gfx950 orders no store-data reads)
+#pragma unroll
+            for (int k = 0; k < (STAGE + 1023) / 1024; ++k) {
+                const uint4 q = pf.v[k];
+                __asm__ volatile("" : : "v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w));
+            }
+#endif
             wave_lds_sync();
         } else {
+#if HHUFF_PL_EARLY
+            __asm__ volatile("" : "+v"(ns), "+v"(ne) : : "memory");  // (as above, on this rare path too)
+#endif
             if (own && len <= kMaxStrLen) {
                 RegSink sink;
                 sink.init(A.out + cur.s);
@@ -2335,9 +2361,13 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
         }
         if (own) finish_encode(A, (uint32_t)(cur.i0 + lane), len, ol);
         if (!have_next) break;
+#if HHUFF_PL_EARLY
+        if (!cur.fits && nxt.fits) pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
+#else
         if (nxt.fits) {
             pf.commit(stage, A.in, A.in_size, nxt.a0, nxt.span, lane);
         }
+#endif
         cur = nxt;
         t = tn;
     }
@@ -2514,15 +2544,13 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
     struct TIn {
         uint32_t s, e, first, raww;
     };
-    auto issue = [&](uint64_t tt) {
-        TIn r{0u, 0u, 0u, 0u};
-        const uint64_t i = tt * K + lane;
-        if ((uint32_t)lane < K && i < A.n) {
-            r.s = A.in_off[i];
-            r.e = A.in_off[i + 1];
-            r.first = A.first_bytes ? A.first_bytes[i] : 0u;
-            r.raww = A.raw_bits ? A.raw_bits[i >> 5] : 0u;
-        }
+    auto issue = [&](uint64_t tt) {  // (clamped, unconditional loads: see encode_pl_kernel)
+        TIn r;
+        const uint64_t i = min(tt * K + min((uint32_t)lane, K - 1u), (uint64_t)A.n - 1u);
+        r.s = A.in_off[i];
+        r.e = A.in_off[i + 1];
+        r.first = A.first_bytes ? A.first_bytes[i] : 0u;
+        r.raww = A.raw_bits ? A.raw_bits[i >> 5] : 0u;
         return r;
     };
     struct Plan {
