@@ -67,8 +67,8 @@ constexpr int kVmWait0 = 0x0F70;  // s_waitcnt vmcnt(0) (expcnt, lgkmcnt untouch
 // holding the input's end goes through registers (bytes past in_size read as 0).  (A loop of load / wait /
 // ds_write paid one memory latency per KiB; register staging of all chunks spilled in flatten_pl_kernel.)
 template <int NCH>
-__device__ __forceinline__ void stage_span_dma(uint32_t* stage, const uint8_t* __restrict__ in, uint64_t in_size,
-                                               uint32_t a0, uint32_t span, int lane) {
+__device__ __forceinline__ void stage_span_dma_issue(uint32_t* stage, const uint8_t* __restrict__ in, uint64_t in_size,
+                                                     uint32_t a0, uint32_t span, int lane) {
     const uint64_t av = in_size > (uint64_t)a0 ? in_size - a0 : 0u;
     const uint32_t avail = av > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)av;
     const uint32_t sb = lds_addr(stage);
@@ -78,6 +78,13 @@ __device__ __forceinline__ void stage_span_dma(uint32_t* stage, const uint8_t* _
         if (k < span && k + 16u <= avail)
             __builtin_amdgcn_global_load_lds((const void*)(in + a0 + k), (lds_u8*)(size_t)(sb + (uint32_t)c * 1024u), 16, 0, 0);
     }
+}
+// waits for every memory operation in flight (the DMA with them), then the chunk at the input's end
+template <int NCH>
+__device__ __forceinline__ void stage_span_dma_finish(uint32_t* stage, const uint8_t* __restrict__ in, uint64_t in_size,
+                                                      uint32_t a0, uint32_t span, int lane) {
+    const uint64_t av = in_size > (uint64_t)a0 ? in_size - a0 : 0u;
+    const uint32_t avail = av > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)av;
     __builtin_amdgcn_s_waitcnt(kVmWait0);
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
@@ -85,6 +92,12 @@ __device__ __forceinline__ void stage_span_dma(uint32_t* stage, const uint8_t* _
         if (k < span && k + 16u > avail)
             *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(stage) + k) = load16_tail(in, in_size, (uint64_t)a0 + k);
     }
+}
+template <int NCH>
+__device__ __forceinline__ void stage_span_dma(uint32_t* stage, const uint8_t* __restrict__ in, uint64_t in_size,
+                                               uint32_t a0, uint32_t span, int lane) {
+    stage_span_dma_issue<NCH>(stage, in, in_size, a0, span, lane);
+    stage_span_dma_finish<NCH>(stage, in, in_size, a0, span, lane);
 }
 
 // Software pipelining across tiles: the next tile's offsets (and is-name word / destination) and its
@@ -2504,6 +2517,8 @@ __device__ __forceinline__ uint32_t prefix_int_bytes(uint32_t h0, uint32_t v, ui
 // bit-count pass runs for every string because the header's length depends on the Huffman length
 // (qpack.c:1052-1060); raw fallbacks copy their shares after the raw header (qpack.c:1046-1051).
 // ------------------------------------------------------------------------------------------------
+// (Measured and rejected, profiles/r04ad_flatten_ab.log: the next tile's span DMA issued before this tile's
+// stores -- the compiler then waits for that DMA before every LDS access of the copy-out: 0.342 -> 0.429 ms.)
 template <int WAVES, int STAGE>
 __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint32_t K, const uint32_t* __restrict__ kplan,
                                                                 uint64_t rec_cap) {
@@ -2562,8 +2577,9 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
         Plan P;
         P.i0 = tt * K;
         P.kt = (uint32_t)min<uint64_t>(K, A.n - P.i0);
-        P.lo = (uint32_t)__shfl((int)x.s, 0, 64);
-        P.hi = (uint32_t)__shfl((int)x.e, (int)P.kt - 1, 64);
+        // wave-uniform: in SGPRs, so a plan kept across a tile costs no VGPRs
+        P.lo = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)x.s, 0, 64));
+        P.hi = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)x.e, (int)P.kt - 1, 64));
         P.a0 = P.lo & ~15u;
         P.span = P.hi > P.lo ? ((P.hi + 15u) & ~15u) - P.a0 : 0u;
         P.olo = (uint64_t)P.lo + 11u * P.i0;
@@ -2575,13 +2591,14 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
     };
     // (the span is staged when its tile comes up: a register prefetch of it across the tile, as encode_pl_kernel
     // does, took this kernel past 128 VGPRs into scratch -- twice the HBM traffic)
+    constexpr int NCH = (STAGE + 1023) / 1024;
     TIn cx = issue(t);
     for (;;) {
         const uint64_t tn = t + tstride;
         const bool have_next = tn < ntiles;
         const Plan cur = plan(t, cx);
         const TIn nxi = issue(have_next ? tn : t);  // the next tile's offsets: in flight during this tile
-        if (cur.fits) stage_span_dma<(STAGE + 1023) / 1024>(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+        if (cur.fits) stage_span_dma<NCH>(stage, A.in, A.in_size, cur.a0, cur.span, lane);
         // ---- the current tile ----
         const uint32_t kt = cur.kt;
         const bool own = (uint32_t)lane < kt;
