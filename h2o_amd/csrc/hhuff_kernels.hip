@@ -2597,7 +2597,7 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
         const uint64_t tn = t + tstride;
         const bool have_next = tn < ntiles;
         const Plan cur = plan(t, cx);
-        const TIn nxi = issue(have_next ? tn : t);  // the next tile's offsets: in flight during this tile
+        TIn nxi = issue(have_next ? tn : t);  // the next tile's offsets: in flight during this tile
         if (cur.fits) stage_span_dma<NCH>(stage, A.in, A.in_size, cur.a0, cur.span, lane);
         // ---- the current tile ----
         const uint32_t kt = cur.kt;
@@ -2662,9 +2662,13 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
             const uint32_t res = ok ? hn + (huff ? hlen : lj) : kFailLen;
             ol = (uint32_t)__shfl((int)res, (int)L, 64);
             wave_lds_sync();
+            // the next tile's offsets are waited for here, before this tile's stores (not at the next tile's
+            // plan, where the wait would cover the stores too)
+            __asm__ volatile("" : "+v"(nxi.s), "+v"(nxi.e), "+v"(nxi.first), "+v"(nxi.raww) : : "memory");
             region_copy_deferred<true>(A.out, cur.ob, obuf, cur.ospan, cur.olo, cur.ohi, lane, A.edges + 2 * t);
             wave_lds_sync();
         } else {
+            __asm__ volatile("" : "+v"(nxi.s), "+v"(nxi.e), "+v"(nxi.first), "+v"(nxi.raww) : : "memory");
             if (own && len <= kMaxStrLen) {  // tile larger than the stage: one string per lane from global
                 const uint64_t O = (uint64_t)s + 11u * i;  // output slot
                 const GlobalSource src{A.in, A.in_size};

@@ -3,5 +3,5 @@
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 export AB_FLAT=1
-T=${T:-r04ad}
-timeout -k 10 900 bash tools/gcall_ab.sh ${T}_flat c5 pl1 fl0 fl1 || exit 7
+T=${T:-r04ae}
+timeout -k 10 900 bash tools/gcall_ab.sh ${T}_flat c5 fl0 fl2 fl0 fl2 || exit 7
