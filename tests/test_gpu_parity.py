@@ -535,6 +535,39 @@ def test_per_string_symbols(torch_cuda, oracle_codec):
         assert codec.encode_huffman(s) == oracle_codec.encode(s)
 
 
+def test_split_decode_fuzz(torch_cuda, oracle_codec):
+    """split_decode_kernel / split_decode_wave on many seeds: batches of long strings (every segment size from
+    32 bits up, leads of 64/128/256 bits) with random corruptions at random places, against the oracle"""
+    rng = np.random.default_rng(101)
+    syms, p = synth.header_alphabet()
+    for rnd in range(6):
+        plain = [bytes(rng.choice(syms, int(L), p=p)) for L in rng.integers(700, 24000, 40)]
+        data, off = synth.pack(plain)
+        enc, el, _ = oracle_codec.encode_batch(data, off, len(plain), nthreads=8)
+        huff = []
+        for i in range(len(plain)):
+            h = bytearray(enc[int(off[i]):int(off[i]) + int(el[i])].tobytes())
+            for _ in range(int(rng.integers(0, 3))):  # 0-2 corruptions anywhere
+                j = int(rng.integers(0, len(h)))
+                k = int(rng.integers(3))
+                if k == 0:
+                    h[j] ^= 1 << int(rng.integers(8))
+                elif k == 1:
+                    h[j:j + 4] = b"\xff\xff\xff\xff"
+                else:
+                    h[j] = int(rng.integers(256))
+            huff.append(bytes(h))
+        hdata, hoff = synth.pack(huff)
+        m = len(huff)
+        for sub in (m, 12):  # a long-mean batch (4 KB and up listed) and a tiny batch (512 B and up)
+            g = gpu_decode(torch_cuda, hdata, hoff, sub)
+            o = oracle_codec.decode_batch(hdata, hoff, sub, nthreads=8)
+            np.testing.assert_array_equal(g[1], o[1])
+            np.testing.assert_array_equal(g[2], o[2])
+            sl = (hoff[:sub].astype(np.uint64) * 8) // 5
+            assert compact(g[0], sl, g[1]) == compact(o[0], sl, o[1])
+
+
 _LAUNCH_PATH_CHECK = r"""
 import sys, numpy as np
 sys.path.insert(0, ".")
