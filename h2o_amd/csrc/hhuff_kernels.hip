@@ -1031,6 +1031,13 @@ __device__ __forceinline__ void store_range16(uint8_t* __restrict__ g, const uin
     }
 }
 
+// 1: the prefetched window lands before the flush stores, removing the loop-top wait that also waits for them.
+// Measured slower (c3 decode 0.293 -> 0.296 ms, c5 0.426 -> 0.449, profiles/r04ak_stream_early_ab.log): the
+// window's loads, not the stores, are what that wait is for, and landing them earlier only shortens their time
+#ifndef HHUFF_STREAM_EARLY
+#define HHUFF_STREAM_EARLY 0
+#endif
+
 // SEG: flush granularity -- whole SEG-byte aligned output segments leave before a string's end
 template <int WAVES, int NW, int OUT, int SEG = 16>
 __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, unsigned long long* __restrict__ counter) {
@@ -1275,6 +1282,16 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
         }
 
         PROF_MARK(3);
+#if HHUFF_STREAM_EARLY
+        // land the prefetched window before this round's flush stores: loads and stores share one in-order
+        // counter on gfx950, so a wait for it next round, behind the stores, would wait for them too
+#pragma unroll
+        for (int j = 0; j < NW / 4; ++j) {
+            uint32_t a0 = pfv[j].x, a1 = pfv[j].y, a2 = pfv[j].z, a3 = pfv[j].w;
+            asm volatile("" : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) :: "memory");
+            pfv[j] = make_uint4(a0, a1, a2, a3);
+        }
+#endif
         // ---- 4. flush whole chunks, carry the partial one; finish strings ----
         if (busy) {
             flags |= ((accb >> 24) | (accb >> 26) | (acc1 >> 24) | (acc2 >> 26) | (accl >> 14)) & 3u;
