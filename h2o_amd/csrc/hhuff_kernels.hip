@@ -363,6 +363,11 @@ struct DecArgs {
     uint32_t* split_n = nullptr;
     uint32_t split_cap = 0;
     uint32_t split_min = 0xFFFFFFFFu;  // Huffman bytes from which a string is listed
+    // strings of big_min bytes or more go to a second list, decoded by a whole block each (NULL: none)
+    uint32_t* big_list = nullptr;
+    uint32_t* big_n = nullptr;
+    uint32_t big_cap = 0;
+    uint32_t big_min = 0xFFFFFFFFu;
     // with gate: the staged / stream prices select_verdict uses, ps per string and per (tile-padded) byte --
     // the fitted defaults, or the device's calibration (calibrate_prices)
     float price[4] = {40.0f, 1.07f, 184.0f, 1.15f};
@@ -379,6 +384,13 @@ __device__ __forceinline__ void load_dec_tables(uint32_t* s_lut, uint32_t* s_kin
 // decoded by this lane; a full list leaves it here
 __device__ __forceinline__ bool split_push(const DecArgs& A, uint32_t i, uint32_t len) {
     if (A.split_list == nullptr || len < A.split_min || len > kMaxStrLen) return false;
+    if (A.big_list != nullptr && len >= A.big_min) {
+        const uint32_t b = atomicAdd(A.big_n, 1u);
+        if (b < A.big_cap) {
+            A.big_list[b] = i;
+            return true;
+        }
+    }
     const uint32_t k = atomicAdd(A.split_n, 1u);
     if (k >= A.split_cap) return false;
     A.split_list[k] = i;
@@ -963,20 +975,125 @@ __device__ __forceinline__ void split_decode_wave(const Src& src, uint32_t s, ui
     st = ok ? soft_bits(is_name, total, fl & 3u, first, last) : kStatusFail;
 }
 
-template <int WAVES>
+// The same with the whole block (W waves, 64 W segments of at least 128 bits) on one string: lone very long
+// strings (a 1-MB value on one wave walks 16 KB per lane).  The agree-with-the-lane-before check crosses waves
+// through LDS (sx[0]: each wave's last e) with a block barrier per round; the wave totals, flags and first /
+// last bytes meet in sx[1..4].  Every thread of the block calls it with the same string.
+template <int W, class Src>
+__device__ __forceinline__ void split_decode_block(const Src& src, uint32_t s, uint32_t len, bool is_name,
+                                                   uint8_t* dst, const DecTables& T, uint32_t* win,
+                                                   uint32_t (&sx)[5][W], uint32_t& ol, uint8_t& st) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    auto walk = [&](auto emit, uint32_t p0, uint32_t kstart, uint32_t pstop, bool act, RegSink& sink) {
+        return seg_walk<decltype(emit)::value>(src, s, 8u * len, p0, kstart, pstop, act, win, sink, T);
+    };
+    using NoEmit = std::integral_constant<bool, false>;
+    using Emit = std::integral_constant<bool, true>;
+    const uint32_t TB = 8u * len;
+    if (TB == 0) {
+        ol = 0;
+        st = soft_bits(is_name, 0u, 0u, 0u, 0u);
+        return;
+    }
+    constexpr uint32_t N = 64u * W;
+    const uint32_t seg = max((uint32_t)(((uint64_t)TB + N * 32u - 1u) / (N * 32u)) * 32u, 128u);
+    const uint32_t lead = seg <= 64u ? 64u : (seg <= 256u ? 128u : kSplitLead);
+    const uint32_t ks = t * seg;
+    const bool act = ks < TB;
+    const bool lastl = act && ks + seg >= TB;
+    const uint32_t pstop = lastl ? TB : ks + seg;
+    RegSink none;
+    none.init(nullptr);
+    SegWalk w = walk(NoEmit{}, ks > lead ? ks - lead : 0u, ks, pstop, act, none);
+    for (uint32_t it = 0; it < N; ++it) {
+        if (lane == 63u) sx[0][wave] = w.e;
+        __syncthreads();
+        uint32_t pe = (uint32_t)__shfl_up((int)w.e, 1, 64);
+        if (lane == 0u) pe = wave ? sx[0][wave - 1u] : 0u;
+        const bool bad = act && t > 0u && w.f != pe;
+        if (!__syncthreads_or(bad)) break;
+        const SegWalk w2 = walk(NoEmit{}, pe, pe, pstop, bad, none);
+        if (bad) w = w2;
+    }
+    const uint32_t cnt = act ? w.cnt : 0u;
+    const uint32_t place = wave_excl_scan(cnt, (int)lane);
+    uint32_t fl = act ? w.flags : 0u;
+    fl |= (act && w.eos ? 4u : 0u) | (lastl && w.end_ok ? 8u : 0u);
+    fl |= (uint32_t)__shfl_xor((int)fl, 1, 64);
+    fl |= (uint32_t)__shfl_xor((int)fl, 2, 64);
+    fl |= (uint32_t)__shfl_xor((int)fl, 4, 64);
+    fl |= (uint32_t)__shfl_xor((int)fl, 8, 64);
+    fl |= (uint32_t)__shfl_xor((int)fl, 16, 64);
+    fl |= (uint32_t)__shfl_xor((int)fl, 32, 64);
+    const uint64_t has = __builtin_amdgcn_ballot_w64(cnt != 0);
+    uint32_t wf = 0x100u, wl = 0x100u;  // 0x100: no symbol in the wave
+    if (has) {
+        wf = (uint32_t)__shfl((int)w.first, (int)__builtin_ctzll(has), 64) & 0xFFu;
+        wl = (uint32_t)__shfl((int)w.last, 63 - (int)__builtin_clzll(has), 64) & 0xFFu;
+    }
+    const uint32_t wtot = (uint32_t)__builtin_amdgcn_readlane((int)(place + cnt), 63);
+    if (lane == 0u) {
+        sx[1][wave] = wtot;
+        sx[2][wave] = wf;
+        sx[3][wave] = wl;
+        sx[4][wave] = fl;
+    }
+    __syncthreads();
+    uint32_t pre = 0, total = 0, F = 0, first = 0x100u, last = 0x100u;
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)W; ++k) {
+        const uint32_t v = sx[1][k];
+        pre += k < wave ? v : 0u;
+        total += v;
+        F |= sx[4][k];
+        first = first == 0x100u ? sx[2][k] : first;
+        last = sx[3][k] != 0x100u ? sx[3][k] : last;
+    }
+    first &= 0xFFu;
+    last &= 0xFFu;
+    const bool ok = !(F & 4u) && (F & 8u);
+    {
+        const bool em = ok && act && cnt != 0;
+        RegSink sink;
+        sink.init(dst + pre + place);
+        (void)walk(Emit{}, w.f, w.f, pstop, em, sink);
+        if (em) sink.finish();
+    }
+    ol = ok ? total : kFailLen;
+    st = ok ? soft_bits(is_name, total, F & 3u, first, last) : kStatusFail;
+}
+
+// BIG: the block list (a block per string), else the one-wave list
+template <int WAVES, bool BIG>
 __global__ __launch_bounds__(WAVES * 64) void split_decode_kernel(DecArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
     __shared__ uint32_t s_kinfo[32];
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
     __shared__ uint32_t s_win[WAVES * 64][kSplitNW + 1];
-    if (blockIdx.x * WAVES >= min(*A.split_n, A.split_cap)) return;  // (block-uniform) nothing listed for it
+    __shared__ uint32_t s_x[5][WAVES];
+    const uint32_t nl = BIG ? 0u : min(*A.split_n, A.split_cap);
+    const uint32_t nb = BIG ? min(*A.big_n, A.big_cap) : 0u;
+    if (blockIdx.x * WAVES >= nl && blockIdx.x >= nb) return;  // (block-uniform) nothing listed for it
     load_dec_tables(s_lut, s_kinfo, s_ones, WAVES * 64);
     __syncthreads();
     const DecTables T{s_lut, s_kinfo, s_ones};
     const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-    const uint32_t nl = min(*A.split_n, A.split_cap);
     const GlobalSource src{A.in, A.in_size};
-    for (uint32_t j = blockIdx.x * WAVES + wave; j < nl; j += gridDim.x * WAVES) {
+    for (uint32_t j = blockIdx.x; j < nb; j += gridDim.x) {  // block-uniform: the big strings, a block each
+        const uint32_t i = A.big_list[j];
+        const uint32_t s = A.in_off[i];
+        const uint32_t len = A.in_len ? A.in_len[i] : A.in_off[i + 1] - s;
+        const bool is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) : false;
+        const uint64_t d = A.out_off ? (uint64_t)A.out_off[i] : dec_slot(s);
+        uint32_t ol;
+        uint8_t st;
+        split_decode_block<WAVES>(src, s, len, is_name, A.out + d, T, s_win[threadIdx.x], s_x, ol, st);
+        if (threadIdx.x == 0) {
+            A.out_len[i] = ol;
+            A.status[i] = st;
+        }
+    }
+    for (uint32_t j = blockIdx.x * WAVES + wave; j < nl; j += gridDim.x * WAVES) {  // the one-wave strings
         const uint32_t i = A.split_list[j];
         const uint32_t s = A.in_off[i];
         const uint32_t len = A.in_len ? A.in_len[i] : A.in_off[i + 1] - s;  // split_min <= len <= kMaxStrLen
@@ -3360,7 +3477,16 @@ static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint3
 #ifndef HHUFF_SPLIT
 #define HHUFF_SPLIT 1  // 0: no list (A/B builds: every long string decoded by one lane)
 #endif
-constexpr int kSplitWaves = 4;
+#ifndef HHUFF_SPLIT_WAVES
+#define HHUFF_SPLIT_WAVES 4
+#endif
+#ifndef HHUFF_SPLIT_BIG  // 0: no block list (every listed string on one wave)
+#define HHUFF_SPLIT_BIG 1
+#endif
+constexpr int kSplitWaves = HHUFF_SPLIT_WAVES;  // one-wave list: 4-wave blocks (16 measured 8 % slower)
+constexpr int kSplitBlockWaves = 16;             // block list: 1024 segments per string
+// strings this long are decoded by a whole block (split_decode_block): 64 KB in batches, 4 KB in tiny ones
+constexpr uint32_t kSplitBig = 65536, kSplitBigFew = 4096;
 hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, const uint32_t* in_len, uint32_t n,
                          const uint32_t* is_name_bits, uint8_t* out, const uint32_t* out_off, uint32_t* out_len,
                          uint8_t* status, hipStream_t stream, uint64_t sel_bytes) {
@@ -3373,17 +3499,28 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     if (split) {
         A.split_min = smin;
         A.split_cap = (uint32_t)std::min<uint64_t>(n, bytes / smin + 1);
-        hipError_t e = pool_alloc((void**)&sp, 4ull * (A.split_cap + 1), stream);
-        if (e == hipSuccess) e = hipMemsetAsync(sp, 0, 4, stream);
+        A.big_min = n <= 16u ? kSplitBigFew : kSplitBig;
+        A.big_cap = HHUFF_SPLIT_BIG ? (uint32_t)std::min<uint64_t>(n, bytes / A.big_min) : 0u;
+        hipError_t e = pool_alloc((void**)&sp, 4ull * (2 + A.split_cap + A.big_cap), stream);
+        if (e == hipSuccess) e = hipMemsetAsync(sp, 0, 8, stream);
         if (e != hipSuccess) return e;
         A.split_n = sp;
-        A.split_list = sp + 1;
+        A.big_n = sp + 1;
+        A.split_list = sp + 2;
+        A.big_list = A.big_cap ? sp + 2 + A.split_cap : nullptr;
     }
     hipError_t e = launch_decode_kernels(A, in_size, in_len, n, out, out_off, stream, sel_bytes);
     if (split) {
         if (e == hipSuccess) {
             const int grid = (int)std::min<uint32_t>((A.split_cap + kSplitWaves - 1) / kSplitWaves, 512u);
-            hipLaunchKernelGGL(split_decode_kernel<kSplitWaves>, dim3(grid), dim3(kSplitWaves * 64), 0, stream, A);
+            hipLaunchKernelGGL((split_decode_kernel<kSplitWaves, false>), dim3(grid), dim3(kSplitWaves * 64), 0, stream,
+                               A);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess && A.big_cap) {
+            // (at most 128 blocks: the list is almost always empty, and a launch's blocks all start)
+            hipLaunchKernelGGL((split_decode_kernel<kSplitBlockWaves, true>), dim3(std::min<uint32_t>(A.big_cap, 128u)),
+                               dim3(kSplitBlockWaves * 64), 0, stream, A);
             e = hipGetLastError();
         }
         const hipError_t f = hipFreeAsync(sp, stream);
@@ -3647,8 +3784,8 @@ __device__ __forceinline__ DecResult wave_decode(const uint8_t* in, uint32_t len
 // One string per launch: the h2o per-string symbols (h2o_hpack_{de,en}code_huffman).  The string sits in
 // pinned, device-visible host memory, [meta 16 B][input][output]: one launch reads it across PCIe (the
 // block's 16-B loads in one round trip) into LDS, wave 0 codes it from LDS into an LDS output buffer (encode:
-// the service's 64-bytes-a-round wave encoder; decode: split_decode_wave, 64 self-synchronising segments --
-// a lone lane took ~100 us for 1 KB), and the block writes the result and the meta words back -- no copies,
+// the service's 64-bytes-a-round wave encoder; decode: split_decode_block over the block's four waves, 256
+// self-synchronising segments of at least 128 bits -- a lone lane took ~100 us for 1 KB), and the block writes the result and the meta words back -- no copies,
 // one launch, one synchronisation.
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void one_string_kernel(uint8_t* __restrict__ h, uint32_t len, uint32_t in_cap,
@@ -3658,7 +3795,7 @@ __global__ __launch_bounds__(256) void one_string_kernel(uint8_t* __restrict__ h
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
     __shared__ __attribute__((aligned(16))) uint32_t s_in[kOneMax / 4 + 4];
     __shared__ __attribute__((aligned(16))) uint8_t s_out[(kOneMax * 8) / 5 + 64];
-    __shared__ uint32_t s_win[64][kSplitNW + 1];     // decode: wave 0's split windows
+    __shared__ uint32_t s_win[256][kSplitNW + 1];    // decode: the split windows
     uint2* s_enc = reinterpret_cast<uint2*>(s_lut);  // encode: the table takes the LUT's place
     if (encode) {
         for (uint32_t k = threadIdx.x; k < 256; k += 256) s_enc[k] = make_uint2(g_enc_code[k], g_enc_nbits[k]);
@@ -3669,24 +3806,28 @@ __global__ __launch_bounds__(256) void one_string_kernel(uint8_t* __restrict__ h
         *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_in) + k) = *reinterpret_cast<const uint4*>(h + 16 + k);
     __syncthreads();
     __shared__ uint32_t s_res[2];
-    if (threadIdx.x < 64) {  // wave 0: the service's wave encoder, the split decoder over the staged string
-        const uint32_t lane = threadIdx.x;
-        uint32_t ol, st = 0;
-        if (encode) {
-            ol = wave_encode(reinterpret_cast<const uint8_t*>(s_in), len, reinterpret_cast<uint32_t*>(s_out), s_enc,
-                             lane, kOneMax);
-            st = ol == kFailLen ? kStatusFail : 0u;
+    __shared__ uint32_t s_x[5][4];
+    if (encode) {  // (launch-uniform) wave 0: the service's wave encoder
+        if (threadIdx.x < 64) {
+            const uint32_t lane = threadIdx.x;
+            uint32_t ol = wave_encode(reinterpret_cast<const uint8_t*>(s_in), len, reinterpret_cast<uint32_t*>(s_out),
+                                      s_enc, lane, kOneMax);
+            const uint32_t st = ol == kFailLen ? kStatusFail : 0u;
             if (ol != kFailLen) ol = (ol + 7u) >> 3;
-        } else {
-            const LdsSource src{s_in, len ? ((len + 3u) & ~3u) - 4u : 0u};
-            uint8_t st8;
-            split_decode_wave(src, 0u, len, is_name != 0, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane, ol, st8,
-                              s_win[lane]);
-            st = st8;
+            if (lane == 0) {
+                s_res[0] = ol;
+                s_res[1] = st;
+            }
         }
-        if (lane == 0) {
+    } else {  // the block's four waves: the split decoder over the staged string, 256 segments
+        const LdsSource src{s_in, len ? ((len + 3u) & ~3u) - 4u : 0u};
+        uint32_t ol;
+        uint8_t st8;
+        split_decode_block<4>(src, 0u, len, is_name != 0, s_out, DecTables{s_lut, s_kinfo, s_ones},
+                              s_win[threadIdx.x], s_x, ol, st8);
+        if (threadIdx.x == 0) {
             s_res[0] = ol;
-            s_res[1] = st;
+            s_res[1] = st8;
         }
     }
     __syncthreads();

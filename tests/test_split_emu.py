@@ -27,3 +27,23 @@ def test_split_algorithm_matches_oracle(oracle_codec):
         rewalked += rw > 0
     assert rewalked > 0  # the periodic strings exercise the fix-up
     assert E.split_decode(T, b"", 0, 0)[0] == b"" == oracle_codec.decode(b"")[0]
+
+
+def test_split_block_algorithm_matches_oracle(oracle_codec):
+    """split_decode_block's parameters: 64 W = 1024 or 256 segments of at least 128 bits (lead 128 up to 256-bit
+    segments), the fix-up crossing waves."""
+    import emu_split as E
+    from test_gpu_parity import _long_huffman_strings
+
+    T = E.tables()
+    rng = np.random.default_rng(29)
+    lengths = [4096, 4500, 9000, 16384, 20000, 33000] + [int(x) for x in rng.integers(4096, 12000, 6)]
+    huff = _long_huffman_strings(oracle_codec, rng, lengths)
+    rewalked = 0
+    for h in huff:
+        ref, _ = oracle_codec.decode(h)
+        for nseg in (1024, 256):  # split_decode_kernel's block list (16 waves), one_string_kernel (4 waves)
+            got, rw = E.split_decode(T, h, 0, len(h), nseg=nseg, minseg=128)
+            assert got == ref, (nseg, len(h), None if ref is None else len(ref))
+            rewalked += rw > 0
+    assert rewalked > 0

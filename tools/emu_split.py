@@ -77,22 +77,23 @@ def seg_walk(T, data, s, TB, p0, kstart, pstop, emit):
     return r
 
 
-def split_decode(T, data, s, length):
-    """-> (decoded bytes or None, rewalks)"""
+def split_decode(T, data, s, length, nseg=64, minseg=32):
+    """-> (decoded bytes or None, rewalks).  nseg=64: split_decode_wave; nseg=64 W, minseg=128:
+    split_decode_block (W waves)"""
     TB = 8 * length
     if TB == 0:  # an empty string decodes to nothing
         return b"", 0
-    seg = ((TB + 64 * 32 - 1) // (64 * 32)) * 32
+    seg = max(((TB + nseg * 32 - 1) // (nseg * 32)) * 32, minseg)
     W = []
-    for lane in range(64):
+    for lane in range(nseg):
         ks = lane * seg
         act = ks < TB
         pstop = TB if (act and ks + seg >= TB) else ks + seg
         lead = 64 if seg <= 64 else (128 if seg <= 256 else LEAD)
         W.append(seg_walk(T, data, s, TB, max(ks - lead, 0), ks, pstop, False) if act else None)
     rewalks = 0
-    for _ in range(64):
-        bad = [lane for lane in range(1, 64) if W[lane] is not None and W[lane]["f"] != W[lane - 1]["e"]]
+    for _ in range(nseg):
+        bad = [lane for lane in range(1, nseg) if W[lane] is not None and W[lane]["f"] != W[lane - 1]["e"]]
         if not bad:
             break
         pe = {lane: W[lane - 1]["e"] for lane in bad}

@@ -32,7 +32,7 @@ def main(names, rounds=5, steps=10):
     rng = np.random.default_rng(9)
     syms, p = synth.header_alphabet()
     cases = {"512x4-64K": [int(x) for x in rng.integers(4096, 65536, 512)], "64x256K": [262144] * 64,
-             "1x100K": [100000], "1x1M": [1 << 20], "1x2K": [2000], "8x3K": [3000] * 8}
+             "1x100K": [100000], "1x1M": [1 << 20], "1x2K": [2000], "8x3K": [3000] * 8, "1x16K": [16384], "4x8K": [8192] * 4}
     s = torch.cuda.current_stream().cuda_stream
     res = {}
     for cname, lens in cases.items():
