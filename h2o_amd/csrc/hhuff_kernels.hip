@@ -3469,7 +3469,8 @@ static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint3
 }
 
 // Long strings (kSplitMin Huffman bytes or more) are listed by the decode kernels and decoded afterwards, one
-// wave each, by split_decode_kernel -- in batches whose mean string is long (>= 128 B: QPACK values, cookies)
+// wave each, by split_decode_kernel (kSplitBig bytes or more: a block each, the second list and launch)
+// -- in batches whose mean string is long (>= 128 B: QPACK values, cookies)
 // and in tiny batches (kSplitMinFew: the per-string launch path for strings over the service's 768 B, where a
 // lane would take the whole string's bits one after another).  Elsewhere the list
 // would cost a memset and a launch on every call for strings that are almost never there, and a rare long
