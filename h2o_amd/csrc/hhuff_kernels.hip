@@ -3648,6 +3648,45 @@ __device__ __forceinline__ uint32_t wave_encode(const uint8_t* in, uint32_t len,
     return bits;
 }
 
+// The same with the whole block (W waves) on one string (one_string_kernel): each wave takes a contiguous
+// part of the input (64-byte multiples), a first pass sums its code lengths, a block prefix over the waves
+// places the parts (and decides the verdict from the total, hpack.c:799-800), and a second pass ORs each
+// wave's codes in at its place -- the parts meet inside shared words, hence the LDS OR.  All threads call it.
+template <int W>
+__device__ __forceinline__ uint32_t block_encode(const uint8_t* in, uint32_t len, uint32_t* out32, const uint2* s_enc,
+                                                 uint32_t cap, uint32_t (&sx)[5][W]) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    for (uint32_t k = t; k < len / 4u + 4u; k += 64u * W) out32[k] = 0u;
+    const uint32_t per = ((len + 64u * W - 1u) / (64u * W)) * 64u;
+    const uint32_t b0 = min(wave * per, len), b1 = min(b0 + per, len);
+    uint32_t mine = 0;
+    for (uint32_t j = b0 + lane; j < b1; j += 64u) mine += s_enc[in[j]].y;
+    const uint32_t wsum = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(mine), 63);
+    if (lane == 0u) sx[0][wave] = wsum;
+    __syncthreads();  // (also: the zeroed stage)
+    uint32_t pos = 0, bits = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)W; ++k) {
+        const uint32_t v = sx[0][k];
+        pos += k < wave ? v : 0u;
+        bits += v;
+    }
+    const uint32_t lim = len ? 8u * len - 8u : 0u;  // hpack.c:799-800: ceil(bits / 8) < len
+    if (len == 0 || len > cap || bits > lim) return kFailLen;  // (block-uniform)
+    const uint32_t obase = lds_addr(out32);
+    for (uint32_t j0 = b0; j0 < b1; j0 += 64u) {
+        const uint32_t j = j0 + lane;
+        const uint2 e = j < b1 ? s_enc[in[j]] : make_uint2(0u, 0u);
+        const uint32_t incl = wave_incl_scan(e.y);
+        if (e.y) place_bits(obase, pos + incl - e.y, e.x, e.y);
+        pos += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
+    const uint32_t p = (0u - bits) & 7u;  // fill the last byte with ones (EOS prefix, hpack.c:795-798)
+    if (t == 0u && p) place_bits(obase, bits, (1ull << p) - 1ull, p);
+    __syncthreads();
+    return bits;
+}
+
 // decode s_in bytes [0, len) into out (LDS bytes).  Two candidates per lane: bits W + lane and W + 64 + lane.
 struct WaveStep {  // the step that would start at one candidate bit
     uint32_t nx;    // chain offset of the next step (offset + bits taken), or kStop
@@ -3785,7 +3824,8 @@ __device__ __forceinline__ DecResult wave_decode(const uint8_t* in, uint32_t len
 // One string per launch: the h2o per-string symbols (h2o_hpack_{de,en}code_huffman).  The string sits in
 // pinned, device-visible host memory, [meta 16 B][input][output]: one launch reads it across PCIe (the
 // block's 16-B loads in one round trip) into LDS, wave 0 codes it from LDS into an LDS output buffer (encode:
-// the service's 64-bytes-a-round wave encoder; decode: split_decode_block over the block's four waves, 256
+// block_encode, the service's 64-bytes-a-round wave encoder on a quarter of the string per wave; decode:
+// split_decode_block over the block's four waves, 256
 // self-synchronising segments of at least 128 bits -- a lone lane took ~100 us for 1 KB), and the block writes the result and the meta words back -- no copies,
 // one launch, one synchronisation.
 // ------------------------------------------------------------------------------------------------
@@ -3808,17 +3848,14 @@ __global__ __launch_bounds__(256) void one_string_kernel(uint8_t* __restrict__ h
     __syncthreads();
     __shared__ uint32_t s_res[2];
     __shared__ uint32_t s_x[5][4];
-    if (encode) {  // (launch-uniform) wave 0: the service's wave encoder
-        if (threadIdx.x < 64) {
-            const uint32_t lane = threadIdx.x;
-            uint32_t ol = wave_encode(reinterpret_cast<const uint8_t*>(s_in), len, reinterpret_cast<uint32_t*>(s_out),
-                                      s_enc, lane, kOneMax);
-            const uint32_t st = ol == kFailLen ? kStatusFail : 0u;
-            if (ol != kFailLen) ol = (ol + 7u) >> 3;
-            if (lane == 0) {
-                s_res[0] = ol;
-                s_res[1] = st;
-            }
+    if (encode) {  // (launch-uniform) the block's four waves, a quarter of the string each
+        uint32_t ol = block_encode<4>(reinterpret_cast<const uint8_t*>(s_in), len, reinterpret_cast<uint32_t*>(s_out),
+                                      s_enc, kOneMax, s_x);
+        const uint32_t st = ol == kFailLen ? kStatusFail : 0u;
+        if (ol != kFailLen) ol = (ol + 7u) >> 3;
+        if (threadIdx.x == 0) {
+            s_res[0] = ol;
+            s_res[1] = st;
         }
     } else {  // the block's four waves: the split decoder over the staged string, 256 segments
         const LdsSource src{s_in, len ? ((len + 3u) & ~3u) - 4u : 0u};

@@ -585,6 +585,8 @@ syms, p = synth.header_alphabet()
 plain = [bytes(rng.choice(syms, int(L), p=p)) for L in rng.integers(0, 9000, 50)]
 plain += [bytes(rng.choice(syms, int(L), p=p)) for L in (32768, 32769, 40000, 45000)]
 plain += [b"a" * 3000, b"0e" * 1500, bytes(rng.integers(0, 256, 2000, dtype=np.uint8))]
+# the verdict at its edge ('&': 8 bits, 'a': 5): 8 n - 9 bits encodes, 8 n - 6 does not (hpack.c:799-800)
+plain += [b"&" * 5000 + b"aaa", b"&" * 5000 + b"aa", b"aaa" + b"&" * 7000, b"&" * 20000 + b"aa" + b"&" * 9 + b"a"]
 for s in plain:
     h = o.encode(s)
     assert codec.encode_huffman(s) == h, len(s)
