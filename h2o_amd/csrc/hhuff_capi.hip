@@ -52,7 +52,9 @@ struct Ctx {
     uint8_t* h = nullptr;  // pinned, device-visible (the per-string kernel reads and writes it in place)
     size_t hcap = 0;
     ~Ctx() {
-        // thread exit: release what this thread allocated (ignore errors at process teardown)
+        // thread exit: release what this thread allocated (ignore errors at process teardown); a one-string
+        // kernel whose result was taken early (wait_one) may still be retiring
+        if (stream) (void)hipStreamSynchronize(stream);
         if (d) (void)hipFree(d);
         if (h) (void)hipHostFree(h);
         if (stream) (void)hipStreamDestroy(stream);
@@ -64,6 +66,7 @@ struct Ctx {
         HIP_TRY(hipGetDevice(&cur), "hipGetDevice");
         if (device < 0) device = cur;
         if (dev != device) {
+            if (stream) (void)hipStreamSynchronize(stream);
             if (d) (void)hipFree(d), d = nullptr, dcap = 0;
             if (h) (void)hipHostFree(h), h = nullptr, hcap = 0;
             if (stream) (void)hipStreamDestroy(stream), stream = nullptr;
@@ -83,7 +86,7 @@ struct Ctx {
             dcap = cap;
         }
         if (hneed > hcap) {
-            if (h) (void)hipHostFree(h), h = nullptr, hcap = 0;
+            if (h) (void)hipStreamSynchronize(stream), (void)hipHostFree(h), h = nullptr, hcap = 0;  // (wait_one)
             size_t cap = hneed < (1u << 16) ? (1u << 16) : hneed + hneed / 4;
             // coherent (fine-grained): the per-string kernel reads and writes it in place across PCIe
             HIP_TRY(hipHostMalloc(&h, cap, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
@@ -546,6 +549,26 @@ int svc_call(int dev, bool encode, const uint8_t* src, size_t len, int is_name, 
     return 1;
 }
 
+// The one-string kernel stores its result length last (system scope, after every output word): spin on it
+// instead of waiting for the launch's completion signal, for up to 2 ms, then synchronise the stream as before
+// (which also reports a failed launch).  HHUFF_ONE_SYNC=1: always synchronise.
+constexpr uint32_t kOnePending = 0xFFFFFFFEu;  // never a result: lengths stay below 2^16, failures are ~0u
+static hipError_t wait_one(Ctx& c, const uint32_t* meta) {
+    static const bool sync_only = [] {
+        const char* v = getenv("HHUFF_ONE_SYNC");
+        return v && v[0] == '1';
+    }();
+    if (!sync_only) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint64_t k = 0;; ++k) {
+            if (__atomic_load_n(&meta[2], __ATOMIC_ACQUIRE) != kOnePending) return hipSuccess;
+            if ((k & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+            __builtin_ia32_pause();
+        }
+    }
+    return hipStreamSynchronize(c.stream);
+}
+
 size_t per_string(bool encode, uint8_t* dst, const uint8_t* src, size_t len, int is_name, unsigned* soft_errors) {
     __atomic_fetch_add(&g_per_string_calls, 1, __ATOMIC_RELAXED);
     Ctx& c = t_ctx;
@@ -571,9 +594,10 @@ size_t per_string(bool encode, uint8_t* dst, const uint8_t* src, size_t len, int
         uint32_t* meta = reinterpret_cast<uint32_t*>(c.h);
         meta[0] = (uint32_t)len;
         meta[1] = is_name ? 1u : 0u;
+        __atomic_store_n(&meta[2], kOnePending, __ATOMIC_RELAXED);
         memcpy(c.h + 16, src, len);
         hipError_t e = hhuff::launch_one(c.h, (uint32_t)len, (uint32_t)in_cap, is_name != 0, encode, c.stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c.stream);
+        if (e == hipSuccess) e = wait_one(c, meta);
         if (e != hipSuccess) return hip_fail(e, encode ? "encode (one string)" : "decode (one string)"), SIZE_MAX;
         const uint32_t r = __atomic_load_n(&meta[2], __ATOMIC_ACQUIRE);
         if (r == HHUFF_FAIL_LEN) return SIZE_MAX;

@@ -3875,9 +3875,14 @@ __global__ __launch_bounds__(256) void one_string_kernel(uint8_t* __restrict__ h
         const uint32_t v = *reinterpret_cast<const uint32_t*>(s_out + k);
         *reinterpret_cast<uint32_t*>(h + 16 + in_cap + k) = encode ? bswap32(v) : v;
     }
+    // the result length last, after every output word (each thread's fence, then the barrier): the host
+    // may take the result as soon as it sees the length, before the launch's completion signal
+    __threadfence_system();
+    __syncthreads();
     if (threadIdx.x == 0) {
-        reinterpret_cast<uint32_t*>(h)[2] = ol;
-        reinterpret_cast<uint32_t*>(h)[3] = s_res[1];
+        uint32_t* meta = reinterpret_cast<uint32_t*>(h);
+        __hip_atomic_store(&meta[3], s_res[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&meta[2], ol, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
