@@ -3481,6 +3481,9 @@ static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint3
 #ifndef HHUFF_SPLIT_WAVES
 #define HHUFF_SPLIT_WAVES 4
 #endif
+#ifndef HHUFF_BIG_GRID  // most blocks of the block-list launch
+#define HHUFF_BIG_GRID 128u
+#endif
 #ifndef HHUFF_SPLIT_BIG  // 0: no block list (every listed string on one wave)
 #define HHUFF_SPLIT_BIG 1
 #endif
@@ -3519,8 +3522,9 @@ hipError_t launch_decode(const uint8_t* in, uint64_t in_size, const uint32_t* in
             e = hipGetLastError();
         }
         if (e == hipSuccess && A.big_cap) {
-            // (at most 128 blocks: the list is almost always empty, and a launch's blocks all start)
-            hipLaunchKernelGGL((split_decode_kernel<kSplitBlockWaves, true>), dim3(std::min<uint32_t>(A.big_cap, 128u)),
+            // (at most HHUFF_BIG_GRID blocks: the list is almost always empty, and a launch's blocks all start)
+            hipLaunchKernelGGL((split_decode_kernel<kSplitBlockWaves, true>),
+                               dim3(std::min<uint32_t>(A.big_cap, HHUFF_BIG_GRID)),
                                dim3(kSplitBlockWaves * 64), 0, stream, A);
             e = hipGetLastError();
         }
