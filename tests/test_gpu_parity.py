@@ -602,16 +602,18 @@ print("ok", n)
 """
 
 
-def test_per_string_launch_path(torch_cuda):
+@pytest.mark.parametrize("one_sync", ["0", "1"])
+def test_per_string_launch_path(torch_cuda, one_sync):
     """the launch-per-string path (HHUFF_NO_SERVICE=1: one_string_kernel up to 32 KB, the batch kernels beyond):
-    wave encoder and split decoder against the oracle on the KAT strings, header text of 0-45000 B, periodic
-    text, random bytes and corrupted padding"""
+    block encoder and split decoder against the oracle on the KAT strings, header text of 0-45000 B, periodic
+    text, random bytes, corrupted padding and the encode verdict's edge; the result taken when its length lands
+    (wait_one) and after the stream synchronisation (HHUFF_ONE_SYNC=1)"""
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, HHUFF_NO_SERVICE="1")
+    env = dict(os.environ, HHUFF_NO_SERVICE="1", HHUFF_ONE_SYNC=one_sync)
     r = subprocess.run([sys.executable, "-c", _LAUNCH_PATH_CHECK], cwd=root, env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout[-2000:] + r.stderr[-4000:]
