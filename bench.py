@@ -608,9 +608,9 @@ def per_string_latency(codec, calls=2000):
     out["string_bytes"] = len(s)
     # long values (cookies, URIs): past the service's 768 B a call is one launch; decode splits the string over
     # a wave from 512 Huffman bytes (split_decode_kernel)
-    text = (b"session=eyJhbGciOiJIUzI1NiJ9.dXNlcj0xMjM0NTY3ODkw; theme=dark; lang=en-US; " * 300)
+    text = (b"session=eyJhbGciOiJIUzI1NiJ9.dXNlcj0xMjM0NTY3ODkw; theme=dark; lang=en-US; " * 900)
     longs = {}
-    for L in (1024, 4096, 16384):
+    for L in (1024, 4096, 16384, 65536):  # 64 KB: past one_string_kernel, the batch kernels on a batch of one
         ls = text[:L]
         lh = codec.encode_huffman(ls)
         assert codec.decode_huffman(lh, False)[0] == ls

@@ -393,6 +393,9 @@ HHUFF_API int hhuff_qpack_parse_responses(const uint8_t* in, uint64_t in_size, c
 // ---------------------------------------------------------------------------------------------------
 namespace {
 constexpr size_t kMeta = 32;
+#ifndef HHUFF_LONG_ENC_DEFAULT
+#define HHUFF_LONG_ENC_DEFAULT 0
+#endif
 uint64_t g_per_string_calls = 0;  // process-wide, atomic adds (hhuff_per_string_calls)
 
 // ---- the resident per-string service (service_kernel, hhuff_kernels.hip), one grid per device ----
@@ -569,6 +572,16 @@ static hipError_t wait_one(Ctx& c, const uint32_t* meta) {
     return hipStreamSynchronize(c.stream);
 }
 
+// Per-string encode past kOneMax: one block over the string (encode_long_kernel) with HHUFF_LONG_ENC=1 (or a
+// build default of 1), else the batch kernels on a batch of one (one lane: ~8 ms for 64 KB)
+static bool long_encode_block() {
+    static const bool on = [] {
+        const char* v = getenv("HHUFF_LONG_ENC");
+        return v ? v[0] != '0' : HHUFF_LONG_ENC_DEFAULT != 0;
+    }();
+    return on;
+}
+
 size_t per_string(bool encode, uint8_t* dst, const uint8_t* src, size_t len, int is_name, unsigned* soft_errors) {
     __atomic_fetch_add(&g_per_string_calls, 1, __ATOMIC_RELAXED);
     Ctx& c = t_ctx;
@@ -620,7 +633,10 @@ size_t per_string(bool encode, uint8_t* dst, const uint8_t* src, size_t len, int
     uint8_t* h_out = c.h + kMeta + in_cap;
     hipError_t e = hipMemcpyAsync(c.d, c.h, kMeta + len, hipMemcpyHostToDevice, c.stream);
     if (e == hipSuccess)
-        e = encode ? hhuff::launch_encode(d_in, len, d_meta, nullptr, 1, d_out, nullptr, d_meta + 2, nullptr, c.stream)
+        e = encode ? (long_encode_block()
+                          ? hhuff::launch_encode_long(d_in, (uint32_t)len, d_out, d_meta + 2, c.stream)
+                          : hhuff::launch_encode(d_in, len, d_meta, nullptr, 1, d_out, nullptr, d_meta + 2, nullptr,
+                                                 c.stream))
                    : hhuff::launch_decode(d_in, len, d_meta, nullptr, 1, d_meta + 3, d_out, nullptr, d_meta + 2,
                                           reinterpret_cast<uint8_t*>(d_meta + 4), c.stream);
     if (e == hipSuccess) e = hipMemcpyAsync(c.h, c.d, kMeta, hipMemcpyDeviceToHost, c.stream);

@@ -3896,6 +3896,109 @@ hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, b
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// One string past kOneMax to encode (the per-string path's long values; a lone lane took 8 ms for 64 KB):
+// one block of 1,024 threads walks the string in rounds of kLongChunk input bytes, 16 per thread.  Pass 1
+// sums each thread's code bits, a block scan places the threads' codes, and the round total decides the
+// verdict early (hpack.c:799-800: the bits only grow).  Pass 2 ORs each thread's codes into an LDS stage
+// whose word 0 carries the previous round's partial word; the round's whole words go out byte-swapped and
+// the partial one is carried.  The end: the EOS-prefix padding (hpack.c:795-798) and the last word.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kLongChunk = 16384;
+__global__ __launch_bounds__(1024) void encode_long_kernel(const uint8_t* __restrict__ in, uint32_t len,
+                                                          uint8_t* __restrict__ out, uint32_t* __restrict__ out_len) {
+    __shared__ uint2 s_enc[256];
+    __shared__ __attribute__((aligned(16))) uint32_t s_st[(kLongChunk * 30u) / 32u + 8u];
+    __shared__ uint32_t s_w[16];
+    constexpr uint32_t kSt = (kLongChunk * 30u) / 32u + 8u;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    if (t < 256) s_enc[t] = make_uint2(g_enc_code[t], g_enc_nbits[t]);
+    for (uint32_t k = t; k < kSt; k += 1024u) s_st[k] = 0u;
+    __syncthreads();
+    const uint32_t sbase = lds_addr(s_st);
+    uint32_t* out32 = reinterpret_cast<uint32_t*>(out);  // 4-byte aligned (the caller's device buffer)
+    const uint64_t lim = len ? 8ull * len - 8ull : 0ull;
+    bool fail = len == 0;
+    uint64_t P = 0;      // bits placed so far (block-uniform)
+    uint32_t carry = 0;  // the partial word holding bits [P & ~31, P), MSB-first
+    for (uint32_t c0 = 0; c0 < len && !fail; c0 += kLongChunk) {
+        const uint32_t cl = min(kLongChunk, len - c0);
+        const uint32_t b0 = 16u * t, nb = b0 < cl ? min(16u, cl - b0) : 0u;
+        const uint4 v = nb ? load16_bounded(in, len, (uint64_t)c0 + b0) : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        uint32_t bits = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k)
+            if (k < nb) bits += s_enc[(w4[k >> 2] >> (8u * (k & 3u))) & 0xFFu].y;
+        const uint32_t incl = wave_incl_scan(bits);
+        if (lane == 63u) s_w[wave] = incl;
+        __syncthreads();
+        uint32_t pre = 0, T = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 16; ++k) {
+            const uint32_t x = s_w[k];
+            pre += k < wave ? x : 0u;
+            T += x;
+        }
+        if (P + T > lim) {  // (block-uniform)
+            fail = true;
+            break;
+        }
+        const uint32_t base = (uint32_t)(P & 31u);
+        if (t == 0) s_st[0] = carry;  // (word 0 holds only zeros past bit `base`)
+        __syncthreads();
+        {  // this thread's codes from stage bit base + pre + incl - bits, a 64-bit accumulator, one OR a word
+            const uint32_t pos = base + pre + incl - bits;
+            uint32_t wp = pos >> 5, fill = pos & 31u;
+            uint64_t acc = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 16; ++k) {
+                if (k < nb) {
+                    const uint2 e = s_enc[(w4[k >> 2] >> (8u * (k & 3u))) & 0xFFu];
+                    acc |= (uint64_t)e.x << (64u - fill - e.y);
+                    fill += e.y;
+                    if (fill >= 32u) {
+                        lds_or32(sbase + 4u * wp, (uint32_t)(acc >> 32));
+                        ++wp;
+                        acc <<= 32;
+                        fill -= 32u;
+                    }
+                }
+            }
+            if (fill) lds_or32(sbase + 4u * wp, (uint32_t)(acc >> 32));
+        }
+        __syncthreads();
+        const uint32_t nfull = (base + T) >> 5;
+        const uint64_t ow = P >> 5;
+        for (uint32_t k = t; k < nfull; k += 1024u) {
+            out32[ow + k] = bswap32(s_st[k]);
+            s_st[k] = 0u;
+        }
+        __syncthreads();
+        carry = s_st[nfull];
+        __syncthreads();
+        if (t < 3) s_st[nfull + t] = 0u;  // the partial word and what the last ORs may have reached
+        P += T;
+    }
+    if (fail) {
+        if (t == 0) *out_len = kFailLen;
+        return;
+    }
+    if (t == 0) {
+        const uint32_t p = (uint32_t)((0u - (uint32_t)P) & 7u);  // ones to the byte's end (EOS prefix)
+        const uint32_t sh = (uint32_t)(P & 31u);
+        uint32_t w = carry;
+        if (p) w |= (0xFFFFFFFFu >> sh) & ~(sh + p >= 32u ? 0u : 0xFFFFFFFFu >> (sh + p));
+        if (sh) out32[P >> 5] = bswap32(w);  // the last (partial) word
+        *out_len = (uint32_t)((P + 7u) >> 3);
+    }
+}
+
+hipError_t launch_encode_long(const uint8_t* in, uint32_t len, uint8_t* out, uint32_t* out_len, hipStream_t stream) {
+    hipLaunchKernelGGL(encode_long_kernel, dim3(1), dim3(1024), 0, stream, in, len, out, out_len);
+    return hipGetLastError();
+}
+
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }

@@ -16,6 +16,9 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
 // [u32 len, is_name, result len, status][input, in_cap bytes (16-aligned)][output]; len <= kOneMax
 constexpr uint32_t kOneMax = 32768;  // LDS: 32 KB input + 52 KB output beside the 32-KB table
 hipError_t launch_one(uint8_t* h, uint32_t len, uint32_t in_cap, bool is_name, bool encode, hipStream_t stream);
+// One device-resident string past kOneMax, encoded by one block (out: 4-byte aligned, at least 4 ceil(8 len / 32)
+// bytes; out_len: the code bytes or kFailLen)
+hipError_t launch_encode_long(const uint8_t* in, uint32_t len, uint8_t* out, uint32_t* out_len, hipStream_t stream);
 // Resident per-string service (hhuff_capi.hip per_string): one wave polls kSvcSlots mailboxes in pinned,
 // device-visible, coherent host memory and codes each posted string in place; it exits when `stop` is set,
 // after idle_ticks of the 100 MHz real-time counter without a request, or after max_ticks in all.

@@ -587,6 +587,9 @@ plain += [bytes(rng.choice(syms, int(L), p=p)) for L in (32768, 32769, 40000, 45
 plain += [b"a" * 3000, b"0e" * 1500, bytes(rng.integers(0, 256, 2000, dtype=np.uint8))]
 # the verdict at its edge ('&': 8 bits, 'a': 5): 8 n - 9 bits encodes, 8 n - 6 does not (hpack.c:799-800)
 plain += [b"&" * 5000 + b"aaa", b"&" * 5000 + b"aa", b"aaa" + b"&" * 7000, b"&" * 20000 + b"aa" + b"&" * 9 + b"a"]
+# past 32 KB (encode_long_kernel: 16-KB rounds, the verdict decided early, the partial word carried)
+plain += [b"&" * 40000 + b"aaa", b"&" * 40000 + b"aa", b"0e" * 30000, bytes(rng.integers(0, 256, 40000, dtype=np.uint8)),
+          b"a" * 16383 + b"&" * 16385 + b"aaa" + b"z" * 7, bytes(rng.choice(syms, 100000, p=p))]
 for s in plain:
     h = o.encode(s)
     assert codec.encode_huffman(s) == h, len(s)
@@ -602,10 +605,10 @@ print("ok", n)
 """
 
 
-@pytest.mark.parametrize("one_sync", ["0", "1"])
-def test_per_string_launch_path(torch_cuda, one_sync):
+@pytest.mark.parametrize("one_sync,long_enc", [("0", "0"), ("1", "0"), ("0", "1")])
+def test_per_string_launch_path(torch_cuda, one_sync, long_enc):
     """the launch-per-string path (HHUFF_NO_SERVICE=1: one_string_kernel up to 32 KB, the batch kernels beyond):
-    block encoder and split decoder against the oracle on the KAT strings, header text of 0-45000 B, periodic
+    block encoders and split decoder against the oracle on the KAT strings, header text of 0-100000 B, periodic
     text, random bytes, corrupted padding and the encode verdict's edge; the result taken when its length lands
     (wait_one) and after the stream synchronisation (HHUFF_ONE_SYNC=1)"""
     import os
@@ -613,7 +616,7 @@ def test_per_string_launch_path(torch_cuda, one_sync):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, HHUFF_NO_SERVICE="1", HHUFF_ONE_SYNC=one_sync)
+    env = dict(os.environ, HHUFF_NO_SERVICE="1", HHUFF_ONE_SYNC=one_sync, HHUFF_LONG_ENC=long_enc)
     r = subprocess.run([sys.executable, "-c", _LAUNCH_PATH_CHECK], cwd=root, env=env, capture_output=True, text=True,
                        timeout=240)
     assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout[-2000:] + r.stderr[-4000:]

@@ -47,3 +47,20 @@ def test_split_block_algorithm_matches_oracle(oracle_codec):
             assert got == ref, (nseg, len(h), None if ref is None else len(ref))
             rewalked += rw > 0
     assert rewalked > 0
+
+
+def test_encode_long_algorithm_matches_oracle(oracle_codec):
+    """encode_long_kernel's algorithm (tools/emu_encode_long.py, 16-KB rounds and a carried partial word; small
+    rounds here so that several are crossed quickly) against the oracle, with the verdict at its edge"""
+    import emu_encode_long as L
+
+    code, nbits = L.table()
+    rng = np.random.default_rng(41)
+    from h2o_amd import synth
+    syms, p = synth.header_alphabet()
+    cases = [b"&" * 4000 + b"aaa", b"&" * 4000 + b"aa", b"0e" * 3000, bytes(rng.integers(0, 256, 3000, dtype=np.uint8)),
+             b"a" * 1023 + b"&" * 1025 + b"aaa" + b"z" * 7, bytes(rng.choice(syms, 9000, p=p)), b"a", b"&"]
+    for s in cases:
+        for chunk, threads in ((1024, 64), (512, 32), (16384, 1024)):
+            assert L.encode_long(code, nbits, s, chunk=chunk, threads=threads) == oracle_codec.encode(s), \
+                (len(s), chunk)
