@@ -394,7 +394,7 @@ HHUFF_API int hhuff_qpack_parse_responses(const uint8_t* in, uint64_t in_size, c
 namespace {
 constexpr size_t kMeta = 32;
 #ifndef HHUFF_LONG_ENC_DEFAULT
-#define HHUFF_LONG_ENC_DEFAULT 0
+#define HHUFF_LONG_ENC_DEFAULT 1
 #endif
 uint64_t g_per_string_calls = 0;  // process-wide, atomic adds (hhuff_per_string_calls)
 
