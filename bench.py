@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--no-host", action="store_true", help="skip the H2D/D2H-inclusive measurement")
     ap.add_argument("--no-extra", action="store_true", help="skip the other configs and the per-string latency")
     ap.add_argument("--no-packed", action="store_true", help="skip the packed-output legs")
+    ap.add_argument("--force-pg", action="store_true",
+                    help="create the process group (and run the exchange) even in a world of one rank: exercises the "
+                         "RCCL branch on a one-GPU box under torch.distributed.run --nproc-per-node 1")
     return ap.parse_args()
 
 
@@ -178,15 +181,15 @@ def secondary(c):
     return r
 
 
-def timed_events(torch, fns, steps, warmup, world, dist):
-    """warm up, then time `steps` steps of fns (a list of callables, one event pair each) between barriers;
-    returns (wall ms per step, [sorted per-fn ms lists])"""
+def timed_events(torch, fns, steps, warmup, pg, dist):
+    """warm up, then time `steps` steps of fns (a list of callables, one event pair each) between barriers
+    (`pg`: a process group exists); returns (wall ms per step, [sorted per-fn ms lists])"""
     for _ in range(warmup):
         for f in fns:
             f()
     ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in fns]
           for _ in range(steps)]
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -196,7 +199,7 @@ def timed_events(torch, fns, steps, warmup, world, dist):
             f()
             b.record()
     torch.cuda.synchronize()
-    if world > 1:
+    if pg:
         dist.barrier()
     wall = (time.perf_counter() - t0) * 1e3 / steps
     per = [sorted(row[k][0].elapsed_time(row[k][1]) for row in ev) for k in range(len(fns))]
@@ -285,7 +288,10 @@ def main():
     from h2o_amd import dist as hd
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # a process group for N > 1, or (--force-pg) for a launcher-started world of one: the RCCL init, the
+    # device-tensor exchange and the MAX all_reduce then run exactly as on an 8-GPU node
+    pg = world > 1 or (args.force_pg and "WORLD_SIZE" in os.environ)
+    if pg:
         torch.cuda.set_device(local % torch.cuda.device_count())
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -338,7 +344,7 @@ def main():
     # launches alone: "issue" covers the output-byte sum and the all_gather's enqueue, "wait" the part of the
     # exchange the decode did not hide.  With RCCL the collective runs on its own stream; with gloo the
     # device-to-host copy of the sum blocks the host until the encode is done (host-synchronous, no overlap).
-    overlap = world > 1 and do_enc and do_dec
+    overlap = pg and do_enc and do_dec
     pending = []
 
     def run_encode():
@@ -368,9 +374,9 @@ def main():
         slot_enc, slot_dec = 0, 2
     else:
         fns = ([run_encode] if do_enc else []) + ([run_decode] if do_dec else []) + \
-            ([run_exchange] if world > 1 else [])
+            ([run_exchange] if pg else [])
         slot_enc, slot_dec = 0, (1 if do_enc else 0)
-    ms_step, per = timed_events(torch, fns, args.steps, args.warmup, world, dist)
+    ms_step, per = timed_events(torch, fns, args.steps, args.warmup, pg, dist)
     if args.pmc_child and args.config == "c5":  # c5's own operation, flatten_string framing, for its PMC pass
         f_out = torch.empty(P + 11 * n + 16, dtype=torch.uint8, device="cuda")
         f_len = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -399,11 +405,11 @@ def main():
         run_decode_packed()
         torch.cuda.synchronize()
         assert bool((dec_len == lens[idx].to(torch.int32)).all()), "packed decode does not invert encode"
-        pk_ms, pk = timed_events(torch, [run_encode_packed, run_decode_packed], args.steps, args.warmup, world, dist)
+        pk_ms, pk = timed_events(torch, [run_encode_packed, run_decode_packed], args.steps, args.warmup, pg, dist)
         # value: the whole batch over the slowest rank's kernel time (the same rule as the headline)
         packed = {"encode_ms": round(mean(pk[0]), 4), "decode_ms": round(mean(pk[1]), 4), "ms_per_step": round(pk_ms, 4),
                   "_kernel_ms": mean(pk[0]) + mean(pk[1])}
-    if world > 1:
+    if pg:
         vals = [ms_step] + ([packed["_kernel_ms"]] if packed is not None else [])
         t = torch.tensor(vals, device="cuda" if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -458,9 +464,11 @@ def main():
             "roofline": roof,
             "traffic_bytes_per_launch": {k: round(traffic_bytes(v)) for k, v in pmc.items() if traffic_bytes(v)} or None,
         }
-        if world > 1 and not overlap:
+        if pg:
+            line["dist_backend"] = backend
+        if pg and not overlap:
             line["exchange_ms"] = round(mean(per[-1]), 4)
-        elif world > 1:
+        elif pg:
             line["exchange_issue_ms"] = round(mean(per[1]), 4)
             line["exchange_wait_ms"] = round(mean(per[3]), 4)
             line["exchange"] = ("all_gather of (strings, encode output bytes) issued behind the encode on the RCCL "
@@ -490,7 +498,7 @@ def main():
             if not args.no_cpu_baseline:  # rank 0's host cores, on a sample of its shard (N > 1 too)
                 line["cpu_baseline"] = cpu_baseline(b, args)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 

@@ -507,7 +507,14 @@ int svc_call(int dev, bool encode, const uint8_t* src, size_t len, int is_name, 
     // spin for the result.  While the wave is alive nothing else is done; a wave that is gone (idle exit,
     // or exiting just as this request arrived) is launched again -- checked every 64 spins, so a wave that
     // is still starting up is not launched twice (svc_kick sees its stream busy)
-    if (__atomic_load_n(&S.ctrl->alive, __ATOMIC_ACQUIRE) == 0u && svc_kick(S, dev) != HHUFF_OK) return -1;
+    // a grid that is gone is launched again; once the service is broken (another thread's 5-s timeout, a
+    // failed setup) this call is not a Huffman error but a request for the launch path
+    auto revive = [&]() -> int {
+        if (__atomic_load_n(&S.ctrl->alive, __ATOMIC_ACQUIRE) != 0u) return 1;
+        if (svc_kick(S, dev) == HHUFF_OK) return 1;
+        return S.broken ? 0 : -1;
+    };
+    if (const int rv = revive(); rv <= 0) return rv;
     uint64_t spins = 0;
     const auto t0 = std::chrono::steady_clock::now();
     // {done, result, status} arrive as one 16-B store: one 16-B load sees them together
@@ -519,7 +526,7 @@ int svc_call(int dev, bool encode, const uint8_t* src, size_t len, int is_name, 
     for (load16(&sl->done, res4); res4[0] != n; load16(&sl->done, res4)) {
         ++spins;
         if ((spins & 63u) == 0u) {
-            if (__atomic_load_n(&S.ctrl->alive, __ATOMIC_ACQUIRE) == 0u && svc_kick(S, dev) != HHUFF_OK) return -1;
+            if (const int rv = revive(); rv <= 0) return rv;
             if ((spins & 4095u) == 0u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
                 // a busy device (a long batch kernel ahead of the wave) is not a HIP failure: this call and
                 // the later ones take the launch path, so a valid string is still coded
@@ -555,6 +562,9 @@ int svc_call(int dev, bool encode, const uint8_t* src, size_t len, int is_name, 
 // The one-string kernel stores its result length last (system scope, after every output word): spin on it
 // instead of waiting for the launch's completion signal, for up to 2 ms, then synchronise the stream as before
 // (which also reports a failed launch).  HHUFF_ONE_SYNC=1: always synchronise.
+// A result taken early is complete (every output word precedes the length's release store), but an error the
+// kernel raises after that store -- nothing in it runs after the store but the exit -- would surface at the
+// next synchronisation of this thread's stream, i.e. be reported against the thread's next call.
 constexpr uint32_t kOnePending = 0xFFFFFFFEu;  // never a result: lengths stay below 2^16, failures are ~0u
 static hipError_t wait_one(Ctx& c, const uint32_t* meta) {
     static const bool sync_only = [] {
@@ -865,7 +875,12 @@ int pipelined(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* 
         uint8_t* d_out = static_cast<uint8_t*>(dev_ptr(out));
         uint32_t* d_len = static_cast<uint32_t*>(dev_ptr(out_len));
         uint8_t* d_st = static_cast<uint8_t*>(dev_ptr(status));
-        if (d_in && d_off && d_out && d_len && (!status || d_st) && (!is_name_bits || d_nm)) {
+        // the kernels' 16-B staging loads / stores and dword offset loads need the device API's alignment
+        // (hhuff.h: in / out 16-B aligned, arrays 4-B aligned): an offset view of a registered socket buffer
+        // or a numpy slice takes the chunked pipeline instead, whose staged buffers are aligned
+        auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
+        const bool aligned = al(d_in, 16) && al(d_out, 16) && al(d_off, 4) && al(d_len, 4) && al(d_nm, 4);
+        if (aligned && d_in && d_off && d_out && d_len && (!status || d_st) && (!is_name_bits || d_nm)) {
             hipError_t e = decode ? hhuff::launch_decode(d_in, in_size, d_off, nullptr, n, d_nm, d_out, nullptr, d_len, d_st,
                                                          c.stream)
                                   : hhuff::launch_encode(d_in, in_size, d_off, nullptr, n, d_out, nullptr, d_len, d_st, c.stream);

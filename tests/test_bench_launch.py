@@ -91,3 +91,36 @@ def test_bench_self_spawns_two_ranks_end_to_end():
     assert 0 < line["config"]["strings_rank0"] < 262144
     assert "exchange_issue_ms" in line and "exchange_wait_ms" in line and line["dist_backend"] == "gloo"
     assert line["value"] > 0 and line["roofline"]["frac"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_rccl_branch_world_of_one():
+    """The RCCL (`nccl`) branch of bench.py and h2o_amd/dist.py on the one-GPU box: torch.distributed.run starts
+    one rank (from a process that has not touched the GPU), `--force-pg` makes that world of one create the
+    nccl process group with its device id, and the step runs the device-tensor all_gather of (strings, output
+    bytes) behind the encode (dist.exchange_sizes_async) and the MAX all_reduce of the step time -- the same
+    calls the 8-GPU run makes, on a real RCCL communicator (Missing 1)."""
+    import json
+    import socket
+    import subprocess
+
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "HHUFF_DIST_BACKEND", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "1", "--strings",
+           "262144", "--steps", "2", "--warmup", "1", "--no-extra", "--no-host", "--no-cpu-baseline", "--no-traffic",
+           "--force-pg"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-4000:]
+    line = json.loads(lines[0])
+    assert line["dist_backend"] == "nccl"
+    assert line["n_gpus"] == 1 and line["config"]["parallelism"] == "shard1"
+    assert "exchange_issue_ms" in line and "exchange_wait_ms" in line
+    assert "RCCL stream" in line["exchange"]
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0

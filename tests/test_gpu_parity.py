@@ -758,11 +758,13 @@ def test_c5_full_size_framing_vs_oracle(torch_cuda, oracle_codec):
     assert _slot_bytes_equal(torch, f_out, torch.from_numpy(o_out).cuda(), slot_off, slot_len, f_len[:n])
 
 
-@pytest.mark.parametrize("pinned", ["pageable", "pinned", "zero_copy", "pinned_dma"])
+@pytest.mark.parametrize("pinned", ["pageable", "pinned", "zero_copy", "zero_copy_offset", "pinned_dma"])
 def test_pipelined_host_path(torch_cuda, pinned, monkeypatch):
     """host -> device -> host path == the device-resident path: pageable caller buffers (chunked, staged), pinned
     data with pageable offsets (chunked DMA), everything pinned (zero copy: the kernels read and write host
-    memory), everything pinned with HHUFF_HOST_COPY=1 (the chunked DMA pipeline on pinned buffers)"""
+    memory), everything pinned with HHUFF_HOST_COPY=1 (the chunked DMA pipeline on pinned buffers), and
+    everything pinned but the byte buffers offset by 1-15 bytes (a view into a registered socket buffer: the
+    zero-copy launch needs 16-B aligned buffers, so this takes the chunked pipeline)"""
     from h2o_amd import codec
 
     torch = torch_cuda
@@ -774,7 +776,12 @@ def test_pipelined_host_path(torch_cuda, pinned, monkeypatch):
     e_out, e_len, e_st = codec.encode_batch(b["data"], off32, n, in_size=P)
     torch.cuda.synchronize()
 
+    shifts = iter([5, 3, 11, 7])  # byte-buffer offsets for zero_copy_offset, one per byte buffer
+
     def host_buf(nbytes, dt=torch.uint8, meta=False):
+        if pinned == "zero_copy_offset" and dt == torch.uint8 and not meta:
+            k = next(shifts)
+            return torch.zeros(nbytes + 16, dtype=dt, pin_memory=True).numpy()[k:k + nbytes]
         if pinned != "pageable" and (not meta or pinned != "pinned"):
             return torch.zeros(nbytes, dtype=dt, pin_memory=True).numpy()
         return np.zeros(nbytes, {torch.uint8: np.uint8, torch.int32: np.int32}[dt])
