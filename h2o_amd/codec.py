@@ -613,3 +613,12 @@ def set_decode_prices(prices, device=0):
     """pin `device`'s prices (4 floats), or restore the fitted defaults with None (hhuff_set_decode_prices)"""
     buf = None if prices is None else (ctypes.c_float * 4)(*[float(x) for x in prices])
     _check(lib().hhuff_set_decode_prices(device, buf), "hhuff_set_decode_prices")
+
+
+def set_decode_kernel(mode):
+    """which kernel decodes contiguous batches (hhuff_set_decode_kernel): 1 auto (segment kernel above a 40-B mean),
+    0 the staged / stream choice, 2 the segment kernel always; returns the previous mode"""
+    r = lib().hhuff_set_decode_kernel(int(mode))
+    if r < 0:
+        _check(r, "hhuff_set_decode_kernel")
+    return r

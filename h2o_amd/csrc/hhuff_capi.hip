@@ -1061,6 +1061,11 @@ HHUFF_API int hhuff_set_decode_prices(int device, const float* in4) {
     return r == 0 ? HHUFF_OK : hip_fail(hipErrorInvalidDevice, "hhuff_set_decode_prices");
 }
 
+HHUFF_API int hhuff_set_decode_kernel(int mode) {
+    const int r = hhuff::set_decode_kernel(mode);
+    return r < 0 ? arg_fail("decode kernel mode must be 0, 1 or 2") : r;
+}
+
 HHUFF_API int hhuff_grid_size(int device, int which) {
     DeviceGuard guard(device);
     if (guard.err != hipSuccess) return -1;

@@ -17,6 +17,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <type_traits>
 #include <vector>
@@ -3075,6 +3076,495 @@ __global__ void literal_fix_kernel(LitArgs A) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Segment decode: mixed and long strings, contiguous layout, slot output (SURVEY §7 hard part 2; VERDICT r4
+// "next" #1).  One lane per string runs a 64-string tile as long as its longest string (the staged kernel:
+// ~4x the mean on Zipf 8..512 B), and one lane per string streaming its own input and output (the stream
+// kernel) keeps ~260 B of LDS and two memory streams per lane (1.5 waves a SIMD, 1.44x write traffic).  Here
+// the lanes of a wave share the BITS of a tile evenly instead of its strings:
+//   tiles     tile t = the strings starting in bytes [t TB, (t+1) TB) of the batch (seg_plan_kernel writes
+//             tf[t], the first of them), so a tile's span is below TB + its last string; a last string longer
+//             than CAP - TB leaves the span for the split lists (split_decode_kernel) or one lane;
+//   stage     the span goes to LDS with 16-B loads, as big-endian dwords (decode_staged_kernel's stage);
+//   segments  the span's bits are cut into K <= 64 equal segments [b_k, b_k+1); lane k decodes the symbols
+//             that START in its segment, walking from one string into the next;
+//   sync      a lane cannot know where a symbol starts at b_k.  It decodes, counting only, from
+//             max(b_k - kSegLead, the start of the string holding b_k) to the first symbol boundary f_k >= b_k
+//             (Huffman codes resynchronise: on header text ~0.2 % of 256-bit leads are still off the true
+//             boundaries), then its segment into a private LDS region, stopping at e_k = the first boundary
+//             >= b_k+1.  Lane k is right iff f_k == e_k-1 and lane k - 1 is right (lane 0 starts on a string's
+//             first bit); a lane that disagrees decodes its segment again from e_k-1, until no lane changes;
+//   ends      string ends inside a segment cost no checked steps: the window's bits past the current string
+//             read as ones (13 ones are no code, and a valid string's padding is ones), so a bulk step never
+//             takes a symbol of a valid string past its end, and the long-code branch, which sees the ones,
+//             closes the string (EOS, padding rule: hpack.c:88-89, 132-133) and moves the lane to the next
+//             string's first bit.  A lane records the strings it closes (string, region offset, flags,
+//             verdict: <= kSegRecs 16-bit records in four VGPRs);
+//   finish    a wave scan places the parts that continue a string from the lane before, per-string counts,
+//             flags and first / last bytes meet in LDS (atomics), the parts move (lds_move_or) into a
+//             slot-layout stage over the dead input stage, and that goes out with 16-B stores and deferred
+//             edges (edge_fix_kernel).
+// Same results as decode_core for every string.  A sub-tile in which a lane closes more strings than it can
+// record decodes one lane per string from global memory instead (decode_direct).
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kSegLead = 256;     // bits decoded (counting only) before a segment start inside a string
+constexpr uint32_t kSegMinBits = 192;  // shortest segment (small tiles use fewer lanes)
+constexpr uint32_t kSegRecs = 8;       // string closes a lane can record
+constexpr int32_t kSegIdle = (int32_t)0x80000000;
+
+template <uint32_t CAP>
+struct SegGeom {
+    static constexpr uint32_t kInStage = CAP + 64u;                         // 16-aligned span (<= CAP + 32) + read slack
+    static constexpr uint32_t kFS = ((8u * CAP) / 5u + 48u + 15u) & ~15u;  // slot-layout output stage of a span
+    static constexpr uint32_t kStage = kFS > kInStage ? kFS : kInStage;
+    static constexpr uint32_t kSegMax = (8u * (CAP + 32u) + 63u) / 64u;  // bits of a segment at most (K = 64)
+    static constexpr uint32_t kPW = ((kSegMax + 4u) / 5u + 12u + 3u) & ~3u;  // region bytes per lane
+    static constexpr uint32_t kRegOff = 16u + kStage;
+    static constexpr uint32_t kAggOff = kRegOff + 64u * kPW;                 // cnt | flags | first | last [64] u32
+    static constexpr uint32_t kSbtOff = kAggOff + 4u * 64u * 4u;             // string start bits [68] u32
+    static constexpr uint32_t kBuf = kSbtOff + 68u * 4u;
+    static_assert(kPW <= 127u, "region offsets are 7-bit record fields");
+    static_assert(kSegMinBits <= kSegMax, "segment bound");
+};
+
+// tf[t] = the first string starting at or after byte t TB of the batch (relative to in_off[0]), t <= T, where
+// T = (in_off[n] - in_off[0]) / TB + 1 is the batch's tile count (tf[T] = n); edge records of tiles T..T_max-1
+// (the launch sized them from in_size) are cleared.
+__global__ __launch_bounds__(256) void seg_plan_kernel(const uint32_t* __restrict__ in_off, uint32_t n, uint32_t TB,
+                                                       uint32_t T_max, uint32_t* __restrict__ tf, EdgeRec* __restrict__ edges) {
+    const uint32_t base = in_off[0];
+    const uint32_t T = min((in_off[n] - base) / TB + 1u, T_max - 1u);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += stride) {
+        const uint32_t s = in_off[i] - base;
+        const uint32_t t_lo = i == 0 ? 0u : (in_off[i - 1] - base) / TB + 1u;
+        const uint32_t t_hi = i == n ? T : min(s / TB, T - 1u);
+        for (uint32_t t = t_lo; t <= t_hi; ++t) tf[t] = (uint32_t)i;
+    }
+    for (uint64_t r = 2ull * T + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < 2ull * T_max; r += stride)
+        edges[r].m = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// LDS bytes [0, ospan) to global [gbase, gbase + ospan) keeping [keep_lo, keep_hi): whole chunks with 16-B stores;
+// the first / last partial chunk into a deferred-edge record when one is given, else with byte stores (the
+// chunk a sub-tile shares with the next one of the same wave).
+__device__ __forceinline__ void region_copy_seg(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds, uint32_t ospan,
+                                                uint64_t keep_lo, uint64_t keep_hi, int lane, EdgeRec* recL, EdgeRec* recR) {
+    const uint32_t kl = ospan ? (ospan - 1u) & ~15u : 0u;
+    for (uint32_t k = (uint32_t)lane * 16u; k < ospan; k += 64u * 16u) {
+        const uint64_t g = gbase + k;
+        const uint4 v = *reinterpret_cast<const uint4*>(lds + k);
+        const bool full = g >= keep_lo && g + 16 <= keep_hi;
+        const uint32_t lo = keep_lo > g ? (uint32_t)(keep_lo - g) : 0u;
+        const uint32_t hi = keep_hi - g < 16 ? (uint32_t)(keep_hi - g) : 16u;
+        EdgeRec* r = k == 0 && recL ? recL : (k == kl && recR ? recR : nullptr);
+        if (full) {
+            *reinterpret_cast<uint4*>(out + g) = v;
+        } else if (r == nullptr) {
+            for (uint32_t b = lo; b < hi; ++b) out[g + b] = lds[k + b];
+        }
+        if (r) {
+            r->v = v;
+            r->m = make_uint4((uint32_t)g, (uint32_t)(g >> 32), full ? 0u : lo, full ? 0u : hi);
+        }
+        if (k == 0 && kl == 0 && recL && recR) recR->m = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (ospan == 0 && lane == 0) {
+        if (recL) recL->m = make_uint4(0u, 0u, 0u, 0u);
+        if (recR) recR->m = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+template <int WAVES, uint32_t CAP, uint32_t TB>
+__global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const uint32_t* __restrict__ tf, uint32_t tmax) {
+    using G = SegGeom<CAP>;
+    constexpr uint32_t kLMax = CAP - TB;  // longest string a tile keeps as its last one
+    static_assert(TB < CAP, "tile budget");
+    struct __attribute__((aligned(16))) Smem {
+        uint32_t lut[1u << HHUFF_LUT_BITS];
+        uint32_t kinfo[32];
+        uint32_t ones[(HHUFF_ONES_NENT + 3) & ~3];
+        uint8_t buf[WAVES][G::kBuf];
+    };
+    __shared__ Smem sm;
+    load_dec_tables(sm.lut, sm.kinfo, sm.ones, WAVES * 64);
+    __syncthreads();
+    const DecTables Tb{sm.lut, sm.kinfo, sm.ones};
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint8_t* const buf = sm.buf[wave];
+    uint8_t* const stage8 = buf + 16;  // input stage, then (once the walk is done) the slot-layout output stage
+    const lds_u32* st = (const lds_u32*)(uint32_t*)stage8;
+    const uint32_t fsa = lds_addr(stage8);
+    const uint32_t r0 = lds_addr(buf + G::kRegOff) + (uint32_t)lane * G::kPW;  // this lane's region
+    uint32_t* const acnt = reinterpret_cast<uint32_t*>(buf + G::kAggOff);
+    uint32_t* const aflg = acnt + 64;  // bits 0-1 invalid-char flags, 3 verdict ok, 4 closed
+    uint32_t* const afst = acnt + 128;  // (lane << 8 | first byte of the part), min over parts
+    uint32_t* const alst = acnt + 192;  // (lane << 8 | last byte of the part), max over parts
+    uint32_t* const sbt = reinterpret_cast<uint32_t*>(buf + G::kSbtOff);
+    const uint32_t n = A.n;
+    const uint32_t base = A.in_off[0];
+    const uint32_t ntiles = min((A.in_off[n] - base) / TB + 1u, tmax - 1u);  // as seg_plan_kernel
+    const uint32_t tstride = gridDim.x * WAVES;
+
+    for (uint32_t t = blockIdx.x * WAVES + wave; t < ntiles; t += tstride) {
+        const uint32_t i0 = tf[t], i1 = tf[t + 1];
+        EdgeRec* const erec = A.edges + 2ull * t;
+        if (i0 >= i1) {  // inside a long string of an earlier tile: no bytes of ours
+            if (lane == 0) erec[0].m = erec[1].m = make_uint4(0u, 0u, 0u, 0u);
+            continue;
+        }
+        for (uint32_t g0 = i0; g0 < i1; g0 += 64u) {
+            const uint32_t m = min(64u, i1 - g0);
+            const bool first_sub = g0 == i0, last_sub = g0 + 64u >= i1;
+            const bool mine = (uint32_t)lane < m;
+            const uint32_t i = g0 + min((uint32_t)lane, m - 1u);
+            const uint32_t s = A.in_off[i], e = A.in_off[i + 1];
+            const uint32_t len = e - s;
+            const bool is_name = mine && A.is_name_bits && ((A.is_name_bits[i >> 5] >> (i & 31u)) & 1u);
+            // the tile's last string, when longer than the stage allows, leaves the span
+            const bool excl = last_sub && (uint32_t)lane == m - 1u && len > kLMax;
+            const bool exl = __builtin_amdgcn_ballot_w64(excl) != 0;
+            const uint32_t mw = m - (exl ? 1u : 0u);  // strings the lanes walk
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(exl ? s : e), (int)(m - 1u));
+            const uint32_t a0 = lo & ~15u;
+            const uint32_t span = hi > lo ? ((hi + 15u) & ~15u) - a0 : 0u;
+            SpanPrefetch<(G::kInStage + 1023u) / 1024u> pf;
+            pf.issue(A.in, A.in_size, a0, span, lane);
+            const uint32_t Bb = 8u * (lo - a0), Bend = 8u * (hi - a0);
+            acnt[lane] = 0u;
+            aflg[lane] = 0u;
+            afst[lane] = 0xFFFFFFFFu;
+            alst[lane] = 0u;
+            sbt[lane] = (uint32_t)lane < mw ? 8u * (s - a0) : Bend;
+            if (lane < 4) sbt[64 + lane] = Bend;
+            pf.template commit<true>(reinterpret_cast<uint32_t*>(stage8), A.in, A.in_size, a0, span, lane);
+            wave_lds_sync();
+
+            // ---- segments ----
+            const uint32_t total = Bend - Bb;
+            const uint32_t K = total ? min(64u, (total + kSegMinBits - 1u) / kSegMinBits) : 0u;
+            const uint32_t SEG = K ? (total + K - 1u) / K : 0u;
+            const uint32_t bk = Bb + (uint32_t)lane * SEG;
+            const bool act = (uint32_t)lane < K && bk < Bend;
+            const int32_t stop = (int32_t)min(bk + SEG, Bend);
+            // the string holding bit p: the first of the strings starting at p (empty ones first), else the one p
+            // lies inside
+            auto locate = [&](uint32_t p) -> uint32_t {
+                uint32_t l = 0;  // first l with sbt[l] >= p
+#pragma unroll
+                for (uint32_t step = 32; step; step >>= 1)
+                    if (sbt[l + step - 1u] < p) l += step;
+                if (l >= mw || sbt[l] > p) l -= 1u;
+                return l;
+            };
+
+            // per-lane walk state
+            int32_t pm = 0, q = 0, lim = kSegIdle, E = 0;
+            uint32_t x0 = 0, x1 = 0, x2 = 0;
+            auto reload = [&]() {
+                q = pm >> 5;
+                x0 = st[q];
+                x1 = st[q + 1];
+                x2 = st[q + 2];
+            };
+            auto advance = [&](int32_t cons) {
+                pm += cons;
+                const int32_t qn = pm >> 5;
+                const bool adv = qn != q;
+                x0 = adv ? x1 : x0;
+                x1 = adv ? x2 : x1;
+                q = qn;
+                x2 = st[q + 2];
+            };
+            auto long_entry = [&](uint32_t w) -> uint32_t {  // the leading-ones table entry for window w
+                const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                const uint32_t ki = Tb.kinfo[k];
+                return Tb.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+            };
+
+            // ---- lead: count from max(b_k - kSegLead, string start) to the first boundary f >= b_k ----
+            uint32_t f = bk;
+            {
+                const uint32_t j = act ? locate(bk) : 0u;
+                const uint32_t Bj = act ? sbt[j] : 0u;
+                const uint32_t ls = bk - Bj <= kSegLead ? Bj : bk - kSegLead;
+                bool lend = false;
+                if (act) {
+                    pm = (int32_t)ls - 1;
+                    E = (int32_t)sbt[j + 1u];
+                    reload();
+                    lim = ls < bk ? (int32_t)bk - 26 : kSegIdle;
+                }
+                auto lstep = [&](bool longchk) {
+                    if (pm < lim) {
+                        const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                        const uint32_t e = Tb.lut[w >> (32 - HHUFF_LUT_BITS)];
+                        const uint32_t sl = (uint32_t)((int32_t)e >> 31);
+                        uint32_t cons = lut_l12(e);
+                        const uint32_t eb = Tb.lut[(w << cons) >> (32 - HHUFF_LUT_BITS)];
+                        cons += lut_l12(eb);
+                        if (longchk && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
+                            if (sl) {
+                                const int32_t L = (int32_t)((long_entry(w) >> 9) & 31u);
+                                const bool fits = L + pm < E;
+                                cons = fits ? (uint32_t)L : 0u;
+                                if (!fits) lend = true, lim = kSegIdle;
+                            }
+                        }
+                        advance((int32_t)cons);
+                    }
+                };
+                for (;;) {
+                    lstep(false);
+                    lstep(true);
+                    if (!__any(pm < lim)) break;
+                }
+                for (;;) {  // one symbol a step up to b_k
+                    const bool go = act && !lend && pm + 1 < (int32_t)bk;
+                    if (!__any(go)) break;
+                    if (go) {
+                        const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                        const uint32_t e = Tb.lut[w >> (32 - HHUFF_LUT_BITS)];
+                        const int32_t L = (int32_t)e < 0 ? (int32_t)((long_entry(w) >> 9) & 31u) : (int32_t)lut_l1(e);
+                        if (L + pm < E)
+                            advance(L);
+                        else
+                            lend = true;  // no code fits: the string's padding (its verdict is the lane before's)
+                    }
+                }
+                if (act) f = lend ? (uint32_t)E : (uint32_t)(pm + 1);
+            }
+
+            // ---- walk [f, first boundary >= stop) into the region; again from e_k-1 where lanes disagree ----
+            uint32_t o = r0, pstart = 0, nrec = 0, accb = 0, accl = 0, l = 0, lf = 0, ek = f;
+            uint64_t rlo = 0, rhi = 0;
+            bool need = act;
+            for (uint32_t round = 0;; ++round) {  // <= K + 1 rounds: lane r is final after round r
+                bool done = true;
+                if (need) {
+                    l = lf = locate(f);
+                    E = (int32_t)sbt[l + 1u];
+                    pm = (int32_t)f - 1;
+                    reload();
+                    o = r0;
+                    pstart = nrec = accb = accl = 0;
+                    rlo = rhi = 0;
+                    done = (int32_t)f >= stop || l >= mw;
+                    lim = done ? kSegIdle : stop - 26;
+                } else {
+                    lim = kSegIdle;
+                }
+                // close the current string: verdict, record, next string's first bit
+                auto close = [&](bool ok) {
+                    const uint32_t fl = ((accb >> 24) | (accb >> 26) | (accl >> 14)) & 3u;
+                    const uint32_t off = ok ? o - r0 : pstart;  // a failed string keeps no bytes
+                    const uint32_t rec = l | (off << 6) | (fl << 13) | ((ok ? 1u : 0u) << 15);
+                    rhi = (rhi << 16) | (rlo >> 48);
+                    rlo = (rlo << 16) | rec;
+                    nrec += 1u;
+                    o = r0 + off;
+                    pstart = off;
+                    accb = accl = 0;
+                    pm = E - 1;
+                    q = pm >> 5;
+                    x0 = st[q];
+                    x1 = st[q + 1];
+                    l += 1u;
+                    const bool end = l >= mw || E >= stop;
+                    E = (int32_t)sbt[l + 1u];  // l + 1 <= 65: sbt[mw..67] = Bend
+                    if (end) done = true, lim = kSegIdle;
+                };
+                auto sstep = [&](bool longchk) {
+                    if (pm < lim) {
+                        const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                        const int32_t d = E - pm - 1;  // string bits left
+                        const uint32_t wm = w | (uint32_t)(0xFFFFFFFFull >> (uint32_t)min(max(d, 0), 32));
+                        const uint32_t e = Tb.lut[wm >> (32 - HHUFF_LUT_BITS)];
+                        const uint32_t sl = (uint32_t)((int32_t)e >> 31);
+                        bulk_put2(o, e, 0u);
+                        o += (e >> 28) & 3u;
+                        accb |= e;
+                        uint32_t cons = lut_l12(e);
+                        {
+                            const uint32_t eb = Tb.lut[(wm << cons) >> (32 - HHUFF_LUT_BITS)];
+                            bulk_put2(o, eb, 0u);
+                            o += (eb >> 28) & 3u;
+                            accb |= eb;
+                            cons += lut_l12(eb);
+                        }
+                        if (longchk && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
+                            if (sl) {
+                                const uint32_t le = long_entry(wm);
+                                const int32_t L = (int32_t)((le >> 9) & 31u);
+                                const bool eos = (le & 0x1FFu) == kEos;
+                                if (L <= d && !eos) {
+                                    lds_st8(o, le);
+                                    o += 1u;
+                                    accl |= le;
+                                    cons = (uint32_t)L;
+                                } else {  // EOS inside the string (hpack.c:88-89), or no code fits: the string ends
+                                    close(!(eos && L <= d) && d >= 0 && d <= 7 && wm == 0xFFFFFFFFu);
+                                    cons = 0u;
+                                }
+                            }
+                        }
+                        advance((int32_t)cons);
+                    }
+                };
+                for (;;) {
+                    sstep(false);
+                    sstep(true);
+                    if (!__any(pm < lim)) break;
+                }
+                for (;;) {  // one symbol a step up to the stop
+                    const bool go = !done && pm + 1 < stop;
+                    if (!__any(go)) break;
+                    if (go) {
+                        const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                        const int32_t d = E - pm - 1;
+                        const uint32_t wm = w | (uint32_t)(0xFFFFFFFFull >> (uint32_t)min(max(d, 0), 32));
+                        const uint32_t e = Tb.lut[wm >> (32 - HHUFF_LUT_BITS)];
+                        uint32_t sym = e, L = lut_l1(e), fl = e & (3u << 24);
+                        bool eos = false;
+                        if ((int32_t)e < 0) {
+                            const uint32_t le = long_entry(wm);
+                            sym = le;
+                            L = (le >> 9) & 31u;
+                            fl = (le >> 14) << 24 & (3u << 24);
+                            eos = (le & 0x1FFu) == kEos;
+                        }
+                        if ((int32_t)L <= d && !eos) {
+                            lds_st8(o, sym);
+                            o += 1u;
+                            accb |= fl;
+                            advance((int32_t)L);
+                        } else {
+                            close(!(eos && (int32_t)L <= d) && d >= 0 && d <= 7 && wm == 0xFFFFFFFFu);
+                            advance(0);
+                        }
+                    }
+                }
+                // a string whose last symbol ends exactly here is closed by the lane that took that symbol (no
+                // padding bits: the next string starts here, past the stop or not)
+                if (!done && pm + 1 == E) close(true);
+                if (need) ek = (uint32_t)(pm + 1);
+                const uint32_t eprev = (uint32_t)__shfl((int)ek, lane > 0 ? lane - 1 : 0);
+                const bool mism = act && lane > 0 && f != eprev;
+                if (__builtin_amdgcn_ballot_w64(mism) == 0 || round > 65u) break;
+                need = mism;
+                if (mism) f = eprev;
+            }
+            const bool ovf = act && nrec > kSegRecs;
+            if (__builtin_amdgcn_ballot_w64(ovf) != 0) {
+                // more closes than records: one lane per string from global memory (output byte-exact)
+                if (mine && (uint32_t)lane < mw) {
+                    uint32_t ol;
+                    uint8_t stt;
+                    decode_direct(A, s, len, is_name, A.out + dec_slot(s), Tb, ol, stt);
+                    A.out_len[i] = ol;
+                    A.status[i] = stt;
+                }
+                if (lane == 0) {
+                    if (first_sub) erec[0].m = make_uint4(0u, 0u, 0u, 0u);
+                    if (last_sub) erec[1].m = make_uint4(0u, 0u, 0u, 0u);
+                }
+            } else {
+                // ---- places: the part continuing the lane before's last string follows it (affine scan) ----
+                const uint32_t tlen = act ? (o - r0) - pstart : 0u;  // the trailing part's bytes
+                const bool cont = act && f < Bend && f > sbt[lf];
+                const bool through = act && nrec == 0u;
+                const uint32_t tprev = (uint32_t)__shfl((int)tlen, lane > 0 ? lane - 1 : 0);
+                const bool thprev = __shfl((int)through, lane > 0 ? lane - 1 : 0) != 0;
+                uint32_t sa = cont && thprev && lane > 0 ? 1u : 0u, sbv = cont && lane > 0 ? tprev : 0u;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t ap = (uint32_t)__shfl_up((int)sa, d), bp = (uint32_t)__shfl_up((int)sbv, d);
+                    if (lane >= d) {
+                        sbv = sa ? bp + sbv : sbv;
+                        sa = sa & ap;
+                    }
+                }
+                const uint32_t prefix = sbv;
+                // the lane's parts, oldest first: its records, then the trailing part
+                auto part = [&](uint32_t k, uint32_t& pl, uint32_t& pend, uint32_t& pfl) {
+                    if (k < nrec) {
+                        const uint32_t sh = nrec - 1u - k;
+                        const uint32_t rec = (uint32_t)((sh < 4u ? rlo >> (16u * sh) : rhi >> (16u * (sh - 4u))) & 0xFFFFu);
+                        pl = rec & 63u;
+                        pend = (rec >> 6) & 127u;
+                        pfl = ((rec >> 13) & 3u) | (1u << 4) | ((rec >> 15) << 3);
+                    } else {
+                        pl = l;
+                        pend = o - r0;
+                        pfl = ((accb >> 24) | (accb >> 26) | (accl >> 14)) & 3u;
+                    }
+                };
+                if (act) {
+                    uint32_t ps = 0;
+                    for (uint32_t k = 0; k <= nrec; ++k) {
+                        uint32_t pl, pend, pfl;
+                        part(k, pl, pend, pfl);
+                        if (pl < mw) {
+                            atomicOr(&aflg[pl], pfl);
+                            if (pend > ps) {
+                                atomicAdd(&acnt[pl], pend - ps);
+                                atomicMin(&afst[pl], ((uint32_t)lane << 8) | lds_ld8(r0 + ps));
+                                atomicMax(&alst[pl], ((uint32_t)lane << 8) | lds_ld8(r0 + pend - 1u));
+                            }
+                        }
+                        ps = pend;
+                    }
+                }
+                const uint64_t obase = dec_slot(lo) & ~15ull;
+                const uint32_t ospan = hi > lo ? (uint32_t)(((dec_slot(hi) + 15u) & ~15ull) - obase) : 0u;
+                wave_lds_sync();
+                lds_zero(stage8, 0u, (ospan + 15u) & ~15u, lane);
+                wave_lds_sync();
+                if (act) {
+                    uint32_t ps = 0;
+                    for (uint32_t k = 0; k <= nrec; ++k) {
+                        uint32_t pl, pend, pfl;
+                        part(k, pl, pend, pfl);
+                        if (pl < mw && pend > ps && (aflg[pl] & 0x18u) == 0x18u) {
+                            const uint32_t dst = (uint32_t)(dec_slot(a0 + sbt[pl] / 8u) - obase) + (k == 0 && cont ? prefix : 0u);
+                            lds_move_or(r0 + ps, fsa + dst, pend - ps);
+                        }
+                        ps = pend;
+                    }
+                }
+                wave_lds_sync();
+                region_copy_seg(A.out, obase, stage8, ospan, dec_slot(lo), dec_slot(hi), lane, first_sub ? erec : nullptr,
+                                last_sub ? erec + 1 : nullptr);
+                if (mine && (uint32_t)lane < mw) {
+                    if (len == 0) {
+                        A.out_len[i] = 0u;
+                        A.status[i] = soft_bits(is_name, 0u, 0u, 0u, 0u);
+                    } else {
+                        const uint32_t fl = aflg[lane], cnt = acnt[lane];
+                        const bool ok = (fl & 0x18u) == 0x18u;
+                        A.out_len[i] = ok ? cnt : kFailLen;
+                        A.status[i] = ok ? soft_bits(is_name, cnt, fl & 3u, afst[lane] & 0xFFu, alst[lane] & 0xFFu) : kStatusFail;
+                    }
+                }
+            }
+            if (excl) {  // the long last string: too long, listed for split decode, or this lane
+                if (len > kMaxStrLen) {
+                    A.out_len[i] = kFailLen;
+                    A.status[i] = kStatusTooLong;
+                } else if (!split_push(A, i, len)) {
+                    uint32_t ol;
+                    uint8_t stt;
+                    decode_direct(A, s, len, is_name, A.out + dec_slot(s), Tb, ol, stt);
+                    A.out_len[i] = ol;
+                    A.status[i] = stt;
+                }
+            }
+            wave_lds_sync();
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // launch configuration (LDS per workgroup in brackets)
 //   decode staged:        16 waves/WG, 3 KiB in + 4.5 KiB out per wave   [~158 KiB, 1 WG/CU]
 //   decode staged (long):  6 waves/WG, 8 KiB in + 12.9 KiB out per wave [~144 KiB, 1 WG/CU]
@@ -3404,8 +3894,70 @@ int set_decode_prices(int device, const float* in4) {
     return 0;
 }
 
+// Segment decode (decode_seg_kernel): contiguous layout, slot output, mean string above kSegMean bytes (the staged
+// kernels keep short strings, where a 64-string tile barely waits for its longest string).  HHUFF_DEC_SEG=0 turns
+// it off (the staged / stream choice of round 4), =1 takes it for every contiguous batch (tests).
+constexpr uint32_t kSegCap = 2560, kSegTB = 1920;  // stage bytes per tile; tile budget (longest kept last string: 640)
+constexpr int kSegWaves = 12;                      // 12 x 10.3 KiB + 33.5 KiB of tables per CU
+constexpr uint64_t kSegMean = 40;
+#define DEC_G decode_seg_kernel<kSegWaves, kSegCap, kSegTB>
+static std::atomic<int> g_seg_mode{-1};
+static int seg_mode() {
+    int m = g_seg_mode.load(std::memory_order_relaxed);
+    if (m < 0) {
+        const char* v = getenv("HHUFF_DEC_SEG");
+        const int env = v && *v ? (v[0] == '0' ? 0 : (v[0] == '1' ? 2 : 1)) : 1;
+        int expect = -1;
+        g_seg_mode.compare_exchange_strong(expect, env);
+        m = g_seg_mode.load(std::memory_order_relaxed);
+    }
+    return m;
+}
+int set_decode_kernel(int mode) {
+    if (mode < 0 || mode > 2) return -1;
+    const int prev = seg_mode();
+    g_seg_mode.store(mode);
+    return prev;
+}
+static bool use_seg(uint64_t bytes, uint32_t n, const uint32_t* in_len, const uint32_t* out_off) {
+    const int m = seg_mode();
+    if (m == 0 || in_len != nullptr || out_off != nullptr || n == 0) return false;
+    return m == 2 || bytes / n > kSegMean;
+}
+static hipError_t launch_seg(DecArgs A, uint64_t in_size, uint32_t n, uint8_t* out, hipStream_t stream) {
+    const uint64_t tmax64 = in_size / kSegTB + 2u;  // tiles + 1 (the plan needs tf[T], T <= in_size / TB + 1)
+    if (tmax64 >= (1ull << 31)) return hipErrorInvalidValue;
+    const uint32_t tmax = (uint32_t)tmax64;
+    uint32_t* tf = nullptr;
+    hipError_t e = pool_alloc((void**)&tf, 4ull * tmax, stream);
+    if (e != hipSuccess) return e;
+    e = pool_alloc((void**)&A.edges, 2ull * tmax * sizeof(EdgeRec), stream);
+    if (e != hipSuccess) {
+        (void)hipFreeAsync(tf, stream);
+        return e;
+    }
+    const uint32_t pblocks = (uint32_t)std::min<uint64_t>(((uint64_t)n + 256u) / 256u, 4096u);
+    hipLaunchKernelGGL(seg_plan_kernel, dim3(pblocks), dim3(256), 0, stream, A.in_off, n, kSegTB, tmax, tf, A.edges);
+    e = hipGetLastError();
+    if (e == hipSuccess) {
+        static int cus[64] = {};
+        const int dev = current_device();
+        int& c = cus[dev >= 0 && dev < 64 ? dev : 0];
+        if (c == 0 && (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c < 1)) c = 256;
+        const uint64_t want = (tmax64 + kSegWaves - 1) / kSegWaves;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)c);
+        hipLaunchKernelGGL(DEC_G, dim3(grid), dim3(kSegWaves * 64), 0, stream, A, (const uint32_t*)tf, tmax);
+        e = finish_deferred(out, A.edges, n, stream, nullptr, 2ull * tmax);
+    } else {
+        (void)hipFreeAsync(A.edges, stream);
+    }
+    const hipError_t f = hipFreeAsync(tf, stream);
+    return e != hipSuccess ? e : f;
+}
+
 static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint32_t* in_len, uint32_t n, uint8_t* out,
                                         const uint32_t* out_off, hipStream_t stream, uint64_t sel_bytes) {
+    if (use_seg(sel_bytes ? sel_bytes : in_size, n, in_len, out_off)) return launch_seg(A, in_size, n, out, stream);
 #ifdef HHUFF_MIX_STREAM  // A/B builds: mixed lengths go to the stream kernel alone
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n) == kDecL ? (int)kDecT : pick_decode(sel_bytes ? sel_bytes : in_size, n);
 #else

@@ -363,6 +363,7 @@ def test_mixed_length_decode_select(torch_cuda, oracle_codec, lengths, verdict):
     assert 40 < hdata.size // m <= 128
     from h2o_amd import codec
 
+    prev = codec.set_decode_kernel(0)  # the staged / stream choice (the segment kernel takes these by default)
     prices = (40.0, 1.07, 184.0, 1.15)  # pinned (the fitted MI355X defaults): the verdict is fixed
     codec.set_decode_prices(prices, 0)
     assert codec.decode_prices(0) == pytest.approx(prices)
@@ -385,6 +386,7 @@ def test_mixed_length_decode_select(torch_cuda, oracle_codec, lengths, verdict):
     np.testing.assert_array_equal(g[2], o[2])
     sl = (starts.astype(np.uint64) * 8) // 5
     assert compact(g[0], out_off, g[1]) == compact(o[0], sl, o[1])
+    codec.set_decode_kernel(prev)
 
 
 def test_decode_price_calibration(torch_cuda):
