@@ -130,6 +130,14 @@ def lib():
         L.hhuff_set_decode_prices.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_float)]
         L.hhuff_pool_trim.restype = ctypes.c_int
         L.hhuff_pool_trim.argtypes = []
+        L.hhuff_set_decode_kernel.restype = ctypes.c_int
+        L.hhuff_set_decode_kernel.argtypes = [ctypes.c_int]
+        L.hhuff_decode_batch_host_packed.restype = ctypes.c_int
+        L.hhuff_decode_batch_host_packed.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64,
+                                                     _vp, _vp, _vp, ctypes.c_int]
+        L.hhuff_encode_batch_host_packed.restype = ctypes.c_int
+        L.hhuff_encode_batch_host_packed.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, ctypes.c_uint64,
+                                                     _vp, _vp, _vp, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -144,7 +152,8 @@ EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decod
             "hhuff_encode_batch_host_pipelined", "hhuff_version", "hhuff_last_error_string", "hhuff_per_string_calls",
             "hhuff_grid_size", "hhuff_decode_prices", "hhuff_calibrate_decode_prices", "hhuff_set_decode_prices",
             "hhuff_pool_trim", "hhuff_service_stamps", "hhuff_hpack_enc_scratch_size",
-            "hhuff_hpack_flatten_responses", "hhuff_qpack_flatten_responses")
+            "hhuff_hpack_flatten_responses", "hhuff_qpack_flatten_responses", "hhuff_set_decode_kernel",
+            "hhuff_decode_batch_host_packed", "hhuff_encode_batch_host_packed")
 
 
 def _check(rc, what):
@@ -535,6 +544,14 @@ def hpack_flatten_responses(data, hdr, res, conn_first, nres, out_off, server_of
 # ---------------------------------------------------------------------------------------------------
 # host batch API (numpy arrays; H2D/D2H inside the library)
 # ---------------------------------------------------------------------------------------------------
+def _np(a, dt):
+    """a C-contiguous numpy view of `a` with dtype dt (u32 data may arrive as int32)"""
+    a = np.asarray(a)
+    if a.dtype != dt:
+        a = a.view(dt) if a.dtype.itemsize == np.dtype(dt).itemsize else a.astype(dt)
+    return np.ascontiguousarray(a)
+
+
 def _hp(a):
     if a is None:
         return None
@@ -592,6 +609,36 @@ def encode_batch_host_pipelined(data, in_off, n, out=None, chunk_bytes=0, device
                                                    _hp(out_len), _hp(status), device, chunk_bytes),
            "hhuff_encode_batch_host_pipelined")
     return out, out_len[:n], status[:n]
+
+
+def decode_batch_host_packed(data, in_off, n, is_name_bits=None, out=None, device=0, out_off=None, out_len=None,
+                             status=None):
+    """hhuff_decode_batch_host_packed on numpy arrays: the packed layout (tile runs, out_off[n + 1]); pinned arrays are
+    read and written by the kernels in place (zero copy).  Returns (out, out_off[:n + 1], out_len[:n], status[:n])"""
+    data, in_off = _np(data, np.uint8), _np(in_off, np.uint32)
+    size = decode_slot_size(int(in_off[n]))
+    out = np.zeros(size, np.uint8) if out is None else out
+    out_off = np.zeros(n + 1, np.uint32) if out_off is None else out_off
+    out_len = np.zeros(max(1, n), np.uint32) if out_len is None else out_len
+    status = np.zeros(max(1, n), np.uint8) if status is None else status
+    names = None if is_name_bits is None else _np(is_name_bits, np.uint32)
+    _check(lib().hhuff_decode_batch_host_packed(_hp(data), data.size, _hp(in_off), n, _hp(names), _hp(out), out.size,
+                                                _hp(out_off), _hp(out_len), _hp(status), device),
+           "hhuff_decode_batch_host_packed")
+    return out, out_off[:n + 1], out_len[:n], status[:n]
+
+
+def encode_batch_host_packed(data, in_off, n, out=None, device=0, out_off=None, out_len=None, status=None):
+    """hhuff_encode_batch_host_packed on numpy arrays (see decode_batch_host_packed)"""
+    data, in_off = _np(data, np.uint8), _np(in_off, np.uint32)
+    out = np.zeros(int(in_off[n]) + 16, np.uint8) if out is None else out
+    out_off = np.zeros(n + 1, np.uint32) if out_off is None else out_off
+    out_len = np.zeros(max(1, n), np.uint32) if out_len is None else out_len
+    status = np.zeros(max(1, n), np.uint8) if status is None else status
+    _check(lib().hhuff_encode_batch_host_packed(_hp(data), data.size, _hp(in_off), n, _hp(out), out.size, _hp(out_off),
+                                                _hp(out_len), _hp(status), device),
+           "hhuff_encode_batch_host_packed")
+    return out, out_off[:n + 1], out_len[:n], status[:n]
 
 
 def decode_prices(device=0):

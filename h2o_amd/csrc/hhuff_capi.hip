@@ -985,7 +985,91 @@ int pipelined(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* 
     return HHUFF_OK;
 }
 
+// (3c) packed host path: the packed kernels (hhuff_*_batch_packed) on host buffers.  With every caller array pinned
+// and aligned the kernels read the strings and write only the outputs' bytes, out_off, out_len and status across
+// PCIe (zero copy; the slot layout's tails, ~45 % of a decode slot and ~25 % of an encode slot on header text,
+// never cross the link); otherwise one staged round trip through device memory.
+int host_packed(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+                const uint32_t* is_name_bits, uint8_t* out, uint64_t out_size, uint32_t* out_off, uint32_t* out_len,
+                uint8_t* status, int device) {
+    if (n == 0) return HHUFF_OK;
+    if (!in || !in_off || !out || !out_off || !out_len || (decode && !status)) return arg_fail("NULL array");
+    if (in_off[n] > in_size) return arg_fail("in_off[n] > in_size");
+    const uint64_t slot_end = decode ? ((uint64_t)in_off[n] * 8) / 5 : in_off[n];
+    if (out_size < slot_end) return arg_fail("out_size below the output slots of the batch");
+    if ((decode ? (in_size * 8) / 5 : in_size) >= 0xFFFFFFFFull) return arg_fail("in_size too large for u32 packed offsets");
+    DeviceGuard guard(device);
+    if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+    Ctx& c = t_ctx;
+    int rc = c.bind(device);
+    if (rc) return rc;
+    auto dev_ptr = [](const void* p) -> void* {
+        if (!p) return nullptr;
+        hipPointerAttribute_t a;
+        if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
+    };
+    auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
+    const uint8_t* z_in = static_cast<const uint8_t*>(dev_ptr(in));
+    const uint32_t* z_off = static_cast<const uint32_t*>(dev_ptr(in_off));
+    const uint32_t* z_nm = static_cast<const uint32_t*>(dev_ptr(is_name_bits));
+    uint8_t* z_out = static_cast<uint8_t*>(dev_ptr(out));
+    uint32_t* z_ooff = static_cast<uint32_t*>(dev_ptr(out_off));
+    uint32_t* z_len = static_cast<uint32_t*>(dev_ptr(out_len));
+    uint8_t* z_st = static_cast<uint8_t*>(dev_ptr(status));
+    const bool zero = z_in && z_off && (!is_name_bits || z_nm) && z_out && z_ooff && z_len && (!status || z_st) &&
+                      al(z_in, 16) && al(z_out, 16) && al(z_off, 4) && al(z_nm, 4) && al(z_ooff, 4) && al(z_len, 4);
+    hipStream_t s = c.stream;
+    if (zero) {
+        hipError_t e = decode ? hhuff::launch_decode_packed(z_in, in_size, z_off, n, z_nm, z_out, z_ooff, z_len, z_st, s)
+                              : hhuff::launch_encode_packed(z_in, in_size, z_off, n, z_out, z_ooff, z_len, z_st, s);
+        if (e != hipSuccess) return hip_fail(e, decode ? "packed decode launch (zero copy)" : "packed encode launch (zero copy)");
+        HIP_TRY(hipStreamSynchronize(s), "sync");
+        return HHUFF_OK;
+    }
+    const size_t nw = ((size_t)n + 31) / 32;
+    const size_t need = up16(in_size ? in_size : 1) + up16(((size_t)n + 1) * 4) + (is_name_bits ? up16(nw * 4) : 0) +
+                        up16(slot_end + 16) + up16(((size_t)n + 1) * 4) + up16((size_t)n * 4) + up16(n);
+    rc = c.reserve(need, 0);
+    if (rc) return rc;
+    Carve cv{c.d};
+    uint8_t* d_in = cv.take<uint8_t>(in_size ? in_size : 1);
+    uint32_t* d_off = cv.take<uint32_t>((size_t)n + 1);
+    uint32_t* d_nm = is_name_bits ? cv.take<uint32_t>(nw) : nullptr;
+    uint8_t* d_out = cv.take<uint8_t>(slot_end + 16);
+    uint32_t* d_ooff = cv.take<uint32_t>((size_t)n + 1);
+    uint32_t* d_len = cv.take<uint32_t>(n);
+    uint8_t* d_st = cv.take<uint8_t>(n);
+    HIP_TRY(hipMemcpyAsync(d_in, in, in_size, hipMemcpyHostToDevice, s), "H2D in");
+    HIP_TRY(hipMemcpyAsync(d_off, in_off, ((size_t)n + 1) * 4, hipMemcpyHostToDevice, s), "H2D in_off");
+    if (is_name_bits) HIP_TRY(hipMemcpyAsync(d_nm, is_name_bits, nw * 4, hipMemcpyHostToDevice, s), "H2D is_name");
+    hipError_t e = decode ? hhuff::launch_decode_packed(d_in, in_size, d_off, n, d_nm, d_out, d_ooff, d_len, d_st, s)
+                          : hhuff::launch_encode_packed(d_in, in_size, d_off, n, d_out, d_ooff, d_len, status ? d_st : nullptr, s);
+    if (e != hipSuccess) return hip_fail(e, decode ? "packed decode launch" : "packed encode launch");
+    HIP_TRY(hipMemcpyAsync(out, d_out, slot_end, hipMemcpyDeviceToHost, s), "D2H out");
+    HIP_TRY(hipMemcpyAsync(out_off, d_ooff, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, s), "D2H out_off");
+    HIP_TRY(hipMemcpyAsync(out_len, d_len, (size_t)n * 4, hipMemcpyDeviceToHost, s), "D2H out_len");
+    if (status) HIP_TRY(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, s), "D2H status");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    return HHUFF_OK;
+}
+
 }  // namespace
+
+HHUFF_API int hhuff_decode_batch_host_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+                                             const uint32_t* is_name_bits, uint8_t* out, uint64_t out_size, uint32_t* out_off,
+                                             uint32_t* out_len, uint8_t* status, int device) {
+    return host_packed(true, in, in_size, in_off, n, is_name_bits, out, out_size, out_off, out_len, status, device);
+}
+
+HHUFF_API int hhuff_encode_batch_host_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
+                                             uint8_t* out, uint64_t out_size, uint32_t* out_off, uint32_t* out_len,
+                                             uint8_t* status, int device) {
+    return host_packed(false, in, in_size, in_off, n, nullptr, out, out_size, out_off, out_len, status, device);
+}
 
 HHUFF_API int hhuff_decode_batch_host_pipelined(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
                                                 const uint32_t* is_name_bits, uint8_t* out, uint64_t out_size,

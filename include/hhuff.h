@@ -518,6 +518,20 @@ int hhuff_encode_batch_host_pipelined(const uint8_t *in, uint64_t in_size, const
                                       uint8_t *out, uint64_t out_size, uint32_t *out_len, uint8_t *status,
                                       int device, uint64_t chunk_bytes);
 
+/* (3c) Packed host path: hhuff_decode_batch_packed / hhuff_encode_batch_packed on host arrays (same layout: every
+ *     64-string tile's outputs back to back from the tile's slot position, out_off[n + 1]).  Contiguous layout.
+ *     With every array pinned (hipHostMalloc / hipHostRegister), `in` and `out` 16-byte aligned and the u32 arrays
+ *     4-byte aligned, the kernels read the input and write the results in host memory themselves and only the
+ *     output bytes cross PCIe (the slot layout's unused slot tails do not); otherwise the call stages the batch
+ *     through device memory.  out_size >= the slot end (decode floor(8 in_off[n] / 5), encode in_off[n]).
+ *     Synchronous. */
+int hhuff_decode_batch_host_packed(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, uint32_t n,
+                                   const uint32_t *is_name_bits, uint8_t *out, uint64_t out_size, uint32_t *out_off,
+                                   uint32_t *out_len, uint8_t *status, int device);
+int hhuff_encode_batch_host_packed(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, uint32_t n,
+                                   uint8_t *out, uint64_t out_size, uint32_t *out_off, uint32_t *out_len,
+                                   uint8_t *status, int device);
+
 /* ---------------------------------------------------------------------------------------------
  * (4) library info
  * ------------------------------------------------------------------------------------------- */

@@ -820,6 +820,75 @@ def test_pipelined_host_path(torch_cuda, pinned, monkeypatch):
     assert (h_len != FAIL).sum() > n // 10  # slot tails make most of these garbage; parity is the point
 
 
+@pytest.mark.parametrize("kind", ["zero_copy", "zero_copy_offset", "pageable"])
+def test_host_packed_path(torch_cuda, kind):
+    """hhuff_{en,de}code_batch_host_packed == the device packed API: pinned aligned arrays (zero copy: only the
+    output bytes cross PCIe), pinned byte buffers at odd offsets and pageable arrays (staged through the device)"""
+    from h2o_amd import codec
+
+    torch = torch_cuda
+    b = synth.make_batch_torch("c4", n=1 << 18, seed=29)
+    n, P = b["n"], int(b["total"])
+    off32 = b["off"].to(torch.int32)
+    de_out = torch.zeros(P + 16, dtype=torch.uint8, device="cuda")
+    de_off = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
+    de_out, de_off, de_len, de_st = codec.encode_batch_packed(b["data"], off32, n, out=de_out, out_off=de_off, in_size=P)
+    torch.cuda.synchronize()
+    shifts = iter([5, 3, 11, 7, 9, 13])
+
+    def hbuf(count, dt):
+        npdt = {torch.uint8: np.uint8, torch.int32: np.int32}[dt]
+        if kind == "pageable":
+            return np.zeros(count, npdt)
+        if kind == "zero_copy_offset" and dt == torch.uint8:
+            k = next(shifts)
+            return torch.zeros(count + 16, dtype=dt, pin_memory=True).numpy()[k:k + count]
+        return torch.zeros(count, dtype=dt, pin_memory=True).numpy()
+
+    data = hbuf(P, torch.uint8)
+    data[:] = b["data"].cpu().numpy()
+    off = hbuf(n + 1, torch.int32).view(np.uint32)
+    off[:] = off32.cpu().numpy().view(np.uint32)
+    out, ooff, olen, ost = codec.encode_batch_host_packed(
+        data, off, n, out=hbuf(P + 16, torch.uint8), out_off=hbuf(n + 1, torch.int32).view(np.uint32),
+        out_len=hbuf(n, torch.int32).view(np.uint32), status=hbuf(n, torch.uint8))
+    g_len = de_len.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(olen, g_len)
+    np.testing.assert_array_equal(ost, de_st.cpu().numpy())
+    np.testing.assert_array_equal(ooff, de_off.cpu().numpy().view(np.uint32))
+    assert compact(out, ooff[:n], olen) == compact(de_out.cpu().numpy(), ooff[:n], g_len)
+    # decode the compressible strings packed back to back (the wire) both ways
+    ok = np.nonzero(g_len != FAIL)[0]
+    hl = g_len[ok].astype(np.int64)
+    h_off = np.zeros(hl.size + 1, np.int64)
+    h_off[1:] = np.cumsum(hl)
+    huff_np = _gather(de_out.cpu().numpy(), ooff[:n], g_len)
+    m, H = int(hl.size), int(h_off[-1])
+    names = synth.bits_from_bools(np.random.default_rng(3).random(m) < 0.3)
+    dd_out = torch.zeros(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
+    dd_off = torch.zeros(m + 1, dtype=torch.int32, device="cuda")
+    dd_out, dd_off, dd_len, dd_st = codec.decode_batch_packed(_dev(torch, huff_np), _dev(torch, h_off.astype(np.uint32)),
+                                                              m, is_name_bits=_dev(torch, names), out=dd_out,
+                                                              out_off=dd_off, in_size=H)
+    torch.cuda.synchronize()
+    src = hbuf(H, torch.uint8)
+    src[:] = huff_np
+    hoff = hbuf(m + 1, torch.int32).view(np.uint32)
+    hoff[:] = h_off.astype(np.uint32)
+    hn = hbuf(names.size, torch.int32).view(np.uint32)
+    hn[:] = names
+    out, ooff, olen, ost = codec.decode_batch_host_packed(
+        src, hoff, m, is_name_bits=hn, out=hbuf(codec.decode_slot_size(H), torch.uint8),
+        out_off=hbuf(m + 1, torch.int32).view(np.uint32), out_len=hbuf(m, torch.int32).view(np.uint32),
+        status=hbuf(m, torch.uint8))
+    d_len = dd_len.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(olen, d_len)
+    np.testing.assert_array_equal(ost, dd_st.cpu().numpy())
+    np.testing.assert_array_equal(ooff, dd_off.cpu().numpy().view(np.uint32))
+    assert compact(out, ooff[:m], olen) == compact(dd_out.cpu().numpy(), ooff[:m], d_len)
+    assert int((olen != FAIL).sum()) == m
+
+
 # ------------------------------------------------------------------------------------------------
 # string literals in header blocks (HPACK decode_string, QPACK literal decode)
 # ------------------------------------------------------------------------------------------------
