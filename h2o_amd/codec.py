@@ -663,8 +663,8 @@ def set_decode_prices(prices, device=0):
 
 
 def set_decode_kernel(mode):
-    """which kernel decodes contiguous batches (hhuff_set_decode_kernel): 1 auto (segment kernel above a 40-B mean),
-    0 the staged / stream choice, 2 the segment kernel always; returns the previous mode"""
+    """which kernel decodes contiguous batches (hhuff_set_decode_kernel): 0 (default) the staged / stream choice,
+    1 the segment kernel above a 40-B mean, 2 the segment kernel always; returns the previous mode"""
     r = lib().hhuff_set_decode_kernel(int(mode))
     if r < 0:
         _check(r, "hhuff_set_decode_kernel")

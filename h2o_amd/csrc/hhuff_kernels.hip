@@ -3106,7 +3106,10 @@ __global__ void literal_fix_kernel(LitArgs A) {
 // Same results as decode_core for every string.  A sub-tile in which a lane closes more strings than it can
 // record decodes one lane per string from global memory instead (decode_direct).
 // ------------------------------------------------------------------------------------------------
-constexpr uint32_t kSegLead = 256;     // bits decoded (counting only) before a segment start inside a string
+#ifndef HHUFF_SEG_LEAD
+#define HHUFF_SEG_LEAD 256
+#endif
+constexpr uint32_t kSegLead = HHUFF_SEG_LEAD;  // bits decoded (counting only) before a segment start inside a string
 constexpr uint32_t kSegMinBits = 192;  // shortest segment (small tiles use fewer lanes)
 constexpr uint32_t kSegRecs = 8;       // string closes a lane can record
 constexpr int32_t kSegIdle = (int32_t)0x80000000;
@@ -3204,12 +3207,55 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
     const uint32_t base = A.in_off[0];
     const uint32_t ntiles = min((A.in_off[n] - base) / TB + 1u, tmax - 1u);  // as seg_plan_kernel
     const uint32_t tstride = gridDim.x * WAVES;
+    PROF_DECL  // profile builds: setup / lead / bulk / checked / places+moves / copy-out / fallback, slot 0
 
-    for (uint32_t t = blockIdx.x * WAVES + wave; t < ntiles; t += tstride) {
-        const uint32_t i0 = tf[t], i1 = tf[t + 1];
+    using PF = SpanPrefetch<(G::kInStage + 1023u) / 1024u>;
+    // Tiles in batches of 64 per wave (lane j: tile tb + j tstride): string range and span (after the last
+    // string's exclusion) come in one round of loads per batch; then each tile's offsets and span are loaded
+    // into registers while the tile before is decoded, and waited for before that tile's stores (loads and
+    // stores complete in order on gfx950: a load waited for behind stores would wait for them too).
+    for (uint32_t tb = blockIdx.x * WAVES + wave; tb < ntiles; tb += 64u * tstride) {
+        const uint32_t nt = min(64u, (ntiles - tb + tstride - 1u) / tstride);
+        const uint32_t tj = tb + min((uint32_t)lane, nt - 1u) * tstride;
+        const uint32_t ti0 = tf[tj], ti1 = tf[tj + 1u];
+        const uint32_t tlo = A.in_off[ti0], thi = A.in_off[ti1], tpl = A.in_off[ti1 > ti0 ? ti1 - 1u : ti0];
+        const bool tex = ti1 > ti0 && thi - tpl > kLMax;  // the tile's last string leaves the span
+        const uint32_t thi2 = tex ? tpl : thi;
+        const uint64_t texm = __builtin_amdgcn_ballot_w64(tex);
+        PF pf;
+        uint32_t nx_s = 0, nx_e = 0, nx_nm = 0;
+        auto issue = [&](uint32_t j) {  // tile j's first 64 strings' offsets and its span, into registers
+            const uint32_t i0 = (uint32_t)__builtin_amdgcn_readlane((int)ti0, (int)j);
+            const uint32_t i1 = (uint32_t)__builtin_amdgcn_readlane((int)ti1, (int)j);
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)tlo, (int)j);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)thi2, (int)j);
+            const uint32_t m = min(64u, i1 - i0);
+            const uint32_t i = min(i0 + min((uint32_t)lane, m ? m - 1u : 0u), n - 1u);
+            nx_s = A.in_off[i];
+            nx_e = A.in_off[i + 1u];
+            nx_nm = A.is_name_bits ? A.is_name_bits[i >> 5] : 0u;
+            const uint32_t a0 = lo & ~15u;
+            pf.issue(A.in, A.in_size, a0, hi > lo ? ((hi + 15u) & ~15u) - a0 : 0u, lane);
+        };
+        auto consume_next = [&]() {  // wait for the prefetched registers (before a tile's stores)
+            __asm__ volatile("" : : "v"(nx_s), "v"(nx_e), "v"(nx_nm));
+#pragma unroll
+            for (int c = 0; c < (int)((G::kInStage + 1023u) / 1024u); ++c)
+                __asm__ volatile("" : : "v"(pf.v[c].x), "v"(pf.v[c].y), "v"(pf.v[c].z), "v"(pf.v[c].w));
+        };
+        issue(0u);
+    for (uint32_t j = 0; j < nt; ++j) {
+        const uint32_t t = tb + j * tstride;
+        const uint32_t i0 = (uint32_t)__builtin_amdgcn_readlane((int)ti0, (int)j);
+        const uint32_t i1 = (uint32_t)__builtin_amdgcn_readlane((int)ti1, (int)j);
+        const uint32_t t_lo = (uint32_t)__builtin_amdgcn_readlane((int)tlo, (int)j);
+        const uint32_t t_hi = (uint32_t)__builtin_amdgcn_readlane((int)thi2, (int)j);
+        const bool t_ex = ((texm >> j) & 1ull) != 0;
+        const uint32_t c_s = nx_s, c_e = nx_e, c_nm = nx_nm;  // this tile's prefetched offsets (first 64 strings)
         EdgeRec* const erec = A.edges + 2ull * t;
         if (i0 >= i1) {  // inside a long string of an earlier tile: no bytes of ours
             if (lane == 0) erec[0].m = erec[1].m = make_uint4(0u, 0u, 0u, 0u);
+            if (j + 1u < nt) issue(j + 1u);
             continue;
         }
         for (uint32_t g0 = i0; g0 < i1; g0 += 64u) {
@@ -3217,19 +3263,22 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
             const bool first_sub = g0 == i0, last_sub = g0 + 64u >= i1;
             const bool mine = (uint32_t)lane < m;
             const uint32_t i = g0 + min((uint32_t)lane, m - 1u);
-            const uint32_t s = A.in_off[i], e = A.in_off[i + 1];
+            uint32_t s = c_s, e = c_e, nmw = c_nm;
+            if (!first_sub) {  // later sub-tiles of a tile of more than 64 strings: loaded here
+                s = A.in_off[i];
+                e = A.in_off[i + 1];
+                nmw = A.is_name_bits ? A.is_name_bits[i >> 5] : 0u;
+            }
             const uint32_t len = e - s;
-            const bool is_name = mine && A.is_name_bits && ((A.is_name_bits[i >> 5] >> (i & 31u)) & 1u);
+            const bool is_name = mine && A.is_name_bits && ((nmw >> (i & 31u)) & 1u);
             // the tile's last string, when longer than the stage allows, leaves the span
-            const bool excl = last_sub && (uint32_t)lane == m - 1u && len > kLMax;
-            const bool exl = __builtin_amdgcn_ballot_w64(excl) != 0;
+            const bool exl = last_sub && t_ex;
+            const bool excl = exl && (uint32_t)lane == m - 1u;
             const uint32_t mw = m - (exl ? 1u : 0u);  // strings the lanes walk
-            const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
-            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(exl ? s : e), (int)(m - 1u));
+            const uint32_t lo = first_sub ? t_lo : (uint32_t)__builtin_amdgcn_readfirstlane((int)s);
+            const uint32_t hi = last_sub ? t_hi : (uint32_t)__builtin_amdgcn_readlane((int)e, (int)(m - 1u));
             const uint32_t a0 = lo & ~15u;
             const uint32_t span = hi > lo ? ((hi + 15u) & ~15u) - a0 : 0u;
-            SpanPrefetch<(G::kInStage + 1023u) / 1024u> pf;
-            pf.issue(A.in, A.in_size, a0, span, lane);
             const uint32_t Bb = 8u * (lo - a0), Bend = 8u * (hi - a0);
             acnt[lane] = 0u;
             aflg[lane] = 0u;
@@ -3237,9 +3286,17 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
             alst[lane] = 0u;
             sbt[lane] = (uint32_t)lane < mw ? 8u * (s - a0) : Bend;
             if (lane < 4) sbt[64 + lane] = Bend;
-            pf.template commit<true>(reinterpret_cast<uint32_t*>(stage8), A.in, A.in_size, a0, span, lane);
+            if (first_sub) {
+                pf.template commit<true>(reinterpret_cast<uint32_t*>(stage8), A.in, A.in_size, a0, span, lane);
+                if (j + 1u < nt) issue(j + 1u);  // in flight during this tile's walk
+            } else {
+                PF pf2;
+                pf2.issue(A.in, A.in_size, a0, span, lane);
+                pf2.template commit<true>(reinterpret_cast<uint32_t*>(stage8), A.in, A.in_size, a0, span, lane);
+            }
             wave_lds_sync();
 
+            PROF_MARK(0);
             // ---- segments ----
             const uint32_t total = Bend - Bb;
             const uint32_t K = total ? min(64u, (total + kSegMinBits - 1u) / kSegMinBits) : 0u;
@@ -3334,6 +3391,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
                 }
                 if (act) f = lend ? (uint32_t)E : (uint32_t)(pm + 1);
             }
+            PROF_MARK(1);
 
             // ---- walk [f, first boundary >= stop) into the region; again from e_k-1 where lanes disagree ----
             uint32_t o = r0, pstart = 0, nrec = 0, accb = 0, accl = 0, l = 0, lf = 0, ek = f;
@@ -3416,6 +3474,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
                     sstep(true);
                     if (!__any(pm < lim)) break;
                 }
+                PROF_MARK(2);
                 for (;;) {  // one symbol a step up to the stop
                     const bool go = !done && pm + 1 < stop;
                     if (!__any(go)) break;
@@ -3448,6 +3507,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
                 // padding bits: the next string starts here, past the stop or not)
                 if (!done && pm + 1 == E) close(true);
                 if (need) ek = (uint32_t)(pm + 1);
+                PROF_MARK(3);
                 const uint32_t eprev = (uint32_t)__shfl((int)ek, lane > 0 ? lane - 1 : 0);
                 const bool mism = act && lane > 0 && f != eprev;
                 if (__builtin_amdgcn_ballot_w64(mism) == 0 || round > 65u) break;
@@ -3468,6 +3528,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
                     if (first_sub) erec[0].m = make_uint4(0u, 0u, 0u, 0u);
                     if (last_sub) erec[1].m = make_uint4(0u, 0u, 0u, 0u);
                 }
+                PROF_MARK(6);
             } else {
                 // ---- places: the part continuing the lane before's last string follows it (affine scan) ----
                 const uint32_t tlen = act ? (o - r0) - pstart : 0u;  // the trailing part's bytes
@@ -3518,6 +3579,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
                 const uint64_t obase = dec_slot(lo) & ~15ull;
                 const uint32_t ospan = hi > lo ? (uint32_t)(((dec_slot(hi) + 15u) & ~15ull) - obase) : 0u;
                 wave_lds_sync();
+#ifndef HHUFF_SEG_NOFIN  // ablation builds: no moves and no copy-out (output wrong by design)
                 lds_zero(stage8, 0u, (ospan + 15u) & ~15u, lane);
                 wave_lds_sync();
                 if (act) {
@@ -3533,8 +3595,17 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
                     }
                 }
                 wave_lds_sync();
+                consume_next();
+                PROF_MARK(4);
                 region_copy_seg(A.out, obase, stage8, ospan, dec_slot(lo), dec_slot(hi), lane, first_sub ? erec : nullptr,
                                 last_sub ? erec + 1 : nullptr);
+#else
+                consume_next();
+                if (lane == 0) {
+                    if (first_sub) erec[0].m = make_uint4(0u, 0u, 0u, 0u);
+                    if (last_sub) erec[1].m = make_uint4(0u, 0u, 0u, 0u);
+                }
+#endif
                 if (mine && (uint32_t)lane < mw) {
                     if (len == 0) {
                         A.out_len[i] = 0u;
@@ -3547,6 +3618,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
                     }
                 }
             }
+            PROF_MARK(5);
             if (excl) {  // the long last string: too long, listed for split decode, or this lane
                 if (len > kMaxStrLen) {
                     A.out_len[i] = kFailLen;
@@ -3562,6 +3634,8 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
             wave_lds_sync();
         }
     }
+    }
+    PROF_FLUSH(0);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3894,11 +3968,18 @@ int set_decode_prices(int device, const float* in4) {
     return 0;
 }
 
-// Segment decode (decode_seg_kernel): contiguous layout, slot output, mean string above kSegMean bytes (the staged
-// kernels keep short strings, where a 64-string tile barely waits for its longest string).  HHUFF_DEC_SEG=0 turns
-// it off (the staged / stream choice of round 4), =1 takes it for every contiguous batch (tests).
-constexpr uint32_t kSegCap = 2560, kSegTB = 1920;  // stage bytes per tile; tile budget (longest kept last string: 640)
-constexpr int kSegWaves = 12;                      // 12 x 10.3 KiB + 33.5 KiB of tables per CU
+// Segment decode (decode_seg_kernel) is a selectable alternative, not the default: measured against the stream kernel
+// in one process on c3 (1M Zipf strings) 0.343 vs 0.290 ms and on c5 0.65 vs 0.45 ms (profiles/r05*_dec_ab.jsonl,
+// DESIGN (e)).  Modes (hhuff_set_decode_kernel / HHUFF_DEC_SEG): 0 (default) the staged / stream choice, 1 the
+// segment kernel for contiguous batches with a mean string above kSegMean bytes, 2 for every contiguous batch.
+#ifndef HHUFF_SEG_CAP  // A/B builds: stage bytes per tile, tile budget, waves per CU
+#define HHUFF_SEG_CAP 2560
+#define HHUFF_SEG_TB 1920
+#define HHUFF_SEG_WAVES 12
+#endif
+constexpr uint32_t kSegCap = HHUFF_SEG_CAP, kSegTB = HHUFF_SEG_TB;  // stage bytes per tile; tile budget (longest kept
+                                                                   // last string: CAP - TB = 640)
+constexpr int kSegWaves = HHUFF_SEG_WAVES;                         // 12 x 10.3 KiB + 33.5 KiB of tables per CU
 constexpr uint64_t kSegMean = 40;
 #define DEC_G decode_seg_kernel<kSegWaves, kSegCap, kSegTB>
 static std::atomic<int> g_seg_mode{-1};
@@ -3906,7 +3987,7 @@ static int seg_mode() {
     int m = g_seg_mode.load(std::memory_order_relaxed);
     if (m < 0) {
         const char* v = getenv("HHUFF_DEC_SEG");
-        const int env = v && *v ? (v[0] == '0' ? 0 : (v[0] == '1' ? 2 : 1)) : 1;
+        const int env = v && *v ? (v[0] == '2' ? 2 : (v[0] == '1' ? 1 : 0)) : 0;
         int expect = -1;
         g_seg_mode.compare_exchange_strong(expect, env);
         m = g_seg_mode.load(std::memory_order_relaxed);

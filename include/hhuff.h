@@ -554,9 +554,10 @@ int hhuff_calibrate_decode_prices(int device, float *out4);
 int hhuff_set_decode_prices(int device, const float *in4);
 int hhuff_grid_size(int device, int which /* 0 decode, 1 encode */);
 /* Which kernel decodes contiguous batches (process-wide; the results are the same, only the speed differs):
- * 1 (default) the segment kernel for a mean Huffman length above 40 B, the staged kernels below; 0 the staged /
- * stream choice of earlier versions; 2 the segment kernel for every contiguous batch.  The HHUFF_DEC_SEG
- * environment variable sets the start value.  Returns the previous mode, or HHUFF_EINVAL. */
+ * 0 (default) the staged kernels for short strings and the device-side staged / stream choice for mixed and long
+ * ones; 1 the segment kernel (a tile's bits shared evenly over a wave's lanes) for a mean Huffman length above
+ * 40 B; 2 the segment kernel for every contiguous batch.  The HHUFF_DEC_SEG environment variable sets the start
+ * value.  Returns the previous mode, or HHUFF_EINVAL. */
 int hhuff_set_decode_kernel(int mode);
 /* Return the memory the library's stream-ordered pool on the caller's current device keeps between calls
  * (batch workspaces, edge records) to the driver.  Synchronises the device first.  HHUFF_OK or an error. */

@@ -24,7 +24,7 @@ def main():
         bt = synth.make_batch_torch(cfg, seed=1000)
         huff, h_off, m, H, P_ok = packed_huffman(torch, codec, bt)
         ok = None
-        names = hd.bool_to_bits(torch.rand(m, device="cuda") < 0.3)
+        names = None if os.environ.get("NO_NAMES") else hd.bool_to_bits(torch.rand(m, device="cuda") < 0.3)
         outs = {}
         for mode in (a, b):
             out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
@@ -50,7 +50,7 @@ def main():
         same = ok and bool((hd.compact_results(outs[a][0], slots, la)[1] == hd.compact_results(outs[b][0], slots, lb)[1]).all())
         med = {k: sorted(v)[len(v) // 2] for k, v in t.items()}
         B = H + P_ok + 9 * m + 4 + (m + 7) // 8
-        print(json.dumps({"config": cfg, "strings": m, "huffman_bytes": H, "mode_a": a, "mode_b": b,
+        print(json.dumps({"lib": os.path.basename(codec.LIB_PATH), "names": names is not None, "config": cfg, "strings": m, "huffman_bytes": H, "mode_a": a, "mode_b": b,
                           "ms_a": round(med[a], 4), "ms_b": round(med[b], 4),
                           "frac_a": round(B / (med[a] * 1e-3) / 8e12, 4), "frac_b": round(B / (med[b] * 1e-3) / 8e12, 4),
                           "equal": same, "decoded": int((keep > 0).sum())}), flush=True)
