@@ -3076,6 +3076,204 @@ __global__ void literal_fix_kernel(LitArgs A) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Length-sorted decode chunks (contiguous layout, slot output, short strings: c2, c4).  A 64-string tile of the
+// staged kernel runs as long as its longest string (U[24,72] plain = U[18,54] Huffman bytes: the tile's max is
+// ~1.47x its mean).  As encode_sorted_kernel does for encode, a group of 4 waves stages the span of 256
+// consecutive strings, counting-sorts them by length and hands wave w the w-th group of 64, so a wave's lanes
+// finish nearly together; the slot-layout output of the 256 strings goes out as one region (16-B stores, two
+// deferred edges).  The decode tables need one 32-KiB LUT per workgroup, so a workgroup is 16 waves in four
+// independent groups (one wave of each group per SIMD), each group on its own chunks with a group barrier of its
+// own: an LDS counter and LDS-only fences (s_barrier would make the 16 waves wait for the slowest group, and a
+// workgroup-scope fence for their global stores).  While a group's short-string waves wait for its long-string
+// wave, the other groups' waves use the SIMD.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kDsStr = 256;  // strings per chunk (one per thread of a group)
+__device__ __forceinline__ void group_sync(uint32_t* ctr, uint32_t& target, uint32_t lane) {
+    target += 4u;  // four waves a group, one arrival each
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (lane == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <uint32_t CH>
+__global__ __launch_bounds__(1024) void decode_sorted_kernel(DecArgs A) {
+    constexpr int NV = (CH + 16 * kDsStr - 1) / (16 * kDsStr);  // 16-B span chunks per thread
+    constexpr uint32_t OUTS = ((8u * (CH + 16u)) / 5u + 64u + 15u) & ~15u;
+    struct __attribute__((aligned(16))) Group {
+        uint32_t in[CH / 4 + 16];        // the chunk's span, big-endian dwords (+ read slack)
+        uint8_t out[OUTS + 4 * kDsStr];  // slot-layout output of the chunk, then a trash dword per thread
+        uint2 str[kDsStr];               // {offset in the span, length | is_name << 31}, then {out_len, status}
+        uint16_t perm[kDsStr];
+        uint32_t bin[kSortBins];
+        uint32_t ctr;
+    };
+    struct __attribute__((aligned(16))) Smem {
+        uint32_t lut[1u << HHUFF_LUT_BITS];
+        uint32_t kinfo[32];
+        uint32_t ones[(HHUFF_ONES_NENT + 3) & ~3];
+        Group g[4];
+    };
+    __shared__ Smem sm;
+    load_dec_tables(sm.lut, sm.kinfo, sm.ones, 1024);
+    const uint32_t grp = threadIdx.x >> 8, t = threadIdx.x & 255u, lane = t & 63u;
+    Group& G = sm.g[grp];
+    if (t < kSortBins) G.bin[t] = 0u;
+    if (t == 0) G.ctr = 0u;
+    __syncthreads();
+    const DecTables T{sm.lut, sm.kinfo, sm.ones};
+    uint32_t target = 0;
+    const uint64_t nch = ((uint64_t)A.n + kDsStr - 1) / kDsStr;
+    const uint64_t cstride = (uint64_t)gridDim.x * 4u;
+    uint64_t c = (uint64_t)blockIdx.x * 4u + grp;
+    if (c >= nch) return;  // (group-uniform; the other groups never wait for this one)
+    struct Chunk {
+        uint32_t s, e, lo, hi, nw;
+    };
+    auto issue = [&](uint64_t cc) {  // clamped: every load issues
+        const uint64_t cb = cc * kDsStr;
+        const uint64_t i = min(cb + t, (uint64_t)A.n - 1u);
+        Chunk q;
+        q.s = A.in_off[i];
+        q.e = A.in_off[i + 1];
+        q.lo = A.in_off[min(cb, (uint64_t)A.n - 1u)];
+        q.hi = A.in_off[min(cb + kDsStr, (uint64_t)A.n)];
+        q.nw = A.is_name_bits ? A.is_name_bits[i >> 5] : 0u;
+        return q;
+    };
+    auto span_of = [](const Chunk& q) { return q.hi > q.lo ? ((q.hi + 15u) & ~15u) - (q.lo & ~15u) : 0u; };
+    uint4 pv[NV];
+    auto issue_span = [&](const Chunk& q) {
+        const uint32_t a0 = q.lo & ~15u, span = span_of(q);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const uint32_t k = (uint32_t)j * (16u * kDsStr) + t * 16u;
+            const uint64_t g = (uint64_t)a0 + k;
+            if (k < span && span <= CH && g + 16 <= A.in_size) pv[j] = *reinterpret_cast<const uint4*>(A.in + g);
+        }
+    };
+    uint32_t bin = 0, rank = 0;
+    // the chunk's span into the input stage (big-endian dwords), its strings' records and their length ranks
+    auto prepare = [&](const Chunk& q, uint64_t cc) {
+        const uint32_t sp = span_of(q);
+        if (sp > CH) return;  // group-uniform: the per-thread path needs none of it
+        const uint32_t a0 = q.lo & ~15u;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const uint32_t k = (uint32_t)j * (16u * kDsStr) + t * 16u;
+            const uint64_t g = (uint64_t)a0 + k;
+            if (k < sp) {
+                uint4 x = g + 16 <= A.in_size ? pv[j] : load16_tail(A.in, A.in_size, g);
+                x = make_uint4(bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w));
+                *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(G.in) + k) = x;
+            }
+        }
+        const uint64_t i = cc * kDsStr + t;
+        const uint32_t ln = i < A.n ? q.e - q.s : 0u;
+        const uint32_t nm = i < A.n && A.is_name_bits ? ((q.nw >> (i & 31u)) & 1u) : 0u;
+        G.str[t] = make_uint2(q.s - a0, min(ln, kMaxStrLen + 1u) | (nm << 31));
+        bin = min(ln, kSortBins - 1u);  // the bulk loop's trip count follows the length
+        rank = atomicAdd(&G.bin[bin], 1u);
+    };
+    Chunk cur = issue(c);
+    issue_span(cur);
+    prepare(cur, c);
+    Chunk nxt = issue(c + cstride < nch ? c + cstride : c);
+    __asm__ volatile("" : "+v"(nxt.s), "+v"(nxt.e), "+v"(nxt.lo), "+v"(nxt.hi), "+v"(nxt.nw) : : "memory");
+    for (;;) {
+        const uint64_t cb = c * kDsStr, i = cb + t;
+        const bool valid = i < A.n;
+        const uint32_t lo = cur.lo, hi = cur.hi, a0 = lo & ~15u, span = span_of(cur);
+        EdgeRec* rec = A.edges + 2 * c;
+        const uint64_t cn = c + cstride, cn2 = cn + cstride;
+        const bool more = cn < nch;
+        group_sync(&G.ctr, target, lane);  // the chunk's stage, records and ranks are in
+        if (span > CH) {  // (group-uniform) larger than the stage: one thread per string, global memory
+            if (valid) {
+                uint32_t ol;
+                uint8_t st;
+                const bool nm = A.is_name_bits && ((cur.nw >> (i & 31u)) & 1u);
+                if (!split_push(A, (uint32_t)i, cur.e - cur.s)) {
+                    decode_direct(A, cur.s, cur.e - cur.s, nm, A.out + dec_slot(cur.s), T, ol, st);
+                    A.out_len[i] = ol;
+                    A.status[i] = st;
+                }
+            }
+            if (t < 2) rec[t].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges to defer
+            if (!more) break;
+            issue_span(nxt);
+            prepare(nxt, cn);
+            Chunk nn = issue(cn2 < nch ? cn2 : cn);
+            __asm__ volatile("" : "+v"(nn.s), "+v"(nn.e), "+v"(nn.lo), "+v"(nn.hi), "+v"(nn.nw) : : "memory");
+            cur = nxt;
+            nxt = nn;
+            c = cn;
+            continue;
+        }
+        {  // every wave scans the bin counts (two per lane) and places its threads' strings
+            const uint32_t x0 = G.bin[2 * lane], x1 = G.bin[2 * lane + 1];
+            const uint32_t ex = wave_excl_scan(x0 + x1, (int)lane);
+            const uint32_t eb = (uint32_t)__shfl((int)ex, (int)(bin >> 1)), xb = (uint32_t)__shfl((int)x0, (int)(bin >> 1));
+            G.perm[eb + ((bin & 1u) ? xb : 0u) + rank] = (uint16_t)t;
+        }
+        group_sync(&G.ctr, target, lane);
+        if (t < kSortBins) G.bin[t] = 0u;  // read by every wave above: cleared for the next chunk
+        if (more) issue_span(nxt);          // the next chunk's span: in flight during the decode
+        Chunk nn = issue(cn2 < nch ? cn2 : (more ? cn : c));
+        // sorted position t: wave w of the group decodes the w-th length group
+        const uint32_t j = G.perm[t];
+        const uint2 sj = G.str[j];
+        const uint32_t lj = sj.y & 0x7FFFFFFFu;
+        const bool vj = cb + j < A.n;
+        const uint32_t op0 = (uint32_t)(dec_slot(a0 + sj.x) - (dec_slot(lo) & ~15ull));
+        const bool act = vj && lj <= kMaxStrLen;
+        const DecResult r = decode_staged_lane_v7(G.in, sj.x, act ? lj : 0u, act, G.out, op0, OUTS + 4u * t, T);
+        uint32_t ol = kFailLen, st = kStatusFail;
+        if (vj && lj > kMaxStrLen) {
+            st = kStatusTooLong;
+        } else if (vj && r.ok) {
+            ol = r.len;
+            st = soft_bits((sj.y >> 31) != 0, r.len, r.flags, r.len ? G.out[op0] : 0u, r.len ? G.out[op0 + r.len - 1] : 0u);
+        }
+        G.str[j] = make_uint2(ol, st);  // back to the string's own record: stored in string order below
+        group_sync(&G.ctr, target, lane);
+        const uint2 res = G.str[t];
+        if (more) prepare(nxt, cn);  // the input stage and the records are free: the next chunk goes in now
+        // the chunk after next's offsets are waited for here, before this chunk's stores (in-order vmcnt)
+        __asm__ volatile("" : "+v"(nn.s), "+v"(nn.e), "+v"(nn.lo), "+v"(nn.hi), "+v"(nn.nw) : : "memory");
+        if (valid) {
+            A.out_len[i] = res.x;
+            A.status[i] = (uint8_t)res.y;
+        }
+        // the slot-layout output region; its first and last 16-B chunks are deferred (edge_fix_kernel)
+        {
+            const uint64_t olo = dec_slot(lo), ohi = dec_slot(hi), obase = olo & ~15ull;
+            const uint32_t ospan = hi > lo ? (uint32_t)(((ohi + 15u) & ~15ull) - obase) : 0u;
+            const uint32_t kl = ospan ? (ospan - 1u) & ~15u : 0u;
+            for (uint32_t k = t * 16u; k < ospan; k += 16u * kDsStr) {
+                const uint64_t g = obase + k;
+                const uint4 v = *reinterpret_cast<const uint4*>(G.out + k);
+                const bool full = g >= olo && g + 16 <= ohi;
+                if (full) *reinterpret_cast<uint4*>(A.out + g) = v;
+                if (k == 0 || k == kl) {
+                    const uint32_t elo = olo > g ? (uint32_t)(olo - g) : 0u;
+                    const uint32_t ehi = ohi - g < 16 ? (uint32_t)(ohi - g) : 16u;
+                    EdgeRec* e = rec + (k == 0 ? 0 : 1);
+                    e->v = v;
+                    e->m = make_uint4((uint32_t)g, (uint32_t)(g >> 32), full ? 0u : elo, full ? 0u : ehi);
+                }
+            }
+            if (t == 0 && (kl == 0 || ospan == 0)) rec[1].m = make_uint4(0u, 0u, 0u, 0u);
+            if (t == 0 && ospan == 0) rec[0].m = make_uint4(0u, 0u, 0u, 0u);
+        }
+        if (!more) break;
+        cur = nxt;
+        nxt = nn;
+        c = cn;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Segment decode: mixed and long strings, contiguous layout, slot output (SURVEY §7 hard part 2; VERDICT r4
 // "next" #1).  One lane per string runs a 64-string tile as long as its longest string (the staged kernel:
 // ~4x the mean on Zipf 8..512 B), and one lane per string streaming its own input and output (the stream
@@ -4036,9 +4234,37 @@ static hipError_t launch_seg(DecArgs A, uint64_t in_size, uint32_t n, uint8_t* o
     return e != hipSuccess ? e : f;
 }
 
+// Length-sorted decode chunks (decode_sorted_kernel) for the short-string contiguous layout; HHUFF_DEC_SORTED=0 keeps
+// the 64-string tiles of decode_staged_kernel (A/B)
+#ifndef HHUFF_DS_CH
+#define HHUFF_DS_CH 10240
+#endif
+static bool sorted_decode_on() {
+    static const bool on = [] {
+        const char* v = getenv("HHUFF_DEC_SORTED");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+static hipError_t launch_sorted_decode(DecArgs A, uint32_t n, uint8_t* out, hipStream_t stream) {
+    const uint64_t nch = ((uint64_t)n + kDsStr - 1) / kDsStr;
+    hipError_t e = pool_alloc((void**)&A.edges, 2ull * nch * sizeof(EdgeRec), stream);
+    if (e != hipSuccess) return e;
+    static int cus[64] = {};
+    const int dev = current_device();
+    int& cu = cus[dev >= 0 && dev < 64 ? dev : 0];
+    if (cu == 0 && (hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cu < 1)) cu = 256;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((nch + 3) / 4, (uint64_t)cu);
+    hipLaunchKernelGGL(decode_sorted_kernel<HHUFF_DS_CH>, dim3(grid), dim3(1024), 0, stream, A);
+    return finish_deferred(out, A.edges, n, stream, nullptr, 2ull * nch);
+}
+
 static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint32_t* in_len, uint32_t n, uint8_t* out,
                                         const uint32_t* out_off, hipStream_t stream, uint64_t sel_bytes) {
     if (use_seg(sel_bytes ? sel_bytes : in_size, n, in_len, out_off)) return launch_seg(A, in_size, n, out, stream);
+    if (in_len == nullptr && out_off == nullptr && sorted_decode_on() &&
+        pick_decode(sel_bytes ? sel_bytes : in_size, n) == kDecS)
+        return launch_sorted_decode(A, n, out, stream);
 #ifdef HHUFF_MIX_STREAM  // A/B builds: mixed lengths go to the stream kernel alone
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n) == kDecL ? (int)kDecT : pick_decode(sel_bytes ? sel_bytes : in_size, n);
 #else
@@ -4333,7 +4559,7 @@ struct WaveStep {  // the step that would start at one candidate bit
     uint32_t w, R;  // window at the candidate, string bits left there
     bool eos;       // EOS symbol (a chain end that fails)
 };
-constexpr uint32_t kStop = 255u;
+constexpr uint32_t kStop = 0xFFFFu;  // past every window offset (up to 64 NC + 30)
 __device__ __forceinline__ WaveStep wave_step(const uint8_t* in, uint32_t TB, uint32_t p, uint32_t off, const DecTables& T) {
     WaveStep s;
     const uint32_t q = (p >> 5) * 4u;  // the aligned dword holding bit p; bits past the string are don't-care
@@ -4388,7 +4614,7 @@ __device__ __forceinline__ DecResult wave_decode(const uint8_t* in, uint32_t len
         uint32_t c = 0;
         bool end = false;
         if constexpr (JUMP) {
-            const uint32_t n1 = s[0].nx;  // < 64: the next step starts in this window (kStop = 255 is not)
+            const uint32_t n1 = s[0].nx;  // < 64: the next step starts in this window (kStop is not)
             const uint32_t n2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((n1 < 64u ? n1 : lane) << 2), (int)n1);
             while (c < 64u) {
                 const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)n1, (int)c);  // both reads hang on c only
@@ -4447,6 +4673,126 @@ __device__ __forceinline__ DecResult wave_decode(const uint8_t* in, uint32_t len
             break;
         }
         W += c;
+    }
+    uint32_t fa = 0;  // OR over the wave (4 flag bits)
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) fa |= __builtin_amdgcn_ballot_w64(((flags >> k) & 1u) != 0u) != 0 ? 1u << k : 0u;
+    r.len = opos;
+    r.flags = (fa | (fa >> 2)) & 3u;
+    r.status = 0;
+    return r;
+}
+
+// The per-string service's decode (round 5): NC columns of 64 candidates per round (bits W .. W + 64 NC - 1), the
+// table steps of all of them in one LDS phase (wave_step_bf: the long-code lookups done for every candidate, not
+// behind a branch, so the columns' loads issue back to back: input dwords, then LUT and leading-ones info, then
+// the long-code entry), then the chain walked column by column -- each column's next offsets read with v_readlane
+// from that column's own register (a per-step column select made NC = 2 slower in round 3), two links a step
+// through a per-column jump table (ds_bpermute).  A 48-B string is one round instead of six.
+__device__ __forceinline__ WaveStep wave_step_bf(const uint8_t* in, uint32_t TB, uint32_t p, uint32_t off, const DecTables& T) {
+    WaveStep s;
+    const uint32_t q = (p >> 5) * 4u;
+    const uint64_t x = (uint64_t)bswap32(*reinterpret_cast<const uint32_t*>(in + q)) << 32 |
+                       bswap32(*reinterpret_cast<const uint32_t*>(in + q + 4u));
+    s.w = (uint32_t)((x << (p & 31u)) >> 32);
+    s.R = p < TB ? TB - p : 0u;
+    const uint32_t e = T.lut[s.w >> (32 - HHUFF_LUT_BITS)];
+    const uint32_t k = min((uint32_t)__builtin_clz(~s.w | 1u), 30u);
+    const uint32_t ki = T.kinfo[k];
+    const uint32_t le = T.ones[(ki & 0xFFFFu) + (((s.w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+    if (e & kLong) {
+        const uint32_t L = (le >> 9) & 31u, sym = le & 0x1FFu;
+        const bool stop = L > s.R || sym == kEos;
+        s.eos = L <= s.R && sym == kEos;
+        s.nx = stop ? kStop : off + L;
+        s.ns = stop ? 0u : 1u;
+        s.syms = sym;
+        s.fl = (le >> 14) & 3u;
+    } else {
+        const uint32_t L1 = lut_l1(e), L12 = lut_l12(e);
+        const bool two = (e & kHas2) && L12 <= s.R;
+        const bool stop = L1 > s.R;
+        s.eos = false;
+        s.nx = stop ? kStop : off + (two ? L12 : L1);
+        s.ns = stop ? 0u : (two ? 2u : 1u);
+        s.syms = lut_pair(e);
+        s.fl = (e >> 24) & (two ? 15u : 3u);
+    }
+    return s;
+}
+template <int NC>
+__device__ __forceinline__ DecResult wave_decode_cols(const uint8_t* in, uint32_t len, uint8_t* out, const DecTables& T,
+                                                      uint32_t lane) {
+    constexpr uint32_t kWin = 64u * NC;
+    const uint32_t TB = 8u * len;
+    uint32_t W = 0, opos = 0, flags = 0;
+    DecResult r;
+    r.ok = false;
+    for (;;) {
+        WaveStep s[NC];
+#pragma unroll
+        for (int j = 0; j < NC; ++j) s[j] = wave_step_bf(in, TB, W + 64u * j + lane, 64u * j + lane, T);
+        uint64_t on[NC];
+        uint32_t c = 0, endj = 0;
+        bool end = false;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            on[j] = 0;
+            const uint32_t lo = 64u * j, hi = lo + 64u;
+            const uint32_t n1 = s[j].nx;
+            // the step after each candidate's, when it starts in this column (else the lane's own value, unused)
+            const uint32_t n2 = (uint32_t)__builtin_amdgcn_ds_bpermute(
+                (int)(((n1 >= lo && n1 < hi) ? n1 - lo : lane) << 2), (int)n1);
+            while (!end && c < hi) {  // c >= lo: a link moves at most 30 bits, so no column is skipped
+                const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)n1, (int)(c - lo));
+                const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)n2, (int)(c - lo));
+                if (a == kStop) {
+                    end = true, endj = j;
+                    break;
+                }
+                on[j] |= 1ull << (c - lo);
+                if (a >= hi) {
+                    c = a;
+                    break;
+                }
+                if (b == kStop) {
+                    c = a;
+                    end = true, endj = j;
+                    break;
+                }
+                on[j] |= 1ull << (a - lo);
+                c = b;
+            }
+        }
+        uint32_t base = opos;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            const uint32_t n = ((on[j] >> lane) & 1u) ? s[j].ns : 0u;
+            const uint32_t incl = wave_incl_scan(n);
+            if (n) {
+                out[base + incl - n] = (uint8_t)s[j].syms;
+                if (n == 2u) out[base + incl - 1u] = (uint8_t)(s[j].syms >> 8);
+                flags |= s[j].fl;
+            }
+            base += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        opos = base;
+        if (end) {
+            // padding: at most 7 bits, all ones (mkhufftbl.py:374-381, hpack.c:132-133); EOS fails (hpack.c:88-89)
+            uint32_t wc = 0, Rc = 0, ec = 0;
+#pragma unroll
+            for (int j = 0; j < NC; ++j)
+                if (endj == (uint32_t)j) {
+                    const int cl = (int)(c - 64u * j);
+                    wc = (uint32_t)__builtin_amdgcn_readlane((int)s[j].w, cl);
+                    Rc = (uint32_t)__builtin_amdgcn_readlane((int)s[j].R, cl);
+                    ec = (uint32_t)__builtin_amdgcn_readlane((int)(s[j].eos ? 1u : 0u), cl);
+                }
+            r.ok = ec == 0u && Rc <= 7u && ((wc >> 24) | (0xFFu >> Rc)) == 0xFFu;
+            break;
+        }
+        W += c;  // c >= kWin: the chain left this round's window
+        (void)kWin;
     }
     uint32_t fa = 0;  // OR over the wave (4 flag bits)
 #pragma unroll
@@ -4691,7 +5037,7 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
     __shared__ uint32_t s_kinfo[32];
     __shared__ uint32_t s_ones[HHUFF_ONES_NENT];
     __shared__ __attribute__((aligned(16))) uint2 s_enc[256];
-    __shared__ __attribute__((aligned(16))) uint32_t s_in[kSvcMax / 4 + 8];  // [input][slack]
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[kSvcMax / 4 + 24];  // [input][slack: a round reads 384 bits past W]
     __shared__ __attribute__((aligned(16))) uint8_t s_out[(kSvcMax * 8) / 5 + 64];
     const uint32_t lane = threadIdx.x;
     const uint32_t G = gridDim.x, g = blockIdx.x;  // G divides kSvcSlots (launch_service)
@@ -4766,7 +5112,9 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
                 st = ol == kFailLen ? kStatusFail : 0u;
                 if (ol != kFailLen) ol = (ol + 7u) >> 3;
             } else {
-                const DecResult d = wave_decode<NC, JUMP>(in, len, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane);
+                const DecResult d = NC >= 3 ? wave_decode_cols<NC>(in, len, s_out, DecTables{s_lut, s_kinfo, s_ones}, lane)
+                                            : wave_decode<NC < 3 ? NC : 1, JUMP>(in, len, s_out,
+                                                                                 DecTables{s_lut, s_kinfo, s_ones}, lane);
                 wave_lds_sync();
                 ol = d.ok ? d.len : kFailLen;
                 st = d.ok ? soft_bits(is_name != 0, d.len, d.flags, d.len ? s_out[0] : 0u, d.len ? s_out[d.len - 1] : 0u)
@@ -4822,12 +5170,18 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
 hipError_t launch_service(SvcSlot* slots, SvcCtrl* ctrl, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream) {
     // decode walk (A/B knob HHUFF_SVC_NC): 1 = one candidate per lane, one step per chain link; 2 = two
     // candidates per lane; default: one candidate per lane, two steps per link (the jump table)
+    // ("j": the round-4 default, one candidate per lane, jump table); from round 5 on by default: six columns of
+    // 64 candidates per round, walked column by column (wave_decode_cols), "4": four columns
     static const int nc = [] {
         const char* e = getenv("HHUFF_SVC_NC");
-        return e && *e == '2' ? 2 : e && *e == '1' ? 1 : 3;
+        return e && *e == '2' ? 2 : e && *e == '1' ? 1 : e && *e == 'j' ? 3 : e && *e == '4' ? 4 : 6;
     }();
     const uint32_t G = service_waves();
-    if (nc == 2)
+    if (nc == 6)
+        hipLaunchKernelGGL(service_kernel<6>, dim3(G), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
+    else if (nc == 4)
+        hipLaunchKernelGGL(service_kernel<4>, dim3(G), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
+    else if (nc == 2)
         hipLaunchKernelGGL(service_kernel<2>, dim3(G), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
     else if (nc == 1)
         hipLaunchKernelGGL(service_kernel<1>, dim3(G), dim3(64), 0, stream, slots, ctrl, idle_ticks, max_ticks);
