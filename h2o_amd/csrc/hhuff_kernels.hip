@@ -4234,15 +4234,17 @@ static hipError_t launch_seg(DecArgs A, uint64_t in_size, uint32_t n, uint8_t* o
     return e != hipSuccess ? e : f;
 }
 
-// Length-sorted decode chunks (decode_sorted_kernel) for the short-string contiguous layout; HHUFF_DEC_SORTED=0 keeps
-// the 64-string tiles of decode_staged_kernel (A/B)
+// Length-sorted decode chunks (decode_sorted_kernel) for the short-string contiguous layout, HHUFF_DEC_SORTED=1 (A/B;
+// off by default: c4 decode 0.588 -> 0.606 ms in two alternating runs each, profiles/r05i_sorted_decode_ab.jsonl --
+// the waves of a group that wait for its longest-string wave leave their SIMD fewer waves to hide the LUT chain's
+// latency, which the balanced lanes do not win back)
 #ifndef HHUFF_DS_CH
 #define HHUFF_DS_CH 10240
 #endif
 static bool sorted_decode_on() {
     static const bool on = [] {
         const char* v = getenv("HHUFF_DEC_SORTED");
-        return !(v && v[0] == '0');
+        return v && v[0] == '1';
     }();
     return on;
 }
@@ -5170,11 +5172,12 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
 hipError_t launch_service(SvcSlot* slots, SvcCtrl* ctrl, uint64_t idle_ticks, uint64_t max_ticks, hipStream_t stream) {
     // decode walk (A/B knob HHUFF_SVC_NC): 1 = one candidate per lane, one step per chain link; 2 = two
     // candidates per lane; default: one candidate per lane, two steps per link (the jump table)
-    // ("j": the round-4 default, one candidate per lane, jump table); from round 5 on by default: six columns of
-    // 64 candidates per round, walked column by column (wave_decode_cols), "4": four columns
+    // ("6" / "4": six / four columns of 64 candidates per round walked column by column, wave_decode_cols -- measured
+    // slower per call than the jump table, 9.2 vs 8.5 us median through bench.py's ctypes call,
+    // profiles/r05i_per_string_ab.jsonl)
     static const int nc = [] {
         const char* e = getenv("HHUFF_SVC_NC");
-        return e && *e == '2' ? 2 : e && *e == '1' ? 1 : e && *e == 'j' ? 3 : e && *e == '4' ? 4 : 6;
+        return e && *e == '2' ? 2 : e && *e == '1' ? 1 : e && *e == '6' ? 6 : e && *e == '4' ? 4 : 3;
     }();
     const uint32_t G = service_waves();
     if (nc == 6)
