@@ -1500,6 +1500,272 @@ __device__ __forceinline__ void store_range16v(uint8_t* __restrict__ g, uint4 v,
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Stream decode with the output in registers (round 5; VERDICT r4 "next" #1 route b).  decode_stream_kernel keeps
+// a 160-B LDS output buffer per lane beside its 100-B window: 6 waves a CU, 1.5 a SIMD, 56 % of wave cycles
+// parked.  Here a lane's output goes into one 16-B chunk held in four VGPRs, aligned to the output's 16-B grid:
+// a full chunk leaves with one 16-B store (the first chunk of a string, shared with the string before, with
+// byte-exact stores), the partial chunk simply stays in its registers from round to round, and the string's
+// last chunk leaves byte-exact at its end.  No output buffer and no flush phase: 16 waves a CU fit the LDS (the
+// 32-KiB LUT + 100 B of window per lane).  (Round 2 measured a register output with a 4-B store per dword: c3
+// 0.316 -> 0.360 ms; here one 16-B store per 16 bytes, no more stores than the LDS version's flush.)
+// ------------------------------------------------------------------------------------------------
+struct RegChunk {  // 16 output bytes at global [g, g + 16): L = bytes 0..7, H = 8..15; p bytes filled; lo = first ours
+    uint64_t L, H;
+    uint64_t g;
+    uint32_t p, lo;
+    __device__ __forceinline__ void start(uint64_t dst) {
+        g = dst & ~15ull;
+        p = lo = (uint32_t)(dst & 15u);
+        L = H = 0;
+    }
+    __device__ __forceinline__ void flush_full(uint8_t* __restrict__ out) {
+        const uint4 v = make_uint4((uint32_t)L, (uint32_t)(L >> 32), (uint32_t)H, (uint32_t)(H >> 32));
+        if (lo == 0)
+            *reinterpret_cast<uint4*>(out + g) = v;
+        else
+            store_range16v(out + g, v, lo, 16u);
+    }
+    __device__ __forceinline__ void flush_part(uint8_t* __restrict__ out) {  // the string's last bytes
+        if (p > lo) store_range16v(out + g, make_uint4((uint32_t)L, (uint32_t)(L >> 32), (uint32_t)H, (uint32_t)(H >> 32)),
+                                   lo, p);
+    }
+    // n (0..2) bytes of v at position p; a chunk that fills up leaves at once (the second byte of a pair at p = 15
+    // starts the next chunk)
+    __device__ __forceinline__ void put(uint8_t* __restrict__ out, uint32_t v, uint32_t n) {
+        const uint64_t x = (uint64_t)(v & (n >= 2u ? 0xFFFFu : (n ? 0xFFu : 0u)));
+        const uint32_t sh = 8u * p;
+        L |= sh < 64u ? x << sh : 0ull;
+        H |= sh >= 64u ? x << (sh - 64u) : (sh > 48u ? x >> (64u - sh) : 0ull);
+        p += n;
+        if (p >= 16u) {
+            flush_full(out);
+            g += 16u;
+            lo = 0;
+            p -= 16u;
+            L = p ? x >> 8 : 0ull;  // (p is 0 or 1)
+            H = 0;
+        }
+    }
+};
+
+template <int WAVES, int NW>
+__global__ __launch_bounds__(WAVES * 64) void decode_stream_rk_kernel(DecArgs A, unsigned long long* __restrict__ counter) {
+    static_assert(NW >= 8 && NW % 4 == 0, "window shape");
+    constexpr uint32_t kWS = NW + 1;  // odd dword stride: lanes at the same q hit distinct banks
+    struct __attribute__((aligned(16))) Smem {
+        uint32_t lut[1u << HHUFF_LUT_BITS];
+        uint32_t kinfo[32];
+        uint32_t ones[(HHUFF_ONES_NENT + 3) & ~3];
+        uint32_t win[WAVES * 64][kWS];  // [0]: the dword before the window (read, never used)
+    };
+    if (A.gate && *A.gate != kGateStream) return;  // block-uniform: decode_select_kernel chose the staged kernel
+    __shared__ Smem sm;
+    load_dec_tables(sm.lut, sm.kinfo, sm.ones, WAVES * 64);
+    __syncthreads();
+    const DecTables T{sm.lut, sm.kinfo, sm.ones};
+    const int lane = threadIdx.x & 63;
+    uint32_t* win = &sm.win[threadIdx.x][1];
+    const lds_u32* st = (const lds_u32*)win;
+    constexpr int32_t kLimW = 32 * (NW - 2) - 30;  // bulk steps start below this window bit
+    constexpr int32_t kFinal = 32 * (NW - 2);      // a string ending at or before this bit ends in the window
+
+    uint4 pfv[NW / 4];
+    uint64_t pfa = ~0ull;
+    bool busy = false, is_name = false;
+    uint32_t i = 0, s = 0, len = 0, P = 0, ocnt = 0, flags = 0, first = 0, lastb = 0, fail = 0;
+    RegChunk ch;
+    ch.start(0);
+    uint64_t bnext = 0, bend = 0;
+    bool qdone = false;
+    const uint64_t nwork = A.n_dev ? (uint64_t)*A.n_dev : (uint64_t)A.n;
+
+    for (;;) {
+        // ---- 1. idle lanes take strings ----
+        for (int it = 0; it < 2; ++it) {
+            const uint64_t need = __builtin_amdgcn_ballot_w64(!busy);
+            if (need == 0) break;
+            if (bnext >= bend) {
+                if (qdone) break;
+                uint64_t b = 0;
+                if (lane == 0) b = atomicAdd(counter, 64ull);
+                b = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
+                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+                if (b >= nwork) {
+                    qdone = true;
+                    break;
+                }
+                bnext = b;
+                bend = min(b + 64u, nwork);
+            }
+            const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            if (!busy && bnext + rank < bend) {
+                i = (uint32_t)(bnext + rank);
+                s = A.in_off[i];
+                len = A.in_len ? A.in_len[i] : A.in_off[i + 1] - s;
+                is_name = A.is_name_bits ? ((A.is_name_bits[i >> 5] >> (i & 31)) & 1u) : false;
+                const uint64_t dst = A.out_off ? (uint64_t)A.out_off[i] : dec_slot(s);
+                if (len > kMaxStrLen) {
+                    A.out_len[i] = kFailLen;
+                    A.status[i] = kStatusTooLong;
+                } else if (!split_push(A, i, len)) {
+                    busy = true;
+                    ch.start(dst);
+                    P = ocnt = flags = first = lastb = fail = 0;
+                }
+            }
+            bnext = min(bend, bnext + (uint64_t)__builtin_popcountll(need));
+        }
+        if (!__any(busy)) {
+            if (qdone) break;
+            continue;
+        }
+
+        // ---- 2. the lane's window (as decode_stream_kernel) ----
+        const uint64_t cur = (uint64_t)s + (P >> 3);
+        const uint64_t wb = cur & ~3ull;
+        const uint64_t rem = (uint64_t)len * 8u - P;
+        if (busy) {
+            if (wb != pfa) {
+#pragma unroll
+                for (int j = 0; j < NW / 4; ++j) pfv[j] = load16_bounded(A.in, A.in_size, wb + 16u * j);
+            }
+#pragma unroll
+            for (int j = 0; j < NW / 4; ++j) {
+                win[4 * j + 0] = bswap32(pfv[j].x);
+                win[4 * j + 1] = bswap32(pfv[j].y);
+                win[4 * j + 2] = bswap32(pfv[j].z);
+                win[4 * j + 3] = bswap32(pfv[j].w);
+            }
+            pfa = rem + 8u * (uint32_t)(cur - wb) + (P & 7u) > 32u * (NW - 2) ? wb + 4u * (NW - 3) : ~0ull;
+            if (pfa != ~0ull) {
+#pragma unroll
+                for (int j = 0; j < NW / 4; ++j) pfv[j] = load16_bounded(A.in, A.in_size, pfa + 16u * j);
+            }
+        }
+        int32_t pm = busy ? (int32_t)(8u * (uint32_t)(cur - wb) + (P & 7u)) - 1 : -1;
+        const int32_t pm0 = pm;
+        const int32_t end = busy ? (int32_t)min((uint64_t)(pm + 1) + rem, (uint64_t)0x40000000u) : 0;
+        const bool fin = busy && end <= kFinal;
+        int32_t q = pm >> 5;
+        uint32_t x0 = st[q], x1 = st[q + 1], x2 = st[q + 2];
+        uint32_t accb = 0, acc1 = 0, acc2 = 0, accl = 0, parked = busy ? 0u : 1u;
+        uint32_t made = 0;
+        int32_t lim = busy ? min(end - 26, kLimW) : (int32_t)0x80000000;
+        auto advance = [&](int32_t cons) {
+            pm += cons;
+            const int32_t qn = pm >> 5;
+            const bool adv = qn != q;
+            x0 = adv ? x1 : x0;
+            x1 = adv ? x2 : x1;
+            q = qn;
+            x2 = st[q + 2];
+        };
+        // n symbol bytes (the low n of v) to the output, first / last byte remembered
+        auto emit = [&](uint32_t v, uint32_t n) {
+            first = (ocnt + made) == 0u && n ? (v & 0xFFu) : first;
+            lastb = n == 2u ? ((v >> 8) & 0xFFu) : (n ? (v & 0xFFu) : lastb);
+            made += n;
+            ch.put(A.out, v, n);
+        };
+
+        // ---- 3a. bulk ----
+        auto bstep = [&](bool longchk) {
+            if (pm < lim) {
+                const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+                const uint32_t sl = (uint32_t)((int32_t)e >> 31);
+                emit(lut_pair(e), (e >> 28) & 3u);
+                accb |= e;
+                uint32_t cons = lut_l12(e);
+                {
+                    const uint32_t eb = T.lut[(w << cons) >> (32 - HHUFF_LUT_BITS)];
+                    emit(lut_pair(eb), (eb >> 28) & 3u);
+                    accb |= eb;
+                    cons += lut_l12(eb);
+                }
+                if (longchk && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
+                    if (sl) {
+                        const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                        const uint32_t ki = T.kinfo[k];
+                        const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                        const int32_t L = (le >> 9) & 31u;
+                        const bool fits = L + pm < end;
+                        const bool eos = (le & 0x1FFu) == kEos;
+                        fail |= fits && eos ? 1u : 0u;  // EOS inside the string (hpack.c:88-89)
+                        if (fits && !eos) {
+                            emit(le, 1u);
+                            accl |= le;
+                            cons = (uint32_t)L;
+                        } else {
+                            parked = 1u;
+                            lim = (int32_t)0x80000000;
+                        }
+                    }
+                }
+                advance((int32_t)cons);
+            }
+        };
+        for (;;) {
+            bstep(false);
+            bstep(true);
+            if (!__any(pm < lim)) break;
+        }
+
+        // ---- 3b. tail: lanes whose string ends in this window, one symbol a step checked against the end ----
+        bool tdone = !(fin && !parked);
+        for (;;) {
+            const bool go = !tdone;
+            if (!__any(go)) break;
+            if (go) {
+                const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+                uint32_t sym = e, L = lut_l1(e), fl = e & (3u << 24);
+                bool eos = false;
+                if ((int32_t)e < 0) {
+                    const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                    const uint32_t ki = T.kinfo[k];
+                    const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (k + 1)) >> 1) >> (31 - (ki >> 16)))];
+                    sym = le;
+                    L = (le >> 9) & 31u;
+                    fl = ((le >> 14) & 3u) << 24;
+                    eos = (le & 0x1FFu) == kEos;
+                }
+                const int32_t R = end - 1 - pm;  // string bits left
+                if ((int32_t)L <= R && !eos) {
+                    emit(sym, 1u);
+                    acc1 |= fl;
+                    advance((int32_t)L);
+                } else {
+                    fail |= eos && (int32_t)L <= R ? 1u : 0u;  // EOS inside the string (hpack.c:88-89)
+                    tdone = true;  // no code fits: the padding
+                }
+            }
+        }
+
+        // ---- 4. finish strings ----
+        if (busy) {
+            flags |= ((accb >> 24) | (accb >> 26) | (acc1 >> 24) | (accl >> 14)) & 3u;
+            const bool done = parked || fin;
+            bool ok = false;
+            if (fin && !parked && !fail) {  // padding: at most 7 bits, all ones (hpack.c:132-133)
+                const int32_t R = end - 1 - pm;
+                const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                ok = R >= 0 && R <= 7 && (w | (0xFFFFFFFFu >> R)) == 0xFFFFFFFFu;
+            }
+            ocnt += made;
+            P += (uint32_t)(pm - pm0);
+            if (done) {
+                if (ok) ch.flush_part(A.out);
+                A.out_len[i] = ok ? ocnt : kFailLen;
+                A.status[i] = ok ? soft_bits(is_name, ocnt, flags, first, lastb) : kStatusFail;
+                busy = false;
+            }
+        }
+    }
+}
+
 struct StreamBatch {  // lane l: string b + l of a claimed batch of 64 (cnt of them exist)
     uint64_t b;
     uint32_t cnt;
@@ -3853,6 +4119,9 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
 #define HHUFF_ENCO_NS 256
 #define HHUFF_ENCO_CH 16384
 #endif
+#ifndef HHUFF_RK_W  // stream decode with register output: waves per block (16 x 6.4 KiB of windows + the LUT)
+#define HHUFF_RK_W 16
+#endif
 #ifndef HHUFF_DECT  // stream decode: waves per block, window dwords, output bytes per lane
 // (6 waves of 24-dword windows: c3 -2.2 %, c5 -1.3 % against 8 x 16; 6 x 16 and 4 x 32 lose on c5 or c3,
 // 12 and 16 waves lose on both: profiles/r04k_stream_shapes.log, profiles/r04_ab_runs.log t12 / t16b)
@@ -3860,7 +4129,12 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
 #define HHUFF_DECT_NW 24
 #define HHUFF_DECT_OUT 160
 #endif
-constexpr int kDecSWaves = 16, kDecTWaves = HHUFF_DECT_W, kEncSWaves = 16, kEncOStr = HHUFF_ENCO_NS;
+#ifdef HHUFF_STREAM_RK
+constexpr int kDecTWaves = HHUFF_RK_W;
+#else
+constexpr int kDecTWaves = HHUFF_DECT_W;
+#endif
+constexpr int kDecSWaves = 16, kEncSWaves = 16, kEncOStr = HHUFF_ENCO_NS;
 #define DEC_S decode_staged_kernel<kDecSWaves, 3072, 4608, false>
 #define DEC_L decode_staged_kernel<6, 8192, 12928, false>
 #define DEC_SP decode_staged_kernel<kDecSWaves, 3072, 4608, true>
@@ -3872,7 +4146,12 @@ constexpr int kDecSWaves = 16, kDecTWaves = HHUFF_DECT_W, kEncSWaves = 16, kEncO
 #ifndef HHUFF_DECT_SEG
 #define HHUFF_DECT_SEG 16
 #endif
+#ifdef HHUFF_STREAM_RK  // A/B builds: register output, 16 waves (c3 0.437 / c5 0.687 ms against 0.294 / 0.430:
+                        // the per-symbol register packing costs more than the occupancy gains, r05j_stream_rk_ab)
+#define DEC_T decode_stream_rk_kernel<HHUFF_RK_W, HHUFF_DECT_NW>
+#else
 #define DEC_T decode_stream_kernel<kDecTWaves, HHUFF_DECT_NW, HHUFF_DECT_OUT, HHUFF_DECT_SEG>
+#endif
 #endif
 #define ENC_S encode_staged_kernel<kEncSWaves, 3584, false>
 #define ENC_O encode_sorted_kernel<kEncOStr, HHUFF_ENCO_CH>
