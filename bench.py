@@ -653,7 +653,7 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, re
     res = {}
     # packed: the same pinned buffers through hhuff_*_batch_host_packed (zero copy, the packed kernels: only the
     # output bytes, out_off, out_len and status cross the link, not the slot tails)
-    for kind in ("pinned", "packed", "pinned_dma", "pageable"):
+    for kind in ("pinned", "packed", "packed_off", "pinned_dma", "pageable"):
         # pinned: the library's default for device-visible caller buffers (zero copy: the kernels read and
         # write host memory across PCIe); pinned_dma: the chunked DMA pipeline on the same buffers
         if kind == "pinned_dma":
@@ -674,7 +674,7 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, re
         names_np = h_names.numpy().view(np.uint32)
         if kind == "pageable":
             off_np, hoff_np, names_np = off_np.copy(), hoff_np.copy(), names_np.copy()
-        if kind == "packed":
+        if kind == "packed_off":  # out_off and the encode status returned as well (5 more bytes a string)
             oo_e, oo_d = hbuf(n + 1, torch.int32).view(np.uint32), hbuf(n_ok + 1, torch.int32).view(np.uint32)
 
             def run_enc():
@@ -683,6 +683,14 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, re
             def run_dec():
                 codec.decode_batch_host_packed(src_h, hoff_np, n_ok, is_name_bits=names_np, out=out_d, out_off=oo_d,
                                                out_len=dl, status=ds)
+        elif kind == "packed":  # lengths (and decode statuses) only: positions follow from them (packed_positions)
+            def run_enc():
+                codec.encode_batch_host_packed(src_p, off_np, n, out=out_e, out_len=el, with_off=False,
+                                               with_status=False)
+
+            def run_dec():
+                codec.decode_batch_host_packed(src_h, hoff_np, n_ok, is_name_bits=names_np, out=out_d, out_len=dl,
+                                               status=ds, with_off=False)
         else:
             def run_enc():
                 codec.encode_batch_host_pipelined(src_p, off_np, n, out=out_e, out_len=el, status=es)
@@ -697,7 +705,7 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, re
             run_dec()
             ts.append(time.perf_counter() - t0)
         res[kind] = min(ts[1:])
-        if kind in ("pinned", "packed"):
+        if kind in ("pinned", "packed", "packed_off"):
             # the two legs are independent (a server's requests and responses): on two host threads, each with
             # the library's own per-thread stream, they share the link's two directions at once
             import threading
@@ -713,9 +721,10 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, re
             assert int(np.asarray(dl).astype(np.int64).sum()) > 0
             if kind == "packed":  # bytes across the link per step (zero copy): in, offsets, names | out bytes, meta
                 h2d = P + 4 * (n + 1) + H + 4 * (n_ok + 1) + 4 * names_np.size
-                d2h = int(np.asarray(el).astype(np.int64)[np.asarray(el) != 0xFFFFFFFF].sum()) + 9 * n + 4 + \
-                    int(np.asarray(dl).astype(np.int64)[np.asarray(dl) != 0xFFFFFFFF].sum()) + 9 * n_ok + 4
-                link = {"h2d_bytes": h2d, "d2h_bytes": d2h}
+                d2h = int(np.asarray(el).astype(np.int64)[np.asarray(el) != 0xFFFFFFFF].sum()) + 4 * n + \
+                    int(np.asarray(dl).astype(np.int64)[np.asarray(dl) != 0xFFFFFFFF].sum()) + 5 * n_ok
+                link = {"h2d_bytes": h2d, "d2h_bytes": d2h,
+                        "d2h_bytes_with_offsets": d2h + 5 * n + 4 + 4 * n_ok + 4}
     os.environ.pop("HHUFF_HOST_COPY", None)
     best = min(("pinned", "pinned_concurrent", "packed", "packed_concurrent"), key=lambda k: res[k])
     t = res[best]
@@ -726,6 +735,7 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, re
             "concurrent_value": round(P / GIB / res["pinned_concurrent"], 3),
             "packed_value": round(P / GIB / res["packed"], 3),
             "packed_concurrent_value": round(P / GIB / res["packed_concurrent"], 3),
+            "packed_with_offsets_value": round(P / GIB / min(res["packed_off"], res["packed_off_concurrent"]), 3),
             "packed_link_bytes": link,
             "pcie": pcie_rates(torch),
             "pinned_dma_value": round(P / GIB / res["pinned_dma"], 3),
@@ -736,7 +746,9 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, re
                     "buffers are read and written by the kernels in place (zero copy), pinned_dma is the chunked DMA "
                     "pipeline on the same buffers (64 MiB chunks, 3 streams), pageable buffers go through it with "
                     "host staging; packed: hhuff_{encode,decode}_batch_host_packed on the pinned buffers (zero copy, "
-                    "tile-packed outputs: only output bytes cross the link); value: the fastest pinned step, its "
+                    "tile-packed outputs: only output bytes cross the link; out_len and the decode status returned, "
+                    "positions implied by them; packed_with_offsets: out_off and the encode status too); value: "
+                    "the fastest pinned step, its "
                     "encode and decode legs one after the other or on two host threads at once (`best`); "
                     "best of %d" % reps}
 

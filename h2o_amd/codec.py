@@ -612,33 +612,51 @@ def encode_batch_host_pipelined(data, in_off, n, out=None, chunk_bytes=0, device
 
 
 def decode_batch_host_packed(data, in_off, n, is_name_bits=None, out=None, device=0, out_off=None, out_len=None,
-                             status=None):
+                             status=None, with_off=True):
     """hhuff_decode_batch_host_packed on numpy arrays: the packed layout (tile runs, out_off[n + 1]); pinned arrays are
-    read and written by the kernels in place (zero copy).  Returns (out, out_off[:n + 1], out_len[:n], status[:n])"""
+    read and written by the kernels in place (zero copy).  Returns (out, out_off[:n + 1], out_len[:n], status[:n]);
+    with_off=False passes out_off NULL (not returned, out_off None: see packed_positions)"""
     data, in_off = _np(data, np.uint8), _np(in_off, np.uint32)
     size = decode_slot_size(int(in_off[n]))
     out = np.zeros(size, np.uint8) if out is None else out
-    out_off = np.zeros(n + 1, np.uint32) if out_off is None else out_off
+    out_off = None if not with_off else np.zeros(n + 1, np.uint32) if out_off is None else out_off
     out_len = np.zeros(max(1, n), np.uint32) if out_len is None else out_len
     status = np.zeros(max(1, n), np.uint8) if status is None else status
     names = None if is_name_bits is None else _np(is_name_bits, np.uint32)
     _check(lib().hhuff_decode_batch_host_packed(_hp(data), data.size, _hp(in_off), n, _hp(names), _hp(out), out.size,
                                                 _hp(out_off), _hp(out_len), _hp(status), device),
            "hhuff_decode_batch_host_packed")
-    return out, out_off[:n + 1], out_len[:n], status[:n]
+    return out, None if out_off is None else out_off[:n + 1], out_len[:n], status[:n]
 
 
-def encode_batch_host_packed(data, in_off, n, out=None, device=0, out_off=None, out_len=None, status=None):
-    """hhuff_encode_batch_host_packed on numpy arrays (see decode_batch_host_packed)"""
+def encode_batch_host_packed(data, in_off, n, out=None, device=0, out_off=None, out_len=None, status=None,
+                             with_off=True, with_status=True):
+    """hhuff_encode_batch_host_packed on numpy arrays (see decode_batch_host_packed; with_status=False passes
+    status NULL: out_len's HHUFF_FAIL_LEN already says which strings stay plain)"""
     data, in_off = _np(data, np.uint8), _np(in_off, np.uint32)
     out = np.zeros(int(in_off[n]) + 16, np.uint8) if out is None else out
-    out_off = np.zeros(n + 1, np.uint32) if out_off is None else out_off
+    out_off = None if not with_off else np.zeros(n + 1, np.uint32) if out_off is None else out_off
     out_len = np.zeros(max(1, n), np.uint32) if out_len is None else out_len
-    status = np.zeros(max(1, n), np.uint8) if status is None else status
+    status = None if not with_status else np.zeros(max(1, n), np.uint8) if status is None else status
     _check(lib().hhuff_encode_batch_host_packed(_hp(data), data.size, _hp(in_off), n, _hp(out), out.size, _hp(out_off),
                                                 _hp(out_len), _hp(status), device),
            "hhuff_encode_batch_host_packed")
-    return out, out_off[:n + 1], out_len[:n], status[:n]
+    return (out, None if out_off is None else out_off[:n + 1], out_len[:n],
+            None if status is None else status[:n])
+
+
+def packed_positions(in_off, out_len, decode):
+    """Where the packed layout put each string when out_off was not returned: tile t = i // 64 starts at its slot
+    position (decode floor(8 in_off[64 t] / 5), encode in_off[64 t]) and its strings follow back to back; failed
+    strings (HHUFF_FAIL_LEN) take no bytes.  Returns int64 starts[n]"""
+    in_off = np.asarray(in_off, np.int64)
+    ln = np.asarray(out_len, np.uint32)
+    n = ln.size
+    kept = np.where(ln == FAIL_LEN, 0, ln).astype(np.int64)
+    t0 = np.arange(0, n, 64)
+    base = in_off[t0] * 8 // 5 if decode else in_off[t0]
+    cs = np.cumsum(kept) - kept                                  # exclusive prefix over the batch
+    return np.repeat(base - cs[t0], np.diff(np.append(t0, n))) + cs
 
 
 def decode_prices(device=0):

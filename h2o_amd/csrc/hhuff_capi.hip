@@ -988,12 +988,14 @@ int pipelined(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* 
 // (3c) packed host path: the packed kernels (hhuff_*_batch_packed) on host buffers.  With every caller array pinned
 // and aligned the kernels read the strings and write only the outputs' bytes, out_off, out_len and status across
 // PCIe (zero copy; the slot layout's tails, ~45 % of a decode slot and ~25 % of an encode slot on header text,
-// never cross the link); otherwise one staged round trip through device memory.
+// never cross the link); otherwise one staged round trip through device memory.  out_off may be NULL (the caller
+// places string i at its tile's position plus the kept lengths before it in the tile) and so may an encode's
+// status (out_len says HHUFF_FAIL_LEN): 4 and 1 bytes a string fewer across the link.
 int host_packed(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
                 const uint32_t* is_name_bits, uint8_t* out, uint64_t out_size, uint32_t* out_off, uint32_t* out_len,
                 uint8_t* status, int device) {
     if (n == 0) return HHUFF_OK;
-    if (!in || !in_off || !out || !out_off || !out_len || (decode && !status)) return arg_fail("NULL array");
+    if (!in || !in_off || !out || !out_len || (decode && !status)) return arg_fail("NULL array");
     if (in_off[n] > in_size) return arg_fail("in_off[n] > in_size");
     const uint64_t slot_end = decode ? ((uint64_t)in_off[n] * 8) / 5 : in_off[n];
     if (out_size < slot_end) return arg_fail("out_size below the output slots of the batch");
@@ -1020,10 +1022,16 @@ int host_packed(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t
     uint32_t* z_ooff = static_cast<uint32_t*>(dev_ptr(out_off));
     uint32_t* z_len = static_cast<uint32_t*>(dev_ptr(out_len));
     uint8_t* z_st = static_cast<uint8_t*>(dev_ptr(status));
-    const bool zero = z_in && z_off && (!is_name_bits || z_nm) && z_out && z_ooff && z_len && (!status || z_st) &&
-                      al(z_in, 16) && al(z_out, 16) && al(z_off, 4) && al(z_nm, 4) && al(z_ooff, 4) && al(z_len, 4);
+    const bool zero = z_in && z_off && (!is_name_bits || z_nm) && z_out && (!out_off || z_ooff) && z_len &&
+                      (!status || z_st) && al(z_in, 16) && al(z_out, 16) && al(z_off, 4) && al(z_nm, 4) &&
+                      al(z_ooff, 4) && al(z_len, 4);
     hipStream_t s = c.stream;
     if (zero) {
+        if (!out_off) {  // not returned: the kernels' offsets stay in device scratch and never cross the link
+            rc = c.reserve(up16(((size_t)n + 1) * 4), 0);
+            if (rc) return rc;
+            z_ooff = reinterpret_cast<uint32_t*>(c.d);
+        }
         hipError_t e = decode ? hhuff::launch_decode_packed(z_in, in_size, z_off, n, z_nm, z_out, z_ooff, z_len, z_st, s)
                               : hhuff::launch_encode_packed(z_in, in_size, z_off, n, z_out, z_ooff, z_len, z_st, s);
         if (e != hipSuccess) return hip_fail(e, decode ? "packed decode launch (zero copy)" : "packed encode launch (zero copy)");
@@ -1050,7 +1058,7 @@ int host_packed(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t
                           : hhuff::launch_encode_packed(d_in, in_size, d_off, n, d_out, d_ooff, d_len, status ? d_st : nullptr, s);
     if (e != hipSuccess) return hip_fail(e, decode ? "packed decode launch" : "packed encode launch");
     HIP_TRY(hipMemcpyAsync(out, d_out, slot_end, hipMemcpyDeviceToHost, s), "D2H out");
-    HIP_TRY(hipMemcpyAsync(out_off, d_ooff, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, s), "D2H out_off");
+    if (out_off) HIP_TRY(hipMemcpyAsync(out_off, d_ooff, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, s), "D2H out_off");
     HIP_TRY(hipMemcpyAsync(out_len, d_len, (size_t)n * 4, hipMemcpyDeviceToHost, s), "D2H out_len");
     if (status) HIP_TRY(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, s), "D2H status");
     HIP_TRY(hipStreamSynchronize(s), "sync");

@@ -524,7 +524,10 @@ int hhuff_encode_batch_host_pipelined(const uint8_t *in, uint64_t in_size, const
  *     4-byte aligned, the kernels read the input and write the results in host memory themselves and only the
  *     output bytes cross PCIe (the slot layout's unused slot tails do not); otherwise the call stages the batch
  *     through device memory.  out_size >= the slot end (decode floor(8 in_off[n] / 5), encode in_off[n]).
- *     Synchronous. */
+ *     out_off may be NULL: the offsets are then not returned (4 bytes a string fewer across the link) and string i
+ *     starts at its tile's position (decode floor(8 in_off[64 t] / 5), encode in_off[64 t], t = i / 64) plus the
+ *     out_len of the tile's earlier strings that did not fail.  An encode's status may be NULL (out_len already
+ *     says HHUFF_FAIL_LEN); a decode's may not.  Synchronous. */
 int hhuff_decode_batch_host_packed(const uint8_t *in, uint64_t in_size, const uint32_t *in_off, uint32_t n,
                                    const uint32_t *is_name_bits, uint8_t *out, uint64_t out_size, uint32_t *out_off,
                                    uint32_t *out_len, uint8_t *status, int device);

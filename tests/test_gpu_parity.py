@@ -1,5 +1,7 @@
 """HIP path parity: the kernels (through the C-ABI) against the reference's golden vectors and the
 CPU restatement on seeded inputs; size-independent properties at full benchmark sizes."""
+import itertools
+
 import numpy as np
 import pytest
 
@@ -834,7 +836,7 @@ def test_host_packed_path(torch_cuda, kind):
     de_off = torch.zeros(n + 1, dtype=torch.int32, device="cuda")
     de_out, de_off, de_len, de_st = codec.encode_batch_packed(b["data"], off32, n, out=de_out, out_off=de_off, in_size=P)
     torch.cuda.synchronize()
-    shifts = iter([5, 3, 11, 7, 9, 13])
+    shifts = itertools.cycle([5, 3, 11, 7, 9, 13])
 
     def hbuf(count, dt):
         npdt = {torch.uint8: np.uint8, torch.int32: np.int32}[dt]
@@ -857,6 +859,15 @@ def test_host_packed_path(torch_cuda, kind):
     np.testing.assert_array_equal(ost, de_st.cpu().numpy())
     np.testing.assert_array_equal(ooff, de_off.cpu().numpy().view(np.uint32))
     assert compact(out, ooff[:n], olen) == compact(de_out.cpu().numpy(), ooff[:n], g_len)
+    # out_off and status not returned (NULL): the same bytes, placed by packed_positions from out_len alone
+    out2, none_off, olen2, none_st = codec.encode_batch_host_packed(
+        data, off, n, out=hbuf(P + 16, torch.uint8), out_len=hbuf(n, torch.int32).view(np.uint32), with_off=False,
+        with_status=False)
+    assert none_off is None and none_st is None
+    np.testing.assert_array_equal(olen2, g_len)
+    pos = codec.packed_positions(off, olen2, decode=False)
+    np.testing.assert_array_equal(pos, ooff[:n].astype(np.int64))
+    assert compact(out2, pos, olen2) == compact(out, ooff[:n], olen)
     # decode the compressible strings packed back to back (the wire) both ways
     ok = np.nonzero(g_len != FAIL)[0]
     hl = g_len[ok].astype(np.int64)
@@ -887,6 +898,15 @@ def test_host_packed_path(torch_cuda, kind):
     np.testing.assert_array_equal(ooff, dd_off.cpu().numpy().view(np.uint32))
     assert compact(out, ooff[:m], olen) == compact(dd_out.cpu().numpy(), ooff[:m], d_len)
     assert int((olen != FAIL).sum()) == m
+    out2, none_off, olen2, ost2 = codec.decode_batch_host_packed(
+        src, hoff, m, is_name_bits=hn, out=hbuf(codec.decode_slot_size(H), torch.uint8),
+        out_len=hbuf(m, torch.int32).view(np.uint32), status=hbuf(m, torch.uint8), with_off=False)
+    assert none_off is None
+    np.testing.assert_array_equal(olen2, d_len)
+    np.testing.assert_array_equal(ost2, ost)
+    pos = codec.packed_positions(hoff, olen2, decode=True)
+    np.testing.assert_array_equal(pos, ooff[:m].astype(np.int64))
+    assert compact(out2, pos, olen2) == compact(out, ooff[:m], olen)
 
 
 # ------------------------------------------------------------------------------------------------
