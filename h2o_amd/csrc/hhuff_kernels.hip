@@ -1427,7 +1427,11 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
             }();
             uint8_t* gchunk = A.out + ((dst + ocnt) & ~(uint64_t)(SEG - 1));
             const uint32_t hs = head ? (uint32_t)(dst & (SEG - 1u)) : 0u;  // head segment: the string starts here
+#ifdef HHUFF_X_NOSTORE
+            if (false) {
+#else
             if (!done || ok) {  // a failed string's output is unspecified: skip its last stores
+#endif
                 // whole 16-B chunks now: all of them at the string's end, else those of whole segments
                 const uint32_t nfull = done ? nb >> 4 : (nb / SEG) * (SEG / 16u);
                 for (uint32_t k = 0; k < nfull; ++k) {
@@ -1451,8 +1455,10 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
             ocnt += made;
             P += (uint32_t)(pm - pm0);
             if (done) {
+#ifndef HHUFF_X_NOSTORE
                 A.out_len[i] = ok ? ocnt : kFailLen;
                 A.status[i] = ok ? soft_bits(is_name, ocnt, flags, first, lastb) : kStatusFail;
+#endif
                 busy = false;
             }
         }
@@ -2071,7 +2077,11 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream2_kernel(DecArgs A, u
             }();
             uint8_t* gchunk = A.out + ((dst + ocnt) & ~15ull);
             const uint32_t hs = (uint32_t)(dst & 15u);  // head chunk: the string's bytes start here
+#ifdef HHUFF_X_NOSTORE  // ablation builds (output wrong by design): no global stores at all
+            if (false) {
+#else
             if (!done || ok) {  // a failed string's output is unspecified: skip its last stores
+#endif
                 const uint32_t nfull = nb >> 4;
                 for (uint32_t k = 0; k < nfull; ++k) {
                     const uint4 v = lds_ld16(obuf + 16u * k);
@@ -2092,8 +2102,10 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream2_kernel(DecArgs A, u
             ocnt += made;
             P += (uint32_t)(pm - pm0);
             if (done) {
+#ifndef HHUFF_X_NOSTORE
                 A.out_len[i] = ok ? ocnt : kFailLen;
                 A.status[i] = ok ? soft_bits(is_name, ocnt, flags, first, lastb) : kStatusFail;
+#endif
                 busy = false;
             }
         }
