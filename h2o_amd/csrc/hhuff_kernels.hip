@@ -2369,19 +2369,33 @@ __device__ __forceinline__ SortChunk sort_chunk_issue(const EncArgs& A, uint64_t
 // 0: the round-3 order, where the compiler's vmcnt waits for those loads also waited for the stores
 #define HHUFF_ENC_EARLY 1
 #endif
-// NS strings per chunk, one thread each (NS / 64 waves); CH bytes of stage
-template <int NS, int CH>
-__global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
-    constexpr uint32_t kSortStr = NS;
-    constexpr int NV = (CH + 16 * NS - 1) / (16 * NS);  // 16-B span chunks per thread
+// NS strings per chunk on NS / SPT threads (SPT strings a thread); CH bytes of stage.  SPT = 2 pairs the
+// sorted ranks t and NS - 1 - t on thread t, so every lane encodes a short and a long string one after the
+// other and the lanes' work (about twice the mean length) is even across the workgroup: no wave waits at the
+// chunk's barriers for a longest length group.
+#ifndef HHUFF_ENCO_SPT
+#define HHUFF_ENCO_SPT 1
+#endif
+#ifndef HHUFF_ENCO_PAD  // A/B builds: extra LDS bytes per workgroup (fewer resident workgroups)
+#define HHUFF_ENCO_PAD 0
+#endif
+template <int NS, int CH, int SPT = 1>
+__global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
+    static_assert(SPT == 1 || SPT == 2, "one string a thread, or a sorted pair");
+    constexpr uint32_t kSortStr = NS, NT = NS / SPT;
+    constexpr int NV = (CH + 16 * NT - 1) / (16 * NT);  // 16-B span chunks per thread
     __shared__ __attribute__((aligned(16))) uint2 s_enc[512];  // 256..511: bytes outside a string
     __shared__ __attribute__((aligned(16))) uint32_t s_in[CH / 4 + 8];
     __shared__ __attribute__((aligned(16))) uint32_t s_out[CH / 4 + 8];
     __shared__ uint2 s_str[kSortStr];  // {offset in the span, length} of chunk string t
     __shared__ uint16_t s_perm[kSortStr];
     __shared__ uint32_t s_bin[kSortBins];  // strings per bin, then the bins' first places
+#if HHUFF_ENCO_PAD
+    __shared__ uint32_t s_pad[HHUFF_ENCO_PAD / 4];
+    if (A.n == 0xFFFFFFFFu) s_pad[threadIdx.x % (HHUFF_ENCO_PAD / 4)] = 0u;  // (never: keeps the bytes allocated)
+#endif
     const uint32_t t = threadIdx.x, lane = t & 63u;
-    for (uint32_t k = t; k < 512; k += NS) s_enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
+    for (uint32_t k = t; k < 512; k += NT) s_enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
     const uint64_t nch = ((uint64_t)A.n + kSortStr - 1) / kSortStr;
     uint64_t c = blockIdx.x;
     if (c >= nch) return;
@@ -2390,7 +2404,7 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         const uint32_t a0 = q.lo & ~15u, span = span_of(q);
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            const uint32_t k = (uint32_t)j * (16u * NS) + t * 16u;
+            const uint32_t k = (uint32_t)j * (16u * NT) + t * 16u;
             const uint64_t g = (uint64_t)a0 + k;
             if (k < span && span <= (uint32_t)CH && g + 16 <= A.in_size) v[j] = *reinterpret_cast<const uint4*>(A.in + g);
         }
@@ -2399,78 +2413,101 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         const uint32_t a0 = q.lo & ~15u, span = span_of(q);
 #pragma unroll
         for (int j = 0; j < NV; ++j) {
-            const uint32_t k = (uint32_t)j * (16u * NS) + t * 16u;
+            const uint32_t k = (uint32_t)j * (16u * NT) + t * 16u;
             const uint64_t g = (uint64_t)a0 + k;
             if (k < span) *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_in) + k) =
                 g + 16 <= A.in_size ? v[j] : load16_tail(A.in, A.in_size, g);
         }
     };
-    if (t < kSortBins) s_bin[t] = 0u;  // then cleared by each chunk once every wave has read it
+    auto issue_chunk = [&](SortChunk (&q)[SPT], uint64_t qb) {
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) q[u] = sort_chunk_issue(A, qb, t + (uint32_t)u * NT, NS);
+    };
+    auto land = [](SortChunk (&q)[SPT]) {  // wait for a chunk's offsets here (see HHUFF_ENC_EARLY)
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) __asm__ volatile("" : "+v"(q[u].s), "+v"(q[u].e), "+v"(q[u].lo), "+v"(q[u].hi) : : "memory");
+    };
+    for (uint32_t k = t; k < kSortBins; k += NT) s_bin[k] = 0u;  // then cleared by each chunk once every wave has read it
     __syncthreads();
     // prepare(q): chunk q's span into the input stage, the output stage zeroed from z0 on ([0, z0) is zero
     // already), its strings' {offset, length} and their ranks within their length bins.  Called once
     // nothing reads those areas any more (three barriers a chunk in all).
     uint4 pv[NV];
-    uint32_t bin = 0, rank = 0;
-    auto prepare = [&](const SortChunk& q, uint64_t qb, uint32_t z0) {
-        const uint32_t sp = span_of(q);
+    uint32_t bin[SPT], rank[SPT];
+    auto prepare = [&](const SortChunk (&q)[SPT], uint64_t qb, uint32_t z0) {
+        const uint32_t sp = span_of(q[0]);
         if (sp > (uint32_t)CH) return;  // workgroup-uniform: the per-thread path needs none of it
-        commit_span(pv, q);
-        for (uint32_t k = z0 + t * 16u; k < sp + 16u; k += 16u * NS)
+        commit_span(pv, q[0]);
+        for (uint32_t k = z0 + t * 16u; k < sp + 16u; k += 16u * NT)
             *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_out) + k) = make_uint4(0u, 0u, 0u, 0u);
-        const uint32_t ln = qb + t < A.n ? q.e - q.s : 0u;
-        s_str[t] = make_uint2(q.s - (q.lo & ~15u), ln);
-        // counting sort by the bulk loop's trip count (encode_chunk_v2: dwords from the string's first aligned
-        // dword to its end), which the wave's longest string sets
-        bin = ln ? min((q.s + ln - (q.s & ~3u)) >> 2, kSortBins - 1u) : 0u;
-        rank = atomicAdd(&s_bin[bin], 1u);
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) {
+            const uint32_t tt = t + (uint32_t)u * NT;
+            const uint32_t ln = qb + tt < A.n ? q[u].e - q[u].s : 0u;
+            s_str[tt] = make_uint2(q[u].s - (q[0].lo & ~15u), ln);
+            // counting sort by the bulk loop's trip count (encode_chunk_v2: dwords from the string's first
+            // aligned dword to its end), which the wave's longest string sets
+            bin[u] = ln ? min((q[u].s + ln - (q[u].s & ~3u)) >> 2, kSortBins - 1u) : 0u;
+            rank[u] = atomicAdd(&s_bin[bin[u]], 1u);
+        }
     };
-    SortChunk cur = sort_chunk_issue(A, c * kSortStr, t, NS);
-    issue_span(pv, cur);
+    SortChunk cur[SPT];
+    issue_chunk(cur, c * kSortStr);
+    issue_span(pv, cur[0]);
     prepare(cur, c * kSortStr, 0u);
 #if HHUFF_ENC_EARLY
     // the next chunk's offsets are loaded a chunk ahead (after barrier 2) and waited for after barrier 3,
     // before the chunk's stores: no load is then waited for behind a data-dependent number of stores
-    SortChunk nxt = sort_chunk_issue(A, (c + gridDim.x < nch ? c + gridDim.x : c) * kSortStr, t, NS);
-    __asm__ volatile("" : "+v"(nxt.s), "+v"(nxt.e), "+v"(nxt.lo), "+v"(nxt.hi) : : "memory");  // (once)
+    SortChunk nxt[SPT];
+    issue_chunk(nxt, (c + gridDim.x < nch ? c + gridDim.x : c) * kSortStr);
+    land(nxt);  // (once)
 #endif
     PROF_DECL  // profile builds: barrier 1 / ranks + barrier 2 / encode / barrier 3 + lengths / copy out / prepare
     for (;;) {
-        const uint64_t cb = c * kSortStr, i = cb + t;
-        const bool valid = i < A.n;
-        const uint32_t len = valid ? cur.e - cur.s : 0u;
-        const uint32_t lo = cur.lo, hi = cur.hi, a0 = lo & ~15u, span = span_of(cur);
+        const uint64_t cb = c * kSortStr;
+        const uint32_t lo = cur[0].lo, hi = cur[0].hi, a0 = lo & ~15u, span = span_of(cur[0]);
         EdgeRec* rec = A.edges + 2 * c;  // two records a chunk (sorted_edge_recs)
         const uint64_t cn = c + gridDim.x;
         const bool more = cn < nch;
 #if !HHUFF_ENC_EARLY
-        SortChunk nxt = sort_chunk_issue(A, (more ? cn : c) * kSortStr, t, NS);  // in flight during this chunk
+        SortChunk nxt[SPT];
+        issue_chunk(nxt, (more ? cn : c) * kSortStr);  // in flight during this chunk
 #endif
         const uint64_t cn2 = cn + gridDim.x;  // (HHUFF_ENC_EARLY) the chunk after next
         (void)cn2;
         __syncthreads();  // the chunk's stage, strings and ranks are in
         PROF_MARK(0);
         if (span > (uint32_t)CH) {  // (workgroup-uniform) a chunk larger than the stage: one thread per string
-            uint32_t ol = kFailLen;
-            if (valid && len <= kMaxStrLen) {
-                RegSink sink;
-                sink.init(A.out + cur.s);
-                ol = encode_core(GlobalSource{A.in, A.in_size}, cur.s, len, sink, s_enc);
+#pragma unroll
+            for (int u = 0; u < SPT; ++u) {
+                const uint64_t i = cb + t + (uint32_t)u * NT;
+                const uint32_t len = i < A.n ? cur[u].e - cur[u].s : 0u;
+                uint32_t ol = kFailLen;
+                if (i < A.n && len <= kMaxStrLen) {
+                    RegSink sink;
+                    sink.init(A.out + cur[u].s);
+                    ol = encode_core(GlobalSource{A.in, A.in_size}, cur[u].s, len, sink, s_enc);
+                }
+                if (i < A.n) finish_encode(A, (uint32_t)i, len, ol);
             }
-            if (valid) finish_encode(A, (uint32_t)i, len, ol);
             if (t < 2) rec[t].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges to defer
             if (!more) break;
-            issue_span(pv, nxt);
+            issue_span(pv, nxt[0]);
             prepare(nxt, cn * kSortStr, 0u);
 #if HHUFF_ENC_EARLY
             {
-                SortChunk nn = sort_chunk_issue(A, (cn2 < nch ? cn2 : cn) * kSortStr, t, NS);
-                __asm__ volatile("" : "+v"(nn.s), "+v"(nn.e), "+v"(nn.lo), "+v"(nn.hi) : : "memory");
-                cur = nxt;
-                nxt = nn;
+                SortChunk nn[SPT];
+                issue_chunk(nn, (cn2 < nch ? cn2 : cn) * kSortStr);
+                land(nn);
+#pragma unroll
+                for (int u = 0; u < SPT; ++u) {
+                    cur[u] = nxt[u];
+                    nxt[u] = nn[u];
+                }
             }
 #else
-            cur = nxt;
+#pragma unroll
+            for (int u = 0; u < SPT; ++u) cur[u] = nxt[u];
 #endif
             c = cn;
             continue;
@@ -2478,46 +2515,58 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         {  // every wave scans the bin counts (two per lane)
             const uint32_t x0 = s_bin[2 * lane], x1 = s_bin[2 * lane + 1];
             const uint32_t ex = wave_excl_scan(x0 + x1, (int)lane);
-            const uint32_t eb = (uint32_t)__shfl((int)ex, (int)(bin >> 1)), xb = (uint32_t)__shfl((int)x0, (int)(bin >> 1));
-            s_perm[eb + ((bin & 1u) ? xb : 0u) + rank] = (uint16_t)t;
+#pragma unroll
+            for (int u = 0; u < SPT; ++u) {
+                const uint32_t eb = (uint32_t)__shfl((int)ex, (int)(bin[u] >> 1)), xb = (uint32_t)__shfl((int)x0, (int)(bin[u] >> 1));
+                s_perm[eb + ((bin[u] & 1u) ? xb : 0u) + rank[u]] = (uint16_t)(t + (uint32_t)u * NT);
+            }
         }
         __syncthreads();
         PROF_MARK(1);
-        if (t < kSortBins) s_bin[t] = 0u;  // read by every wave above: cleared for the next chunk
-        if (more) issue_span(pv, nxt);     // the next chunk's span: in flight during the encode
+        for (uint32_t k = t; k < kSortBins; k += NT) s_bin[k] = 0u;  // read by every wave above: cleared for the next chunk
+        if (more) issue_span(pv, nxt[0]);     // the next chunk's span: in flight during the encode
 #if HHUFF_ENC_EARLY
-        SortChunk nn = sort_chunk_issue(A, (cn2 < nch ? cn2 : (more ? cn : c)) * kSortStr, t, NS);
+        SortChunk nn[SPT];
+        issue_chunk(nn, (cn2 < nch ? cn2 : (more ? cn : c)) * kSortStr);
 #endif
-        // sorted position t = 64 wave + lane: wave w encodes the w-th length group
-        const uint32_t j = s_perm[t];
-        const uint2 sj = s_str[j];
-        const bool vj = cb + j < A.n;
-        const bool act = vj && sj.y != 0 && sj.y <= kMaxStrLen;
-        const uint32_t tb = encode_chunk_v2(s_in, span - 4u, sj.x, sj.y, act, lds_addr(s_out), 8u * sj.x, s_enc,
-                                            act ? 8 * sj.y - 7 : 0xFFFFFFFFu, true);
-        // the encoded length goes back to the string's own record (read by this thread only), so the lengths
-        // and statuses are stored in string order, coalesced
-        s_str[j].x = act && tb != kFailLen ? (tb + 7) >> 3 : kFailLen;
+        // sorted position t = 64 wave + lane: wave w encodes the w-th length group (SPT = 2: then also the
+        // sorted position NS - 1 - t, so the pair's lengths add up to about twice the mean)
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) {
+            const uint32_t j = s_perm[u == 0 ? t : NS - 1u - t];
+            const uint2 sj = s_str[j];
+            const bool vj = cb + j < A.n;
+            const bool act = vj && sj.y != 0 && sj.y <= kMaxStrLen;
+            const uint32_t tb = encode_chunk_v2(s_in, span - 4u, sj.x, sj.y, act, lds_addr(s_out), 8u * sj.x, s_enc,
+                                                act ? 8 * sj.y - 7 : 0xFFFFFFFFu, true);
+            // the encoded length goes back to the string's own record (read by its own thread only), so the
+            // lengths and statuses are stored in string order, coalesced
+            s_str[j].x = act && tb != kFailLen ? (tb + 7) >> 3 : kFailLen;
+        }
         PROF_MARK(2);
         __syncthreads();
+        uint32_t olen[SPT];
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) olen[u] = s_str[t + (uint32_t)u * NT].x;
 #if HHUFF_ENC_EARLY
         // the next chunk goes in now, before this chunk's stores: its span loads (in flight since the encode
         // began) are then waited for with no store ahead of them in the memory counter
-        const uint32_t olen = s_str[t].x;  // (prepare overwrites this thread's record)
-        if (more) prepare(nxt, cn * kSortStr, span);
+        if (more) prepare(nxt, cn * kSortStr, span);  // (overwrites this thread's records: olen read above)
         // the chunk after next's offsets are waited for here too, on every path: `nxt = nn` below then copies
         // registers with no load pending, not behind this chunk's stores
-        __asm__ volatile("" : "+v"(nn.s), "+v"(nn.e), "+v"(nn.lo), "+v"(nn.hi) : : "memory");
+        land(nn);
         PROF_MARK(5);
-        if (valid) finish_encode(A, (uint32_t)i, len, olen);
-#else
-        if (valid) finish_encode(A, (uint32_t)i, len, s_str[t].x);
 #endif
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) {
+            const uint64_t i = cb + t + (uint32_t)u * NT;
+            if (i < A.n) finish_encode(A, (uint32_t)i, cur[u].e - cur[u].s, olen[u]);
+        }
         PROF_MARK(3);
         // the stage's MSB-first words, byte-swapped on the way out (each read chunk is zeroed for the next
         // chunk); the chunk's first and last 16-B chunks are deferred (edge_fix_kernel)
         const uint32_t kl = (span - 1u) & ~15u;
-        for (uint32_t k = t * 16u; k < span; k += 16u * NS) {
+        for (uint32_t k = t * 16u; k < span; k += 16u * NT) {
             const uint64_t g = (uint64_t)a0 + k;
             uint4* sp = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_out) + k);
             uint4 v = *sp;
@@ -2546,10 +2595,13 @@ __global__ __launch_bounds__(NS) void encode_sorted_kernel(EncArgs A) {
         prepare(nxt, cn * kSortStr, span);
         PROF_MARK(5);
 #endif
-        cur = nxt;
+#pragma unroll
+        for (int u = 0; u < SPT; ++u) {
+            cur[u] = nxt[u];
 #if HHUFF_ENC_EARLY
-        nxt = nn;
+            nxt[u] = nn[u];
 #endif
+        }
         c = cn;
     }
 }
@@ -4166,7 +4218,7 @@ constexpr int kDecSWaves = 16, kEncSWaves = 16, kEncOStr = HHUFF_ENCO_NS;
 #endif
 #endif
 #define ENC_S encode_staged_kernel<kEncSWaves, 3584, false>
-#define ENC_O encode_sorted_kernel<kEncOStr, HHUFF_ENCO_CH>
+#define ENC_O encode_sorted_kernel<kEncOStr, HHUFF_ENCO_CH, HHUFF_ENCO_SPT>
 #define ENC_L encode_staged_kernel<8, 8192, false>
 #define ENC_SP encode_staged_kernel<kEncSWaves, 3584, true>
 #define ENC_LP encode_staged_kernel<8, 8192, true>
@@ -4208,7 +4260,7 @@ static int variant_threads(int v) {
         case kDecLP: return 384;
         case kEncL:
         case kEncLP: return 512;
-        case kEncO: return kEncOStr;
+        case kEncO: return kEncOStr / HHUFF_ENCO_SPT;
         case kEncP:
         case kFlatP: return 1024;
         default: return 256;
@@ -4744,7 +4796,7 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     }
     switch (v) {
         case kEncS: hipLaunchKernelGGL(ENC_S, dim3(grid), dim3(kEncSWaves * 64), 0, stream, A); break;
-        case kEncO: hipLaunchKernelGGL(ENC_O, dim3(grid), dim3(kEncOStr), 0, stream, A); break;
+        case kEncO: hipLaunchKernelGGL(ENC_O, dim3(grid), dim3(kEncOStr / HHUFF_ENCO_SPT), 0, stream, A); break;
         case kEncL: hipLaunchKernelGGL(ENC_L, dim3(grid), dim3(512), 0, stream, A); break;
         default: hipLaunchKernelGGL(ENC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }
