@@ -2607,6 +2607,388 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// In-place sorted encode (HHUFF_ENC_INPLACE; review r4 next 3).  encode_sorted_kernel's chunks with one stage
+// instead of two, so a workgroup of 4 waves holds 512 strings and each thread encodes a sorted pair (ranks t and
+// NS - 1 - t): the lanes' work is even across the workgroup (no wave waits at a barrier for a longest length
+// group) at the same 16 waves a CU.  A string's output slot is its own input range, so its codes overwrite its
+// own bytes:
+//   * a lane clears exactly its own bytes of each input word as it reads it (one ds_and_rtn: the word's value
+//     comes back, the neighbours' bytes stay), one word ahead of the word it encodes, so its OR-placed codes
+//     land on zeros and the slot's tail is zero at the end;
+//   * codes that would end past the words it has read (a prefix of long codes outrunning the input) are not
+//     placed: the lane counts on, and a string that stays shorter than its input is encoded again from global
+//     memory after the chunk's encode barrier (`redo`; strings of random bytes fail on their own);
+//   * each thread puts the next chunk's span into the stage piece by piece as it copies its pieces out.
+// Same results as encode_core (hpack.c:774-804).
+// ------------------------------------------------------------------------------------------------
+struct EncIP {
+    const uint2* enc;
+    uint32_t obase;  // LDS byte address of the stage (input and MSB-first output)
+    uint32_t tb;     // next stage bit
+    uint32_t tlim;   // stage bit at which the string fails
+    bool live, fail, haz;
+    // one masked dword (a string's first or last word): rlim = the stage bit below which every word is read
+    __device__ __forceinline__ void put4(uint2 e0, uint2 e1, uint2 e2, uint2 e3, bool on, uint32_t rlim) {
+        const uint32_t n01 = e0.y + e1.y, n23 = e2.y + e3.y, n = n01 + n23;
+        const bool lng = max(max(e0.y, e1.y), max(e2.y, e3.y)) > 16u;
+        const bool over = on && live && tb + n >= tlim;
+        fail = fail || over;
+        live = live && !over;
+        haz = haz || (on && live && tb + n > rlim);
+        const bool put = on && live && !haz;
+        if (__any(put && lng)) {
+            if (put && lng) {
+                place_bits(obase, tb, (uint64_t)e0.x << e1.y | e1.x, n01);
+                place_bits(obase, tb + n01, (uint64_t)e2.x << e3.y | e3.x, n23);
+            }
+        }
+        const bool f = put && !lng;
+        const uint32_t p01 = e0.x << e1.y | e1.x, p23 = e2.x << e3.y | e3.x;
+        const uint64_t cc = f ? ((uint64_t)p01 << n23 | p23) : 0ull;
+        place_bits(obase, tb, cc, f ? n : 0u);
+        tb += (on && live) ? n : 0u;  // a lane past its read words counts on (its verdict decides the redo)
+    }
+    // one whole dword (bulk), predicates as VGPR masks (EncV2::put4m); hzm: sticky "stopped placing" mask
+    __device__ __forceinline__ void put4m(uint2 e0, uint2 e1, uint2 e2, uint2 e3, uint32_t onm, uint32_t rlim,
+                                          uint32_t& hzm) {
+        const uint32_t n01 = e0.y + e1.y, n23 = e2.y + e3.y, n = n01 + n23;
+        const uint32_t mx = max(max(e0.y, e1.y), max(e2.y, e3.y));
+        const uint32_t lngm = (uint32_t)((int32_t)(16u - mx) >> 31);
+        const uint32_t nm = n & onm;
+        const uint32_t okm = (uint32_t)((int32_t)(tb + nm - tlim) >> 31);        // still below the fail bit
+        const uint32_t rdm = ~(uint32_t)((int32_t)(rlim - (tb + nm)) >> 31);     // ends inside the read words
+        hzm |= onm & okm & ~rdm;
+        const uint32_t putm = onm & okm & ~hzm;
+        if (__builtin_amdgcn_ballot_w64((putm & lngm) != 0u) != 0) {
+            if (putm & lngm) {
+                place_bits(obase, tb, (uint64_t)e0.x << e1.y | e1.x, n01);
+                place_bits(obase, tb + n01, (uint64_t)e2.x << e3.y | e3.x, n23);
+            }
+        }
+        const uint32_t fm = putm & ~lngm;
+        const uint32_t p01 = e0.x << e1.y | e1.x, p23 = e2.x << e3.y | e3.x;
+        const uint64_t cc = ((uint64_t)p01 << n23 | p23) & ((uint64_t)fm << 32 | fm);
+        const uint32_t nf = n & fm;
+        const uint64_t t = cc << ((64u - nf) & 63u);
+        const uint32_t sh = tb & 31u;
+        const uint64_t u = t >> sh;
+        const uint32_t a = obase + ((tb >> 3) & ~3u);
+        lds_or32(a, (uint32_t)(u >> 32));
+        lds_or32(a + 4u, (uint32_t)u);
+        if (__builtin_amdgcn_ballot_w64(sh + nf > 64u) != 0) {
+            if (sh + nf > 64u) lds_or32(a + 8u, (uint32_t)t << (32u - sh));
+        }
+        tb += nm;
+    }
+};
+
+// Encode stage bytes [start, start + len) in place (stage at LDS byte address sbase; `last`: the stage's last
+// word offset, where reads are clamped).  Returns the code bits or kFailLen; redo = the codes were counted
+// but not all placed (the string is still to be encoded: encode_redo).
+__device__ __forceinline__ uint32_t encode_inplace_lane(uint32_t sbase, uint32_t last, uint32_t start, uint32_t len,
+                                                        bool active, const uint2* __restrict__ enc, uint32_t limit,
+                                                        bool& redo) {
+    const uint32_t end = start + len;
+    const uint32_t a0 = start & ~3u, a0w = a0 >> 2, lastw = last >> 2;
+    const uint32_t ndw = active ? (end - a0 + 3u) >> 2 : 0u;  // the string's words [a0w, a0w + ndw)
+    const uint32_t jl = active ? (end - a0) >> 2 : 0u;        // whole words [1, jl) after word 0; tail word jl
+    // the stage holds big-endian words (committed byte-swapped): string byte k of a word at bits 31 - 8k, the
+    // same place the MSB-first output puts stream byte k -- so a lane's codes fall on its own bytes
+    const uint32_t mfirst = 0xFFFFFFFFu >> (8u * (start & 3u));
+    const uint32_t mlast = (uint32_t)(0xFFFFFFFFull << ((32u - 8u * (end & 3u)) & 31u));
+    auto mo = [&](uint32_t q) -> uint32_t {  // this string's bytes of its word q
+        const uint32_t m = (q == 0 ? mfirst : 0xFFFFFFFFu) & (q + 1u == ndw ? mlast : 0xFFFFFFFFu);
+        return q < ndw ? m : 0u;
+    };
+    auto rc = [&](uint32_t q) -> uint32_t {  // read word q and clear this string's bytes of it
+        const uint32_t idx = min(a0w + q, lastw);
+        return __hip_atomic_fetch_and((lds_u32*)(size_t)(sbase + 4u * idx), ~mo(q), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    const uint32_t startbit = 8u * start, base = 32u * a0w;
+    EncIP E{enc, sbase, startbit, limit >= 0x40000000u ? 0x7FFFFFFFu : startbit + limit, active, false, false};
+    auto masked = [&](uint32_t w, uint32_t vm, bool on, uint32_t rlim) {
+        vm = on ? vm : 0u;
+        const uint32_t iw = ~vm & 0x01010101u;
+        E.put4(enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)], enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)],
+               enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)], enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0400u)], on, rlim);
+    };
+    const uint32_t w0 = rc(0);
+    uint32_t wn = rc(1);  // one word ahead: read (and cleared) before word 0's codes are placed
+    uint32_t wt = wn;     // the tail word's value (word jl), kept as the bulk loop reads past it
+    masked(w0, mo(0), active && ndw != 0, base + 32u * min(2u, ndw));
+    {
+        const uint32_t jlv = E.live ? jl : 0u;  // a lane that failed in word 0 places nothing more
+        const uint32_t jend = wave_max_u32(jlv);
+        uint32_t hzm = E.haz ? 0xFFFFFFFFu : 0u;
+        for (uint32_t j = 1; j < jend; ++j) {  // bulk: whole words
+            const uint32_t w = wn;
+            wn = rc(j + 1u);
+            wt = j + 1u == jl ? wn : wt;
+            const uint32_t onm = j < jlv ? 0xFFFFFFFFu : 0u;
+            E.put4m(enc[w >> 24], enc[(w >> 16) & 0xFFu], enc[(w >> 8) & 0xFFu], enc[w & 0xFFu], onm,
+                    base + 32u * min(j + 2u, ndw), hzm);
+        }
+        E.haz = E.haz || hzm != 0u;
+    }
+    E.fail = E.fail || (E.live && E.tb >= E.tlim);
+    E.live = E.live && !E.fail;
+    masked(wt, mlast, active && (end & 3u) != 0 && jl >= 1u, base + 32u * ndw);  // tail
+    if (E.fail || !active) return kFailLen;
+    if (E.haz) {
+        redo = true;
+        return E.tb - startbit;
+    }
+    const uint32_t p = (0u - E.tb) & 7u;  // EOS-prefix padding (hpack.c:795-798)
+    place_bits(sbase, E.tb, (1ull << p) - 1ull, p);
+    return E.tb - startbit;
+}
+
+// A string encode_inplace_lane stopped placing: its bytes cleared and its codes placed again, reading the
+// input from global memory (after the chunk's encode barrier: every lane's reads are done).
+__device__ __forceinline__ void encode_redo(uint32_t sbase, const uint8_t* __restrict__ in, uint64_t in_size, uint64_t g0,
+                                         uint32_t start, uint32_t len, const uint2* __restrict__ enc) {
+    const uint32_t end = start + len, a0w = start >> 2, ndw = (end - (start & ~3u) + 3u) >> 2;
+    const uint32_t mfirst = 0xFFFFFFFFu >> (8u * (start & 3u));  // (big-endian stage words)
+    const uint32_t mlast = (uint32_t)(0xFFFFFFFFull << ((32u - 8u * (end & 3u)) & 31u));
+    for (uint32_t q = 0; q < ndw; ++q) {
+        const uint32_t m = (q == 0 ? mfirst : 0xFFFFFFFFu) & (q + 1u == ndw ? mlast : 0xFFFFFFFFu);
+        __hip_atomic_fetch_and((lds_u32*)(size_t)(sbase + 4u * (a0w + q)), ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    const GlobalSource src{in, in_size};
+    uint32_t tb = 8u * start;
+    const uint64_t g1 = g0 + len;
+    for (uint64_t a = g0 & ~3ull; a < g1; a += 4) {
+        const uint32_t w = src.word(a);
+        for (uint32_t k = 0; k < 4; ++k) {
+            if (a + k < g0 || a + k >= g1) continue;
+            const uint2 e = enc[(w >> (8 * k)) & 0xFFu];
+            place_bits(sbase, tb, e.x, e.y);
+            tb += e.y;
+        }
+    }
+    const uint32_t p = (0u - tb) & 7u;
+    place_bits(sbase, tb, (1ull << p) - 1ull, p);
+}
+
+// a chunk's two strings per thread (offsets) and its span bounds (made wave-uniform once landed)
+struct PairChunk {
+    uint32_t s0, e0, s1, e1, lo, hi;
+};
+template <int NS, int CH>
+#ifndef HHUFF_ENCI_EARLY_SPAN
+#define HHUFF_ENCI_EARLY_SPAN 0
+#endif
+#ifndef HHUFF_ENCI_WPE  // waves per SIMD the register allocation is held to (4: 128 VGPRs)
+#define HHUFF_ENCI_WPE 4
+#endif
+__global__ __launch_bounds__(NS / 2) __attribute__((amdgpu_waves_per_eu(HHUFF_ENCI_WPE, HHUFF_ENCI_WPE))) void encode_inplace_kernel(EncArgs A) {
+    constexpr uint32_t NT = NS / 2;
+    constexpr int NV = (CH + 16 * NT - 1) / (16 * NT);  // 16-B span pieces per thread
+    __shared__ __attribute__((aligned(16))) uint2 s_enc[512];  // 256..511: bytes outside a string
+    __shared__ __attribute__((aligned(16))) uint32_t s_st[CH / 4 + 8];
+    __shared__ uint2 s_str[NS];  // {offset in the span, length} of chunk string t (.x: then its encoded length)
+    __shared__ uint16_t s_perm[NS];
+    __shared__ uint32_t s_bin[kSortBins];
+    __shared__ uint32_t s_redo;
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    const uint32_t sbase = lds_addr(s_st);
+    for (uint32_t k = t; k < 512; k += NT) s_enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
+    const uint32_t nch = (uint32_t)(((uint64_t)A.n + NS - 1) / NS);  // (32-bit chunk and string indices)
+    uint32_t c = blockIdx.x;
+    if (c >= nch) return;
+    auto issue_chunk = [&](uint32_t qb) {  // (clamped: every load issues)
+        PairChunk q;
+        const uint32_t i0 = min(qb + t, A.n - 1u), i1 = min(qb + t + NT, A.n - 1u);
+        q.s0 = A.in_off[i0];
+        q.e0 = A.in_off[i0 + 1];
+        q.s1 = A.in_off[i1];
+        q.e1 = A.in_off[i1 + 1];
+        q.lo = A.in_off[min(qb, A.n - 1u)];
+        q.hi = A.in_off[min(qb + NS, A.n)];
+        return q;
+    };
+    auto land = [](PairChunk& q) {  // its loads are waited for here; the bounds then live in SGPRs
+        __asm__ volatile("" : "+v"(q.s0), "+v"(q.e0), "+v"(q.s1), "+v"(q.e1), "+v"(q.lo), "+v"(q.hi) : : "memory");
+        q.lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)q.lo);
+        q.hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)q.hi);
+    };
+    auto span_of = [](const PairChunk& q) { return q.hi > q.lo ? ((q.hi + 15u) & ~15u) - (q.lo & ~15u) : 0u; };
+    auto issue_span = [&](uint4 (&v)[NV], const PairChunk& q) {
+        const uint32_t a0 = q.lo & ~15u, span = span_of(q);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const uint32_t k = (uint32_t)j * (16u * NT) + t * 16u;
+            const uint64_t g = (uint64_t)a0 + k;
+            if (k < span && span <= (uint32_t)CH && g + 16 <= A.in_size) v[j] = *reinterpret_cast<const uint4*>(A.in + g);
+        }
+    };
+    // piece j of q's span (the input's end: bounded), its words byte-swapped: the stage holds big-endian words
+    auto piece = [&](const uint4 (&v)[NV], int j, const PairChunk& q) {
+        const uint64_t g = (uint64_t)(q.lo & ~15u) + (uint32_t)j * (16u * NT) + t * 16u;
+        const uint4 x = g + 16 <= A.in_size ? v[j] : load16_tail(A.in, A.in_size, g);
+        return make_uint4(bswap32(x.x), bswap32(x.y), bswap32(x.z), bswap32(x.w));
+    };
+    uint32_t bin[2], rank[2];
+    auto meta = [&](const PairChunk& q, uint32_t qb) {  // the chunk's string records and length ranks
+        const uint32_t ss[2] = {q.s0, q.s1}, ee[2] = {q.e0, q.e1};
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const uint32_t tt = t + (uint32_t)u * NT;
+            const uint32_t ln = qb + tt < A.n ? ee[u] - ss[u] : 0u;
+            s_str[tt] = make_uint2(ss[u] - (q.lo & ~15u), ln);
+            bin[u] = ln ? min((ss[u] + ln - (ss[u] & ~3u)) >> 2, kSortBins - 1u) : 0u;
+            rank[u] = atomicAdd(&s_bin[bin[u]], 1u);
+        }
+    };
+    for (uint32_t k = t; k < kSortBins; k += NT) s_bin[k] = 0u;
+    if (t == 0) s_redo = 0u;
+    __syncthreads();
+    uint4 pv[NV];
+    PairChunk cur = issue_chunk(c * NS);
+    land(cur);
+    issue_span(pv, cur);
+    if (span_of(cur) <= (uint32_t)CH) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const uint32_t k = (uint32_t)j * (16u * NT) + t * 16u;
+            if (k < span_of(cur)) *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_st) + k) = piece(pv, j, cur);
+        }
+        meta(cur, c * NS);
+    }
+    PairChunk nxt = issue_chunk((c + gridDim.x < nch ? c + gridDim.x : c) * NS);
+    land(nxt);  // (once)
+    for (;;) {
+        const uint32_t cb = c * NS;
+        const uint32_t lo = cur.lo, hi = cur.hi, a0 = lo & ~15u, span = span_of(cur);
+        EdgeRec* rec = A.edges + 2 * c;
+        const uint32_t cn = c + gridDim.x, cn2 = cn + gridDim.x;
+        const bool more = cn < nch;
+        __syncthreads();  // barrier 1: the chunk's stage, records and ranks are in
+        if (span > (uint32_t)CH) {  // (workgroup-uniform) a chunk larger than the stage: one thread per string
+            const uint32_t ss[2] = {cur.s0, cur.s1}, ee[2] = {cur.e0, cur.e1};
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint32_t i = cb + t + (uint32_t)u * NT;
+                const uint32_t len = i < A.n ? ee[u] - ss[u] : 0u;
+                uint32_t ol = kFailLen;
+                if (i < A.n && len <= kMaxStrLen) {
+                    RegSink sink;
+                    sink.init(A.out + ss[u]);
+                    ol = encode_core(GlobalSource{A.in, A.in_size}, ss[u], len, sink, s_enc);
+                }
+                if (i < A.n) finish_encode(A, i, len, ol);
+            }
+            if (t < 2) rec[t].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges to defer
+            if (!more) break;
+            issue_span(pv, nxt);
+            if (span_of(nxt) <= (uint32_t)CH) {
+#pragma unroll
+                for (int j = 0; j < NV; ++j) {
+                    const uint32_t k = (uint32_t)j * (16u * NT) + t * 16u;
+                    if (k < span_of(nxt)) *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_st) + k) = piece(pv, j, nxt);
+                }
+                meta(nxt, cn * NS);
+            }
+            PairChunk nn = issue_chunk((cn2 < nch ? cn2 : cn) * NS);
+            land(nn);
+            cur = nxt;
+            nxt = nn;
+            c = cn;
+            continue;
+        }
+        {  // every wave scans the bin counts (two per lane)
+            const uint32_t x0 = s_bin[2 * lane], x1 = s_bin[2 * lane + 1];
+            const uint32_t ex = wave_excl_scan(x0 + x1, (int)lane);
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint32_t eb = (uint32_t)__shfl((int)ex, (int)(bin[u] >> 1)), xb = (uint32_t)__shfl((int)x0, (int)(bin[u] >> 1));
+                s_perm[eb + ((bin[u] & 1u) ? xb : 0u) + rank[u]] = (uint16_t)(t + (uint32_t)u * NT);
+            }
+        }
+        __syncthreads();  // barrier 2: the sorted order is in
+        for (uint32_t k = t; k < kSortBins; k += NT) s_bin[k] = 0u;
+#if HHUFF_ENCI_EARLY_SPAN  // the next chunk's span in flight during the encode (its 28 VGPRs spill the encode)
+        if (more) issue_span(pv, nxt);
+#endif
+#if HHUFF_ENCI_EARLY_SPAN
+        PairChunk nn = issue_chunk((cn2 < nch ? cn2 : (more ? cn : c)) * NS);
+#endif
+        uint32_t rdo[2] = {0u, 0u};  // a string to encode again: its span offset | its length << 16
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {  // sorted positions t and NS - 1 - t: a short and a long string
+            const uint32_t j = s_perm[u == 0 ? t : NS - 1u - t];
+            const uint2 sj = s_str[j];
+            const bool act = cb + j < A.n && sj.y != 0 && sj.y <= kMaxStrLen;
+            bool rd = false;
+            const uint32_t tb = encode_inplace_lane(sbase, span - 4u, sj.x, sj.y, act, s_enc,
+                                                    act ? 8 * sj.y - 7 : 0xFFFFFFFFu, rd);
+            s_str[j].x = act && tb != kFailLen ? (tb + 7) >> 3 : kFailLen;
+            if (rd) {
+                s_redo = 1u;
+                rdo[u] = sj.x | sj.y << 16;  // (offsets and lengths < CH < 2^16)
+            }
+        }
+        __syncthreads();  // barrier 3: every string encoded (or counted)
+        if (s_redo != 0u) {  // (workgroup-uniform) strings whose codes outran their reads: encoded again
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (rdo[u] >> 16)
+                    encode_redo(sbase, A.in, A.in_size, (uint64_t)a0 + (rdo[u] & 0xFFFFu), rdo[u] & 0xFFFFu, rdo[u] >> 16, s_enc);
+            __syncthreads();
+            if (t == 0) s_redo = 0u;
+        }
+#if !HHUFF_ENCI_EARLY_SPAN
+        // the next chunk's span and the chunk after next's offsets: in flight while the records are read and
+        // ranked (issued during the encode, their registers would spill the encode's)
+        if (more) issue_span(pv, nxt);
+        PairChunk nn = issue_chunk((cn2 < nch ? cn2 : (more ? cn : c)) * NS);
+#endif
+        const uint2 r0 = s_str[t], r1 = s_str[t + NT];  // {encoded length, length} of this thread's strings
+        // the chunk after next's offsets and the next span land here, before this chunk's stores (no load is
+        // waited for behind a data-dependent number of stores)
+        land(nn);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) __asm__ volatile("" : "+v"(pv[j].x), "+v"(pv[j].y), "+v"(pv[j].z), "+v"(pv[j].w) : : "memory");
+        const uint32_t nspan = more ? span_of(nxt) : 0u;
+        const bool ncommit = nspan <= (uint32_t)CH;
+        if (more && ncommit) meta(nxt, cn * NS);  // (s_str is read above)
+        if (cb + t < A.n) finish_encode(A, cb + t, r0.y, r0.x);
+        if (cb + t + NT < A.n) finish_encode(A, cb + t + NT, r1.y, r1.x);
+        // copy out the stage's MSB-first words (byte-swapped) and put the next span in, piece by piece: each
+        // thread writes only the pieces it has just read.  The chunk's first and last pieces are deferred.
+        const uint32_t kl = (span - 1u) & ~15u;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+            const uint32_t k = (uint32_t)j * (16u * NT) + t * 16u;
+            uint4* sp = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_st) + k);
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (k < span) v = *sp;
+            if (ncommit && k < nspan) *sp = piece(pv, j, nxt);
+            if (k < span) {
+                const uint64_t g = (uint64_t)a0 + k;
+                v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
+                const bool full = g >= lo && g + 16 <= hi;
+                if (full) *reinterpret_cast<uint4*>(A.out + g) = v;
+                if (k == 0 || k == kl) {
+                    const uint32_t elo = lo > g ? (uint32_t)(lo - g) : 0u;
+                    const uint32_t ehi = hi - g < 16 ? (uint32_t)(hi - g) : 16u;
+                    EdgeRec* ed = rec + (k == 0 ? 0 : 1);
+                    ed->v = v;
+                    ed->m = make_uint4((uint32_t)g, (uint32_t)(g >> 32), full ? 0u : elo, full ? 0u : ehi);
+                }
+            }
+        }
+        if (t == 0 && (kl == 0 || span == 0)) rec[1].m = make_uint4(0u, 0u, 0u, 0u);  // one piece, or none
+        if (t == 0 && span == 0) rec[0].m = make_uint4(0u, 0u, 0u, 0u);
+        if (!more) break;
+        cur = nxt;
+        nxt = nn;
+        c = cn;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Proportional-lane staged encode (contiguous layout, output slot = in_off: the wire / bench layout).
 // A tile is K consecutive strings staged in LDS.  String j gets g_j = 1 + floor((64 - K) len_j / span)
 // lanes, each encoding an equal share of the string, so every lane has about span / 64 bytes whatever
@@ -4198,7 +4580,19 @@ constexpr int kDecTWaves = HHUFF_RK_W;
 #else
 constexpr int kDecTWaves = HHUFF_DECT_W;
 #endif
-constexpr int kDecSWaves = 16, kEncSWaves = 16, kEncOStr = HHUFF_ENCO_NS;
+#ifndef HHUFF_ENC_INPLACE  // 1: the contiguous short-string encoder is encode_inplace_kernel (512 strings, pairs)
+#define HHUFF_ENC_INPLACE 0
+#endif
+#ifndef HHUFF_ENCI_NS
+#define HHUFF_ENCI_NS 512
+#define HHUFF_ENCI_CH 28672
+#endif
+#if HHUFF_ENC_INPLACE
+constexpr int kEncOStr = HHUFF_ENCI_NS, kEncOThreads = HHUFF_ENCI_NS / 2;
+#else
+constexpr int kEncOStr = HHUFF_ENCO_NS, kEncOThreads = HHUFF_ENCO_NS / HHUFF_ENCO_SPT;
+#endif
+constexpr int kDecSWaves = 16, kEncSWaves = 16;
 #define DEC_S decode_staged_kernel<kDecSWaves, 3072, 4608, false>
 #define DEC_L decode_staged_kernel<6, 8192, 12928, false>
 #define DEC_SP decode_staged_kernel<kDecSWaves, 3072, 4608, true>
@@ -4218,7 +4612,11 @@ constexpr int kDecSWaves = 16, kEncSWaves = 16, kEncOStr = HHUFF_ENCO_NS;
 #endif
 #endif
 #define ENC_S encode_staged_kernel<kEncSWaves, 3584, false>
+#if HHUFF_ENC_INPLACE
+#define ENC_O encode_inplace_kernel<HHUFF_ENCI_NS, HHUFF_ENCI_CH>
+#else
 #define ENC_O encode_sorted_kernel<kEncOStr, HHUFF_ENCO_CH, HHUFF_ENCO_SPT>
+#endif
 #define ENC_L encode_staged_kernel<8, 8192, false>
 #define ENC_SP encode_staged_kernel<kEncSWaves, 3584, true>
 #define ENC_LP encode_staged_kernel<8, 8192, true>
@@ -4260,7 +4658,7 @@ static int variant_threads(int v) {
         case kDecLP: return 384;
         case kEncL:
         case kEncLP: return 512;
-        case kEncO: return kEncOStr / HHUFF_ENCO_SPT;
+        case kEncO: return kEncOThreads;
         case kEncP:
         case kFlatP: return 1024;
         default: return 256;
@@ -4796,7 +5194,7 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     }
     switch (v) {
         case kEncS: hipLaunchKernelGGL(ENC_S, dim3(grid), dim3(kEncSWaves * 64), 0, stream, A); break;
-        case kEncO: hipLaunchKernelGGL(ENC_O, dim3(grid), dim3(kEncOStr / HHUFF_ENCO_SPT), 0, stream, A); break;
+        case kEncO: hipLaunchKernelGGL(ENC_O, dim3(grid), dim3(kEncOThreads), 0, stream, A); break;
         case kEncL: hipLaunchKernelGGL(ENC_L, dim3(grid), dim3(512), 0, stream, A); break;
         default: hipLaunchKernelGGL(ENC_D, dim3(grid), dim3(256), 0, stream, A); break;
     }

@@ -64,3 +64,31 @@ def test_encode_long_algorithm_matches_oracle(oracle_codec):
         for chunk, threads in ((1024, 64), (512, 32), (16384, 1024)):
             assert L.encode_long(code, nbits, s, chunk=chunk, threads=threads) == oracle_codec.encode(s), \
                 (len(s), chunk)
+
+
+def test_encode_inplace_algorithm_matches_plain_encoder():
+    """encode_inplace_kernel's lane algorithm (tools/emu_encode_inplace.py): strings encoded over their own input
+    words with the lanes in a random lock-step order, long-code prefixes re-encoded, random bytes failing --
+    byte for byte equal to a plain encoder of hpack.c:774-804"""
+    import random
+
+    import emu_encode_inplace as emu
+
+    rng = random.Random(7)
+    alpha = b"abcdefghijklmnopqrstuvwxyz0123456789-_./=;, ABCDEFGHIJKLMNOPQRSTUVWXYZ\"{}<>?@[]^|~"
+    redone = 0
+    for _ in range(40):
+        strings = []
+        for _ in range(rng.randint(1, 48)):
+            L = rng.choice([rng.randint(0, 8), rng.randint(24, 72), rng.randint(1, 160)])
+            r = rng.random()
+            if r < 0.05:
+                s = bytes(rng.randrange(256) for _ in range(L))
+            elif r < 0.15:
+                s = bytes(rng.choice(b"{}<>?@[]^|~\\") for _ in range(min(L, 6))) + \
+                    bytes(rng.choice(alpha) for _ in range(max(0, L - 6)))
+            else:
+                s = bytes(rng.choice(alpha) for _ in range(L))
+            strings.append(s)
+        redone += emu.run_chunk(strings, rng)
+    assert redone > 0  # the re-encode path ran
