@@ -2775,15 +2775,16 @@ __device__ __forceinline__ void encode_redo(uint32_t sbase, const uint8_t* __res
 struct PairChunk {
     uint32_t s0, e0, s1, e1, lo, hi;
 };
-template <int NS, int CH>
 #ifndef HHUFF_ENCI_EARLY_SPAN
 #define HHUFF_ENCI_EARLY_SPAN 0
 #endif
 #ifndef HHUFF_ENCI_WPE  // waves per SIMD the register allocation is held to (4: 128 VGPRs)
 #define HHUFF_ENCI_WPE 4
 #endif
-__global__ __launch_bounds__(NS / 2) __attribute__((amdgpu_waves_per_eu(HHUFF_ENCI_WPE, HHUFF_ENCI_WPE))) void encode_inplace_kernel(EncArgs A) {
-    constexpr uint32_t NT = NS / 2;
+template <int NS, int CH, int SPT>
+__global__ __launch_bounds__(NS / SPT) __attribute__((amdgpu_waves_per_eu(HHUFF_ENCI_WPE, HHUFF_ENCI_WPE))) void encode_inplace_kernel(EncArgs A) {
+    static_assert(SPT == 1 || SPT == 2, "one string a thread, or a sorted pair");
+    constexpr uint32_t NT = NS / SPT;
     constexpr int NV = (CH + 16 * NT - 1) / (16 * NT);  // 16-B span pieces per thread
     __shared__ __attribute__((aligned(16))) uint2 s_enc[512];  // 256..511: bytes outside a string
     __shared__ __attribute__((aligned(16))) uint32_t s_st[CH / 4 + 8];
@@ -2802,8 +2803,8 @@ __global__ __launch_bounds__(NS / 2) __attribute__((amdgpu_waves_per_eu(HHUFF_EN
         const uint32_t i0 = min(qb + t, A.n - 1u), i1 = min(qb + t + NT, A.n - 1u);
         q.s0 = A.in_off[i0];
         q.e0 = A.in_off[i0 + 1];
-        q.s1 = A.in_off[i1];
-        q.e1 = A.in_off[i1 + 1];
+        q.s1 = SPT == 2 ? A.in_off[i1] : 0u;
+        q.e1 = SPT == 2 ? A.in_off[i1 + 1] : 0u;
         q.lo = A.in_off[min(qb, A.n - 1u)];
         q.hi = A.in_off[min(qb + NS, A.n)];
         return q;
@@ -2833,7 +2834,7 @@ __global__ __launch_bounds__(NS / 2) __attribute__((amdgpu_waves_per_eu(HHUFF_EN
     auto meta = [&](const PairChunk& q, uint32_t qb) {  // the chunk's string records and length ranks
         const uint32_t ss[2] = {q.s0, q.s1}, ee[2] = {q.e0, q.e1};
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < SPT; ++u) {
             const uint32_t tt = t + (uint32_t)u * NT;
             const uint32_t ln = qb + tt < A.n ? ee[u] - ss[u] : 0u;
             s_str[tt] = make_uint2(ss[u] - (q.lo & ~15u), ln);
@@ -2868,7 +2869,7 @@ __global__ __launch_bounds__(NS / 2) __attribute__((amdgpu_waves_per_eu(HHUFF_EN
         if (span > (uint32_t)CH) {  // (workgroup-uniform) a chunk larger than the stage: one thread per string
             const uint32_t ss[2] = {cur.s0, cur.s1}, ee[2] = {cur.e0, cur.e1};
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < SPT; ++u) {
                 const uint32_t i = cb + t + (uint32_t)u * NT;
                 const uint32_t len = i < A.n ? ee[u] - ss[u] : 0u;
                 uint32_t ol = kFailLen;
@@ -2901,7 +2902,7 @@ __global__ __launch_bounds__(NS / 2) __attribute__((amdgpu_waves_per_eu(HHUFF_EN
             const uint32_t x0 = s_bin[2 * lane], x1 = s_bin[2 * lane + 1];
             const uint32_t ex = wave_excl_scan(x0 + x1, (int)lane);
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
+            for (int u = 0; u < SPT; ++u) {
                 const uint32_t eb = (uint32_t)__shfl((int)ex, (int)(bin[u] >> 1)), xb = (uint32_t)__shfl((int)x0, (int)(bin[u] >> 1));
                 s_perm[eb + ((bin[u] & 1u) ? xb : 0u) + rank[u]] = (uint16_t)(t + (uint32_t)u * NT);
             }
@@ -2916,7 +2917,7 @@ __global__ __launch_bounds__(NS / 2) __attribute__((amdgpu_waves_per_eu(HHUFF_EN
 #endif
         uint32_t rdo[2] = {0u, 0u};  // a string to encode again: its span offset | its length << 16
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {  // sorted positions t and NS - 1 - t: a short and a long string
+        for (int u = 0; u < SPT; ++u) {  // sorted positions t and NS - 1 - t: a short and a long string
             const uint32_t j = s_perm[u == 0 ? t : NS - 1u - t];
             const uint2 sj = s_str[j];
             const bool act = cb + j < A.n && sj.y != 0 && sj.y <= kMaxStrLen;
@@ -2932,7 +2933,7 @@ __global__ __launch_bounds__(NS / 2) __attribute__((amdgpu_waves_per_eu(HHUFF_EN
         __syncthreads();  // barrier 3: every string encoded (or counted)
         if (s_redo != 0u) {  // (workgroup-uniform) strings whose codes outran their reads: encoded again
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int u = 0; u < SPT; ++u)
                 if (rdo[u] >> 16)
                     encode_redo(sbase, A.in, A.in_size, (uint64_t)a0 + (rdo[u] & 0xFFFFu), rdo[u] & 0xFFFFu, rdo[u] >> 16, s_enc);
             __syncthreads();
@@ -2944,7 +2945,7 @@ __global__ __launch_bounds__(NS / 2) __attribute__((amdgpu_waves_per_eu(HHUFF_EN
         if (more) issue_span(pv, nxt);
         PairChunk nn = issue_chunk((cn2 < nch ? cn2 : (more ? cn : c)) * NS);
 #endif
-        const uint2 r0 = s_str[t], r1 = s_str[t + NT];  // {encoded length, length} of this thread's strings
+        const uint2 r0 = s_str[t], r1 = SPT == 2 ? s_str[t + NT] : make_uint2(0u, 0u);  // {encoded length, length}
         // the chunk after next's offsets and the next span land here, before this chunk's stores (no load is
         // waited for behind a data-dependent number of stores)
         land(nn);
@@ -2954,7 +2955,7 @@ __global__ __launch_bounds__(NS / 2) __attribute__((amdgpu_waves_per_eu(HHUFF_EN
         const bool ncommit = nspan <= (uint32_t)CH;
         if (more && ncommit) meta(nxt, cn * NS);  // (s_str is read above)
         if (cb + t < A.n) finish_encode(A, cb + t, r0.y, r0.x);
-        if (cb + t + NT < A.n) finish_encode(A, cb + t + NT, r1.y, r1.x);
+        if (SPT == 2 && cb + t + NT < A.n) finish_encode(A, cb + t + NT, r1.y, r1.x);
         // copy out the stage's MSB-first words (byte-swapped) and put the next span in, piece by piece: each
         // thread writes only the pieces it has just read.  The chunk's first and last pieces are deferred.
         const uint32_t kl = (span - 1u) & ~15u;
@@ -4583,12 +4584,13 @@ constexpr int kDecTWaves = HHUFF_DECT_W;
 #ifndef HHUFF_ENC_INPLACE  // 1: the contiguous short-string encoder is encode_inplace_kernel (512 strings, pairs)
 #define HHUFF_ENC_INPLACE 0
 #endif
-#ifndef HHUFF_ENCI_NS
+#ifndef HHUFF_ENCI_NS  // strings per chunk, stage bytes, strings per thread
 #define HHUFF_ENCI_NS 512
 #define HHUFF_ENCI_CH 28672
+#define HHUFF_ENCI_SPT 2
 #endif
 #if HHUFF_ENC_INPLACE
-constexpr int kEncOStr = HHUFF_ENCI_NS, kEncOThreads = HHUFF_ENCI_NS / 2;
+constexpr int kEncOStr = HHUFF_ENCI_NS, kEncOThreads = HHUFF_ENCI_NS / HHUFF_ENCI_SPT;
 #else
 constexpr int kEncOStr = HHUFF_ENCO_NS, kEncOThreads = HHUFF_ENCO_NS / HHUFF_ENCO_SPT;
 #endif
@@ -4613,7 +4615,7 @@ constexpr int kDecSWaves = 16, kEncSWaves = 16;
 #endif
 #define ENC_S encode_staged_kernel<kEncSWaves, 3584, false>
 #if HHUFF_ENC_INPLACE
-#define ENC_O encode_inplace_kernel<HHUFF_ENCI_NS, HHUFF_ENCI_CH>
+#define ENC_O encode_inplace_kernel<HHUFF_ENCI_NS, HHUFF_ENCI_CH, HHUFF_ENCI_SPT>
 #else
 #define ENC_O encode_sorted_kernel<kEncOStr, HHUFF_ENCO_CH, HHUFF_ENCO_SPT>
 #endif
