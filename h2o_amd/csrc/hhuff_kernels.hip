@@ -262,6 +262,35 @@ struct EdgeRec {
     uint4 m;  // {address lo, address hi, lo, hi}: bytes [lo, hi) of the chunk are ours (lo >= hi: none)
 };
 
+#ifndef HHUFF_NT_STORE  // output pieces as streaming (non-temporal) 16-B stores: c4 decode -2.1 %, encode -0.9 %,
+                        // c2 -3 %, c3 / c5 level (profiles/r05t_nt_store_ab.jsonl; with the per-string lengths and
+                        // statuses streamed too, HHUFF_NT_RES, c4 decode gains less)
+#define HHUFF_NT_STORE 1
+#endif
+#ifndef HHUFF_STATUS_DW  // staged decode: a tile's status bytes stored as dwords
+#define HHUFF_STATUS_DW 0
+#endif
+// result stores the kernel never reads back: streaming (non-temporal) with HHUFF_NT_STORE (HHUFF_NT_RES=1 also for
+// the per-string lengths and statuses)
+#ifndef HHUFF_NT_RES
+#define HHUFF_NT_RES 0
+#endif
+typedef unsigned int hh_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_out(uint8_t* p, uint4 v) {
+#if HHUFF_NT_STORE
+    __builtin_nontemporal_store(hh_u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<hh_u32x4*>(p));
+#else
+    *reinterpret_cast<uint4*>(p) = v;
+#endif
+}
+template <class T>
+__device__ __forceinline__ void st_res(T* p, T v) {
+#if HHUFF_NT_RES
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
 // SWAP: the LDS bytes are MSB-first words (the encode stage), byte-swapped in registers on the way out.
 template <bool SWAP = false>
 __device__ __forceinline__ void region_copy_deferred(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds,
@@ -273,7 +302,7 @@ __device__ __forceinline__ void region_copy_deferred(uint8_t* __restrict__ out, 
         uint4 v = *reinterpret_cast<const uint4*>(lds + k);
         if (SWAP) v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
         const bool full = g >= keep_lo && g + 16 <= keep_hi;
-        if (full) *reinterpret_cast<uint4*>(out + g) = v;
+        if (full) st16_out(out + g, v);  // (streaming: the output is not read again by the kernel)
         if (k == 0 || k == kl) {
             const uint32_t lo = keep_lo > g ? (uint32_t)(keep_lo - g) : 0u;
             const uint32_t hi = keep_hi - g < 16 ? (uint32_t)(keep_hi - g) : 16u;
@@ -657,7 +686,11 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         ti = issue_tile(nbase + 2 * stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
         PROF_MARK(3);  // commit + plan
         // ---- the current tile: stores ----
+#if defined(HHUFF_X_NOSTORE) || defined(HHUFF_X_NOSTORE_OUT)  // ablations (output wrong by design): no output stores
+        if (false) {
+#else
         if (cur.fits) {
+#endif
             if (PACKED) {
                 const uint64_t gb = G & ~15ull;
                 region_copy_deferred(A.out, gb, buf + c0 - ((uint32_t)G & 15u),
@@ -677,9 +710,25 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
             A.edges[2 * (base >> 6)].m = make_uint4(0u, 0u, 0u, 0u);
             A.edges[2 * (base >> 6) + 1].m = make_uint4(0u, 0u, 0u, 0u);
         }
+#if HHUFF_STATUS_DW
+        // a whole tile's status bytes as 16 dword stores (4 lanes' bytes each) instead of 64 byte stores; a listed
+        // string's byte is 0 here and written by split_decode_kernel, which runs after this kernel
+        const bool st_dw = !PACKED && base + 64u <= A.n && (((uintptr_t)(A.status + base)) & 3u) == 0;  // (uniform)
+        if (st_dw) {
+            uint32_t sv = (t.valid && !listed ? (uint32_t)st : 0u) << (8u * ((uint32_t)lane & 3u));
+            sv |= (uint32_t)__shfl_xor((int)sv, 1);
+            sv |= (uint32_t)__shfl_xor((int)sv, 2);
+            if ((lane & 3) == 0) *reinterpret_cast<uint32_t*>(A.status + base + (uint32_t)lane) = sv;
+            if (t.valid && !listed) A.out_len[ti_i] = ol;
+        } else
+#endif
+#if defined(HHUFF_X_NOSTORE) || defined(HHUFF_X_NOSTORE_LEN)  // (no length / status stores)
+        if (false) {
+#else
         if (t.valid && !listed) {
-            A.out_len[ti_i] = ol;
-            A.status[ti_i] = st;
+#endif
+            st_res(A.out_len + ti_i, ol);
+            st_res(A.status + ti_i, st);
             if (PACKED) {
                 A.pk_off[ti_i] = (uint32_t)(G + place);
                 if (ti_i == A.n - 1) A.pk_off[A.n] = (uint32_t)(G + place + (ol != kFailLen ? ol : 0u));
@@ -2135,8 +2184,8 @@ __device__ __forceinline__ void load_enc_table(uint2* s_enc, int nthreads) {
 }
 
 __device__ __forceinline__ void finish_encode(const EncArgs& A, uint32_t i, uint32_t len, uint32_t ol) {
-    A.out_len[i] = ol;
-    if (A.status) A.status[i] = ol == kFailLen ? (len > kMaxStrLen ? kStatusTooLong : kStatusFail) : 0;
+    st_res(A.out_len + i, ol);
+    if (A.status) st_res(A.status + i, (uint8_t)(ol == kFailLen ? (len > kMaxStrLen ? kStatusTooLong : kStatusFail) : 0));
 }
 
 __device__ __forceinline__ uint32_t count_code_bits(const GlobalSource& src, uint32_t start, uint32_t len,
@@ -2573,7 +2622,7 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
             *sp = make_uint4(0u, 0u, 0u, 0u);
             v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
             const bool full = g >= lo && g + 16 <= hi;
-            if (full) *reinterpret_cast<uint4*>(A.out + g) = v;
+            if (full) st16_out(A.out + g, v);
             if (k == 0 || k == kl) {
                 const uint32_t elo = lo > g ? (uint32_t)(lo - g) : 0u;
                 const uint32_t ehi = hi - g < 16 ? (uint32_t)(hi - g) : 16u;
@@ -2970,7 +3019,7 @@ __global__ __launch_bounds__(NS / SPT) __attribute__((amdgpu_waves_per_eu(HHUFF_
                 const uint64_t g = (uint64_t)a0 + k;
                 v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
                 const bool full = g >= lo && g + 16 <= hi;
-                if (full) *reinterpret_cast<uint4*>(A.out + g) = v;
+                if (full) st16_out(A.out + g, v);
                 if (k == 0 || k == kl) {
                     const uint32_t elo = lo > g ? (uint32_t)(lo - g) : 0u;
                     const uint32_t ehi = hi - g < 16 ? (uint32_t)(hi - g) : 16u;
@@ -3441,12 +3490,16 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
     // does, took this kernel past 128 VGPRs into scratch -- twice the HBM traffic)
     constexpr int NCH = (STAGE + 1023) / 1024;
     TIn cx = issue(t);
+    // profile builds: stage issue / shares (+ the stage's wait) / pass 1 / header + pass 2 / raw copies /
+    // copy-out / direct tiles / lengths, in the encode slot
+    PROF_DECL
     for (;;) {
         const uint64_t tn = t + tstride;
         const bool have_next = tn < ntiles;
         const Plan cur = plan(t, cx);
         TIn nxi = issue(have_next ? tn : t);  // the next tile's offsets: in flight during this tile
         if (cur.fits) stage_span_dma<NCH>(stage, A.in, A.in_size, cur.a0, cur.span, lane);
+        PROF_MARK(0);
         // ---- the current tile ----
         const uint32_t kt = cur.kt;
         const bool own = (uint32_t)lane < kt;
@@ -3484,8 +3537,10 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
             const bool ok = act && lj <= kMaxStrLen;
             const uint32_t last = cur.span ? cur.span - 4u : 0u;
             wave_lds_sync();
+            PROF_MARK(1);
             // pass 1: code bits per share -> starting bit of each share, string totals, verdicts
             const uint32_t b = chunk_code_bits_v2(stage, last, cs, clen, ok && !rj && clen != 0, s_enc);
+            PROF_MARK(2);
             const uint32_t x = wave_excl_scan(b, lane);
             const uint32_t xs = (uint32_t)__shfl((int)x, (int)Lj, 64);
             const uint32_t xe = (uint32_t)__shfl((int)(x + b), (int)(Lj + gj - 1), 64);
@@ -3503,6 +3558,7 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
             // pass 2: Huffman shares place their code bits; raw shares copy their bytes
             encode_chunk_v2(stage, last, cs, clen, huff && clen != 0, lds_addr(obuf32), 8u * (orel + hn) + (x - xs), s_enc,
                             0xFFFFFFFFu, c1 == lj);
+            PROF_MARK(3);
             if (ok && !huff && clen) {
                 const uint8_t* in8 = reinterpret_cast<const uint8_t*>(stage);
                 for (uint32_t k = 0; k < clen; ++k) obuf[(orel + hn + c0 + k) ^ 3u] = in8[cs + k];
@@ -3510,11 +3566,13 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
             const uint32_t res = ok ? hn + (huff ? hlen : lj) : kFailLen;
             ol = (uint32_t)__shfl((int)res, (int)L, 64);
             wave_lds_sync();
+            PROF_MARK(4);
             // the next tile's offsets are waited for here, before this tile's stores (not at the next tile's
             // plan, where the wait would cover the stores too)
             __asm__ volatile("" : "+v"(nxi.s), "+v"(nxi.e), "+v"(nxi.first), "+v"(nxi.raww) : : "memory");
             region_copy_deferred<true>(A.out, cur.ob, obuf, cur.ospan, cur.olo, cur.ohi, lane, A.edges + 2 * t);
             wave_lds_sync();
+            PROF_MARK(5);
         } else {
             __asm__ volatile("" : "+v"(nxi.s), "+v"(nxi.e), "+v"(nxi.first), "+v"(nxi.raww) : : "memory");
             if (own && len <= kMaxStrLen) {  // tile larger than the stage: one string per lane from global
@@ -3543,9 +3601,14 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
                 ol = sink.count();
             }
             if (lane < 2) A.edges[2 * t + lane].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges
+            PROF_MARK(6);
         }
         if (own) A.out_len[i] = ol;
-        if (!have_next) break;
+        PROF_MARK(7);
+        if (!have_next) {
+            PROF_FLUSH(1);
+            break;
+        }
         cx = nxi;
         t = tn;
     }
@@ -3967,7 +4030,7 @@ __global__ __launch_bounds__(1024) void decode_sorted_kernel(DecArgs A) {
                 const uint64_t g = obase + k;
                 const uint4 v = *reinterpret_cast<const uint4*>(G.out + k);
                 const bool full = g >= olo && g + 16 <= ohi;
-                if (full) *reinterpret_cast<uint4*>(A.out + g) = v;
+                if (full) st16_out(A.out + g, v);
                 if (k == 0 || k == kl) {
                     const uint32_t elo = olo > g ? (uint32_t)(olo - g) : 0u;
                     const uint32_t ehi = ohi - g < 16 ? (uint32_t)(ohi - g) : 16u;

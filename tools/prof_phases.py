@@ -13,6 +13,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 PHASES = ["plan+issue", "steps", "verdicts/compaction", "commit+plan", "out copy", "len/status", "direct", "-"]
+FLAT_PHASES = ["stage issue", "shares+stage wait", "pass 1 (count)", "header+pass 2", "raw copies", "copy-out",
+               "direct", "lengths"]
 
 
 def main():
@@ -37,6 +39,8 @@ def main():
         "enc_slot": lambda: codec.encode_batch(b["data"], off32, n, in_size=P),
         "enc_packed": lambda: codec.encode_batch_packed(b["data"], off32, n, in_size=P),
     }
+    if cfg == "c5":  # the QPACK framing (flatten_pl_kernel), its own phases
+        runs = {"flatten": lambda: codec.flatten_batch(b["data"], off32, n, 7, in_size=P), **runs}
     for name, fn in runs.items():
         fn()
         torch.cuda.synchronize()
@@ -46,9 +50,10 @@ def main():
         L.hhuff_debug_prof(buf, 1)
         row = list(buf)[0:8] if name.startswith("dec") else list(buf)[8:16]
         tot = float(sum(row)) or 1.0
+        names = FLAT_PHASES if name == "flatten" else PHASES
         print(json.dumps({"run": name, "cycles_sum": int(tot),
-                          "phases": {PHASES[k]: round(row[k] / tot, 4) for k in range(8) if row[k]},
-                          "cycles": {PHASES[k]: int(row[k]) for k in range(8) if row[k]}}), flush=True)
+                          "phases": {names[k]: round(row[k] / tot, 4) for k in range(8) if row[k]},
+                          "cycles": {names[k]: int(row[k]) for k in range(8) if row[k]}}), flush=True)
 
 
 if __name__ == "__main__":
