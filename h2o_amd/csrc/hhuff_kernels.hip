@@ -3539,7 +3539,11 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
             wave_lds_sync();
             PROF_MARK(1);
             // pass 1: code bits per share -> starting bit of each share, string totals, verdicts
+#ifdef HHUFF_X_FLAT_NOCOUNT  // ablation (output wrong by design): no counting pass, every share 6 bits a byte
+            const uint32_t b = ok && !rj ? 6u * clen : 0u;
+#else
             const uint32_t b = chunk_code_bits_v2(stage, last, cs, clen, ok && !rj && clen != 0, s_enc);
+#endif
             PROF_MARK(2);
             const uint32_t x = wave_excl_scan(b, lane);
             const uint32_t xs = (uint32_t)__shfl((int)x, (int)Lj, 64);
@@ -3570,7 +3574,9 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
             // the next tile's offsets are waited for here, before this tile's stores (not at the next tile's
             // plan, where the wait would cover the stores too)
             __asm__ volatile("" : "+v"(nxi.s), "+v"(nxi.e), "+v"(nxi.first), "+v"(nxi.raww) : : "memory");
+#ifndef HHUFF_X_FLAT_NOSTORE  // ablation (output wrong by design): no output stores
             region_copy_deferred<true>(A.out, cur.ob, obuf, cur.ospan, cur.olo, cur.ohi, lane, A.edges + 2 * t);
+#endif
             wave_lds_sync();
             PROF_MARK(5);
         } else {
