@@ -749,6 +749,283 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Staged decode with store waves (HHUFF_DEC_SW; contiguous layout, slot output, deferred edges).  On gfx950
+// loads and stores share one in-order counter, so in decode_staged_kernel the next tile's prefetched span is
+// waited for behind the previous tile's output stores: with no stores at all the c4 decode runs 19 % faster
+// (profiles/r05t_nt_store_ab.jsonl).  Here 15 waves decode and never store: a wave leaves its tile's output
+// stage, lengths, statuses and region in LDS and posts the tile (an LDS flag); the 16th wave reads the stage
+// out into registers, hands it back (another flag) and issues the stores.  A decode wave waits for its stage
+// only before the next tile's steps write into it.  LDS-only fences, so no wave waits on global memory for a
+// hand-over.  Same results as decode_staged_kernel.
+// ------------------------------------------------------------------------------------------------
+#ifndef HHUFF_DEC_SW_NSW  // store waves of decode_staged_sw_kernel's 16, and the tiles one takes at once
+#define HHUFF_DEC_SW_NSW 2
+#endif
+#ifndef HHUFF_DEC_SW_NB
+#define HHUFF_DEC_SW_NB 2
+#endif
+constexpr uint32_t kSwSkip = 0xFFFFFFFEu;  // a posted length the store wave skips (listed / past n)
+struct SwTile {                            // a posted tile: its output region and records
+    uint64_t gbase, keep_lo, keep_hi;
+    uint32_t ospan, rec, base, pad;
+};
+__device__ __forceinline__ uint32_t lds_ld_acq(const uint32_t* p) {
+    const uint32_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    return v;
+}
+__device__ __forceinline__ void lds_st_rel(uint32_t* p, uint32_t v) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <int IN_STAGE, int OUT_STAGE, int NSW>
+__global__ __launch_bounds__(1024) void decode_staged_sw_kernel(DecArgs A) {
+    constexpr int NDW = 16 - NSW;  // decode waves; waves NDW.. store (store wave s serves decode waves s, s + NSW, ...)
+    constexpr int NB = HHUFF_DEC_SW_NB;  // tiles a store wave takes at once
+    constexpr uint32_t Z = IN_STAGE + OUT_STAGE + 256u;
+    constexpr int NCHO = (OUT_STAGE + 1023) / 1024;
+    struct __attribute__((aligned(16))) Smem {
+        uint32_t lut[1u << HHUFF_LUT_BITS];
+        uint32_t kinfo[32];
+        uint32_t ones[(HHUFF_ONES_NENT + 3) & ~3];
+        uint8_t buf[NDW][Z + 16];
+        SwTile tile[NDW];
+        uint32_t len[NDW][64];
+        uint8_t st[NDW][64];
+        uint32_t posted[NDW], drained[NDW], finished;
+    };
+    __shared__ Smem sm;
+    load_dec_tables(sm.lut, sm.kinfo, sm.ones, 1024);
+    if (threadIdx.x < NDW) sm.posted[threadIdx.x] = sm.drained[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) sm.finished = 0u;
+    __syncthreads();
+    const DecTables T{sm.lut, sm.kinfo, sm.ones};
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+    if (wave >= NDW) {  // ---- a store wave ----
+        const int sw = wave - NDW;
+        const bool mine = lane < NDW && lane % NSW == sw;  // lane w watches decode wave w
+        uint32_t drained = 0;  // lane w: tiles of decode wave w stored so far
+        for (;;) {
+            const uint32_t posted = mine ? lds_ld_acq(&sm.posted[lane]) : 0u;
+            const uint64_t ready = __builtin_amdgcn_ballot_w64(mine && posted != drained);
+            if (ready == 0) {
+                if (lds_ld_acq(&sm.finished) == (uint32_t)NDW) {  // every wave is done: one last look
+                    const uint32_t p2 = mine ? lds_ld_acq(&sm.posted[lane]) : 0u;
+                    if (__builtin_amdgcn_ballot_w64(mine && p2 != drained) == 0) break;
+                    continue;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            // up to NB ready tiles at once: their stages read out, handed back with one fence, then stored
+            int ws[NB];
+            SwTile d[NB];
+            uint4 v[NB][NCHO];
+            uint32_t ol[NB];
+            uint8_t stt[NB];
+            uint64_t left = ready;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                ws[b] = left ? __builtin_ctzll(left) : -1;
+                left &= left - 1u;
+                if (ws[b] >= 0) {  // (wave-uniform)
+                    const int w = ws[b];
+                    const SwTile x = sm.tile[w];  // (wave-uniform: into SGPRs)
+                    auto u64 = [](uint64_t q) {
+                        return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)q) |
+                               (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(q >> 32)) << 32;
+                    };
+                    d[b].gbase = u64(x.gbase);
+                    d[b].keep_lo = u64(x.keep_lo);
+                    d[b].keep_hi = u64(x.keep_hi);
+                    d[b].ospan = (uint32_t)__builtin_amdgcn_readfirstlane((int)x.ospan);
+                    d[b].rec = (uint32_t)__builtin_amdgcn_readfirstlane((int)x.rec);
+                    d[b].base = (uint32_t)__builtin_amdgcn_readfirstlane((int)x.base);
+                    const uint8_t* obuf = sm.buf[w] + IN_STAGE;
+#pragma unroll
+                    for (int c = 0; c < NCHO; ++c) {
+                        const uint32_t kk = (uint32_t)c * 1024u + (uint32_t)lane * 16u;
+                        if (kk < d[b].ospan) v[b][c] = *reinterpret_cast<const uint4*>(obuf + kk);
+                    }
+                    ol[b] = sm.len[w][lane];
+                    stt[b] = sm.st[w][lane];
+                }
+            }
+            // the stages and records are in registers: hand the stages back (the fence waits for these reads)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                if (ws[b] >= 0) {
+                    const uint32_t pw = (uint32_t)__builtin_amdgcn_readlane((int)posted, ws[b]);
+                    if (lane == ws[b]) drained = pw;
+                    if (lane == 0) __hip_atomic_store(&sm.drained[ws[b]], pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                if (ws[b] < 0) continue;
+                EdgeRec* rec = A.edges + 2 * (uint64_t)d[b].rec;
+                const uint32_t kl = d[b].ospan ? (d[b].ospan - 1u) & ~15u : 0u;
+#pragma unroll
+                for (int c = 0; c < NCHO; ++c) {
+                    const uint32_t kk = (uint32_t)c * 1024u + (uint32_t)lane * 16u;
+                    if (kk < d[b].ospan) {
+                        const uint64_t g = d[b].gbase + kk;
+                        const bool full = g >= d[b].keep_lo && g + 16 <= d[b].keep_hi;
+                        if (full) st16_out(A.out + g, v[b][c]);
+                        if (kk == 0 || kk == kl) {
+                            const uint32_t lo = d[b].keep_lo > g ? (uint32_t)(d[b].keep_lo - g) : 0u;
+                            const uint32_t hi = d[b].keep_hi - g < 16 ? (uint32_t)(d[b].keep_hi - g) : 16u;
+                            EdgeRec* r = rec + (kk == 0 ? 0 : 1);
+                            r->v = v[b][c];
+                            r->m = make_uint4((uint32_t)g, (uint32_t)(g >> 32), full ? 0u : lo, full ? 0u : hi);
+                            if (kl == 0) rec[1].m = make_uint4(0u, 0u, 0u, 0u);
+                        }
+                    }
+                }
+                if (d[b].ospan == 0 && lane == 0) {
+                    rec[0].m = make_uint4(0u, 0u, 0u, 0u);
+                    rec[1].m = make_uint4(0u, 0u, 0u, 0u);
+                }
+                if (ol[b] != kSwSkip) {
+                    A.out_len[d[b].base + (uint32_t)lane] = ol[b];
+                    A.status[d[b].base + (uint32_t)lane] = stt[b];
+                }
+            }
+        }
+        return;
+    }
+
+    // ---- the decode waves: decode_staged_kernel's pipeline (slot layout), stores handed to the store wave ----
+    uint8_t* const buf = sm.buf[wave];
+    const uint64_t stride = (uint64_t)gridDim.x * NDW * 64;
+    uint64_t base = ((uint64_t)blockIdx.x * NDW + wave) * 64;
+    uint32_t seq = 0;  // tiles this wave has posted
+    if (base >= A.n) {
+        if (lane == 0) __hip_atomic_fetch_add(&sm.finished, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+    }
+    struct Plan {
+        uint32_t s, len, op0;
+        uint32_t lo, hi, ospan;
+        bool valid, fits;
+        __device__ __forceinline__ uint32_t a0() const { return lo & ~15u; }
+        __device__ __forceinline__ uint32_t span() const { return hi > lo ? ((hi + 15u) & ~15u) - a0() : 0u; }
+        __device__ __forceinline__ uint64_t olo() const { return dec_slot(lo); }
+        __device__ __forceinline__ uint64_t ohi() const { return dec_slot(hi); }
+        __device__ __forceinline__ uint64_t obase() const { return olo() & ~15ull; }
+    };
+    auto plan = [&](uint64_t b, const TileIn& ti) {
+        Plan P;
+        const Tile t = finish_tile(b, lane, A.n, ti, false);
+        P.s = t.s;
+        P.len = t.len;
+        P.valid = t.valid;
+        P.lo = __builtin_amdgcn_readfirstlane(t.lo);
+        P.hi = __builtin_amdgcn_readfirstlane(t.hi);
+        P.ospan = P.hi > P.lo ? (uint32_t)(P.ohi() - P.obase()) : 0u;
+        P.op0 = t.len ? (uint32_t)(dec_slot(t.s) - P.obase()) : 0u;
+        P.fits = P.span() <= IN_STAGE && P.ospan <= OUT_STAGE;
+        return P;
+    };
+    SpanPrefetch<(IN_STAGE + 1023) / 1024> pf;
+    TileIn ti = issue_tile(base, lane, A.n, A.in_off, nullptr, A.is_name_bits, nullptr);
+    Plan cur = plan(base, ti);
+    uint32_t cur_name = ti.name_word;
+    if (cur.fits) pf.issue(A.in, A.in_size, cur.a0(), cur.span(), lane);
+    bool have_next = base + stride < A.n;
+    ti = issue_tile(base + stride, lane, A.n, A.in_off, nullptr, A.is_name_bits, nullptr);
+    if (cur.fits) pf.template commit<true>(reinterpret_cast<uint32_t*>(buf), A.in, A.in_size, cur.a0(), cur.span(), lane);
+    Plan nxt;
+    uint32_t nxt_name = 0;
+    if (have_next) {
+        nxt = plan(base + stride, ti);
+        nxt_name = ti.name_word;
+        if (nxt.fits) pf.issue(A.in, A.in_size, nxt.a0(), nxt.span(), lane);
+        ti = issue_tile(base + 2 * stride, lane, A.n, A.in_off, nullptr, A.is_name_bits, nullptr);
+    }
+    uint32_t* stage = reinterpret_cast<uint32_t*>(buf);
+    uint8_t* obuf = buf + IN_STAGE;
+    for (;;) {
+        const uint64_t nbase = base + stride;
+        const Plan& t = cur;
+        const uint32_t ti_i = (uint32_t)base + (uint32_t)lane;
+        const bool is_name = t.valid && A.is_name_bits ? ((cur_name >> (ti_i & 31)) & 1u) : false;
+        uint32_t ol = 0;
+        uint8_t st = 0;
+        bool listed = false;
+        if (cur.fits) {
+            // the store wave has read the last posted tile's stage out before this tile's steps overwrite it
+            while (lds_ld_acq(&sm.drained[wave]) != seq) __builtin_amdgcn_s_sleep(1);
+            wave_lds_sync();
+            const bool act = t.valid && t.len <= kMaxStrLen;
+            const uint32_t rel = t.len ? t.s - cur.a0() : 0u;
+            const DecResult r = decode_staged_lane_v7(stage, rel, t.len, act, obuf, cur.op0, OUT_STAGE + 4u * (uint32_t)lane, T);
+            if (t.valid && t.len > kMaxStrLen) {
+                ol = kFailLen;
+                st = kStatusTooLong;
+            } else if (r.ok) {
+                ol = r.len;
+                const uint32_t first = r.len ? obuf[cur.op0] : 0u, lastc = r.len ? obuf[cur.op0 + r.len - 1] : 0u;
+                st = soft_bits(is_name, r.len, r.flags, first, lastc);
+            } else {
+                ol = kFailLen;
+                st = kStatusFail;
+            }
+            // post the tile: lengths, statuses and region into LDS, then the flag
+            sm.len[wave][lane] = t.valid ? ol : kSwSkip;
+            sm.st[wave][lane] = st;
+            if (lane == 0) {
+                SwTile d;
+                d.gbase = cur.obase();
+                d.keep_lo = cur.olo();
+                d.keep_hi = cur.ohi();
+                d.ospan = cur.ospan;
+                d.rec = (uint32_t)(base >> 6);
+                d.base = (uint32_t)base;
+                d.pad = 0;
+                sm.tile[wave] = d;
+            }
+            ++seq;
+            if (lane == 0) lds_st_rel(&sm.posted[wave], seq);
+        } else if (t.valid) {  // a tile larger than the stages: this wave stores it itself (no edges to defer)
+            if (split_push(A, ti_i, t.len)) {
+                listed = true;
+            } else {
+                decode_direct(A, t.s, t.len, is_name, A.out + dec_slot(t.s), T, ol, st);
+            }
+        }
+        if (!cur.fits) {
+            if (lane == 0) {
+                A.edges[2 * (base >> 6)].m = make_uint4(0u, 0u, 0u, 0u);
+                A.edges[2 * (base >> 6) + 1].m = make_uint4(0u, 0u, 0u, 0u);
+            }
+            if (t.valid && !listed) {
+                A.out_len[ti_i] = ol;
+                A.status[ti_i] = st;
+            }
+        }
+        // ---- the next tile: commit its span (the input stage is free), plan + prefetch the one after ----
+        if (have_next && nxt.fits)
+            pf.template commit<true>(stage, A.in, A.in_size, nxt.a0(), nxt.span(), lane);
+        const bool have_nn = have_next && nbase + stride < A.n;
+        Plan nn = plan(nbase + stride, ti);
+        const uint32_t nn_name = ti.name_word;
+        if (have_nn && nn.fits) pf.issue(A.in, A.in_size, nn.a0(), nn.span(), lane);
+        ti = issue_tile(nbase + 2 * stride, lane, A.n, A.in_off, nullptr, A.is_name_bits, nullptr);
+        if (!have_next) break;
+        cur = nxt;
+        cur_name = nxt_name;
+        nxt = nn;
+        nxt_name = nn_name;
+        have_next = have_nn;
+        base = nbase;
+    }
+    if (lane == 0) __hip_atomic_fetch_add(&sm.finished, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void decode_direct_kernel(DecArgs A) {
     __shared__ __attribute__((aligned(16))) uint32_t s_lut[1u << HHUFF_LUT_BITS];
@@ -4665,6 +4942,11 @@ constexpr int kEncOStr = HHUFF_ENCO_NS, kEncOThreads = HHUFF_ENCO_NS / HHUFF_ENC
 #endif
 constexpr int kDecSWaves = 16, kEncSWaves = 16;
 #define DEC_S decode_staged_kernel<kDecSWaves, 3072, 4608, false>
+#ifndef HHUFF_DEC_SW  // 1: contiguous short-string decode through decode_staged_sw_kernel (a store wave)
+#define HHUFF_DEC_SW 0
+#endif
+
+#define DEC_SW decode_staged_sw_kernel<3072, 4608, HHUFF_DEC_SW_NSW>
 #define DEC_L decode_staged_kernel<6, 8192, 12928, false>
 #define DEC_SP decode_staged_kernel<kDecSWaves, 3072, 4608, true>
 #define DEC_LP decode_staged_kernel<6, 8192, 12928, true>
@@ -5133,6 +5415,12 @@ static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint3
         }
         return e;
     }
+#if HHUFF_DEC_SW
+    if (v == kDecS && defer && A.n_dev == nullptr) {  // the store-wave variant (15 decode waves a block)
+        hipLaunchKernelGGL(DEC_SW, dim3(grid), dim3(1024), 0, stream, A);
+        return finish_deferred(out, A.edges, n, stream);
+    }
+#endif
     switch (v) {
         case kDecS: hipLaunchKernelGGL(DEC_S, dim3(grid), dim3(kDecSWaves * 64), 0, stream, A); break;
         case kDecL: hipLaunchKernelGGL(DEC_L, dim3(grid), dim3(384), 0, stream, A); break;
