@@ -267,6 +267,9 @@ struct EdgeRec {
                         // statuses streamed too, HHUFF_NT_RES, c4 decode gains less)
 #define HHUFF_NT_STORE 1
 #endif
+#ifndef HHUFF_STREAM_NT
+#define HHUFF_STREAM_NT 0
+#endif
 #ifndef HHUFF_STATUS_DW  // staged decode: a tile's status bytes stored as dwords
 #define HHUFF_STATUS_DW 0
 #endif
@@ -1766,7 +1769,11 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                     if (c0 < hs)
                         store_range16(gchunk + c0, obuf + c0, hs - c0, 16u);
                     else
+#if HHUFF_STREAM_NT  // A/B: the flush's whole chunks as streaming stores
+                        st16_out(gchunk + c0, *reinterpret_cast<const uint4*>(obuf + c0));
+#else
                         *reinterpret_cast<uint4*>(gchunk + c0) = *reinterpret_cast<const uint4*>(obuf + c0);
+#endif
                 }
                 const uint32_t c0 = 16u * nfull;
                 if (done) {
