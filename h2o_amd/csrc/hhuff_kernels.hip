@@ -178,6 +178,9 @@ __device__ __forceinline__ Tile finish_tile(uint64_t base, int lane, uint32_t n,
     return t;
 }
 
+#ifndef HHUFF_NT_LOAD  // A/B: tile spans fetched with streaming (non-temporal) loads
+#define HHUFF_NT_LOAD 0
+#endif
 template <int NCH>
 struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lane per KiB
     uint4 v[NCH];
@@ -190,7 +193,15 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
             const uint32_t k = (uint32_t)c * 1024u + (uint32_t)lane * 16u;
+#if HHUFF_NT_LOAD  // A/B: the span as streaming loads (read once)
+            if (k < span && k + 16u <= avail) {
+                typedef unsigned int u32x4l __attribute__((ext_vector_type(4)));
+                const u32x4l x = __builtin_nontemporal_load(reinterpret_cast<const u32x4l*>(src + k));
+                v[c] = make_uint4(x.x, x.y, x.z, x.w);
+            }
+#else
             if (k < span && k + 16u <= avail) v[c] = *reinterpret_cast<const uint4*>(src + k);
+#endif
         }
     }
     template <bool kSwap = false>  // kSwap: store big-endian dwords (the v5 decode window reads them)
@@ -2739,7 +2750,15 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
         for (int j = 0; j < NV; ++j) {
             const uint32_t k = (uint32_t)j * (16u * NT) + t * 16u;
             const uint64_t g = (uint64_t)a0 + k;
+#if HHUFF_NT_LOAD
+            if (k < span && span <= (uint32_t)CH && g + 16 <= A.in_size) {
+                typedef unsigned int u32x4l __attribute__((ext_vector_type(4)));
+                const u32x4l x = __builtin_nontemporal_load(reinterpret_cast<const u32x4l*>(A.in + g));
+                v[j] = make_uint4(x.x, x.y, x.z, x.w);
+            }
+#else
             if (k < span && span <= (uint32_t)CH && g + 16 <= A.in_size) v[j] = *reinterpret_cast<const uint4*>(A.in + g);
+#endif
         }
     };
     auto commit_span = [&](const uint4 (&v)[NV], const SortChunk& q) {
