@@ -34,6 +34,11 @@ def run(names, cfg="c4", rounds=5, steps=10):
     # ablation configs (not product configs): fixed-length strings isolate lane imbalance
     synth.CONFIGS.setdefault("c4u", dict(n=1 << 24, lengths=("uniform", 48, 48), alphabet="header"))
     synth.CONFIGS.setdefault("c3desc", dict(n=1 << 20, lengths=("zipf_desc", 8, 512), alphabet="header"))
+    # c3's two halves at their c3 counts (the zipf's conditional lengths): what a length partition could reach
+    synth.CONFIGS.setdefault("c3lo", dict(n=643000, lengths=("zipf", 8, 96), alphabet="header"))
+    synth.CONFIGS.setdefault("c3hi", dict(n=405000, lengths=("zipf", 97, 512), alphabet="header"))
+    synth.CONFIGS.setdefault("c3hid", dict(n=405000, lengths=("zipf_desc", 97, 512), alphabet="header"))
+    synth.CONFIGS.setdefault("u250", dict(n=405000, lengths=("uniform", 250, 250), alphabet="header"))
     for L in (64, 80, 96, 120, 200, 400):  # fixed lengths at the c3 scale: what length-sorted tiles could reach
         synth.CONFIGS.setdefault("u%d" % L, dict(n=1 << 20, lengths=("uniform", L, L), alphabet="header"))
     torch.cuda.set_device(0)
