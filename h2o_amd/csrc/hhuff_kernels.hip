@@ -3670,6 +3670,13 @@ constexpr int kDecSWaves = 16, kEncSWaves = 16;
 #endif
 
 #define DEC_SW decode_staged_sw_kernel<3072, 4608, HHUFF_DEC_SW_NSW>
+#ifndef HHUFF_DEC_RUN  // 1: the contiguous layout's stream decode runs decode_run_kernel (runs of HHUFF_RUN_RL strings)
+#define HHUFF_DEC_RUN 0
+#endif
+#ifndef HHUFF_RUN_RL
+#define HHUFF_RUN_RL 4
+#endif
+#define DEC_R decode_run_kernel<kDecTWaves, HHUFF_DECT_NW, HHUFF_DECT_OUT, HHUFF_RUN_RL>
 #define DEC_L decode_staged_kernel<6, 8192, 12928, false>
 #define DEC_SP decode_staged_kernel<kDecSWaves, 3072, 4608, true>
 #define DEC_LP decode_staged_kernel<6, 8192, 12928, true>
@@ -4113,8 +4120,14 @@ static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint3
         }
         if (e == hipSuccess) {
             A.edges = nullptr;
-            hipLaunchKernelGGL(DEC_T, dim3(grid_for(kDecT, current_device(), n)), dim3(kDecTWaves * 64), 0, stream, A,
-                               ctr);
+#if HHUFF_DEC_RUN
+            if (in_len == nullptr && out_off == nullptr && A.n_dev == nullptr)
+                hipLaunchKernelGGL(DEC_R, dim3(grid_for(kDecT, current_device(), n)), dim3(kDecTWaves * 64), 0, stream,
+                                   A, ctr);
+            else
+#endif
+                hipLaunchKernelGGL(DEC_T, dim3(grid_for(kDecT, current_device(), n)), dim3(kDecTWaves * 64), 0, stream,
+                                   A, ctr);
             e = hipGetLastError();
         }
         const hipError_t f = hipFreeAsync(sel, stream);
@@ -4129,7 +4142,12 @@ static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint3
         hipError_t e = pool_alloc((void**)&ctr, sizeof(*ctr), stream);
         if (e == hipSuccess) e = hipMemsetAsync(ctr, 0, sizeof(*ctr), stream);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(DEC_T, dim3(grid), dim3(kDecTWaves * 64), 0, stream, A, ctr);
+#if HHUFF_DEC_RUN
+            if (in_len == nullptr && out_off == nullptr && A.n_dev == nullptr)
+                hipLaunchKernelGGL(DEC_R, dim3(grid), dim3(kDecTWaves * 64), 0, stream, A, ctr);
+            else
+#endif
+                hipLaunchKernelGGL(DEC_T, dim3(grid), dim3(kDecTWaves * 64), 0, stream, A, ctr);
             e = hipGetLastError();
         }
         if (ctr) {

@@ -1,7 +1,7 @@
 // hhuff_variants.h -- kernel variants kept for A/B builds (included by hhuff_kernels.hip after every helper
 // they use).  Each was built to parity and measured against the default kernel (DESIGN.md (e), round 5;
 // profiles/r05*): none is instantiated unless its build flag is set (HHUFF_DEC_SW, HHUFF_STREAM2,
-// HHUFF_STREAM_RK, HHUFF_ENC_INPLACE).
+// HHUFF_STREAM_RK, HHUFF_ENC_INPLACE, HHUFF_DEC_RUN).
 #pragma once
 
 // ------------------------------------------------------------------------------------------------
@@ -1310,6 +1310,387 @@ __global__ __launch_bounds__(NS / SPT) __attribute__((amdgpu_waves_per_eu(HHUFF_
         cur = nxt;
         nxt = nn;
         c = cn;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Run decode (HHUFF_DEC_RUN; contiguous layout, slot output; mixed and long lengths).  decode_stream_kernel's
+// lanes take one string at a time, and a lane whose string ends inside its window idles for the rest of the
+// round: on c3's long half that spread costs 24 % against the same bytes at one length (profiles/
+// r05ac_c3_decomposition_ab.jsonl), and every string starts behind a dependent take (counter, offsets, window).
+// Here a lane takes a run of RL consecutive strings (their RL + 1 offsets and is-name word in registers), and a
+// string that ends inside the window is followed at once by the run's next string, whose bytes are already in
+// the window (consecutive strings are adjacent): the round goes on in sub-rounds until every lane has used its
+// window.  Measured slower (c3 0.395 / 0.565 ms with runs of 2 / 4 strings against 0.296; c5 0.631 / 0.822
+// against 0.431, profiles/r05af_run_decode_ab.jsonl): c3 and c5 give a lane only 5-11 strings, so runs leave
+// too few units to balance the lanes, and the sub-rounds cost more than the idle window they recover.
+// A string's output is flushed when it ends (its head and tail chunks byte-exact, as the stream kernel
+// does at a string's end); the next string's output starts a fresh buffer at its own slot.  The continuation
+// window of a run is always the next NW dwords, so it is prefetched a round ahead.
+// ------------------------------------------------------------------------------------------------
+template <int WAVES, int NW, int OUT, int RL>
+__global__ __launch_bounds__(WAVES * 64) void decode_run_kernel(DecArgs A, unsigned long long* __restrict__ counter) {
+    static_assert(NW >= 8 && NW % 4 == 0 && OUT % 16 == 0 && 32 % RL == 0, "window shape; runs inside a name word");
+    static_assert(15 + (32 * (NW - 2)) / 5 + 2 < OUT, "output buffer too small for a window");
+    constexpr uint32_t kWS = NW + 1;
+    struct __attribute__((aligned(16))) Smem {
+        uint32_t lut[1u << HHUFF_LUT_BITS];
+        uint32_t kinfo[32];
+        uint32_t ones[(HHUFF_ONES_NENT + 3) & ~3];
+        uint8_t out[WAVES * 64][OUT];
+        uint32_t win[WAVES * 64][kWS];
+    };
+    __shared__ Smem sm;
+    load_dec_tables(sm.lut, sm.kinfo, sm.ones, WAVES * 64);
+    __syncthreads();
+    const DecTables T{sm.lut, sm.kinfo, sm.ones};
+    const int lane = threadIdx.x & 63;
+    uint32_t* win = &sm.win[threadIdx.x][1];
+    const lds_u32* st = (const lds_u32*)win;
+    uint8_t* obuf = sm.out[threadIdx.x];
+    const uint32_t ob = lds_addr(obuf), trash = ob + OUT - 1u;
+    constexpr int32_t kLimW = 32 * (NW - 2) - 30;
+    constexpr int32_t kFinal = 32 * (NW - 2);
+
+    // per-lane run state: strings [rs + k, rs + kcnt); ro[0], ro[1] bound the current string (popped as strings end)
+    uint32_t ro[RL + 1];
+    uint32_t rs = 0, k = 0, kcnt = 0, nmw = 0, rend = 0;
+    // per-lane string state
+    uint4 pfv[NW / 4];
+    uint64_t pfa = ~0ull;
+    bool busy = false, head = false, is_name = false;
+    uint32_t i = 0, s = 0, len = 0, P = 0, ocnt = 0, flags = 0, first = 0, lastb = 0, fail = 0;
+    uint64_t dst = 0;
+    uint64_t bnext = 0, bend = 0;
+    bool qdone = false;
+    const uint64_t nwork = (uint64_t)A.n;
+    const uint64_t nruns = (nwork + RL - 1) / RL;
+    // the current string of the run (ro[0], ro[1]); too long / listed strings are settled and skipped here
+    auto start_string = [&]() {
+        busy = false;
+        while (k < kcnt) {
+            i = rs + k;
+            s = ro[0];
+            len = ro[1] - ro[0];
+            is_name = ((nmw >> (i & 31u)) & 1u) != 0;
+            dst = dec_slot(s);
+            bool skip = false;
+            if (len > kMaxStrLen) {
+                A.out_len[i] = kFailLen;
+                A.status[i] = kStatusTooLong;
+                skip = true;
+            } else if (split_push(A, i, len)) {
+                skip = true;
+            }
+            if (!skip) {
+                busy = true;
+                head = (dst & 15u) != 0;
+                P = ocnt = flags = first = lastb = fail = 0;
+                return;
+            }
+#pragma unroll
+            for (int j = 0; j < RL; ++j) ro[j] = ro[j + 1];
+            ++k;
+        }
+    };
+    PROF_DECL
+
+    for (;;) {
+        // ---- 1. lanes without a run take one (a wave claims 64 runs at a time) ----
+        for (int it = 0; it < 2; ++it) {
+            const uint64_t need = __builtin_amdgcn_ballot_w64(!busy && k >= kcnt);
+            if (need == 0) break;
+            if (bnext >= bend) {
+                if (qdone) break;
+                uint64_t b = 0;
+                if (lane == 0) b = atomicAdd(counter, 64ull);
+                b = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
+                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+                if (b >= nruns) {
+                    qdone = true;
+                    break;
+                }
+                bnext = b;
+                bend = min(b + 64u, nruns);
+            }
+            const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+            if (!busy && k >= kcnt && bnext + rank < bend) {
+                rs = (uint32_t)((bnext + rank) * RL);
+                kcnt = (uint32_t)min((uint64_t)RL, nwork - rs);
+                k = 0;
+#pragma unroll
+                for (int j = 0; j <= RL; ++j) ro[j] = A.in_off[min((uint64_t)rs + j, nwork)];
+                nmw = A.is_name_bits ? A.is_name_bits[rs >> 5] : 0u;
+                rend = A.in_off[rs + kcnt];  // the run's end byte
+                start_string();
+            }
+            bnext = min(bend, bnext + (uint64_t)__builtin_popcountll(need));
+        }
+        if (!__any(busy)) {
+            if (qdone) {
+                PROF_FLUSH(0);
+                break;
+            }
+            continue;
+        }
+        PROF_MARK(0);
+
+        // ---- 2. the lane's window: NW dwords from its current byte; the run's continuation prefetched ----
+        const uint64_t cur = (uint64_t)s + (P >> 3);
+        // the prefetched window when the lane's byte lies in its first 16 bytes (a run's next round, or a string
+        // that starts past the last round's window), else the dword holding the byte
+        const uint64_t wb = pfa != ~0ull && cur >= pfa && cur < pfa + 16u ? pfa : cur & ~3ull;
+        if (busy) {
+            if (wb != pfa) {
+#pragma unroll
+                for (int j = 0; j < NW / 4; ++j) pfv[j] = load16_bounded(A.in, A.in_size, wb + 16u * j);
+            }
+#pragma unroll
+            for (int j = 0; j < NW / 4; ++j) {
+                win[4 * j + 0] = bswap32(pfv[j].x);
+                win[4 * j + 1] = bswap32(pfv[j].y);
+                win[4 * j + 2] = bswap32(pfv[j].z);
+                win[4 * j + 3] = bswap32(pfv[j].w);
+            }
+            // a round stops at or past window bit kLimW: the run's next round starts in the dword at 4 (NW - 3)
+            pfa = (uint64_t)rend > wb + 4u * (NW - 3) ? wb + 4u * (NW - 3) : ~0ull;
+            if (pfa != ~0ull) {
+#pragma unroll
+                for (int j = 0; j < NW / 4; ++j) pfv[j] = load16_bounded(A.in, A.in_size, pfa + 16u * j);
+            }
+        }
+        // the current string inside this window
+        int32_t pm = busy ? (int32_t)(8u * (uint32_t)(cur - wb) + (P & 7u)) - 1 : -1;
+        int32_t pm0 = pm;
+        int32_t end = busy ? (int32_t)min((uint64_t)(pm + 1) + ((uint64_t)len * 8u - P), (uint64_t)0x40000000u) : 0;
+        bool fin = busy && end <= kFinal;
+        uint32_t h0 = (uint32_t)((dst + ocnt) & 15u);
+        uint32_t o = ob + h0;
+        int32_t q = pm >> 5;
+        uint32_t x0 = st[q], x1 = st[q + 1], x2 = st[q + 2];
+        uint32_t accb = 0, acc1 = 0, acc2 = 0, accl = 0, parked = busy ? 0u : 1u;
+        int32_t lim = busy ? min(end - 26, kLimW) : (int32_t)0x80000000;
+        auto advance = [&](int32_t cons) {
+            pm += cons;
+            const int32_t qn = pm >> 5;
+            const bool adv = qn != q;
+            x0 = adv ? x1 : x0;
+            x1 = adv ? x2 : x1;
+            q = qn;
+            x2 = st[q + 2];
+        };
+        int32_t c = 0;
+        bool waiting = false;  // the lane's string starts past this window: it begins next round
+        for (;;) {  // ---- 3. sub-rounds: bulk, tail, and the run's next strings inside this window ----
+            auto bstep = [&](bool longchk) {
+                if (pm < lim) {
+                    const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                    const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+                    const uint32_t sl = (uint32_t)((int32_t)e >> 31);
+                    bulk_put2(o, e, trash);
+                    o += (e >> 28) & 3u;
+                    accb |= e;
+                    uint32_t cons = lut_l12(e);
+                    {
+                        const uint32_t wb2 = w << cons;
+                        const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
+                        bulk_put2(o, eb, trash);
+                        o += (eb >> 28) & 3u;
+                        accb |= eb;
+                        cons += lut_l12(eb);
+                    }
+                    if (longchk && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
+                        if (sl) {
+                            const uint32_t kk = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                            const uint32_t ki = T.kinfo[kk];
+                            const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (kk + 1)) >> 1) >> (31 - (ki >> 16)))];
+                            const int32_t L = (le >> 9) & 31u;
+                            const uint32_t fits = (uint32_t)((L + pm - end) >> 31);
+                            const uint32_t eos = (le & 0x1FFu) == kEos ? 0xFFFFFFFFu : 0u;
+                            const uint32_t okm = fits & ~eos;
+                            fail |= fits & eos & 1u;
+                            lds_st8(sel_bits(okm, o, trash), le);
+                            o -= okm;
+                            accl |= le & okm;
+                            cons = okm & (uint32_t)L;
+                            parked |= ~okm & 1u;
+                            lim = (int32_t)sel_bits(okm, (uint32_t)lim, 0x80000000u);
+                        }
+                    }
+                    advance((int32_t)cons);
+                }
+            };
+            for (;;) {
+                bstep(false);
+                bstep(true);
+                if (!__any(pm < lim)) break;
+            }
+            c = (fin && !parked) ? pm - end : 0x40000000;
+            if (__any(fin)) {
+                int32_t prog = 0;
+                auto step = [&](bool longchk) {
+                    const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                    const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
+                    const int32_t L1 = lut_l1(e), L12 = lut_l12(e);
+                    const int32_t s1 = L1 + c, s2 = L12 + c;
+                    const uint32_t m1 = (uint32_t)((s1 & ~(int32_t)e) >> 31);
+                    const uint32_t m2 = (uint32_t)((s2 & (int32_t)(e << 1)) >> 31);
+                    int32_t cons = (int32_t)sel_bits(m2, (uint32_t)L12, m1 & (uint32_t)L1);
+                    lds_st8(sel_bits(m1, o - m2, trash), lut_sym2(e));
+                    lds_st8(sel_bits(m1, o, trash), e);
+                    o = o - m1 - m2;
+                    acc1 |= e & m1;
+                    acc2 |= e & m2;
+                    {
+                        const uint32_t wb2 = w << cons;
+                        const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
+                        const int32_t cb = c + cons;
+                        const int32_t L1b = lut_l1(eb), L12b = lut_l12(eb);
+                        const uint32_t m1b = (uint32_t)(((L1b + cb) & ~(int32_t)eb) >> 31);
+                        const uint32_t m2b = (uint32_t)(((L12b + cb) & (int32_t)(eb << 1)) >> 31);
+                        lds_st8(sel_bits(m1b, o - m2b, trash), lut_sym2(eb));
+                        lds_st8(sel_bits(m1b, o, trash), eb);
+                        o = o - m1b - m2b;
+                        acc1 |= eb & m1b;
+                        acc2 |= eb & m2b;
+                        cons += (int32_t)sel_bits(m2b, (uint32_t)L12b, m1b & (uint32_t)L1b);
+                    }
+                    const bool lact = (s1 & (int32_t)e) < 0;
+                    uint32_t consl = 0;
+                    if (longchk && __builtin_amdgcn_ballot_w64(lact) != 0) {
+                        if (lact) {
+                            const uint32_t kk = min((uint32_t)__builtin_clz(~w | 1u), 30u);
+                            const uint32_t ki = T.kinfo[kk];
+                            const uint32_t le = T.ones[(ki & 0xFFFFu) + (((w << (kk + 1)) >> 1) >> (31 - (ki >> 16)))];
+                            const int32_t L = (le >> 9) & 31u;
+                            const uint32_t fits = (uint32_t)((L + c) >> 31);
+                            const uint32_t eos = (le & 0x1FFu) == kEos ? 0xFFFFFFFFu : 0u;
+                            const uint32_t okm = fits & ~eos;
+                            fail |= fits & eos & 1u;
+                            lds_st8(sel_bits(okm, o, trash), le);
+                            o -= okm;
+                            accl |= le & okm;
+                            consl = okm & (uint32_t)L;
+                            c = (int32_t)sel_bits(okm, (uint32_t)c, 0x40000000u);
+                        }
+                    }
+                    cons |= (int32_t)consl;
+                    c += cons;
+                    advance(cons);
+                    prog = cons;
+                };
+                step(true);
+                for (;;) {
+                    step(false);
+                    step(true);
+                    if (!__any(prog != 0)) break;
+                }
+            }
+            // strings that ended in this window: settle and flush them, then the run's next string
+            const bool ended = busy && (parked || fin);
+            if (!__any(ended)) break;
+            bool again = false;
+            if (ended) {
+                flags |= ((accb >> 24) | (accb >> 26) | (acc1 >> 24) | (acc2 >> 26) | (accl >> 14)) & 3u;
+                const uint32_t nb = o - ob;
+                const uint32_t made = nb - h0;
+                if (made) {
+                    if (ocnt == 0) first = obuf[h0];
+                    lastb = obuf[nb - 1u];
+                }
+                const bool ok = fin && !parked && !fail && [&] {
+                    const uint32_t R = ~(uint32_t)c;
+                    const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
+                    return R <= 7 && (w | (0xFFFFFFFFu >> (R & 31u))) == 0xFFFFFFFFu;
+                }();
+                if (ok) {  // a failed string's output is unspecified
+                    uint8_t* gchunk = A.out + ((dst + ocnt) & ~15ull);
+                    const uint32_t hs = head ? (uint32_t)(dst & 15u) : 0u;
+                    const uint32_t nfull = nb >> 4;
+                    for (uint32_t kc = 0; kc < nfull; ++kc) {
+                        const uint32_t c0 = 16u * kc;
+                        if (c0 + 16u <= hs) continue;
+                        if (c0 < hs)
+                            store_range16(gchunk + c0, obuf + c0, hs - c0, 16u);
+                        else
+                            *reinterpret_cast<uint4*>(gchunk + c0) = *reinterpret_cast<const uint4*>(obuf + c0);
+                    }
+                    const uint32_t c0 = 16u * nfull;
+                    const uint32_t lo = hs > c0 ? hs - c0 : 0u;
+                    if (nb - c0 > lo) store_range16(gchunk + c0, obuf + c0, lo, nb - c0);
+                }
+                ocnt += made;
+                A.out_len[i] = ok ? ocnt : kFailLen;
+                A.status[i] = ok ? soft_bits(is_name, ocnt, flags, first, lastb) : kStatusFail;
+                // the run's next string: its bytes follow at once, in this window if it starts before its end
+#pragma unroll
+                for (int j = 0; j < RL; ++j) ro[j] = ro[j + 1];
+                ++k;
+                start_string();
+                if (busy) {
+                    const int64_t rel = (int64_t)s - (int64_t)wb;  // >= 0: runs are contiguous
+                    pm = (int32_t)(8 * rel) - 1;
+                    pm0 = pm;
+                    end = (int32_t)min((uint64_t)(pm + 1) + (uint64_t)len * 8u, (uint64_t)0x40000000u);
+                    fin = end <= kFinal;
+                    h0 = (uint32_t)(dst & 15u);
+                    o = ob + h0;
+                    accb = acc1 = acc2 = accl = 0;
+                    parked = 0;
+                    // bulk only from a start inside the window's bulk range; a start past it waits for the next round
+                    const bool inside = pm + 1 < kFinal;
+                    lim = inside ? min(end - 26, kLimW) : (int32_t)0x80000000;
+                    fin = fin && inside;
+                    if (inside) {
+                        q = pm >> 5;
+                        x0 = st[q];
+                        x1 = st[q + 1];
+                        x2 = st[q + 2];
+                        again = true;
+                    } else {
+                        waiting = true;
+                    }
+                } else {
+                    fin = false;
+                    lim = (int32_t)0x80000000;
+                    parked = 1;
+                }
+            }
+            if (!__any(again)) break;
+        }
+        PROF_MARK(2);
+
+        // ---- 4. strings that go on past this window: whole chunks out, the partial one carried ----
+        if (busy && !waiting) {
+            flags |= ((accb >> 24) | (accb >> 26) | (acc1 >> 24) | (acc2 >> 26) | (accl >> 14)) & 3u;
+            const uint32_t nb = o - ob;
+            const uint32_t made = nb - h0;
+            if (made) {
+                if (ocnt == 0) first = obuf[h0];
+                lastb = obuf[nb - 1u];
+            }
+            uint8_t* gchunk = A.out + ((dst + ocnt) & ~15ull);
+            const uint32_t hs = head ? (uint32_t)(dst & 15u) : 0u;
+            const uint32_t nfull = nb >> 4;
+            for (uint32_t kc = 0; kc < nfull; ++kc) {
+                const uint32_t c0 = 16u * kc;
+                if (c0 + 16u <= hs) continue;
+                if (c0 < hs)
+                    store_range16(gchunk + c0, obuf + c0, hs - c0, 16u);
+                else
+                    *reinterpret_cast<uint4*>(gchunk + c0) = *reinterpret_cast<const uint4*>(obuf + c0);
+            }
+            if (nfull) {
+                head = false;
+                const uint32_t c0 = 16u * nfull;
+                for (uint32_t r = 0; c0 + 16u * r < nb; ++r)
+                    *reinterpret_cast<uint4*>(obuf + 16u * r) = *reinterpret_cast<const uint4*>(obuf + c0 + 16u * r);
+            }
+            ocnt += made;
+            P += (uint32_t)(pm - pm0);
+        }
+        PROF_MARK(4);
     }
 }
 
