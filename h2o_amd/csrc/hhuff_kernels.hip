@@ -221,24 +221,6 @@ struct SpanPrefetch {  // up to NCH x 1 KiB of a tile's input span, 16 B per lan
     }
 };
 
-// Write LDS bytes [0, ospan) to global [gbase, gbase + ospan) (gbase 16-aligned), keeping only the
-// global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
-// (Measured: batching the LDS reads of all chunks, or taking the edge bytes from the loaded registers,
-// made the c4 decode 3.5 % slower -- register pressure / code size in the 16-wave staged kernels.)
-template <int NCH>
-__device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds, uint32_t ospan,
-                                            uint64_t keep_lo, uint64_t keep_hi, int lane) {
-    for (uint32_t k = (uint32_t)lane * 16u; k < ospan; k += 64u * 16u) {
-        const uint64_t g = gbase + k;
-        if (g >= keep_lo && g + 16 <= keep_hi) {
-            *reinterpret_cast<uint4*>(out + g) = *reinterpret_cast<const uint4*>(lds + k);
-        } else {
-            for (uint32_t b = 0; b < 16; ++b)
-                if (g + b >= keep_lo && g + b < keep_hi) out[g + b] = lds[k + b];
-        }
-    }
-}
-
 // Deferred region edges.  Writing the (at most two) 16-byte chunks a tile's output region shares with
 // its neighbours byte by byte costs a serial LDS round trip per byte; measured, it was 11 % of both c4
 // kernels.  Instead the tile writes every whole chunk with 16-B stores, and the lanes holding its first
@@ -297,6 +279,23 @@ __device__ __forceinline__ void st16_out(uint8_t* p, uint4 v) {
     *reinterpret_cast<uint4*>(p) = v;
 #endif
 }
+// bytes [lo, hi) of the 16-B chunk v (in registers) to global g (16-B aligned): whole dwords as dword stores, the
+// partial dword at each end as byte stores -- at most 10 predicated stores
+__device__ __forceinline__ void store_range16r(uint8_t* __restrict__ g, uint4 v, uint32_t lo, uint32_t hi) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        if (lo <= 4u * k && 4u * k + 4u <= hi) *reinterpret_cast<uint32_t*>(g + 4u * k) = w[k];
+    const uint64_t q0 = (uint64_t)v.y << 32 | v.x, q1 = (uint64_t)v.w << 32 | v.z;
+    auto byte_at = [&](uint32_t a) { return (uint32_t)((a < 8u ? q0 : q1) >> (8u * (a & 7u))); };
+    const uint32_t e0 = min(hi, (lo + 3u) & ~3u);
+    const uint32_t s1 = max(max(lo, hi & ~3u), e0);
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) {
+        if (lo + j < e0) g[lo + j] = (uint8_t)byte_at(lo + j);
+        if (s1 + j < hi) g[s1 + j] = (uint8_t)byte_at(s1 + j);
+    }
+}
 template <class T>
 __device__ __forceinline__ void st_res(T* p, T v) {
 #if HHUFF_NT_RES
@@ -305,6 +304,27 @@ __device__ __forceinline__ void st_res(T* p, T v) {
     *p = v;
 #endif
 }
+
+// Write LDS bytes [0, ospan) to global [gbase, gbase + ospan) (gbase 16-aligned), keeping only the
+// global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
+// (Measured: batching the LDS reads of all chunks, or taking the edge bytes from the loaded registers,
+// made the c4 decode 3.5 % slower -- register pressure / code size in the 16-wave staged kernels.)
+template <int NCH>
+__device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds, uint32_t ospan,
+                                            uint64_t keep_lo, uint64_t keep_hi, int lane) {
+    for (uint32_t k = (uint32_t)lane * 16u; k < ospan; k += 64u * 16u) {
+        const uint64_t g = gbase + k;
+        const uint4 v = *reinterpret_cast<const uint4*>(lds + k);
+        if (g >= keep_lo && g + 16 <= keep_hi) {
+            st16_out(out + g, v);
+        } else {  // a chunk shared with a neighbouring tile: only this tile's bytes (at most 10 stores)
+            const uint32_t lo = keep_lo > g ? (uint32_t)min(keep_lo - g, (uint64_t)16) : 0u;
+            const uint32_t hi = keep_hi > g ? (uint32_t)min(keep_hi - g, (uint64_t)16) : 0u;
+            if (hi > lo) store_range16r(out + g, v, lo, hi);
+        }
+    }
+}
+
 // SWAP: the LDS bytes are MSB-first words (the encode stage), byte-swapped in registers on the way out.
 template <bool SWAP = false>
 __device__ __forceinline__ void region_copy_deferred(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds,
@@ -1918,7 +1938,7 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
                 }
                 if (i < A.n) finish_encode(A, (uint32_t)i, len, ol);
             }
-            if (t < 2) rec[t].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges to defer
+            if (A.edges && t < 2) rec[t].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges to defer
             if (!more) break;
             issue_span(pv, nxt[0]);
             prepare(nxt, cn * kSortStr, 0u);
@@ -2005,13 +2025,17 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
             if (k == 0 || k == kl) {
                 const uint32_t elo = lo > g ? (uint32_t)(lo - g) : 0u;
                 const uint32_t ehi = hi - g < 16 ? (uint32_t)(hi - g) : 16u;
-                EdgeRec* e = rec + (k == 0 ? 0 : 1);
-                e->v = v;
-                e->m = make_uint4((uint32_t)g, (uint32_t)(g >> 32), full ? 0u : elo, full ? 0u : ehi);
+                if (A.edges) {
+                    EdgeRec* e = rec + (k == 0 ? 0 : 1);
+                    e->v = v;
+                    e->m = make_uint4((uint32_t)g, (uint32_t)(g >> 32), full ? 0u : elo, full ? 0u : ehi);
+                } else if (!full && ehi > elo) {  // small batches: the shared chunk's own bytes, now
+                    store_range16r(A.out + g, v, elo, ehi);
+                }
             }
         }
-        if (t == 0 && (kl == 0 || span == 0)) rec[1].m = make_uint4(0u, 0u, 0u, 0u);  // one chunk, or none
-        if (t == 0 && span == 0) rec[0].m = make_uint4(0u, 0u, 0u, 0u);
+        if (A.edges && t == 0 && (kl == 0 || span == 0)) rec[1].m = make_uint4(0u, 0u, 0u, 0u);  // one chunk, or none
+        if (A.edges && t == 0 && span == 0) rec[0].m = make_uint4(0u, 0u, 0u, 0u);
         PROF_MARK(4);
         if (!more) {
             PROF_FLUSH(1);
@@ -3854,6 +3878,14 @@ static hipError_t pool_alloc(void** p, uint64_t bytes, hipStream_t stream) {
     }
     return hipMallocFromPoolAsync(p, bytes, pool, stream);
 }
+// Deferred tile edges (records + edge_fix_kernel) for batches of this many strings or more; below it the kernels
+// write a tile's shared chunks byte-exact themselves (store_range16r) and a leg is one launch: the fix-up launch
+// is a fixed ~5 us, which a 1M-string batch feels and a 16M one does not (there the in-kernel byte stores cost
+// more, DESIGN (e) round 4)
+#ifndef HHUFF_DEFER_MIN
+#define HHUFF_DEFER_MIN (1u << 21)
+#endif
+constexpr uint32_t kDeferMin = HHUFF_DEFER_MIN;
 static hipError_t alloc_edges(EdgeRec** p, uint32_t n, hipStream_t stream) {
     return pool_alloc((void**)p, edge_recs(n) * sizeof(EdgeRec), stream);
 }
@@ -4097,7 +4129,7 @@ static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint3
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n);
 #endif
     const int grid = grid_for(v, current_device(), n);
-    const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr;
+    const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr && n >= kDeferMin;
     if (v == kDecL) {  // mixed lengths: the device picks staged or stream (see below)
         prices_in_effect(current_device(), A.price);  // no GPU work: see calibrate_prices
         uint64_t* sel = nullptr;  // [0, 3 kSelBlocks): partial sums; then the verdict and the work counter
@@ -4287,7 +4319,7 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     if (v == kEncS && in_len == nullptr && out_off == nullptr) v = kEncO;
 #endif
     const int grid = grid_for(v, current_device(), n);
-    const bool defer = v != kEncD && in_len == nullptr && out_off == nullptr;
+    const bool defer = v != kEncD && in_len == nullptr && out_off == nullptr && n >= kDeferMin;
     if (defer) {
         hipError_t e = alloc_edges(&A.edges, n, stream);
         if (e != hipSuccess) return e;
