@@ -551,13 +551,17 @@ def other_configs(torch, codec, synth, pmc_cfg=None):
         d_out = torch.empty(codec.decode_slot_size(H), dtype=torch.uint8, device="cuda")
         d_len = torch.empty(n_ok, dtype=torch.int32, device="cuda")
         d_st = torch.empty(n_ok, dtype=torch.uint8, device="cuda")
-        t_dec = BC.timed(torch, lambda: codec.decode_batch(huff, h_off, n_ok, out=d_out, out_len=d_len, status=d_st,
-                                                           in_size=H))
+        dec = lambda: codec.decode_batch(huff, h_off, n_ok, out=d_out, out_len=d_len, status=d_st, in_size=H)
+        t_dec, t_dec_ev = BC.timed_b2b(torch, dec), BC.timed(torch, dec)
         e_out = torch.empty(P + 16, dtype=torch.uint8, device="cuda")
         e_len = torch.empty(n, dtype=torch.int32, device="cuda")
-        t_enc = BC.timed(torch, lambda: codec.encode_batch(b["data"], off32, n, out=e_out, out_len=e_len, in_size=P))
+        enc = lambda: codec.encode_batch(b["data"], off32, n, out=e_out, out_len=e_len, in_size=P)
+        t_enc, t_enc_ev = BC.timed_b2b(torch, enc), BC.timed(torch, enc)
         E = int(torch.clamp(e_len, min=0).to(torch.int64).sum().item())
         pm = pmc_cfg.get(cfg, {})
+        # *_ms: calls back to back (tools/bench_configs.timed_b2b); *_ms_event_pair: an event pair around each
+        # call, the round-4/5 figure, which adds the pair's gap to every call
+        r.update(timing="back_to_back", decode_ms_event_pair=round(t_dec_ev, 4), encode_ms_event_pair=round(t_enc_ev, 4))
         r.update(decode_ms=round(t_dec, 4), decode_gibps=round(P_ok / GIB / (t_dec * 1e-3), 2),
                  encode_ms=round(t_enc, 4), encode_gibps=round(P / GIB / (t_enc * 1e-3), 2),
                  round_trip_gibps=round(P / GIB / ((t_enc + t_dec) * 1e-3), 2),
@@ -567,7 +571,9 @@ def other_configs(torch, codec, synth, pmc_cfg=None):
         if cfg == "c5":  # QPACK values: flatten_string(prefix 7) framing, the config's own operation
             f_out = torch.empty(P + 11 * n + 16, dtype=torch.uint8, device="cuda")
             f_len = torch.empty(n, dtype=torch.int32, device="cuda")
-            t = BC.timed(torch, lambda: codec.flatten_batch(b["data"], off32, n, 7, out=f_out, out_len=f_len, in_size=P))
+            flat = lambda: codec.flatten_batch(b["data"], off32, n, 7, out=f_out, out_len=f_len, in_size=P)
+            t, t_ev = BC.timed_b2b(torch, flat), BC.timed(torch, flat)
+            r.update(flatten_ms_event_pair=round(t_ev, 4))
             F = int(f_len.to(torch.int64).sum().item())
             r.update(flatten_ms=round(t, 4), flatten_gibps=round(P / GIB / (t * 1e-3), 2),
                      flatten_roofline=kernel_roofline(P + F + 8 * n + 4, t, pm, "flatten"))

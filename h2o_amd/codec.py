@@ -132,6 +132,8 @@ def lib():
         L.hhuff_pool_trim.argtypes = []
         L.hhuff_set_decode_kernel.restype = ctypes.c_int
         L.hhuff_set_decode_kernel.argtypes = [ctypes.c_int]
+        L.hhuff_set_edge_defer_min.restype = ctypes.c_uint32
+        L.hhuff_set_edge_defer_min.argtypes = [ctypes.c_uint32]
         L.hhuff_decode_batch_host_packed.restype = ctypes.c_int
         L.hhuff_decode_batch_host_packed.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64,
                                                      _vp, _vp, _vp, ctypes.c_int]
@@ -153,7 +155,7 @@ EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decod
             "hhuff_grid_size", "hhuff_decode_prices", "hhuff_calibrate_decode_prices", "hhuff_set_decode_prices",
             "hhuff_pool_trim", "hhuff_service_stamps", "hhuff_hpack_enc_scratch_size",
             "hhuff_hpack_flatten_responses", "hhuff_qpack_flatten_responses", "hhuff_set_decode_kernel",
-            "hhuff_decode_batch_host_packed", "hhuff_encode_batch_host_packed")
+            "hhuff_decode_batch_host_packed", "hhuff_encode_batch_host_packed", "hhuff_set_edge_defer_min")
 
 
 def _check(rc, what):
@@ -678,6 +680,12 @@ def set_decode_prices(prices, device=0):
     """pin `device`'s prices (4 floats), or restore the fitted defaults with None (hhuff_set_decode_prices)"""
     buf = None if prices is None else (ctypes.c_float * 4)(*[float(x) for x in prices])
     _check(lib().hhuff_set_decode_prices(device, buf), "hhuff_set_decode_prices")
+
+
+def set_edge_defer_min(n):
+    """batches of at least n strings defer their tiles' shared 16-B chunks to edge records and a fix-up kernel
+    (hhuff_set_edge_defer_min; default 2^21); returns the previous threshold"""
+    return int(lib().hhuff_set_edge_defer_min(int(n)))
 
 
 def set_decode_kernel(mode):

@@ -1158,6 +1158,8 @@ HHUFF_API int hhuff_set_decode_kernel(int mode) {
     return r < 0 ? arg_fail("decode kernel mode must be 0, 1 or 2") : r;
 }
 
+HHUFF_API uint32_t hhuff_set_edge_defer_min(uint32_t n) { return hhuff::set_edge_defer_min(n); }
+
 HHUFF_API int hhuff_grid_size(int device, int which) {
     DeviceGuard guard(device);
     if (guard.err != hipSuccess) return -1;

@@ -309,12 +309,14 @@ __device__ __forceinline__ void st_res(T* p, T v) {
 // global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
 // (Measured: batching the LDS reads of all chunks, or taking the edge bytes from the loaded registers,
 // made the c4 decode 3.5 % slower -- register pressure / code size in the 16-wave staged kernels.)
-template <int NCH>
+// SWAP: the LDS bytes are MSB-first words (the encode stage), byte-swapped in registers on the way out.
+template <int NCH, bool SWAP = false>
 __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds, uint32_t ospan,
                                             uint64_t keep_lo, uint64_t keep_hi, int lane) {
     for (uint32_t k = (uint32_t)lane * 16u; k < ospan; k += 64u * 16u) {
         const uint64_t g = gbase + k;
-        const uint4 v = *reinterpret_cast<const uint4*>(lds + k);
+        uint4 v = *reinterpret_cast<const uint4*>(lds + k);
+        if (SWAP) v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
         if (g >= keep_lo && g + 16 <= keep_hi) {
             st16_out(out + g, v);
         } else {  // a chunk shared with a neighbouring tile: only this tile's bytes (at most 10 stores)
@@ -325,7 +327,7 @@ __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t 
     }
 }
 
-// SWAP: the LDS bytes are MSB-first words (the encode stage), byte-swapped in registers on the way out.
+// (SWAP as region_copy)
 template <bool SWAP = false>
 __device__ __forceinline__ void region_copy_deferred(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds,
                                                      uint32_t ospan, uint64_t keep_lo, uint64_t keep_hi, int lane,
@@ -530,16 +532,16 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     uint32_t* s_lut = sm.lut;
     uint32_t* s_kinfo = sm.kinfo;
     uint32_t* s_ones = sm.ones;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t stride = (uint64_t)gridDim.x * WAVES * 64;
+    uint64_t base = ((uint64_t)blockIdx.x * WAVES + wave) * 64;
     load_dec_tables(s_lut, s_kinfo, s_ones, WAVES * 64);
     __syncthreads();
     const DecTables T{s_lut, s_kinfo, s_ones};
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint8_t* const buf = sm.buf[wave];
     const uint32_t bufa = lds_addr(buf);
     const bool region = A.in_len == nullptr && A.out_off == nullptr;
     const bool pairs = A.in_len != nullptr;
-    const uint64_t stride = (uint64_t)gridDim.x * WAVES * 64;
-    uint64_t base = ((uint64_t)blockIdx.x * WAVES + wave) * 64;
     if (base >= A.n) return;
 
     // per-tile layout: input span and output stage extent.  Per lane: the string and its stage offset;
@@ -2114,6 +2116,7 @@ __device__ __forceinline__ uint32_t plan_tile_strings(const uint32_t* __restrict
 // plan can pick (rec_cap records); the records of tiles that K does not make are cleared here, so
 // edge_fix_kernel reads all rec_cap of them
 __device__ __forceinline__ void pl_clear_spare_edges(EdgeRec* edges, uint64_t ntiles, uint64_t rec_cap) {
+    if (!edges) return;  // edges stored in the kernel
     const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t r = 2 * ntiles + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rec_cap; r += nth)
         edges[r].m = make_uint4(0u, 0u, 0u, 0u);
@@ -2266,8 +2269,11 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
             __asm__ volatile("" : "+v"(ns), "+v"(ne) : : "memory");
 #endif
             // byte-swapped on the way out; the (at most two) 16-B chunks shared with the neighbouring tiles
-            // are deferred to edge_fix_kernel
-            region_copy_deferred<true>(A.out, cur.a0, obuf, cur.span, cur.lo, cur.hi, lane, A.edges + 2 * t);
+            // are deferred to edge_fix_kernel, or stored by byte range here (no records: small batches)
+            if (A.edges)
+                region_copy_deferred<true>(A.out, cur.a0, obuf, cur.span, cur.lo, cur.hi, lane, A.edges + 2 * t);
+            else
+                region_copy<(STAGE + 1023) / 1024, true>(A.out, cur.a0, obuf, cur.span, cur.lo, cur.hi, lane);
 #if HHUFF_PL_EARLY
             // (the prefetch registers stay allocated across the copy: were they reused as its store data, the
             // next tile's loads into them would wait for those stores -- gfx950 orders no store-data reads)
@@ -2287,7 +2293,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
                 sink.init(A.out + cur.s);
                 ol = encode_core(GlobalSource{A.in, A.in_size}, cur.s, len, sink, s_enc);
             }
-            if (lane < 2) A.edges[2 * t + lane].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges
+            if (A.edges && lane < 2) A.edges[2 * t + lane].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges
         }
         if (own) finish_encode(A, (uint32_t)(cur.i0 + lane), len, ol);
         if (!have_next) break;
@@ -2595,7 +2601,10 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
             // plan, where the wait would cover the stores too)
             __asm__ volatile("" : "+v"(nxi.s), "+v"(nxi.e), "+v"(nxi.first), "+v"(nxi.raww) : : "memory");
 #ifndef HHUFF_X_FLAT_NOSTORE  // ablation (output wrong by design): no output stores
-            region_copy_deferred<true>(A.out, cur.ob, obuf, cur.ospan, cur.olo, cur.ohi, lane, A.edges + 2 * t);
+            if (A.edges)
+                region_copy_deferred<true>(A.out, cur.ob, obuf, cur.ospan, cur.olo, cur.ohi, lane, A.edges + 2 * t);
+            else
+                region_copy<1, true>(A.out, cur.ob, obuf, cur.ospan, cur.olo, cur.ohi, lane);
 #endif
             wave_lds_sync();
             PROF_MARK(5);
@@ -2626,7 +2635,7 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
                 }
                 ol = sink.count();
             }
-            if (lane < 2) A.edges[2 * t + lane].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges
+            if (A.edges && lane < 2) A.edges[2 * t + lane].m = make_uint4(0u, 0u, 0u, 0u);  // direct stores: no edges
             PROF_MARK(6);
         }
         if (own) A.out_len[i] = ol;
@@ -3885,7 +3894,13 @@ static hipError_t pool_alloc(void** p, uint64_t bytes, hipStream_t stream) {
 #ifndef HHUFF_DEFER_MIN
 #define HHUFF_DEFER_MIN (1u << 21)
 #endif
-constexpr uint32_t kDeferMin = HHUFF_DEFER_MIN;
+// hhuff_set_edge_defer_min (tests reach both ways with any batch size).  The proportional-lane encoder and
+// flatten use 1/32 of it: their tiles carry 2-3 KB of output each, so the fix-up is small next to the kernel,
+// and in-kernel edges measured c3 encode +0.5 %, c5 encode +0.3 %, flatten +0.8 % at 0.5-1M strings
+// (profiles/r05aj_edges_ab.jsonl); below 64K strings one launch matters more than that.
+static std::atomic<uint32_t> g_defer_min{HHUFF_DEFER_MIN};
+static uint32_t defer_min_pl() { return g_defer_min.load(std::memory_order_relaxed) >> 5; }
+uint32_t set_edge_defer_min(uint32_t n) { return g_defer_min.exchange(n); }
 static hipError_t alloc_edges(EdgeRec** p, uint32_t n, hipStream_t stream) {
     return pool_alloc((void**)p, edge_recs(n) * sizeof(EdgeRec), stream);
 }
@@ -4129,7 +4144,7 @@ static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint3
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n);
 #endif
     const int grid = grid_for(v, current_device(), n);
-    const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr && n >= kDeferMin;
+    const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr && n >= g_defer_min.load(std::memory_order_relaxed);
     if (v == kDecL) {  // mixed lengths: the device picks staged or stream (see below)
         prices_in_effect(current_device(), A.price);  // no GPU work: see calibrate_prices
         uint64_t* sel = nullptr;  // [0, 3 kSelBlocks): partial sums; then the verdict and the work counter
@@ -4286,12 +4301,13 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         const int g = grid_for(kEncP, current_device(), 0xFFFFFFFFu);
         const uint64_t want = (tiles + 15) / 16;
         const int grid = (int)(want < (uint64_t)g ? (want ? want : 1) : g);
-        const uint64_t recs = 2 * tiles;  // deferred edges: 2 per tile of the smallest K the plan can pick
-        hipError_t e = pool_alloc((void**)&A.edges, recs * sizeof(EdgeRec), stream);
+        const bool defer = n >= defer_min_pl();  // small batches: edges stored in the kernel, one launch
+        const uint64_t recs = defer ? 2 * tiles : 0;  // deferred edges: 2 per tile of the smallest K the plan can pick
+        hipError_t e = defer ? pool_alloc((void**)&A.edges, recs * sizeof(EdgeRec), stream) : hipSuccess;
         if (e != hipSuccess) return e;
         if (!sample) {
             hipLaunchKernelGGL(ENC_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)nullptr, recs);
-            return finish_deferred(out, A.edges, n, stream, nullptr, recs);
+            return defer ? finish_deferred(out, A.edges, n, stream, nullptr, recs) : hipGetLastError();
         }
         uint32_t* part = nullptr;
         e = pool_alloc((void**)&part, 6 * kPlBlocks * sizeof(uint32_t), stream);
@@ -4309,17 +4325,17 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
             if (e == hipSuccess) e = f;
         }
         if (e != hipSuccess) {
-            (void)hipFreeAsync(A.edges, stream);
+            if (defer) (void)hipFreeAsync(A.edges, stream);
             return e;
         }
-        return finish_deferred(out, A.edges, n, stream, nullptr, recs);
+        return defer ? finish_deferred(out, A.edges, n, stream, nullptr, recs) : hipSuccess;
     }
     int v = pick_encode(in_size, n);
 #ifndef HHUFF_ENC_TILES  // contiguous layout: length-sorted chunks (A/B builds -DHHUFF_ENC_TILES: 64-string tiles)
     if (v == kEncS && in_len == nullptr && out_off == nullptr) v = kEncO;
 #endif
     const int grid = grid_for(v, current_device(), n);
-    const bool defer = v != kEncD && in_len == nullptr && out_off == nullptr && n >= kDeferMin;
+    const bool defer = v != kEncD && in_len == nullptr && out_off == nullptr && n >= g_defer_min.load(std::memory_order_relaxed);
     if (defer) {
         hipError_t e = alloc_edges(&A.edges, n, stream);
         if (e != hipSuccess) return e;
@@ -5187,12 +5203,13 @@ hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* i
         const int g = grid_for(kFlatP, current_device(), 0xFFFFFFFFu);
         const uint64_t want = (tiles + 15) / 16;
         const int grid = (int)(want < (uint64_t)g ? (want ? want : 1) : g);
-        const uint64_t recs = 2 * tiles;  // deferred edges (see encode_pl_kernel)
-        hipError_t e = pool_alloc((void**)&A.edges, recs * sizeof(EdgeRec), stream);
+        const bool defer = n >= defer_min_pl();  // small batches: edges stored in the kernel, one launch
+        const uint64_t recs = defer ? 2 * tiles : 0;  // deferred edges (see encode_pl_kernel)
+        hipError_t e = defer ? pool_alloc((void**)&A.edges, recs * sizeof(EdgeRec), stream) : hipSuccess;
         if (e != hipSuccess) return e;
         if (!sample) {
             hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)nullptr, recs);
-            return finish_deferred(out, A.edges, n, stream, nullptr, recs);
+            return defer ? finish_deferred(out, A.edges, n, stream, nullptr, recs) : hipGetLastError();
         }
         uint32_t* part = nullptr;
         e = pool_alloc((void**)&part, 6 * kPlBlocks * sizeof(uint32_t), stream);
@@ -5209,10 +5226,10 @@ hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* i
             if (e == hipSuccess) e = f;
         }
         if (e != hipSuccess) {
-            (void)hipFreeAsync(A.edges, stream);
+            if (defer) (void)hipFreeAsync(A.edges, stream);
             return e;
         }
-        return finish_deferred(out, A.edges, n, stream, nullptr, recs);
+        return defer ? finish_deferred(out, A.edges, n, stream, nullptr, recs) : hipSuccess;
     }
     const int grid = grid_for(kFlatD, current_device(), n);
     hipLaunchKernelGGL(FLAT_D, dim3(grid), dim3(256), 0, stream, A);

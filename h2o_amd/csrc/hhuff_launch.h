@@ -135,4 +135,5 @@ int decode_prices_of(int device, float out[4], int calibrate);
 // pin the prices of `device` (in4 NULL: back to the fitted defaults); 0, -1 bad device, -2 bad value
 int set_decode_prices(int device, const float* in4);
 int set_decode_kernel(int mode);  // hhuff_set_decode_kernel: previous mode, -1 for a bad one
+uint32_t set_edge_defer_min(uint32_t n);  // hhuff_set_edge_defer_min: the previous threshold
 }  // namespace hhuff

@@ -1018,3 +1018,23 @@ def test_framing_vs_oracle(torch_cuda, oracle_codec, cfg, n, pb):
     np.testing.assert_array_equal(g_len, o_len)
     slots = b["off"][:n].astype(np.uint64) + 11 * np.arange(n, dtype=np.uint64)
     assert compact(g_out, slots, g_len) == compact(o_out, slots, o_len)
+
+
+@pytest.mark.parametrize("defer_min", [0, 0xFFFFFFFF])
+def test_edges_deferred_and_inline(torch_cuda, oracle_codec, defer_min):
+    """the tiles' shared 16-B output chunks both ways (hhuff_set_edge_defer_min): 0 defers them to edge records
+    and the merging fix-up kernel for every batch, 2^32 - 1 stores them in the codec kernels -- staged and sorted
+    encode, staged and stream decode, the proportional-lane encoder and the flatten kernel, with empty strings,
+    whole empty chunks, oversized chunks and ragged ends"""
+    from h2o_amd import codec
+
+    prev = codec.set_edge_defer_min(defer_min)
+    try:
+        for cfg, n, seed in [("c2", 30000, 11), ("c3", 12000, 12), ("c4", 30000, 13), ("c5", 3000, 14)]:
+            test_random_batches_vs_oracle(torch_cuda, oracle_codec, cfg, n, seed)
+        test_contiguous_encode_sorted_chunks_and_oversized(torch_cuda, oracle_codec)
+        test_contiguous_mixed_lengths_proportional_lanes(torch_cuda, oracle_codec)
+        for cfg, n, pb in [("c5", 5000, 7), ("c2", 20000, 5), ("c3", 8000, 3)]:
+            test_framing_vs_oracle(torch_cuda, oracle_codec, cfg, n, pb)
+    finally:
+        codec.set_edge_defer_min(prev)

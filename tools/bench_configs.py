@@ -22,6 +22,26 @@ sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 
 
+def timed_b2b(torch, fn, steps=20, warmup=3, reps=5):
+    """device time per call with `steps` calls enqueued back to back between one event pair (the median of `reps`
+    such runs): a server's sustained rate, without the gap an event pair around every call adds (2-4 us, which is
+    a tenth of a c2 call)"""
+    for _ in range(warmup):
+        fn()
+    t = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record()
+        for _ in range(steps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        t.append(a.elapsed_time(b) / steps)
+    t.sort()
+    return t[len(t) // 2]
+
+
 def timed(torch, fn, steps=20, warmup=3):
     for _ in range(warmup):
         fn()
