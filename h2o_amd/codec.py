@@ -684,7 +684,7 @@ def set_decode_prices(prices, device=0):
 
 def set_edge_defer_min(n):
     """batches of at least n strings defer their tiles' shared 16-B chunks to edge records and a fix-up kernel
-    (hhuff_set_edge_defer_min; default 2^21); returns the previous threshold"""
+    (hhuff_set_edge_defer_min; default 2^32 - 1: never); returns the previous threshold"""
     return int(lib().hhuff_set_edge_defer_min(int(n)))
 
 

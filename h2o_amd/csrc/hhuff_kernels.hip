@@ -309,6 +309,25 @@ __device__ __forceinline__ void st_res(T* p, T v) {
 // global bytes in [keep_lo, keep_hi); 16-byte stores for whole chunks, byte stores at the edges.
 // (Measured: batching the LDS reads of all chunks, or taking the edge bytes from the loaded registers,
 // made the c4 decode 3.5 % slower -- register pressure / code size in the 16-wave staged kernels.)
+#ifndef HHUFF_EDGE_BYTES
+// 1: a tile's two shared 16-B chunks are stored one byte a lane (lanes 0-15 the first chunk, 16-31 the last: one
+// LDS byte read and one byte-store instruction a tile); 0: by byte range from the chunk's registers (<= 10
+// predicated stores each)
+#define HHUFF_EDGE_BYTES 1
+#endif
+// The region's two edge chunks (first and last; the whole region is [gbase, gbase + ospan), gbase 16-aligned),
+// one byte a lane: lanes 0-15 the first chunk, lanes 16-31 the last, each storing its byte when it lies in
+// [keep_lo, keep_hi) and its chunk is partial (a full chunk went out whole).
+template <bool SWAP>
+__device__ __forceinline__ void edge_bytes(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds, uint32_t ospan,
+                                           uint64_t keep_lo, uint64_t keep_hi, int lane) {
+    if (ospan == 0 || lane >= 32) return;
+    const uint32_t kl = (ospan - 1u) & ~15u, b = (uint32_t)lane & 15u;
+    const uint32_t k = lane < 16 ? 0u : kl;
+    const uint64_t g = gbase + k, G = g + b;
+    const bool part = !(g >= keep_lo && g + 16 <= keep_hi);
+    if ((lane < 16 || kl != 0) && part && G >= keep_lo && G < keep_hi) out[G] = lds[k + (SWAP ? b ^ 3u : b)];
+}
 // SWAP: the LDS bytes are MSB-first words (the encode stage), byte-swapped in registers on the way out.
 template <int NCH, bool SWAP = false>
 __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds, uint32_t ospan,
@@ -319,12 +338,13 @@ __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t 
         if (SWAP) v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
         if (g >= keep_lo && g + 16 <= keep_hi) {
             st16_out(out + g, v);
-        } else {  // a chunk shared with a neighbouring tile: only this tile's bytes (at most 10 stores)
+        } else if (!HHUFF_EDGE_BYTES) {  // a chunk shared with a neighbouring tile: only this tile's bytes
             const uint32_t lo = keep_lo > g ? (uint32_t)min(keep_lo - g, (uint64_t)16) : 0u;
             const uint32_t hi = keep_hi > g ? (uint32_t)min(keep_hi - g, (uint64_t)16) : 0u;
             if (hi > lo) store_range16r(out + g, v, lo, hi);
         }
     }
+    if (HHUFF_EDGE_BYTES) edge_bytes<SWAP>(out, gbase, lds, ospan, keep_lo, keep_hi, lane);
 }
 
 // (SWAP as region_copy)
@@ -729,9 +749,12 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
 #endif
             if (PACKED) {
                 const uint64_t gb = G & ~15ull;
-                region_copy_deferred(A.out, gb, buf + c0 - ((uint32_t)G & 15u),
-                                     (uint32_t)(((G + T_run + 15u) & ~15ull) - gb), G, G + T_run, lane,
-                                     A.edges + 2 * (base >> 6));
+                const uint32_t ps = (uint32_t)(((G + T_run + 15u) & ~15ull) - gb);
+                if (A.edges)
+                    region_copy_deferred(A.out, gb, buf + c0 - ((uint32_t)G & 15u), ps, G, G + T_run, lane,
+                                         A.edges + 2 * (base >> 6));
+                else
+                    region_copy<(OUT_STAGE + 1023) / 1024>(A.out, gb, buf + c0 - ((uint32_t)G & 15u), ps, G, G + T_run, lane);
             } else if (region) {
                 if (A.edges)
                     region_copy_deferred(A.out, cur.obase(), obuf, cur.ospan, cur.olo(), cur.ohi(), lane,
@@ -1718,9 +1741,13 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
                 PROF_MARK(2);
                 PROF_MARK(3);
                 const uint64_t gb = G & ~15ull;
-                region_copy_deferred(A.out, gb, reinterpret_cast<const uint8_t*>(stage),
-                                     (uint32_t)(((G + T_run + 15u) & ~15ull) - gb), G, G + T_run, lane,
-                                     A.edges + 2 * (base >> 6));
+                const uint32_t ps = (uint32_t)(((G + T_run + 15u) & ~15ull) - gb);
+                if (A.edges)
+                    region_copy_deferred(A.out, gb, reinterpret_cast<const uint8_t*>(stage), ps, G, G + T_run, lane,
+                                         A.edges + 2 * (base >> 6));
+                else
+                    region_copy<(STAGE + 1023) / 1024>(A.out, gb, reinterpret_cast<const uint8_t*>(stage), ps, G, G + T_run,
+                                                       lane);
                 if (t.valid) {
                     A.pk_off[t.i] = (uint32_t)(G + place);
                     if (t.i == A.n - 1) A.pk_off[A.n] = (uint32_t)(G + place + keep);
@@ -2020,9 +2047,10 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
             const uint64_t g = (uint64_t)a0 + k;
             uint4* sp = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_out) + k);
             uint4 v = *sp;
-            *sp = make_uint4(0u, 0u, 0u, 0u);
-            v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
             const bool full = g >= lo && g + 16 <= hi;
+            // (a partial edge chunk stored one byte a lane below is zeroed there, after its bytes are read)
+            if (full || A.edges || !HHUFF_EDGE_BYTES) *sp = make_uint4(0u, 0u, 0u, 0u);
+            v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
             if (full) st16_out(A.out + g, v);
             if (k == 0 || k == kl) {
                 const uint32_t elo = lo > g ? (uint32_t)(lo - g) : 0u;
@@ -2031,9 +2059,18 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
                     EdgeRec* e = rec + (k == 0 ? 0 : 1);
                     e->v = v;
                     e->m = make_uint4((uint32_t)g, (uint32_t)(g >> 32), full ? 0u : elo, full ? 0u : ehi);
-                } else if (!full && ehi > elo) {  // small batches: the shared chunk's own bytes, now
+                } else if (!HHUFF_EDGE_BYTES && !full && ehi > elo) {  // small batches: the shared chunk's own bytes
                     store_range16r(A.out + g, v, elo, ehi);
                 }
+            }
+        }
+        if (HHUFF_EDGE_BYTES && !A.edges && t < 64u) {  // small batches: the two partial chunks, a byte a lane (wave 0)
+            const uint8_t* so = reinterpret_cast<const uint8_t*>(s_out);
+            edge_bytes<true>(A.out, a0, so, span, lo, hi, (int)t);
+            if (t < 32u && span != 0) {  // zero the bytes read (the chunk was left in place above when partial)
+                const uint32_t ke = t < 16u ? 0u : kl;
+                if (!((uint64_t)a0 + ke >= lo && (uint64_t)a0 + ke + 16 <= hi))
+                    reinterpret_cast<uint8_t*>(s_out)[ke + (t & 15u)] = 0;
             }
         }
         if (A.edges && t == 0 && (kl == 0 || span == 0)) rec[1].m = make_uint4(0u, 0u, 0u, 0u);  // one chunk, or none
@@ -3891,16 +3928,17 @@ static hipError_t pool_alloc(void** p, uint64_t bytes, hipStream_t stream) {
 // write a tile's shared chunks byte-exact themselves (store_range16r) and a leg is one launch: the fix-up launch
 // is a fixed ~5 us, which a 1M-string batch feels and a 16M one does not (there the in-kernel byte stores cost
 // more, DESIGN (e) round 4)
+// Edge records and edge_fix_kernel for batches of at least this many strings; below it the codec kernels store
+// their regions' shared 16-B chunks themselves, one byte a lane (edge_bytes).  Default: never deferred -- the
+// byte-lane edges measured c4 decode -5.5 %, c3 encode -5.3 %, c5 encode -5.6 %, flatten -6.6 %, c2 decode -9 %
+// against the records and the fix-up kernel (profiles/r05ao_edge_bytes_ab.jsonl).  hhuff_set_edge_defer_min
+// moves it (tests run both ways).
 #ifndef HHUFF_DEFER_MIN
-#define HHUFF_DEFER_MIN (1u << 21)
+#define HHUFF_DEFER_MIN 0xFFFFFFFFu
 #endif
-// hhuff_set_edge_defer_min (tests reach both ways with any batch size).  The proportional-lane encoder and
-// flatten use 1/32 of it: their tiles carry 2-3 KB of output each, so the fix-up is small next to the kernel,
-// and in-kernel edges measured c3 encode +0.5 %, c5 encode +0.3 %, flatten +0.8 % at 0.5-1M strings
-// (profiles/r05aj_edges_ab.jsonl); below 64K strings one launch matters more than that.
 static std::atomic<uint32_t> g_defer_min{HHUFF_DEFER_MIN};
-static uint32_t defer_min_pl() { return g_defer_min.load(std::memory_order_relaxed) >> 5; }
 uint32_t set_edge_defer_min(uint32_t n) { return g_defer_min.exchange(n); }
+static bool defer_edges(uint32_t n) { return n >= g_defer_min.load(std::memory_order_relaxed); }
 static hipError_t alloc_edges(EdgeRec** p, uint32_t n, hipStream_t stream) {
     return pool_alloc((void**)p, edge_recs(n) * sizeof(EdgeRec), stream);
 }
@@ -4144,7 +4182,7 @@ static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint3
     const int v = pick_decode(sel_bytes ? sel_bytes : in_size, n);
 #endif
     const int grid = grid_for(v, current_device(), n);
-    const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr && n >= g_defer_min.load(std::memory_order_relaxed);
+    const bool defer = (v == kDecS || v == kDecL) && in_len == nullptr && out_off == nullptr && defer_edges(n);
     if (v == kDecL) {  // mixed lengths: the device picks staged or stream (see below)
         prices_in_effect(current_device(), A.price);  // no GPU work: see calibrate_prices
         uint64_t* sel = nullptr;  // [0, 3 kSelBlocks): partial sums; then the verdict and the work counter
@@ -4301,7 +4339,7 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
         const int g = grid_for(kEncP, current_device(), 0xFFFFFFFFu);
         const uint64_t want = (tiles + 15) / 16;
         const int grid = (int)(want < (uint64_t)g ? (want ? want : 1) : g);
-        const bool defer = n >= defer_min_pl();  // small batches: edges stored in the kernel, one launch
+        const bool defer = defer_edges(n);  // else edges stored in the kernel, one launch
         const uint64_t recs = defer ? 2 * tiles : 0;  // deferred edges: 2 per tile of the smallest K the plan can pick
         hipError_t e = defer ? pool_alloc((void**)&A.edges, recs * sizeof(EdgeRec), stream) : hipSuccess;
         if (e != hipSuccess) return e;
@@ -4335,7 +4373,7 @@ hipError_t launch_encode(const uint8_t* in, uint64_t in_size, const uint32_t* in
     if (v == kEncS && in_len == nullptr && out_off == nullptr) v = kEncO;
 #endif
     const int grid = grid_for(v, current_device(), n);
-    const bool defer = v != kEncD && in_len == nullptr && out_off == nullptr && n >= g_defer_min.load(std::memory_order_relaxed);
+    const bool defer = v != kEncD && in_len == nullptr && out_off == nullptr && defer_edges(n);
     if (defer) {
         hipError_t e = alloc_edges(&A.edges, n, stream);
         if (e != hipSuccess) return e;
@@ -5142,14 +5180,15 @@ hipError_t launch_decode_packed(const uint8_t* in, uint64_t in_size, const uint3
     if (mean > 128) return pack_via_scratch(true, in, in_size, in_off, n, is_name_bits, out, pk_off, out_len, status, stream);
     DecArgs A{in, in_size, in_off, nullptr, n, is_name_bits, out, nullptr, out_len, status, nullptr, nullptr, nullptr, pk_off, nullptr};
     const int v = mean <= 40 ? kDecSP : kDecLP;
-    hipError_t e = alloc_edges(&A.edges, n, stream);
+    const bool defer = defer_edges(n);
+    hipError_t e = defer ? alloc_edges(&A.edges, n, stream) : hipSuccess;
     if (e != hipSuccess) return e;
     const int grid = grid_for(v, current_device(), n);
     if (v == kDecSP)
         hipLaunchKernelGGL(DEC_SP, dim3(grid), dim3(kDecSWaves * 64), 0, stream, A);
     else
         hipLaunchKernelGGL(DEC_LP, dim3(grid), dim3(384), 0, stream, A);
-    return finish_deferred(out, A.edges, n, stream);
+    return defer ? finish_deferred(out, A.edges, n, stream) : hipGetLastError();
 }
 
 hipError_t launch_encode_packed(const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n, uint8_t* out,
@@ -5159,14 +5198,15 @@ hipError_t launch_encode_packed(const uint8_t* in, uint64_t in_size, const uint3
     if (mean > 120) return pack_via_scratch(false, in, in_size, in_off, n, nullptr, out, pk_off, out_len, status, stream);
     EncArgs A{in, in_size, in_off, nullptr, n, out, nullptr, out_len, status, nullptr, pk_off};
     const int v = mean <= 52 ? kEncSP : kEncLP;
-    hipError_t e = alloc_edges(&A.edges, n, stream);
+    const bool defer = defer_edges(n);
+    hipError_t e = defer ? alloc_edges(&A.edges, n, stream) : hipSuccess;
     if (e != hipSuccess) return e;
     const int grid = grid_for(v, current_device(), n);
     if (v == kEncSP)
         hipLaunchKernelGGL(ENC_SP, dim3(grid), dim3(kEncSWaves * 64), 0, stream, A);
     else
         hipLaunchKernelGGL(ENC_LP, dim3(grid), dim3(512), 0, stream, A);
-    return finish_deferred(out, A.edges, n, stream);
+    return defer ? finish_deferred(out, A.edges, n, stream) : hipGetLastError();
 }
 
 static hipError_t pack_via_scratch(bool dec, const uint8_t* in, uint64_t in_size, const uint32_t* in_off, uint32_t n,
@@ -5203,7 +5243,7 @@ hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* i
         const int g = grid_for(kFlatP, current_device(), 0xFFFFFFFFu);
         const uint64_t want = (tiles + 15) / 16;
         const int grid = (int)(want < (uint64_t)g ? (want ? want : 1) : g);
-        const bool defer = n >= defer_min_pl();  // small batches: edges stored in the kernel, one launch
+        const bool defer = defer_edges(n);  // else edges stored in the kernel, one launch
         const uint64_t recs = defer ? 2 * tiles : 0;  // deferred edges (see encode_pl_kernel)
         hipError_t e = defer ? pool_alloc((void**)&A.edges, recs * sizeof(EdgeRec), stream) : hipSuccess;
         if (e != hipSuccess) return e;

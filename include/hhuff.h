@@ -562,10 +562,10 @@ int hhuff_grid_size(int device, int which /* 0 decode, 1 encode */);
  * 40 B; 2 the segment kernel for every contiguous batch.  The HHUFF_DEC_SEG environment variable sets the start
  * value.  Returns the previous mode, or HHUFF_EINVAL. */
 int hhuff_set_decode_kernel(int mode);
-/* Batches of at least `n` strings (default 2^21; n / 32 for contiguous encodes and framings of a mean of 53 B or
- * more) leave the 16-B output chunks their tiles share to edge records and a fix-up kernel launched behind the
- * codec kernel; smaller batches store those chunks in the codec kernel (one launch).  Process-wide; the results
- * are the same, only the speed differs.  Returns the previous value. */
+/* Batches of at least `n` strings leave the 16-B output chunks their tiles share to edge records and a fix-up
+ * kernel launched behind the codec kernel; smaller batches store those chunks in the codec kernel (one launch).
+ * Default 0xFFFFFFFF: every batch stores them in the kernel.  Process-wide; the results are the same, only the
+ * speed differs.  Returns the previous value. */
 uint32_t hhuff_set_edge_defer_min(uint32_t n);
 /* Return the memory the library's stream-ordered pool on the caller's current device keeps between calls
  * (batch workspaces, edge records) to the driver.  Synchronises the device first.  HHUFF_OK or an error. */

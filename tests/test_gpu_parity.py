@@ -1023,7 +1023,7 @@ def test_framing_vs_oracle(torch_cuda, oracle_codec, cfg, n, pb):
 @pytest.mark.parametrize("defer_min", [0, 0xFFFFFFFF])
 def test_edges_deferred_and_inline(torch_cuda, oracle_codec, defer_min):
     """the tiles' shared 16-B output chunks both ways (hhuff_set_edge_defer_min): 0 defers them to edge records
-    and the merging fix-up kernel for every batch, 2^32 - 1 stores them in the codec kernels -- staged and sorted
+    and the fix-up kernel for every batch, 2^32 - 1 (the default) stores them in the codec kernels -- staged and sorted
     encode, staged and stream decode, the proportional-lane encoder and the flatten kernel, with empty strings,
     whole empty chunks, oversized chunks and ragged ends"""
     from h2o_amd import codec

@@ -196,3 +196,17 @@ def test_packed_c4_full_size(torch_cuda):
     got = d_out[torch.repeat_interleave(d_off[:-1].to(torch.int64) & 0xFFFFFFFF, dk) + drel]
     exp = b["data"][torch.repeat_interleave(b["off"][:-1][ok], dk) + drel]
     assert bool((got == exp).all())
+
+
+def test_packed_edges_deferred(torch_cuda, oracle_codec):
+    """the packed kernels with their shared 16-B chunks deferred to edge records and edge_fix_kernel
+    (hhuff_set_edge_defer_min(0)); the default stores them in the kernels, one byte a lane"""
+    from h2o_amd import codec
+
+    prev = codec.set_edge_defer_min(0)
+    try:
+        for cfg, n, seed in [("c2", 20000, 11), ("c4", 20000, 13), ("c3", 8000, 12)]:
+            test_packed_vs_oracle(torch_cuda, oracle_codec, cfg, n, seed)
+        test_packed_tiles_past_the_stage(torch_cuda, oracle_codec)
+    finally:
+        codec.set_edge_defer_min(prev)
