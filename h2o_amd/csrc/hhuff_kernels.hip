@@ -4958,7 +4958,9 @@ __device__ __forceinline__ void sys_poll(const void* pa, uint64_t ma, const void
 }
 
 // (The service's strings measured faster on the candidate chain than on split_decode_wave: 48 B, 3.0 against
-// 7.6 us from input to coded, profiles/r04pq_per_string_ab.jsonl.)
+// 7.6 us from input to coded, profiles/r04pq_per_string_ab.jsonl; and than lane 0 alone running the staged
+// kernels' lane decoder: 8,284 against 7,280 shader cycles at the full 2.4 GHz clock, HHUFF_SVC_CLK stamps,
+// profiles/r05as_per_string_clk.jsonl.)
 template <int NC, bool JUMP = false>
 __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots, SvcCtrl* __restrict__ ctrl,
                                                      uint64_t idle_ticks, uint64_t max_ticks) {
@@ -5034,6 +5036,9 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
             }
             wave_lds_sync();
             const uint32_t t_data = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#ifdef HHUFF_SVC_CLK
+            const uint64_t c_data = __builtin_amdgcn_s_memtime();
+#endif
             const uint8_t* in = reinterpret_cast<const uint8_t*>(s_in);
             uint32_t ol, st = 0;
             if (op == 1u) {
@@ -5050,6 +5055,9 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
                           : kStatusFail;
             }
             const uint32_t t_coded = (uint32_t)__builtin_amdgcn_s_memrealtime();
+#ifdef HHUFF_SVC_CLK
+            const uint64_t c_coded = __builtin_amdgcn_s_memtime();
+#endif
             const uint32_t n = ol == kFailLen ? 0u : ol;
             // the output as tagged 16-B chunks and then the result chunk, no wait between them (SvcSlot)
             for (uint32_t k = lane; 12u * k < n; k += 64u) {  // encode's stage holds MSB-first words
@@ -5059,7 +5067,11 @@ __global__ __launch_bounds__(64) void service_kernel(SvcSlot* __restrict__ slots
                             op == 1u ? bswap32(c) : c);
             }
             if (lane == 0) {
+#ifdef HHUFF_SVC_CLK  // diagnostic builds: the 4th stamp is t_coded + the shader-clock cycles of the coding
+                sys_store16(&sl->t_seen, t_seen, t_data, t_coded, t_coded + (uint32_t)(c_coded - c_data));
+#else
                 sys_store16(&sl->t_seen, t_seen, t_data, t_coded, (uint32_t)__builtin_amdgcn_s_memrealtime());
+#endif
                 sys_store(&ctrl->last[g], t_seen);
                 sys_store16(&sl->done, r, ol, st, 0u);
             }
