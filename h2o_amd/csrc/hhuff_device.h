@@ -901,6 +901,40 @@ __device__ __forceinline__ uint32_t chunk_code_bits_v2(const uint32_t* stage, ui
     return tb + bulk + masked(jl, active && (end & 3u) != 0 && jl >= jf);  // + tail
 }
 
+// The same count from a byte table of code lengths (nb[0..255]; nb[256] = 0 for the bytes outside the string):
+// an ASCII byte's entry sits in LDS dwords 8..31, each on its own bank, so a wave's lookups meet no bank
+// conflict (the .y word of the {code, nbits} table puts 96 ASCII entries on 16 banks: ~3.5 cycles a lane group).
+__device__ __forceinline__ uint32_t chunk_code_bits_nb(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
+                                                       bool active, const uint8_t* __restrict__ nb) {
+    const uint32_t end = start + len;
+    const uint32_t a0 = start & ~3u;
+    const uint32_t ndw = active ? (end - a0 + 3u) >> 2 : 0u;
+    const uint32_t jf = (start & 3u) ? 1u : 0u;  // whole dwords: [jf, jl)
+    const uint32_t jl = active ? (end - a0) >> 2 : 0u;
+    const uint32_t mfirst = 0xFFFFFFFFu << (8u * (start & 3u));
+    const uint32_t mlast = (uint32_t)(0xFFFFFFFFull >> ((32u - 8u * (end & 3u)) & 31u));
+    auto masked = [&](uint32_t j, bool on) {
+        uint32_t vm = j == 0 ? mfirst : 0xFFFFFFFFu;
+        vm &= (j + 1 == ndw) ? mlast : 0xFFFFFFFFu;
+        vm = on ? vm : 0u;
+        const uint32_t w = stage[min(a0 + 4u * j, last) >> 2] & vm;  // bytes outside: index 256 (one entry)
+        const uint32_t iw = ~vm & 0x01010101u;
+        return (uint32_t)nb[__builtin_amdgcn_perm(iw, w, 0x0C0C0400u)] + nb[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)] +
+               nb[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)] + nb[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)];
+    };
+    uint32_t tb = masked(0, active && jf != 0);  // head
+    const uint32_t* sw = stage + (a0 >> 2);
+    const uint32_t jlast = (last >> 2) - (a0 >> 2);
+    const uint32_t jend = wave_max_u32(jl);
+    uint32_t bulk = 0;
+    for (uint32_t j = 0; j < jend; ++j) {
+        const uint32_t w = sw[min(j, jlast)];
+        const uint32_t n = (uint32_t)nb[w & 0xFFu] + nb[(w >> 8) & 0xFFu] + nb[(w >> 16) & 0xFFu] + nb[w >> 24];
+        bulk += (j >= jf && j < jl) ? n : 0u;
+    }
+    return tb + bulk + masked(jl, active && (end & 3u) != 0 && jl >= jf);  // + tail
+}
+
 // Code bits of the stage bytes [start, start + len) (pass 1 of the proportional-lane encode).
 __device__ __forceinline__ uint32_t chunk_code_bits(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
                                                     bool active, const uint2* __restrict__ enc, uint32_t jmax) {

@@ -2159,6 +2159,9 @@ __device__ __forceinline__ void pl_clear_spare_edges(EdgeRec* edges, uint64_t nt
         edges[r].m = make_uint4(0u, 0u, 0u, 0u);
 }
 
+#ifndef HHUFF_NB8  // pass 1 of the proportional-lane kernels counts with a byte table of code lengths
+#define HHUFF_NB8 1
+#endif
 #ifndef HHUFF_PL_EARLY
 // 1: the next span committed and the next offsets waited for before the tile's stores (with the clamped,
 // unconditional offset loads: c5 encode 0.331 -> 0.320 ms, c3 0.226 -> 0.222, profiles/r04ac_pl_ab.log)
@@ -2172,11 +2175,13 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
         uint32_t in[WAVES][STAGE / 4];
         uint32_t out[WAVES][STAGE / 4 + 4];
         uint32_t lmap[WAVES][64];
+        uint8_t nb[272];  // code lengths for pass 1 (chunk_code_bits_nb); 256: outside the share
     };
     __shared__ Smem sm;
     __shared__ uint32_t s_k;
     for (uint32_t k = threadIdx.x; k < 512; k += WAVES * 64)
         sm.enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
+    for (uint32_t k = threadIdx.x; k < 272; k += WAVES * 64) sm.nb[k] = k < 256 ? (uint8_t)g_enc_nbits[k] : (uint8_t)0;
     if (kplan && threadIdx.x < 64) {  // tile size from encode_plan_kernel's samples (K is then its ceiling)
         const uint32_t k = plan_tile_strings(kplan, K);
         if (threadIdx.x == 0) s_k = k;
@@ -2278,7 +2283,11 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
             bool sfail = false;
             wave_lds_sync();
             if (__any(multi && big)) {  // pass 1: code bits of every share, then starting bits and totals
+#if HHUFF_NB8
+                const uint32_t b = chunk_code_bits_nb(stage, last, cs, clen, big && multi && clen != 0, sm.nb);
+#else
                 const uint32_t b = chunk_code_bits_v2(stage, last, cs, clen, big && multi && clen != 0, s_enc);
+#endif
                 const uint32_t x = wave_excl_scan(b, lane);
                 const uint32_t xs = (uint32_t)__shfl((int)x, (int)Lj, 64);
                 const uint32_t xe = (uint32_t)__shfl((int)(x + b), (int)(Lj + gj - 1), 64);
@@ -2488,11 +2497,13 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
         uint32_t in[WAVES][STAGE / 4];
         uint32_t out[WAVES][OSTAGE / 4 + 4];
         uint32_t lmap[WAVES][64];
+        uint8_t nb[272];  // code lengths for pass 1 (chunk_code_bits_nb)
     };
     __shared__ Smem sm;
     __shared__ uint32_t s_k;
     for (uint32_t k = threadIdx.x; k < 512; k += WAVES * 64)
         sm.enc[k] = k < 256 ? make_uint2(g_enc_code[k], g_enc_nbits[k]) : make_uint2(0u, 0u);
+    for (uint32_t k = threadIdx.x; k < 272; k += WAVES * 64) sm.nb[k] = k < 256 ? (uint8_t)g_enc_nbits[k] : (uint8_t)0;
     if (kplan && threadIdx.x < 64) {  // tile size from encode_plan_kernel's samples (as encode_pl_kernel)
         const uint32_t k = plan_tile_strings(kplan, K);
         if (threadIdx.x == 0) s_k = k;
@@ -2605,7 +2616,11 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
 #ifdef HHUFF_X_FLAT_NOCOUNT  // ablation (output wrong by design): no counting pass, every share 6 bits a byte
             const uint32_t b = ok && !rj ? 6u * clen : 0u;
 #else
+#if HHUFF_NB8
+            const uint32_t b = chunk_code_bits_nb(stage, last, cs, clen, ok && !rj && clen != 0, sm.nb);
+#else
             const uint32_t b = chunk_code_bits_v2(stage, last, cs, clen, ok && !rj && clen != 0, s_enc);
+#endif
 #endif
             PROF_MARK(2);
             const uint32_t x = wave_excl_scan(b, lane);
