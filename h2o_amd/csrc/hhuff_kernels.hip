@@ -457,6 +457,8 @@ struct DecArgs {
     // with gate: the staged / stream prices select_verdict uses, ps per string and per (tile-padded) byte --
     // the fitted defaults, or the device's calibration (calibrate_prices)
     float price[4] = {40.0f, 1.07f, 184.0f, 1.15f};
+    // stream kernel: strings a wave takes from the batch counter at a time (stream_claim)
+    uint32_t claim = 64;
 };
 
 __device__ __forceinline__ void load_dec_tables(uint32_t* s_lut, uint32_t* s_kinfo, uint32_t* s_ones, int nthreads) {
@@ -1313,7 +1315,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
             if (bnext >= bend) {
                 if (qdone) break;
                 uint64_t b = 0;
-                if (lane == 0) b = atomicAdd(counter, 64ull);
+                if (lane == 0) b = atomicAdd(counter, (unsigned long long)A.claim);
                 b = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
                 if (b >= nwork) {
@@ -1321,7 +1323,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                     break;
                 }
                 bnext = b;
-                bend = min(b + 64u, nwork);
+                bend = min(b + A.claim, nwork);
             }
             const uint32_t rank = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
@@ -3902,6 +3904,18 @@ __global__ __launch_bounds__(64) void decode_select_kernel(DecArgs A, uint64_t* 
     }
 }
 
+// The stream kernel's claim: about HHUFF_STREAM_CLAIM_BYTES of input a wave, 64 to 256 strings.  Every claim is
+// one atomic on the batch counter, and waves wait for it: c3 (89-B mean) decodes 6.7 % faster taking 128
+// strings a claim instead of 64, while c5 (~400 B) loses 1 % at 128 and 24 % at 256 to the grid's tail
+// (profiles/r05az_stream_claim_ab.jsonl).
+#ifndef HHUFF_STREAM_CLAIM_BYTES
+#define HHUFF_STREAM_CLAIM_BYTES 11520u
+#endif
+static uint32_t stream_claim(uint64_t in_size, uint32_t n) {
+    const uint64_t mean = n ? std::max<uint64_t>(in_size / n, 1) : 1;
+    const uint64_t c = HHUFF_STREAM_CLAIM_BYTES / mean;
+    return c >= 256 ? 256u : c >= 192 ? 192u : c >= 128 ? 128u : 64u;
+}
 static int pick_decode(uint64_t in_size, uint32_t n) {
     const uint64_t mean = n ? in_size / n : 0;  // in_size bounds the bytes the batch can address
     if (mean <= 40) return kDecS;
@@ -4025,6 +4039,7 @@ static void calibrate_prices(int dev) {
              hipStreamSynchronize(s) == hipSuccess;
         DecArgs A{in, (uint64_t)kN[p] * kL[p], off, nullptr, kN[p], nullptr, out, nullptr, olen, st,
                   nullptr, nullptr, nullptr, nullptr, nullptr};
+        A.claim = stream_claim((uint64_t)kN[p] * kL[p], kN[p]);
         for (int k = 0; ok && k < 2; ++k) {
             float best = 1e30f;
             for (int r = 0; ok && r < 4; ++r) {
@@ -4187,6 +4202,7 @@ static hipError_t launch_sorted_decode(DecArgs A, uint32_t n, uint8_t* out, hipS
 
 static hipError_t launch_decode_kernels(DecArgs A, uint64_t in_size, const uint32_t* in_len, uint32_t n, uint8_t* out,
                                         const uint32_t* out_off, hipStream_t stream, uint64_t sel_bytes) {
+    A.claim = stream_claim(sel_bytes ? sel_bytes : in_size, n);
     if (use_seg(sel_bytes ? sel_bytes : in_size, n, in_len, out_off)) return launch_seg(A, in_size, n, out, stream);
     if (in_len == nullptr && out_off == nullptr && sorted_decode_on() &&
         pick_decode(sel_bytes ? sel_bytes : in_size, n) == kDecS)
