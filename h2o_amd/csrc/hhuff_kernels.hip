@@ -3726,11 +3726,13 @@ __global__ __launch_bounds__(WAVES * 64) void decode_seg_kernel(DecArgs A, const
 #define HHUFF_RK_W 16
 #endif
 #ifndef HHUFF_DECT  // stream decode: waves per block, window dwords, output bytes per lane
-// (6 waves of 24-dword windows: c3 -2.2 %, c5 -1.3 % against 8 x 16; 6 x 16 and 4 x 32 lose on c5 or c3,
-// 12 and 16 waves lose on both: profiles/r04k_stream_shapes.log, profiles/r04_ab_runs.log t12 / t16b)
-#define HHUFF_DECT_W 6
-#define HHUFF_DECT_NW 24
-#define HHUFF_DECT_OUT 160
+// 8 waves of 20-dword windows (the most the LDS holds beside the window table at these windows): against the
+// round-4 shape of 6 x 24, c3 0.274 -> 0.244 ms, c5 0.436 -> 0.400 once the claims take ~11.5 KB each (9 or 10
+// waves of 16-dword windows: c3 level, c5 +9 %; profiles/r05be_stream_shape_ab.jsonl).  Round 4, with
+// 64-string claims, had 6 x 24 ahead of 8 x 16 (profiles/r04k_stream_shapes.log).
+#define HHUFF_DECT_W 8
+#define HHUFF_DECT_NW 20
+#define HHUFF_DECT_OUT 144
 #endif
 #ifdef HHUFF_STREAM_RK
 constexpr int kDecTWaves = HHUFF_RK_W;
