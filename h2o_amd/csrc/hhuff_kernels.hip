@@ -3908,10 +3908,10 @@ __global__ __launch_bounds__(64) void decode_select_kernel(DecArgs A, uint64_t* 
 
 // The stream kernel's claim: about HHUFF_STREAM_CLAIM_BYTES of input a wave, 64 to 256 strings.  Every claim is
 // one atomic on the batch counter, and waves wait for it: c3 (89-B mean) decodes 6.7 % faster taking 128
-// strings a claim instead of 64, while c5 (~400 B) loses 1 % at 128 and 24 % at 256 to the grid's tail
-// (profiles/r05az_stream_claim_ab.jsonl).
+// strings a claim instead of 64 (6 waves a CU), 2 % faster again at 256 with 8 waves, while c5 (~400 B) loses
+// 1 % at 128 and 24 % at 256 to the grid's tail (profiles/r05az_stream_claim_ab.jsonl, r05bg_stream_claim8_ab.jsonl).
 #ifndef HHUFF_STREAM_CLAIM_BYTES
-#define HHUFF_STREAM_CLAIM_BYTES 11520u
+#define HHUFF_STREAM_CLAIM_BYTES 23040u
 #endif
 static uint32_t stream_claim(uint64_t in_size, uint32_t n) {
     const uint64_t mean = n ? std::max<uint64_t>(in_size / n, 1) : 1;
