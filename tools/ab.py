@@ -39,6 +39,9 @@ def run(names, cfg="c4", rounds=5, steps=10):
     synth.CONFIGS.setdefault("c3hi", dict(n=405000, lengths=("zipf", 97, 512), alphabet="header"))
     synth.CONFIGS.setdefault("c3hid", dict(n=405000, lengths=("zipf_desc", 97, 512), alphabet="header"))
     synth.CONFIGS.setdefault("u250", dict(n=405000, lengths=("uniform", 250, 250), alphabet="header"))
+    # mixed-length batches near the staged / stream boundary (the select test's two distributions)
+    synth.CONFIGS.setdefault("m120", dict(n=1 << 20, lengths=("uniform", 110, 130), alphabet="header"))
+    synth.CONFIGS.setdefault("m60", dict(n=1 << 20, lengths=("uniform", 40, 100), alphabet="header"))
     for L in (64, 80, 96, 120, 200, 400):  # fixed lengths at the c3 scale: what length-sorted tiles could reach
         synth.CONFIGS.setdefault("u%d" % L, dict(n=1 << 20, lengths=("uniform", L, L), alphabet="header"))
     torch.cuda.set_device(0)
