@@ -472,7 +472,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_rk_kernel(DecArgs A,
         const bool fin = busy && end <= kFinal;
         int32_t q = pm >> 5;
         uint32_t x0 = st[q], x1 = st[q + 1], x2 = st[q + 2];
-        uint32_t accb = 0, acc1 = 0, acc2 = 0, accl = 0, parked = busy ? 0u : 1u;
+        uint32_t accb = 0, acc1 = 0, accl = 0, parked = busy ? 0u : 1u;
         uint32_t made = 0;
         int32_t lim = busy ? min(end - 26, kLimW) : (int32_t)0x80000000;
         auto advance = [&](int32_t cons) {
