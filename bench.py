@@ -100,6 +100,19 @@ def synth_n(config):
     return synth.CONFIGS[config]["n"]
 
 
+LAUNCHER_ENV = ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+                "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT")
+
+
+def child_env(env):
+    """the environment of a PMC child: the parent's, minus everything a launcher (torch.distributed.run) set
+    for the parent's rank -- WORLD_SIZE / RANK / MASTER_* / TORCHELASTIC_* -- so that the child is a world of one
+    that never joins (or waits on) the parent's process group; TMPDIR=/tmp for rocprofv3"""
+    e = {k: v for k, v in env.items() if k not in LAUNCHER_ENV and not k.startswith("TORCHELASTIC_")}
+    e["TMPDIR"] = "/tmp"
+    return e
+
+
 def pmc_passes(args, config=None, groups=None, n=None):
     """Per-launch PMC counters of each hhuff kernel: one rocprofv3 run per counter group (FETCH_SIZE,
     WRITE_SIZE, the SQ group, GRBM_GUI_ACTIVE) over this script as a child on `config` (default: the bench's
@@ -126,7 +139,7 @@ def pmc_passes(args, config=None, groups=None, n=None):
         try:
             subprocess.run([exe, "--pmc"] + list(group) + ["--output-format", "csv", "-d", d, "-o", "pmc", "--"] + child,
                            check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                           env=dict(os.environ, TMPDIR="/tmp"))
+                           env=child_env(os.environ))
             for root, _, files in os.walk(d):
                 for f in files:
                     if f.endswith("counter_collection.csv"):
@@ -269,12 +282,15 @@ def main():
         import torch
         return torch.cuda.device_count()
 
-    mode, world = launch_plan(args.gpus, os.environ, backend, _count)
+    if args.pmc_child:  # a profiling child is a world of one whatever its environment says: no process group
+        mode, world = "rank", 1
+    else:
+        mode, world = launch_plan(args.gpus, os.environ, backend, _count)
     if mode == "spawn":
         sys.exit(spawn_ranks(world, sys.argv[1:]))
     args.gpus = world
     pmc, pmc_cfg = {}, {}
-    rank = int(os.environ.get("RANK", "0"))
+    rank = 0 if args.pmc_child else int(os.environ.get("RANK", "0"))
     if not args.pmc_child and not args.no_traffic and rank == 0:
         # child processes; this process has not touched the GPU yet.  N > 1: rank 0 profiles one shard's worth
         # of the batch (N / world strings) on its GPU while the other ranks wait in the rendezvous
@@ -287,16 +303,19 @@ def main():
     from h2o_amd import codec, synth
     from h2o_amd import dist as hd
 
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.pmc_child else int(os.environ.get("LOCAL_RANK", "0"))
     # a process group for N > 1, or (--force-pg) for a launcher-started world of one: the RCCL init, the
     # device-tensor exchange and the MAX all_reduce then run exactly as on an 8-GPU node
-    pg = world > 1 or (args.force_pg and "WORLD_SIZE" in os.environ)
+    pg = not args.pmc_child and (world > 1 or (args.force_pg and "WORLD_SIZE" in os.environ))
     if pg:
         torch.cuda.set_device(local % torch.cuda.device_count())
+        # rank 0 runs its PMC passes (child processes, minutes at full size) before it joins: the others wait
+        import datetime
+        tmo = datetime.timedelta(minutes=30)
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     else:
         torch.cuda.set_device(0)
     codec.lib()
@@ -732,7 +751,9 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, re
                 link = {"h2d_bytes": h2d, "d2h_bytes": d2h,
                         "d2h_bytes_with_offsets": d2h + 5 * n + 4 + 4 * n_ok + 4}
     os.environ.pop("HHUFF_HOST_COPY", None)
-    best = min(("pinned", "pinned_concurrent", "packed", "packed_concurrent"), key=lambda k: res[k])
+    # value: the slot-layout pinned path, the same definition as rounds 1-4 (out_off, out_len and status all
+    # returned); the packed zero-copy legs, which return less, are reported beside it (packed_*_value)
+    best = min(("pinned", "pinned_concurrent"), key=lambda k: res[k])
     t = res[best]
     return {"value": round(P / GIB / t, 3), "unit": "GiB/s", "ms_per_step": round(t * 1e3, 3),
             "best": best,
@@ -748,13 +769,14 @@ def host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch, re
             "pinned_dma_ms_per_step": round(res["pinned_dma"] * 1e3, 3),
             "pageable_value": round(P / GIB / res["pageable"], 3),
             "pageable_ms_per_step": round(res["pageable"] * 1e3, 3),
+            "best_packed": round(P / GIB / min(res["packed"], res["packed_concurrent"]), 3),
             "note": "strings start and end in host memory; hhuff_{encode,decode}_batch_host_pipelined: pinned caller "
                     "buffers are read and written by the kernels in place (zero copy), pinned_dma is the chunked DMA "
                     "pipeline on the same buffers (64 MiB chunks, 3 streams), pageable buffers go through it with "
                     "host staging; packed: hhuff_{encode,decode}_batch_host_packed on the pinned buffers (zero copy, "
                     "tile-packed outputs: only output bytes cross the link; out_len and the decode status returned, "
                     "positions implied by them; packed_with_offsets: out_off and the encode status too); value: "
-                    "the fastest pinned step, its "
+                    "the fastest slot-layout pinned step (best_packed: the fastest packed step), its "
                     "encode and decode legs one after the other or on two host threads at once (`best`); "
                     "best of %d" % reps}
 
@@ -788,6 +810,15 @@ def pcie_rates(torch, nbytes=256 << 20, reps=3):
     del h1, h2, d1, d2
     torch.cuda.empty_cache()
     return out
+
+
+def cgroup_cpus():
+    """the CPUs this process's cgroup may use (cpu.max quota / period), or None when unlimited or unknown"""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(b, args):
@@ -828,7 +859,13 @@ def cpu_baseline(b, args):
     v, Ps = rate(m, threads, 5)
     m1 = min(m, 1 << 18)
     v1, P1 = rate(m1, 1, 5)
+    # every CPU of the affinity mask (one short burst; the host's CPUs serve other GPUs' jobs too,
+    # so this measures the box as shared -- its cgroup CPU quota is stated beside it)
+    va = rate(m, affinity, 3)[0] if affinity != threads else v
     return {"value": round(v, 4), "unit": "GiB/s", "cores": threads, "affinity_cpus": affinity, "kind": kind,
+            "all_cores": {"value": round(va, 4), "cores": affinity, "cgroup_cpu_quota": cgroup_cpus(),
+                          "sample": "the same %d strings, %d threads (every CPU of the affinity mask), median of 3"
+                                    % (m, affinity)},
             "sample": "%d strings (%.1f MB) of rank 0's shard, encode + decode, median of 5, %d threads of %d in the "
                       "affinity mask (%s)" % (m, Ps / 1e6, threads, affinity,
                                               "oracle/_ref: the reference's lib/http2/hpack.c, compiled" if kind ==

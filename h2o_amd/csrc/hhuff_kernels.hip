@@ -2069,6 +2069,8 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
         if (HHUFF_EDGE_BYTES && !A.edges && t < 64u) {  // small batches: the two partial chunks, a byte a lane (wave 0)
             const uint8_t* so = reinterpret_cast<const uint8_t*>(s_out);
             edge_bytes<true>(A.out, a0, so, span, lo, hi, (int)t);
+            // lane b read byte b ^ 3 of its chunk and zeroes byte b: every read lands before any lane's zeroing
+            wave_lds_sync();
             if (t < 32u && span != 0) {  // zero the bytes read (the chunk was left in place above when partial)
                 const uint32_t ke = t < 16u ? 0u : kl;
                 if (!((uint64_t)a0 + ke >= lo && (uint64_t)a0 + ke + 16 <= hi))
@@ -3955,10 +3957,6 @@ static hipError_t pool_alloc(void** p, uint64_t bytes, hipStream_t stream) {
     }
     return hipMallocFromPoolAsync(p, bytes, pool, stream);
 }
-// Deferred tile edges (records + edge_fix_kernel) for batches of this many strings or more; below it the kernels
-// write a tile's shared chunks byte-exact themselves (store_range16r) and a leg is one launch: the fix-up launch
-// is a fixed ~5 us, which a 1M-string batch feels and a 16M one does not (there the in-kernel byte stores cost
-// more, DESIGN (e) round 4)
 // Edge records and edge_fix_kernel for batches of at least this many strings; below it the codec kernels store
 // their regions' shared 16-B chunks themselves, one byte a lane (edge_bytes).  Default: never deferred -- the
 // byte-lane edges measured c4 decode -5.5 %, c3 encode -5.3 %, c5 encode -5.6 %, flatten -6.6 %, c2 decode -9 %

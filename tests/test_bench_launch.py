@@ -41,6 +41,19 @@ def test_launcher_world_size_must_match():
         bench.launch_plan(0, {}, "nccl", _never)
 
 
+def test_pmc_child_env_drops_the_launcher():
+    """a PMC child of rank 0 must not see the launcher's rank variables (it would join the process group as a
+    second rank 0 and hang the N > 1 run: VERDICT r5, What's weak 1)"""
+    env = {"WORLD_SIZE": "8", "RANK": "0", "LOCAL_RANK": "0", "LOCAL_WORLD_SIZE": "8", "GROUP_RANK": "0",
+           "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": "29500", "TORCHELASTIC_RUN_ID": "x",
+           "TORCHELASTIC_USE_AGENT_STORE": "True", "ROLE_RANK": "0", "PATH": "/usr/bin", "OMP_NUM_THREADS": "16",
+           "HSA_ENABLE_IPC_MODE_LEGACY": "0"}
+    e = bench.child_env(env)
+    assert e == {"PATH": "/usr/bin", "OMP_NUM_THREADS": "16", "HSA_ENABLE_IPC_MODE_LEGACY": "0", "TMPDIR": "/tmp"}
+    # the child's own plan from that environment: a world of one
+    assert bench.launch_plan(None, e, "nccl", _never) == ("rank", 1)
+
+
 def test_rank_command():
     cmd = bench.rank_command(4, ["--steps", "5"], 29511)
     i = cmd.index("torch.distributed.run")
@@ -124,3 +137,57 @@ def test_bench_rccl_branch_world_of_one():
     assert "exchange_issue_ms" in line and "exchange_wait_ms" in line
     assert "RCCL stream" in line["exchange"]
     assert line["value"] > 0 and line["roofline"]["frac"] > 0
+
+
+def _run_traffic_on(cmd, env):
+    import json
+    import subprocess
+
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=540, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-4000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_with_traffic_passes():
+    """`bench.py --gpus 2` WITH its rocprofv3 PMC passes on, as the driver's N > 1 runs start it: rank 0's
+    profiling children must run as worlds of one (no second rank 0 in the process group); one JSON line, with the
+    traffic of one shard's worth measured"""
+    import shutil
+
+    if not (shutil.which("rocprofv3") or os.path.exists("/opt/rocm/bin/rocprofv3")):
+        pytest.skip("rocprofv3 not installed")
+    env = dict(os.environ, HHUFF_DIST_BACKEND="gloo")
+    for k in bench.LAUNCHER_ENV:
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--strings", "262144", "--steps", "2",
+           "--warmup", "1", "--no-extra", "--no-host", "--no-cpu-baseline"]
+    line = _run_traffic_on(cmd, env)
+    assert line["n_gpus"] == 2 and line["dist_backend"] == "gloo"
+    assert "traffic_note" in line and "131072 strings" in line["traffic_note"]
+    assert line["roofline"]["traffic"] is not None and line["roofline"]["traffic"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_rccl_world_of_one_with_traffic_passes():
+    """the RCCL world of one (torch.distributed.run, --force-pg) with the PMC passes on: the children start with
+    the launcher's WORLD_SIZE / RANK / MASTER_* removed and never create a process group"""
+    import shutil
+    import socket
+
+    if not (shutil.which("rocprofv3") or os.path.exists("/opt/rocm/bin/rocprofv3")):
+        pytest.skip("rocprofv3 not installed")
+    env = dict(os.environ)
+    for k in bench.LAUNCHER_ENV + ("HHUFF_DIST_BACKEND",):
+        env.pop(k, None)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"), "--gpus", "1", "--strings",
+           "262144", "--steps", "2", "--warmup", "1", "--no-extra", "--no-host", "--no-cpu-baseline", "--force-pg"]
+    line = _run_traffic_on(cmd, env)
+    assert line["dist_backend"] == "nccl" and line["n_gpus"] == 1
+    assert line["roofline"]["traffic"] is not None and line["roofline"]["traffic"] > 0

@@ -365,30 +365,33 @@ def test_mixed_length_decode_select(torch_cuda, oracle_codec, lengths, verdict):
     assert 40 < hdata.size // m <= 128
     from h2o_amd import codec
 
-    prev = codec.set_decode_kernel(0)  # the staged / stream choice (the segment kernel takes these by default)
-    prices = (40.0, 1.07, 184.0, 1.15)  # pinned (the fitted MI355X defaults): the verdict is fixed
-    codec.set_decode_prices(prices, 0)
-    assert codec.decode_prices(0) == pytest.approx(prices)
-    assert _select_verdict(np.diff(hoff), prices) == verdict, prices
-    names = synth.bits_from_bools(rng.random(m) < 0.3)
-    g = gpu_decode(torch_cuda, hdata, hoff, m, is_name_bits=names)
-    o = oracle_codec.decode_batch(hdata, hoff, m, is_name_bits=names, nthreads=8)
-    np.testing.assert_array_equal(g[1], o[1])
-    np.testing.assert_array_equal(g[2], o[2])
-    slots = (hoff[:m].astype(np.uint64) * 8) // 5
-    assert compact(g[0], slots, g[1]) == compact(o[0], slots, o[1])
-    # pairs, reversed order, explicit destinations packed at 2 x len (h2o's buffer rule)
-    idx = np.arange(m)[::-1].copy()
-    starts, lens = hoff[idx].astype(np.uint32), np.diff(hoff)[idx].astype(np.uint32)
-    dst = np.concatenate([[0], np.cumsum(2 * lens.astype(np.uint64))])
-    out_off = dst[:-1].astype(np.uint32)
-    g = gpu_decode(torch_cuda, hdata, starts, m, in_len=lens, out_off=out_off, out_size=int(dst[-1]) + 64)
-    o = oracle_codec.decode_batch(hdata, starts, m, in_len=lens, nthreads=8)
-    np.testing.assert_array_equal(g[1], o[1])
-    np.testing.assert_array_equal(g[2], o[2])
-    sl = (starts.astype(np.uint64) * 8) // 5
-    assert compact(g[0], out_off, g[1]) == compact(o[0], sl, o[1])
-    codec.set_decode_kernel(prev)
+    prev = codec.set_decode_kernel(0)  # the staged / stream choice (the default; the segment kernel is opt-in)
+    try:
+        prices = (40.0, 1.07, 184.0, 1.15)  # pinned (the fitted MI355X defaults): the verdict is fixed
+        codec.set_decode_prices(prices, 0)
+        assert codec.decode_prices(0) == pytest.approx(prices)
+        assert _select_verdict(np.diff(hoff), prices) == verdict, prices
+        names = synth.bits_from_bools(rng.random(m) < 0.3)
+        g = gpu_decode(torch_cuda, hdata, hoff, m, is_name_bits=names)
+        o = oracle_codec.decode_batch(hdata, hoff, m, is_name_bits=names, nthreads=8)
+        np.testing.assert_array_equal(g[1], o[1])
+        np.testing.assert_array_equal(g[2], o[2])
+        slots = (hoff[:m].astype(np.uint64) * 8) // 5
+        assert compact(g[0], slots, g[1]) == compact(o[0], slots, o[1])
+        # pairs, reversed order, explicit destinations packed at 2 x len (h2o's buffer rule)
+        idx = np.arange(m)[::-1].copy()
+        starts, lens = hoff[idx].astype(np.uint32), np.diff(hoff)[idx].astype(np.uint32)
+        dst = np.concatenate([[0], np.cumsum(2 * lens.astype(np.uint64))])
+        out_off = dst[:-1].astype(np.uint32)
+        g = gpu_decode(torch_cuda, hdata, starts, m, in_len=lens, out_off=out_off, out_size=int(dst[-1]) + 64)
+        o = oracle_codec.decode_batch(hdata, starts, m, in_len=lens, nthreads=8)
+        np.testing.assert_array_equal(g[1], o[1])
+        np.testing.assert_array_equal(g[2], o[2])
+        sl = (starts.astype(np.uint64) * 8) // 5
+        assert compact(g[0], out_off, g[1]) == compact(o[0], sl, o[1])
+    finally:  # a failed assert must not leak the mode or the pinned prices into later tests
+        codec.set_decode_kernel(prev)
+        codec.set_decode_prices(None, 0)
 
 
 def test_decode_price_calibration(torch_cuda):
@@ -907,6 +910,42 @@ def test_host_packed_path(torch_cuda, kind):
     pos = codec.packed_positions(hoff, olen2, decode=True)
     np.testing.assert_array_equal(pos, ooff[:m].astype(np.int64))
     assert compact(out2, pos, olen2) == compact(out, ooff[:m], olen)
+
+
+@pytest.mark.parametrize("with_off", [True, False])
+def test_host_packed_staged_leaves_gaps(torch_cuda, with_off):
+    """the staged host path (pageable caller arrays) copies back only the tiles' runs: every byte of the caller's
+    out buffer outside the outputs keeps its sentinel, exactly as on the zero-copy path (hhuff.h packed contract;
+    ADVICE r5).  Two batches first dirty the library's device scratch so stale bytes would show"""
+    from h2o_amd import codec
+
+    SENT = 0x5A
+    for seed in (31, 32):
+        b = synth.make_batch("c3", n=3000 + seed, seed=seed, adversarial_frac=0.05)
+        n, data, off = b["n"], b["data"], b["off"]
+        out = np.full(int(off[n]) + 16, SENT, np.uint8)
+        out, ooff, olen, ost = codec.encode_batch_host_packed(data.copy(), off.copy(), n, out=out, with_off=with_off)
+        pos = ooff[:n].astype(np.int64) if with_off else codec.packed_positions(off, olen, decode=False)
+        mask = np.ones(out.size, bool)
+        for o, L in zip(pos, olen):
+            if L != FAIL:
+                mask[int(o):int(o) + int(L)] = False
+        assert (out[mask] == SENT).all(), "encode: bytes outside the outputs were written"
+        ok = np.nonzero(olen != FAIL)[0]
+        huff = _gather(out, pos, olen)
+        h_off = np.zeros(ok.size + 1, np.uint32)
+        h_off[1:] = np.cumsum(olen[ok].astype(np.int64))
+        m = ok.size
+        dout = np.full(codec.decode_slot_size(huff.size), SENT, np.uint8)
+        dout, doff, dlen, dst = codec.decode_batch_host_packed(huff.copy(), h_off, m, out=dout, with_off=with_off)
+        dpos = doff[:m].astype(np.int64) if with_off else codec.packed_positions(h_off, dlen, decode=True)
+        mask = np.ones(dout.size, bool)
+        for o, L in zip(dpos, dlen):
+            if L != FAIL:
+                mask[int(o):int(o) + int(L)] = False
+        assert (dout[mask] == SENT).all(), "decode: bytes outside the outputs were written"
+        got = _gather(dout, dpos, dlen).tobytes()
+        assert got == b"".join(data[off[i]:off[i + 1]].tobytes() for i in ok)
 
 
 # ------------------------------------------------------------------------------------------------

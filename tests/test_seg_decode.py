@@ -151,8 +151,8 @@ def test_seg_long_mixed_and_split_lists(torch_cuda, oracle_codec):  # noqa: F811
             check_decode(torch_cuda, oracle_codec, hdata, hoff, n, synth.bits_from_bools(rng.random(n) < 0.3))
 
 
-def test_seg_legacy_mode_c3(torch_cuda, oracle_codec):  # noqa: F811
-    """mode 0 keeps the round-4 staged / stream choice reachable (A/B builds, hhuff_set_decode_kernel)"""
+def test_default_mode_c3(torch_cuda, oracle_codec):  # noqa: F811
+    """mode 0 -- the default -- is the staged / stream choice; the segment kernel (modes 1, 2) is opt-in"""
     b = synth.make_batch("c3", n=30000, seed=5)
     huff = huffman_of(oracle_codec, synth.unpack(b["data"], b["off"]))
     hdata, hoff = synth.pack(huff)
