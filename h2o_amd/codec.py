@@ -140,6 +140,14 @@ def lib():
         L.hhuff_encode_batch_host_packed.restype = ctypes.c_int
         L.hhuff_encode_batch_host_packed.argtypes = [_vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, ctypes.c_uint64,
                                                      _vp, _vp, _vp, ctypes.c_int]
+        L.hhuff_decode_batch_multi.restype = ctypes.c_int
+        L.hhuff_decode_batch_multi.argtypes = [ctypes.c_int, _vp, ctypes.c_int, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32,
+                                               _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp]
+        L.hhuff_encode_batch_multi.restype = ctypes.c_int
+        L.hhuff_encode_batch_multi.argtypes = [ctypes.c_int, _vp, ctypes.c_int, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32,
+                                               _vp, ctypes.c_uint64, _vp, _vp, _vp]
+        L.hhuff_shard_bounds.restype = ctypes.c_int
+        L.hhuff_shard_bounds.argtypes = [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _vp]
         _lib = L
     return _lib
 
@@ -155,7 +163,8 @@ EXPORTED = ("h2o_hpack_decode_huffman", "h2o_hpack_encode_huffman", "hhuff_decod
             "hhuff_grid_size", "hhuff_decode_prices", "hhuff_calibrate_decode_prices", "hhuff_set_decode_prices",
             "hhuff_pool_trim", "hhuff_service_stamps", "hhuff_hpack_enc_scratch_size",
             "hhuff_hpack_flatten_responses", "hhuff_qpack_flatten_responses", "hhuff_set_decode_kernel",
-            "hhuff_decode_batch_host_packed", "hhuff_encode_batch_host_packed", "hhuff_set_edge_defer_min")
+            "hhuff_decode_batch_host_packed", "hhuff_encode_batch_host_packed", "hhuff_set_edge_defer_min",
+            "hhuff_decode_batch_multi", "hhuff_encode_batch_multi", "hhuff_shard_bounds")
 
 
 def _check(rc, what):
@@ -645,6 +654,80 @@ def encode_batch_host_packed(data, in_off, n, out=None, device=0, out_off=None, 
            "hhuff_encode_batch_host_packed")
     return (out, None if out_off is None else out_off[:n + 1], out_len[:n],
             None if status is None else status[:n])
+
+
+HOST_MEMORY = -1
+
+
+def shard_bounds(in_off, n, nshards, align=64):
+    """hhuff_shard_bounds: the C library's byte-balanced cut of a contiguous batch (host arrays, no GPU work)
+    -> uint32 bounds[nshards + 1]"""
+    in_off = _np(in_off, np.uint32)
+    b = np.zeros(nshards + 1, np.uint32)
+    _check(lib().hhuff_shard_bounds(_hp(in_off), n, nshards, align, _hp(b)), "hhuff_shard_bounds")
+    return b
+
+
+def _devs(devices):
+    arr = (ctypes.c_int * len(devices))(*devices)
+    return arr, ctypes.cast(arr, _vp)
+
+
+def decode_batch_multi(devices, data, in_off, n, is_name_bits=None, out=None, out_len=None, status=None, stream=None):
+    """hhuff_decode_batch_multi.  numpy arrays: the host mode (every device runs its shard through the host path);
+    torch tensors on one device: the device mode (shards on other devices by peer copy), asynchronous on `stream`.
+    Returns (out, out_len, status) in the one-device slot layout"""
+    devs, dp = _devs(devices)
+    if isinstance(data, np.ndarray):
+        data, in_off = _np(data, np.uint8), _np(in_off, np.uint32)
+        out = np.zeros(decode_slot_size(int(in_off[n])), np.uint8) if out is None else out
+        out_len = np.zeros(max(1, n), np.uint32) if out_len is None else out_len
+        status = np.zeros(max(1, n), np.uint8) if status is None else status
+        names = None if is_name_bits is None else _np(is_name_bits, np.uint32)
+        _check(lib().hhuff_decode_batch_multi(len(devices), dp, HOST_MEMORY, _hp(data), data.size, _hp(in_off), n,
+                                              _hp(names), _hp(out), out.size, _hp(out_len), _hp(status), None),
+               "hhuff_decode_batch_multi")
+        return out, out_len[:n], status[:n]
+    import torch
+
+    dev = data.device
+    if out is None:
+        out = torch.empty(decode_slot_size(data.numel()), dtype=torch.uint8, device=dev)
+    if out_len is None:
+        out_len = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    _check(lib().hhuff_decode_batch_multi(len(devices), dp, dev.index, _dp(data), data.numel(), _dp(in_off), n,
+                                          _dp(is_name_bits), _dp(out), out.numel(), _dp(out_len), _dp(status),
+                                          _stream(stream)), "hhuff_decode_batch_multi")
+    return out, out_len, status
+
+
+def encode_batch_multi(devices, data, in_off, n, out=None, out_len=None, status=None, stream=None):
+    """hhuff_encode_batch_multi (see decode_batch_multi)"""
+    devs, dp = _devs(devices)
+    if isinstance(data, np.ndarray):
+        data, in_off = _np(data, np.uint8), _np(in_off, np.uint32)
+        out = np.zeros(int(in_off[n]) + 16, np.uint8) if out is None else out
+        out_len = np.zeros(max(1, n), np.uint32) if out_len is None else out_len
+        status = np.zeros(max(1, n), np.uint8) if status is None else status
+        _check(lib().hhuff_encode_batch_multi(len(devices), dp, HOST_MEMORY, _hp(data), data.size, _hp(in_off), n,
+                                              _hp(out), out.size, _hp(out_len), _hp(status), None),
+               "hhuff_encode_batch_multi")
+        return out, out_len[:n], status[:n]
+    import torch
+
+    dev = data.device
+    if out is None:
+        out = torch.empty(data.numel() + 16, dtype=torch.uint8, device=dev)
+    if out_len is None:
+        out_len = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    if status is None:
+        status = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    _check(lib().hhuff_encode_batch_multi(len(devices), dp, dev.index, _dp(data), data.numel(), _dp(in_off), n,
+                                          _dp(out), out.numel(), _dp(out_len), _dp(status), _stream(stream)),
+           "hhuff_encode_batch_multi")
+    return out, out_len, status
 
 
 def packed_positions(in_off, out_len, decode):

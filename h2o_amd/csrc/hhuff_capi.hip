@@ -10,6 +10,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <string>
 #include <immintrin.h>
 #include <mutex>
 #include <thread>
@@ -881,9 +884,12 @@ int pipelined(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t* 
         auto al = [](const void* p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
         const bool aligned = al(d_in, 16) && al(d_out, 16) && al(d_off, 4) && al(d_len, 4) && al(d_nm, 4);
         if (aligned && d_in && d_off && d_out && d_len && (!status || d_st) && (!is_name_bits || d_nm)) {
+            // (the kernel variant follows the batch's own bytes: a shard of a larger buffer passes in_off + lo)
+            const uint64_t sel = (uint64_t)in_off[n] - in_off[0];
             hipError_t e = decode ? hhuff::launch_decode(d_in, in_size, d_off, nullptr, n, d_nm, d_out, nullptr, d_len, d_st,
-                                                         c.stream)
-                                  : hhuff::launch_encode(d_in, in_size, d_off, nullptr, n, d_out, nullptr, d_len, d_st, c.stream);
+                                                         c.stream, sel)
+                                  : hhuff::launch_encode(d_in, in_size, d_off, nullptr, n, d_out, nullptr, d_len, d_st, c.stream,
+                                                         sel);
             if (e != hipSuccess) return hip_fail(e, decode ? "decode launch (zero copy)" : "encode launch (zero copy)");
             HIP_TRY(hipStreamSynchronize(c.stream), "sync");
             return HHUFF_OK;
@@ -1057,11 +1063,42 @@ int host_packed(bool decode, const uint8_t* in, uint64_t in_size, const uint32_t
     hipError_t e = decode ? hhuff::launch_decode_packed(d_in, in_size, d_off, n, d_nm, d_out, d_ooff, d_len, d_st, s)
                           : hhuff::launch_encode_packed(d_in, in_size, d_off, n, d_out, d_ooff, d_len, status ? d_st : nullptr, s);
     if (e != hipSuccess) return hip_fail(e, decode ? "packed decode launch" : "packed encode launch");
-    HIP_TRY(hipMemcpyAsync(out, d_out, slot_end, hipMemcpyDeviceToHost, s), "D2H out");
-    if (out_off) HIP_TRY(hipMemcpyAsync(out_off, d_ooff, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, s), "D2H out_off");
+    // the metadata first: the tiles' runs follow from out_off / out_len, and only the runs go back to the caller
+    // (the gaps between them were never written by the kernels; the caller's bytes there stay untouched, as on
+    // the zero-copy path: hhuff.h's packed contract)
+    std::vector<uint32_t> tmp_off(out_off ? 0 : (size_t)n + 1);
+    uint32_t* h_ooff = out_off ? out_off : tmp_off.data();
+    HIP_TRY(hipMemcpyAsync(h_ooff, d_ooff, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, s), "D2H out_off");
     HIP_TRY(hipMemcpyAsync(out_len, d_len, (size_t)n * 4, hipMemcpyDeviceToHost, s), "D2H out_len");
     if (status) HIP_TRY(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, s), "D2H status");
     HIP_TRY(hipStreamSynchronize(s), "sync");
+    // run of tile t: [its slot position, end of its last kept string); chunks of the device output go through the
+    // context's pinned buffer and each run's part of a chunk is copied out of it
+    const uint32_t ntiles = (n + 63) / 64;
+    auto run_lo = [&](uint32_t t) -> uint64_t {
+        const uint64_t o = in_off[(size_t)t * 64];
+        return decode ? (o * 8) / 5 : o;
+    };
+    auto run_hi = [&](uint32_t t) -> uint64_t {
+        const uint32_t last = (t + 1) * 64 < n ? (t + 1) * 64 - 1 : n - 1;
+        return (uint64_t)h_ooff[last] + (out_len[last] != HHUFF_FAIL_LEN ? out_len[last] : 0);
+    };
+    const size_t chunk = (size_t)64 << 20;
+    rc = c.reserve(need, std::min<size_t>(chunk, up16(slot_end + 16)));
+    if (rc) return rc;
+    uint32_t t = 0;
+    for (uint64_t lo = 0; lo < slot_end && t < ntiles; lo += chunk) {
+        const uint64_t hi = std::min<uint64_t>(slot_end, lo + chunk);
+        while (t < ntiles && run_hi(t) <= lo) ++t;  // runs ending before this chunk (empty runs included)
+        if (t >= ntiles || run_lo(t) >= hi) continue;  // nothing of any run in this chunk
+        HIP_TRY(hipMemcpyAsync(c.h, d_out + lo, hi - lo, hipMemcpyDeviceToHost, s), "D2H out");
+        HIP_TRY(hipStreamSynchronize(s), "sync");
+        for (uint32_t u = t; u < ntiles; ++u) {
+            const uint64_t a = std::max(run_lo(u), lo), b = std::min(run_hi(u), hi);
+            if (run_lo(u) >= hi) break;
+            if (b > a) memcpy(out + a, c.h + (a - lo), b - a);
+        }
+    }
     return HHUFF_OK;
 }
 
@@ -1107,6 +1144,310 @@ HHUFF_API int hhuff_encode_batch_host(const uint8_t* in, uint64_t in_size, const
                                       uint32_t n, uint8_t* out, uint64_t out_size, const uint32_t* out_off,
                                       uint32_t* out_len, uint8_t* status, int device) {
     return host_batch(false, in, in_size, in_off, in_len, n, nullptr, out, out_size, out_off, out_len, status, device);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// (3d) multi-device batch: one batch over several GPUs of this process (include/hhuff.h (3d)).  Offsets stay
+// absolute, so a shard is just a sub-range of in_off with `in` / `out` (and, for a shard copied to another
+// device, its scratch shifted back by the shard's base) -- the same addressing as the chunked host pipeline.
+// ---------------------------------------------------------------------------------------------------
+namespace {
+
+// the byte-balanced cut (hhuff_shard_bounds): the first string at or past the k/ns quantile of the bytes, rounded
+// down to a multiple of align -- a lower_bound over in_off[0 .. n], the same search as dist.byte_balanced_bounds
+__host__ __device__ inline uint32_t shard_bound(const uint32_t* in_off, uint32_t n, uint32_t k, uint32_t ns,
+                                                uint32_t align) {
+    if (k == 0) return 0;
+    if (k >= ns) return n;
+    const uint64_t base = in_off[0];
+    const uint64_t end = in_off[n];
+    const uint64_t target = base + (end > base ? ((uint64_t)k * (end - base)) / ns : 0);
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = lo + (hi - lo) / 2;
+        if ((uint64_t)in_off[mid] < target)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return align > 1 ? lo - lo % align : lo;
+}
+
+// device-resident batches: the cut and the byte offsets at the cut, into mapped host memory (b[0 .. ns], then
+// in_off[b[k]] at b[ns + 1 + k])
+__global__ void shard_bounds_kernel(const uint32_t* in_off, uint32_t n, uint32_t ns, uint32_t align, uint32_t* b) {
+    const uint32_t k = threadIdx.x;
+    if (k <= ns) {
+        const uint32_t i = shard_bound(in_off, n, k, ns, align);
+        b[k] = i;
+        b[ns + 1 + k] = in_off[i];
+    }
+}
+
+constexpr int kMaxDev = 64;
+// HHUFF_MULTI_COPY=1: shards on the source device go through the copy path too (a device-to-device copy there):
+// the peer path's addressing, tested on a one-GPU box
+bool force_copy() {
+    const char* v = getenv("HHUFF_MULTI_COPY");  // read per call (tests switch it within one process)
+    return v && v[0] == '1';
+}
+constexpr uint32_t kShardAlign = 64;  // a shard starts on a tile (and on an is-name word)
+
+int check_devices(int ndev, const int* devices, int* dv) {
+    if (ndev < 1 || ndev > kMaxDev) return arg_fail("ndev must be in [1, 64]");
+    int count = 0;
+    HIP_TRY(hipGetDeviceCount(&count), "hipGetDeviceCount");
+    for (int k = 0; k < ndev; ++k) {
+        dv[k] = devices ? devices[k] : k;
+        if (dv[k] < 0 || dv[k] >= count) return arg_fail("device id out of range");
+    }
+    return HHUFF_OK;
+}
+
+// host arrays: one persistent library thread per device (its thread-local stream, scratch and pinned staging
+// persist across calls), each running its shard through the host path
+struct DevWorker {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::function<void()> job;
+    bool has = false, done = false;
+    DevWorker() {
+        std::thread([this] {
+            for (;;) {
+                std::function<void()> j;
+                {
+                    std::unique_lock<std::mutex> l(mu);
+                    cv.wait(l, [this] { return has; });
+                    j = std::move(job);
+                    has = false;
+                }
+                j();
+                {
+                    std::lock_guard<std::mutex> l(mu);
+                    done = true;
+                }
+                cv.notify_all();
+            }
+        }).detach();
+    }
+    void post(std::function<void()> f) {
+        {
+            std::lock_guard<std::mutex> l(mu);
+            job = std::move(f);
+            has = true;
+            done = false;
+        }
+        cv.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [this] { return done; });
+    }
+};
+std::mutex g_multi_mu;                       // one multi-device host call at a time (each uses every device)
+DevWorker* g_workers[kMaxDev] = {};          // created on first use, never destroyed (detached threads)
+
+int multi_host(bool decode, int ndev, const int* dv, const uint8_t* in, uint64_t in_size, const uint32_t* in_off,
+               uint32_t n, const uint32_t* names, uint8_t* out, uint64_t out_size, uint32_t* out_len, uint8_t* status) {
+    if (in_off[n] > in_size) return arg_fail("in_off[n] > in_size");
+    std::vector<uint32_t> b(ndev + 1);
+    for (int k = 0; k <= ndev; ++k) b[k] = shard_bound(in_off, n, (uint32_t)k, (uint32_t)ndev, kShardAlign);
+    std::lock_guard<std::mutex> g(g_multi_mu);
+    std::vector<int> rc(ndev, HHUFF_OK);
+    std::vector<std::string> err(ndev);
+    std::vector<int> posted;
+    for (int k = 0; k < ndev; ++k) {
+        const uint32_t lo = b[k], m = b[k + 1] - b[k];
+        if (m == 0) continue;
+        DevWorker*& w = g_workers[k];
+        if (!w) w = new DevWorker();
+        const int dev = dv[k];
+        w->post([=, &rc, &err] {
+            rc[k] = pipelined(decode, in, in_size, in_off + lo, m, names ? names + lo / 32 : nullptr, out, out_size,
+                              out_len + lo, status ? status + lo : nullptr, dev, 0);
+            if (rc[k]) err[k] = t_err;
+        });
+        posted.push_back(k);
+    }
+    for (int k : posted) g_workers[k]->wait();
+    for (int k = 0; k < ndev; ++k)
+        if (rc[k]) {
+            snprintf(t_err, sizeof(t_err), "shard %d (device %d): %s", k, dv[k], err[k].c_str());
+            return rc[k];
+        }
+    return HHUFF_OK;
+}
+
+// device arrays on src: per calling thread, one stream per device and the mapped words the cut comes back in
+struct MultiCtx {
+    hipStream_t s[kMaxDev] = {};
+    uint32_t* hb = nullptr;  // mapped host memory: 2 (kMaxDev + 1) words
+    bool peer[kMaxDev][kMaxDev] = {};
+    ~MultiCtx() {
+        for (auto& x : s)
+            if (x) (void)hipStreamDestroy(x);
+        if (hb) (void)hipHostFree(hb);
+    }
+};
+thread_local MultiCtx t_multi;
+
+int multi_device(bool decode, int ndev, const int* dv, int src, const uint8_t* in, uint64_t in_size,
+                 const uint32_t* in_off, uint32_t n, const uint32_t* names, uint8_t* out, uint64_t out_size,
+                 uint32_t* out_len, uint8_t* status, hipStream_t stream) {
+    DeviceGuard guard(src);
+    if (guard.err != hipSuccess) return hip_fail(guard.err, "hipSetDevice");
+    MultiCtx& X = t_multi;
+    if (!X.hb) HIP_TRY(hipHostMalloc(&X.hb, 8 * (kMaxDev + 1), hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc");
+    uint32_t* d_hb = nullptr;
+    HIP_TRY(hipHostGetDevicePointer((void**)&d_hb, X.hb, 0), "hipHostGetDevicePointer");
+    hipLaunchKernelGGL(shard_bounds_kernel, dim3(1), dim3(kMaxDev + 1), 0, stream, in_off,
+                       n, (uint32_t)ndev, kShardAlign, d_hb);
+    HIP_TRY(hipGetLastError(), "shard bounds launch");
+    HIP_TRY(hipStreamSynchronize(stream), "sync (the cut)");
+    std::vector<uint32_t> b(X.hb, X.hb + ndev + 1), boff(X.hb + ndev + 1, X.hb + 2 * ndev + 2);
+    auto slot_of = [&](uint64_t pos) { return decode ? (pos * 8) / 5 : pos; };
+    if (boff[ndev] > in_size) return arg_fail("in_off[n] > in_size");
+    if (out_size < slot_of(boff[ndev])) return arg_fail("out_size below the output slots of the batch");
+    hipEvent_t ready;
+    HIP_TRY(hipEventCreateWithFlags(&ready, hipEventDisableTiming), "hipEventCreate");
+    std::vector<hipEvent_t> fin;
+    int rc = HHUFF_OK;
+    auto fail = [&](hipError_t e, const char* where) {
+        if (rc == HHUFF_OK) rc = hip_fail(e, where);
+    };
+    hipError_t e = hipEventRecord(ready, stream);
+    if (e != hipSuccess) fail(e, "hipEventRecord");
+    for (int k = 0; k < ndev && rc == HHUFF_OK; ++k) {
+        const uint32_t lo = b[k], m = b[k + 1] - b[k];
+        if (m == 0) continue;
+        const int dev = dv[k];
+        const uint64_t s0 = boff[k], e0 = boff[k + 1];
+        if (dev == src && !force_copy()) {  // in place, on the caller's stream
+            e = decode ? hhuff::launch_decode(in, in_size, in_off + lo, nullptr, m, names ? names + lo / 32 : nullptr, out,
+                                              nullptr, out_len + lo, status + lo, stream, e0 - s0)
+                       : hhuff::launch_encode(in, in_size, in_off + lo, nullptr, m, out, nullptr, out_len + lo,
+                                              status ? status + lo : nullptr, stream, e0 - s0);
+            if (e != hipSuccess) fail(e, "shard launch (source device)");
+            continue;
+        }
+        if ((e = hipSetDevice(dev)) != hipSuccess) {
+            fail(e, "hipSetDevice");
+            break;
+        }
+        if (!X.s[dev] && (e = hipStreamCreateWithFlags(&X.s[dev], hipStreamNonBlocking)) != hipSuccess) {
+            fail(e, "hipStreamCreate");
+            break;
+        }
+        if (dev != src && !X.peer[dev][src]) {  // direct xGMI reads / writes of src's memory where the link allows it
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, dev, src) == hipSuccess && can) {
+                const hipError_t pe = hipDeviceEnablePeerAccess(src, 0);
+                if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) {
+                    fail(pe, "hipDeviceEnablePeerAccess");
+                    break;
+                }
+                (void)hipGetLastError();
+            }
+            X.peer[dev][src] = true;
+        }
+        hipStream_t ms = X.s[dev];
+        // the shard's layout on its device (as one chunk of the host pipeline): [in bytes from base][in_off m + 1]
+        // [names][out slots from slot_of(base)][out_len m][status m]; base a multiple of 80 keeps the decode slot
+        // floor(8 base / 5) 16-byte aligned
+        const uint64_t base = (s0 / 80) * 80, nbytes = e0 - base;
+        const uint64_t olo = slot_of(s0), ohi = std::min<uint64_t>(slot_of(e0), out_size), obase = slot_of(base);
+        const uint64_t ocap = slot_of(e0) - obase + 16;
+        const size_t nw = names ? ((size_t)m + 31) / 32 : 0;
+        const size_t o_off = up16(nbytes + 16), o_nm = o_off + up16(((size_t)m + 1) * 4), o_out = o_nm + up16(nw * 4),
+                     o_len = o_out + up16(ocap), o_st = o_len + up16((size_t)m * 4), need = o_st + up16(m);
+        uint8_t* d = nullptr;
+        if ((e = hipStreamWaitEvent(ms, ready, 0)) != hipSuccess || (e = hhuff::work_alloc((void**)&d, need, ms)) != hipSuccess) {
+            fail(e, "shard scratch");
+            break;
+        }
+        uint32_t* d_off = reinterpret_cast<uint32_t*>(d + o_off);
+        uint32_t* d_nm = nw ? reinterpret_cast<uint32_t*>(d + o_nm) : nullptr;
+        uint32_t* d_len = reinterpret_cast<uint32_t*>(d + o_len);
+        uint8_t* d_st = d + o_st;
+        if ((e = hipMemcpyPeerAsync(d, dev, in + base, src, nbytes, ms)) != hipSuccess ||
+            (e = hipMemcpyPeerAsync(d_off, dev, in_off + lo, src, ((size_t)m + 1) * 4, ms)) != hipSuccess ||
+            (nw && (e = hipMemcpyPeerAsync(d_nm, dev, names + lo / 32, src, nw * 4, ms)) != hipSuccess)) {
+            fail(e, "peer copy in");
+            break;
+        }
+        e = decode ? hhuff::launch_decode(d - base, e0, d_off, nullptr, m, d_nm, d + o_out - obase, nullptr, d_len, d_st,
+                                          ms, e0 - s0)
+                   : hhuff::launch_encode(d - base, e0, d_off, nullptr, m, d + o_out - obase, nullptr, d_len,
+                                          status ? d_st : nullptr, ms, e0 - s0);
+        if (e != hipSuccess) {
+            fail(e, "shard launch (peer device)");
+            break;
+        }
+        if ((ohi > olo && (e = hipMemcpyPeerAsync(out + olo, src, d + o_out + (olo - obase), dev, ohi - olo, ms)) != hipSuccess) ||
+            (e = hipMemcpyPeerAsync(out_len + lo, src, d_len, dev, (size_t)m * 4, ms)) != hipSuccess ||
+            (status && (e = hipMemcpyPeerAsync(status + lo, src, d_st, dev, m, ms)) != hipSuccess)) {
+            fail(e, "peer copy out");
+            break;
+        }
+        if ((e = hipFreeAsync(d, ms)) != hipSuccess) {
+            fail(e, "hipFreeAsync");
+            break;
+        }
+        hipEvent_t f;
+        if ((e = hipEventCreateWithFlags(&f, hipEventDisableTiming)) != hipSuccess || (e = hipEventRecord(f, ms)) != hipSuccess) {
+            fail(e, "hipEventRecord");
+            break;
+        }
+        fin.push_back(f);
+    }
+    (void)hipSetDevice(src);
+    for (hipEvent_t f : fin) {  // the caller's stream goes on once every shard is back
+        e = hipStreamWaitEvent(stream, f, 0);
+        if (e != hipSuccess) fail(e, "hipStreamWaitEvent");
+        (void)hipEventDestroy(f);  // released once it completes
+    }
+    (void)hipEventDestroy(ready);
+    return rc;
+}
+
+int batch_multi(bool decode, int ndev, const int* devices, int src, const uint8_t* in, uint64_t in_size,
+                const uint32_t* in_off, uint32_t n, const uint32_t* names, uint8_t* out, uint64_t out_size, uint32_t* out_len,
+                uint8_t* status, void* stream) {
+    int dv[kMaxDev];
+    int rc = check_devices(ndev, devices, dv);
+    if (rc) return rc;
+    if (n == 0) return HHUFF_OK;
+    if (!in || !in_off || !out || !out_len || (decode && !status)) return arg_fail("NULL array");
+    if (src == HHUFF_HOST_MEMORY)
+        return multi_host(decode, ndev, dv, in, in_size, in_off, n, names, out, out_size, out_len, status);
+    int count = 0;
+    HIP_TRY(hipGetDeviceCount(&count), "hipGetDeviceCount");
+    if (src < 0 || src >= count) return arg_fail("src_device out of range");
+    return multi_device(decode, ndev, dv, src, in, in_size, in_off, n, names, out, out_size, out_len, status,
+                        static_cast<hipStream_t>(stream));
+}
+
+}  // namespace
+
+HHUFF_API int hhuff_decode_batch_multi(int ndev, const int* devices, int src_device, const uint8_t* in, uint64_t in_size,
+                                       const uint32_t* in_off, uint32_t n, const uint32_t* is_name_bits, uint8_t* out,
+                                       uint64_t out_size, uint32_t* out_len, uint8_t* status, void* stream) {
+    return batch_multi(true, ndev, devices, src_device, in, in_size, in_off, n, is_name_bits, out, out_size, out_len,
+                       status, stream);
+}
+
+HHUFF_API int hhuff_encode_batch_multi(int ndev, const int* devices, int src_device, const uint8_t* in, uint64_t in_size,
+                                       const uint32_t* in_off, uint32_t n, uint8_t* out, uint64_t out_size, uint32_t* out_len,
+                                       uint8_t* status, void* stream) {
+    return batch_multi(false, ndev, devices, src_device, in, in_size, in_off, n, nullptr, out, out_size, out_len, status,
+                       stream);
+}
+
+HHUFF_API int hhuff_shard_bounds(const uint32_t* in_off, uint32_t n, uint32_t nshards, uint32_t align, uint32_t* bounds) {
+    if (!in_off || !bounds) return arg_fail("NULL array");
+    if (nshards < 1) return arg_fail("nshards must be >= 1");
+    for (uint32_t k = 0; k <= nshards; ++k) bounds[k] = shard_bound(in_off, n, k, nshards, align);
+    return HHUFF_OK;
 }
 
 // ---------------------------------------------------------------------------------------------------

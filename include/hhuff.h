@@ -535,6 +535,36 @@ int hhuff_encode_batch_host_packed(const uint8_t *in, uint64_t in_size, const ui
                                    uint8_t *out, uint64_t out_size, uint32_t *out_off, uint32_t *out_len,
                                    uint8_t *status, int device);
 
+/* (3d) Multi-device batch (SURVEY 2 new component 5, 8e): one batch over several GPUs of one process, for h2o's
+ *     C callers (lib/http2/hpack.c:241, lib/http3/qpack.c:228 -- worker threads, src/main.c:5512) that have no
+ *     torch.distributed.  The contiguous layout of hhuff_decode_batch / hhuff_encode_batch (in_off[n + 1], implicit
+ *     output slots: decode floor(8 in_off[i] / 5), encode in_off[i]) is cut byte-balanced into ndev shards
+ *     (hhuff_shard_bounds with align 64) and shard k runs on devices[k] (NULL: devices 0 .. ndev-1).  Offsets
+ *     stay absolute, so every string lands where the one-device call puts it: the shards' outputs are already
+ *     concatenated in shard order, and out_len / status are byte for byte the one-device call's.
+ *       src_device == HHUFF_HOST_MEMORY: every array is host memory; each device runs its shard through the host
+ *         path (zero copy on pinned, aligned arrays, else the chunked pipeline of 3b), all devices at once, each
+ *         from its own library thread.  Synchronous; `stream` is ignored.
+ *       src_device >= 0: every array is device memory of src_device, ordered on `stream` (a stream of src_device,
+ *         NULL the null stream).  The call waits for the work queued before it on `stream` (the cut reads
+ *         in_off), then enqueues: the src device's own shard in place on an internal stream of src_device, every
+ *         other shard as peer copies (xGMI) of its input bytes, offsets and name bits to scratch on its device,
+ *         the kernel there, and peer copies of its output slots, lengths and statuses back; `stream` then waits
+ *         for every shard.  Returns once all is enqueued (asynchronous, like hhuff_decode_batch).
+ *     ndev == 1 with devices[0] == src_device is the one-device call. */
+#define HHUFF_HOST_MEMORY (-1)
+int hhuff_decode_batch_multi(int ndev, const int *devices, int src_device, const uint8_t *in, uint64_t in_size,
+                             const uint32_t *in_off, uint32_t n, const uint32_t *is_name_bits, uint8_t *out,
+                             uint64_t out_size, uint32_t *out_len, uint8_t *status, void *stream);
+int hhuff_encode_batch_multi(int ndev, const int *devices, int src_device, const uint8_t *in, uint64_t in_size,
+                             const uint32_t *in_off, uint32_t n, uint8_t *out, uint64_t out_size, uint32_t *out_len,
+                             uint8_t *status, void *stream);
+/* The byte-balanced cut (host arrays, no GPU): bounds[0] = 0, bounds[nshards] = n and, for 0 < k < nshards,
+ * bounds[k] = the first string i with in_off[i] >= in_off[0] + floor(k (in_off[n] - in_off[0]) / nshards), rounded
+ * down to a multiple of `align` (0 or 1: no rounding).  Non-decreasing.  With align 1 it equals h2o_amd/dist.py
+ * byte_balanced_bounds (the torch.distributed path's split). */
+int hhuff_shard_bounds(const uint32_t *in_off, uint32_t n, uint32_t nshards, uint32_t align, uint32_t *bounds);
+
 /* ---------------------------------------------------------------------------------------------
  * (4) library info
  * ------------------------------------------------------------------------------------------- */

@@ -82,12 +82,15 @@ import pytest  # noqa: E402
 
 @pytest.mark.gpu
 def test_c_translation_unit_on_the_gpu():
-    """per-string symbols from 8 concurrent threads, a NULL-stream batch, the host API on device 0"""
+    """per-string symbols from 8 concurrent threads, a NULL-stream batch, the host API on device 0, the
+    multi-device batch against the one-device call"""
     import subprocess
 
-    r = subprocess.run([build_capi_check()], capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stdout + r.stderr
-    assert "capi_check: ok" in r.stdout
+    for copy in ("0", "1"):  # HHUFF_MULTI_COPY=1: the multi-device call's peer-copy path on this one GPU
+        r = subprocess.run([build_capi_check()], capture_output=True, text=True, timeout=120,
+                           env=dict(os.environ, HHUFF_MULTI_COPY=copy))
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "capi_check: ok" in r.stdout
 
 
 def test_argument_checks_need_no_gpu():
