@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md); the line also carries the measured copy peak
+GUIDE_COPY_GBPS = 6290.0  # MI355X_MICROARCH.md: 6.29 TB/s measured with a float4 copy kernel (79 % of the spec)
 N_SIMD, N_CU = 1024, 256
 GIB = float(1 << 30)
 METRIC = "GiB/s device-resident Huffman decode+encode, 16M header strings mean 48B"
@@ -297,6 +298,9 @@ def main():
         pmc = pmc_passes(args, n=None if world == 1 else -(-(args.n or synth_n(args.config)) // world))
         if not args.no_extra and world == 1:  # HBM traffic of the other configs' kernels (two passes each)
             pmc_cfg = {c: pmc_passes(args, config=c, groups=(("FETCH_SIZE",), ("WRITE_SIZE",))) for c in ("c2", "c3", "c5")}
+    c_caller = None
+    if not args.pmc_child and not args.no_extra and world == 1:
+        c_caller = per_string_c_caller()  # a child process too, before this one touches the GPU
     import torch
     import torch.distributed as dist
 
@@ -456,8 +460,10 @@ def main():
             roof["secondary"] = sec
         cp = copy_peak(torch)
         if cp:
-            roof["measured_copy_peak"] = cp
-            roof["frac_of_measured"] = round(ach / cp, 4)
+            roof["measured_copy_peak"] = cp  # torch copy_ (the runtime's blit / SDMA copy)
+        # the guide's measured float4 (16 B a lane) copy, MI355X_MICROARCH.md: what a streaming kernel reaches
+        roof["guide_copy_peak"] = GUIDE_COPY_GBPS
+        roof["frac_of_measured"] = round(ach / max(cp or 0.0, GUIDE_COPY_GBPS), 4)
         line = {
             "metric": METRIC,
             "value": round(P_all / GIB / (ms_step * 1e-3), 3),
@@ -512,6 +518,7 @@ def main():
                 line["configs"] = other_configs(torch, codec, synth, pmc_cfg)
                 line["f4"] = f4_lines(torch, codec)
                 line["per_string_latency_us"] = per_string_latency(codec)
+                line["per_string_latency_us"]["c_caller"] = c_caller
             if world == 1 and not args.no_host:
                 line["host_inclusive"] = host_inclusive(b, off32, n, huff, h_off32, n_ok, names_bits, P, H, torch)
             if not args.no_cpu_baseline:  # rank 0's host cores, on a sample of its shard (N > 1 too)
@@ -620,6 +627,25 @@ def f4_lines(torch, codec):
             res[name] = {"error": str(e)}
         torch.cuda.empty_cache()
     return res
+
+
+def per_string_c_caller(threads=(1, 16)):
+    """h2o's per-string symbols called from C the way h2o's event-loop threads call them (tools/per_string_bench:
+    T pthreads, 2,000 encode then 2,000 decode calls each of one 48-B header string): per thread count, the
+    aggregate strings/s and the per-call median / p99 (us).  Run as a child process before the bench touches the
+    GPU; None when the program is not built"""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tools", "per_string_bench")
+    if not os.path.exists(exe):
+        return None
+    try:
+        r = subprocess.run([exe] + [str(t) for t in threads], capture_output=True, text=True, timeout=120,
+                           env=child_env(os.environ))
+        recs = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    except Exception as e:  # a report, not a gate
+        return {"error": str(e)}
+    return {"threads": {str(x.get("threads")): x for x in recs}, "tool": "tools/per_string_bench.c"}
 
 
 def per_string_latency(codec, calls=2000):
