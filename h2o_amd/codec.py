@@ -772,8 +772,9 @@ def set_edge_defer_min(n):
 
 
 def set_decode_kernel(mode):
-    """which kernel decodes contiguous batches (hhuff_set_decode_kernel): 0 (default) the staged / stream choice,
-    1 the segment kernel above a 40-B mean, 2 the segment kernel always; returns the previous mode"""
+    """which kernel decodes contiguous batches (hhuff_set_decode_kernel): 0 (default) the staged / stream choice;
+    1 / 2 (the segment kernel above a 40-B mean / always) only in A/B builds (HhuffError here); returns the
+    previous mode"""
     r = lib().hhuff_set_decode_kernel(int(mode))
     if r < 0:
         _check(r, "hhuff_set_decode_kernel")

@@ -588,9 +588,10 @@ int hhuff_set_decode_prices(int device, const float *in4);
 int hhuff_grid_size(int device, int which /* 0 decode, 1 encode */);
 /* Which kernel decodes contiguous batches (process-wide; the results are the same, only the speed differs):
  * 0 (default) the staged kernels for short strings and the device-side staged / stream choice for mixed and long
- * ones; 1 the segment kernel (a tile's bits shared evenly over a wave's lanes) for a mean Huffman length above
- * 40 B; 2 the segment kernel for every contiguous batch.  The HHUFF_DEC_SEG environment variable sets the start
- * value.  Returns the previous mode, or HHUFF_EINVAL. */
+ * ones.  Modes 1 and 2 (the segment kernel -- a tile's bits shared evenly over a wave's lanes -- above a 40-B mean,
+ * or for every contiguous batch) exist only in A/B builds of the library (tools/ab.py, -DHHUFF_AB_VARIANTS=1; there
+ * HHUFF_DEC_SEG sets the start value): the product library accepts 0 and returns HHUFF_EINVAL for them.
+ * Returns the previous mode, or HHUFF_EINVAL. */
 int hhuff_set_decode_kernel(int mode);
 /* Batches of at least `n` strings leave the 16-B output chunks their tiles share to edge records and a fix-up
  * kernel launched behind the codec kernel; smaller batches store those chunks in the codec kernel (one launch).

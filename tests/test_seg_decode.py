@@ -1,5 +1,7 @@
-"""decode_seg_kernel (segment decode: a tile's bits shared evenly over the lanes, hhuff_kernels.hip) against the
-CPU restatement.  hhuff_set_decode_kernel(2) sends every contiguous batch to it, so the golden sets and short-string
+"""decode_seg_kernel (segment decode: a tile's bits shared evenly over the lanes, tools/ab/hhuff_ab_decoders.h) against
+the CPU restatement.  The segment decoder lost its A/B (DESIGN (e)) and is not in libhhuff.so: these tests skip on the
+product library and run against an A/B build (HHUFF_AB_LIB=build/ab/libhhuff_NAME.so, built with
+-DHHUFF_AB_VARIANTS=1).  hhuff_set_decode_kernel(2) sends every contiguous batch to it, so the golden sets and short-string
 batches run through it too; the cases below aim at its own edges: tiles of more than 64 strings (sub-tiles),
 lanes closing more strings than they can record (the one-lane fallback), empty strings at tile and span ends,
 last strings just under / over the 640-byte keep limit (split lists or one lane), batches not starting at offset
@@ -23,7 +25,10 @@ FAIL = 0xFFFFFFFF
 def decode_kernel(mode):
     from h2o_amd import codec
 
-    prev = codec.set_decode_kernel(mode)
+    try:
+        prev = codec.set_decode_kernel(mode)
+    except codec.HhuffError:  # the segment decoder is A/B-only: run these against such a build via HHUFF_AB_LIB
+        pytest.skip("segment decoder not in this library (tools/ab.py build NAME -DHHUFF_AB_VARIANTS=1)")
     try:
         yield
     finally:

@@ -2,6 +2,7 @@
 """In-process A/B timing of libhhuff builds (MI355X methodology rule: interleaved rounds, one process).
 
     python tools/ab.py build NAME -DFLAG ...     # hipcc the library into build/ab/libhhuff_NAME.so
+                                                  # (-DHHUFF_AB_VARIANTS=1: with the tools/ab variant kernels)
     python tools/ab.py run NAME1 NAME2 ...        # time c4 encode + decode for each build, interleaved
 """
 import ctypes
@@ -20,7 +21,9 @@ def build(name, flags):
 
     os.makedirs(ABDIR, exist_ok=True)
     out = os.path.join(ABDIR, "libhhuff_%s.so" % name)
-    cmd = ["/opt/rocm/bin/hipcc", "-shared"] + hb.HIPCC_FLAGS + flags + ["-I" + os.path.join(ROOT, "include"), "-I" + hb.CSRC] + \
+    # tools/ab holds the variant kernels that are not in libhhuff.so (-DHHUFF_AB_VARIANTS=1 or a flag selecting one)
+    cmd = ["/opt/rocm/bin/hipcc", "-shared"] + hb.HIPCC_FLAGS + flags + ["-I" + os.path.join(ROOT, "include"), "-I" + hb.CSRC,
+                                                                         "-I" + os.path.join(ROOT, "tools", "ab")] + \
         hb.sources() + ["-o", out]
     subprocess.run(cmd, check=True)
     print(out)
