@@ -799,8 +799,15 @@ struct EncV2 {
         const uint32_t sh = tb & 31u;
         const uint64_t u = t >> sh;
         const uint32_t a = obase + ((tb >> 3) & ~3u);
+#if defined(HHUFF_X_ENC_ORW)  // ablation (output wrong by design): plain stores in place of the ORs
+        lds_st32(a, (uint32_t)(u >> 32));
+        lds_st32(a + 4u, (uint32_t)u);
+#elif defined(HHUFF_X_ENC_NOOR)  // ablation: no placement at all (one OR per dword keeps the values live)
+        if (__builtin_amdgcn_ballot_w64((uint32_t)u == 0x12345u) != 0) lds_or32(a, (uint32_t)(u >> 32));
+#else
         lds_or32(a, (uint32_t)(u >> 32));
         lds_or32(a + 4u, (uint32_t)u);
+#endif
         if (__builtin_amdgcn_ballot_w64(sh + nf > 64u) != 0) {
             if (sh + nf > 64u) lds_or32(a + 8u, (uint32_t)t << (32u - sh));
         }
@@ -842,7 +849,23 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
             const uint32_t w = wn;
             wn = sw[min(j + 1u, jlast)];
             const uint32_t onm = ~(uint32_t)((int32_t)((j - jf) | (jlv - 1u - j)) >> 31);  // jf <= j < jlv
+#if defined(HHUFF_X_ENC_TABCF)  // ablation (output wrong by design): conflict-free table reads (entry = lane % 32 + 32)
+            const uint32_t lq = (uint32_t)(__lane_id() & 31) + 32u + (w & 0u);
+            E.put4m(enc[lq], enc[lq ^ 1u], enc[lq ^ 2u], enc[lq ^ 3u], onm);
+#elif defined(HHUFF_X_ENC_TABDEP) || defined(HHUFF_X_ENC_TABBC)
+            // ablations: the same conflict-free (TABDEP) / single-entry broadcast (TABBC) reads, still dependent on the
+            // input word (an opaque zero from it), so the input reads and the chain stay
+            uint32_t z;
+            __asm__ volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(w));
+#if defined(HHUFF_X_ENC_TABDEP)
+            const uint32_t lq = (uint32_t)(__lane_id() & 31) + 32u + z;
+#else
+            const uint32_t lq = 0x61u + z;
+#endif
+            E.put4m(enc[lq], enc[lq ^ 1u], enc[lq ^ 2u], enc[lq ^ 3u], onm);
+#else
             E.put4m(enc[w & 0xFFu], enc[(w >> 8) & 0xFFu], enc[(w >> 16) & 0xFFu], enc[w >> 24], onm);
+#endif
         }
     }
     E.fail = E.fail || (E.live && E.tb >= E.tlim);
