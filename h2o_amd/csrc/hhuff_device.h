@@ -738,19 +738,29 @@ __device__ __forceinline__ uint32_t encode_chunk(const uint32_t* stage, uint32_t
 // last, partial dword).  Head and tail use the masked lookups (entries 256..511 are zero); bulk steps
 // run for lanes inside their whole-dword range with the others switched off (exec mask).
 // ---------------------------------------------------------------------------------------------------
-__device__ __forceinline__ void place_bits(uint32_t obase, uint32_t tb, uint64_t c, uint32_t n) {
+// The output stage is addressed either by its LDS byte address (uint32_t) or by a word pointer derived from the
+// __shared__ array itself (uint32_t*): with the pointer the compiler can tell the stage from other LDS objects
+// (an LDS-DMA in flight into another buffer then needs no wait before an OR; round 6's double-buffered framing
+// kernel used it, and lost: profiles/r06h_flatten_double_buffer_ab.jsonl).
+__device__ __forceinline__ void or_word(uint32_t obase, uint32_t wi, uint32_t v) { lds_or32(obase + 4u * wi, v); }
+__device__ __forceinline__ void or_word(uint32_t* o32, uint32_t wi, uint32_t v) {
+    __hip_atomic_fetch_or(o32 + wi, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <class O>
+__device__ __forceinline__ void place_bits(O obase, uint32_t tb, uint64_t c, uint32_t n) {
     const uint64_t t = c << ((64u - n) & 63u);  // left-aligned (n == 0 needs c == 0)
     const uint32_t sh = tb & 31u;
     const uint64_t u = t >> sh;
-    const uint32_t a = obase + ((tb >> 3) & ~3u);
-    lds_or32(a, (uint32_t)(u >> 32));
-    lds_or32(a + 4u, (uint32_t)u);
-    if (sh + n > 64u) lds_or32(a + 8u, (uint32_t)t << (32u - sh));  // sh > 0 here
+    const uint32_t a = tb >> 5;
+    or_word(obase, a, (uint32_t)(u >> 32));
+    or_word(obase, a + 1u, (uint32_t)u);
+    if (sh + n > 64u) or_word(obase, a + 2u, (uint32_t)t << (32u - sh));  // sh > 0 here
 }
 
+template <class O>
 struct EncV2 {
     const uint2* enc;
-    uint32_t obase;  // LDS byte address of the MSB-first output stage
+    O obase;  // the MSB-first output stage: LDS byte address or word pointer (see or_word)
     uint32_t tb;     // next stage bit
     uint32_t tlim;   // stage bit at which the string fails (~0: no limit)
     bool live, fail;
@@ -798,18 +808,15 @@ struct EncV2 {
         const uint64_t t = cc << ((64u - nf) & 63u);
         const uint32_t sh = tb & 31u;
         const uint64_t u = t >> sh;
-        const uint32_t a = obase + ((tb >> 3) & ~3u);
-#if defined(HHUFF_X_ENC_ORW)  // ablation (output wrong by design): plain stores in place of the ORs
-        lds_st32(a, (uint32_t)(u >> 32));
-        lds_st32(a + 4u, (uint32_t)u);
-#elif defined(HHUFF_X_ENC_NOOR)  // ablation: no placement at all (one OR per dword keeps the values live)
-        if (__builtin_amdgcn_ballot_w64((uint32_t)u == 0x12345u) != 0) lds_or32(a, (uint32_t)(u >> 32));
+        const uint32_t a = tb >> 5;
+#if defined(HHUFF_X_ENC_NOOR)  // ablation (output wrong by design): no placement (one OR keeps the values live)
+        if (__builtin_amdgcn_ballot_w64((uint32_t)u == 0x12345u) != 0) or_word(obase, a, (uint32_t)(u >> 32));
 #else
-        lds_or32(a, (uint32_t)(u >> 32));
-        lds_or32(a + 4u, (uint32_t)u);
+        or_word(obase, a, (uint32_t)(u >> 32));
+        or_word(obase, a + 1u, (uint32_t)u);
 #endif
         if (__builtin_amdgcn_ballot_w64(sh + nf > 64u) != 0) {
-            if (sh + nf > 64u) lds_or32(a + 8u, (uint32_t)t << (32u - sh));
+            if (sh + nf > 64u) or_word(obase, a + 2u, (uint32_t)t << (32u - sh));
         }
         tb += nm;
     }
@@ -817,8 +824,9 @@ struct EncV2 {
 
 // Encode stage bytes [start, start + len) to stage bit `startbit` of the MSB-first output stage at LDS
 // byte address `obase`.  `limit`, `pad`: as encode_chunk.  Returns the code bits or kFailLen.
+template <class O>
 __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
-                                                    bool active, uint32_t obase, uint32_t startbit,
+                                                    bool active, O obase, uint32_t startbit,
                                                     const uint2* __restrict__ enc, uint32_t limit, bool pad) {
     const uint32_t end = start + len;
     const uint32_t a0 = start & ~3u;
@@ -828,7 +836,7 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
     const uint32_t mfirst = 0xFFFFFFFFu << (8u * (start & 3u));
     const uint32_t mlast = (uint32_t)(0xFFFFFFFFull >> ((32u - 8u * (end & 3u)) & 31u));
     // tlim < 2^31 keeps tb + n - tlim a signed quantity (stage bits are < 2^20)
-    EncV2 E{enc, obase, startbit, limit >= 0x40000000u ? 0x7FFFFFFFu : startbit + limit, active, false};
+    EncV2<O> E{enc, obase, startbit, limit >= 0x40000000u ? 0x7FFFFFFFu : startbit + limit, active, false};
     auto masked = [&](uint32_t j, bool on) {  // one dword with byte masks (head / tail)
         const uint32_t w = stage[min(a0 + 4u * j, last) >> 2];
         uint32_t vm = j == 0 ? mfirst : 0xFFFFFFFFu;

@@ -3052,6 +3052,7 @@ constexpr int kDecSWaves = 16, kEncSWaves = 16;
 #define FLAT_D flatten_direct_kernel<4>
 #define ENC_P encode_pl_kernel<16, kPlStage>
 #define FLAT_P flatten_pl_kernel<16, kPlStage>
+#define FLAT_P_THREADS 1024
 
 enum Variant { kDecS, kDecL, kDecD, kEncS, kEncL, kEncD, kFlatD, kEncP, kFlatP, kDecT, kDecSP, kDecLP, kEncSP, kEncLP,
                kEncO, kNumVariants };
@@ -3087,8 +3088,8 @@ static int variant_threads(int v) {
         case kEncL:
         case kEncLP: return 512;
         case kEncO: return kEncOThreads;
-        case kEncP:
-        case kFlatP: return 1024;
+        case kEncP: return 1024;
+        case kFlatP: return FLAT_P_THREADS;
         default: return 256;
     }
 }
@@ -4455,14 +4456,14 @@ hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* i
         const uint32_t kmin = sample ? kPlCand[5] : K;
         const uint64_t tiles = ((uint64_t)n + kmin - 1) / kmin;
         const int g = grid_for(kFlatP, current_device(), 0xFFFFFFFFu);
-        const uint64_t want = (tiles + 15) / 16;
+        const uint64_t want = (tiles + FLAT_P_THREADS / 64 - 1) / (FLAT_P_THREADS / 64);
         const int grid = (int)(want < (uint64_t)g ? (want ? want : 1) : g);
         const bool defer = defer_edges(n);  // else edges stored in the kernel, one launch
         const uint64_t recs = defer ? 2 * tiles : 0;  // deferred edges (see encode_pl_kernel)
         hipError_t e = defer ? pool_alloc((void**)&A.edges, recs * sizeof(EdgeRec), stream) : hipSuccess;
         if (e != hipSuccess) return e;
         if (!sample) {
-            hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)nullptr, recs);
+            hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(FLAT_P_THREADS), 0, stream, A, K, (const uint32_t*)nullptr, recs);
             return defer ? finish_deferred(out, A.edges, n, stream, nullptr, recs) : hipGetLastError();
         }
         uint32_t* part = nullptr;
@@ -4472,7 +4473,7 @@ hipError_t launch_flatten(const uint8_t* in, uint64_t in_size, const uint32_t* i
             e = hipGetLastError();
         }
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(1024), 0, stream, A, K, (const uint32_t*)part, recs);
+            hipLaunchKernelGGL(FLAT_P, dim3(grid), dim3(FLAT_P_THREADS), 0, stream, A, K, (const uint32_t*)part, recs);
             e = hipGetLastError();
         }
         if (part) {
