@@ -12,7 +12,8 @@ Fixture sets (numpy .npz, arrays only, no pickles):
                    blocks, our own HPACK walker), decoded by the reference; raw literals encoded by it
   random_<cfg>.npz seeded synthetic batches per benchmark configuration (h2o_amd/synth.py), encoded and
                    re-decoded by the reference, plus the plain bytes decoded as (mostly invalid) Huffman
-  adversarial.npz  hand-built decode edge cases (padding, EOS, truncation, long codes, names/values)
+  adversarial.npz  hand-built decode edge cases (padding, EOS, truncation, long codes, names/values) and encode
+                   edge cases ('X'-only strings, the ceil(bits / 8) < len verdict's edge, long codes, every byte)
   framing.npz      HPACK h2o_hpack_encode_string and QPACK flatten_string (prefix 3/5/7) outputs
   resp.npz         response header blocks / sections as h2o's clients parse them (h2o_hpack_parse_response,
                    h2o_qpack_parse_response run by the reference itself): verdicts, records, fields
@@ -300,6 +301,34 @@ def adversarial_set(seed=7):
         cases.append(int(bits, 2).to_bytes(len(bits) // 8, "big"))
     is_name = rng.random(len(cases)) < 0.5
     return ref_decode_set(cases, is_name)
+
+
+def adversarial_encode_strings(seed=8):
+    """encode edge cases, verdicts from the compiled reference (h2o_hpack_encode_huffman, hpack.c:774-804):
+    'X'-only strings, which never compress ('X' is an 8-bit code: t/40http3/test.pl:194 relies on it); strings
+    at the verdict's edge (hpack.c:799-800: ceil(bits / 8) < len passes, == len fails), built from 5-bit and
+    8-bit symbols so the total is 8n - 9 .. 8n - 1 bits; long-code-only strings (control bytes, 0x80+, up to 30-bit
+    codes); every single byte; the empty string; all 256 bytes in a row; and random mixes"""
+    rng = np.random.default_rng(seed)
+    out = [b"", bytes(range(256)), bytes(range(255, -1, -1))]
+    out += [b"X" * L for L in range(0, 300, 7)] + [b"X" * 4096]
+    out += [bytes([b]) for b in range(256)]
+    for n in range(2, 60):
+        for k in range(0, 9):  # n - k symbols 'X' (8 bits) and k symbols 'a' (5 bits): 8n - 3k bits
+            if k <= n:
+                out.append(b"X" * (n - k) + b"a" * k)
+                out.append(bytes(rng.permutation(list(b"X" * (n - k) + b"a" * k)).astype(np.uint8)))
+    for _ in range(400):
+        L = int(rng.integers(1, 64))
+        out.append(bytes(rng.choice(np.r_[0:32, 127:256], L).astype(np.uint8)))
+    syms, p = synth.header_alphabet()
+    for _ in range(600):
+        L = int(rng.integers(1, 200))
+        a = rng.choice(syms, L, p=p).astype(np.uint8)
+        bad = rng.random(L) < rng.choice([0.0, 0.05, 0.3, 1.0])
+        a[bad] = rng.integers(0, 256, int(bad.sum()), dtype=np.uint8)
+        out.append(bytes(a))
+    return out
 
 
 def framing_set(seed=11):
@@ -919,6 +948,14 @@ def main():
     if "--only-qpenc" in sys.argv:
         np.savez_compressed(os.path.join(GOLDEN, "qpenc.npz"), **qpenc_set())
         return
+    if "--only-adversarial-encode" in sys.argv:  # add the encode vectors to adversarial.npz, decode ones unchanged
+        path = os.path.join(GOLDEN, "adversarial.npz")
+        with np.load(path, allow_pickle=False) as z:
+            arrays = {k: z[k] for k in z.files if not k.startswith("enc_")}
+        arrays.update(ref_encode_set(adversarial_encode_strings()))
+        np.savez_compressed(path, **arrays)
+        print("adversarial: encode %d" % len(arrays["enc_len"]))
+        return
     if "--only-hpenc" in sys.argv:
         np.savez_compressed(os.path.join(GOLDEN, "hpenc.npz"), **hpenc_set())
         return
@@ -940,6 +977,7 @@ def main():
     for cfg, n, seed in (("c2", 3000, 101), ("c3", 1200, 102), ("c4", 3000, 103), ("c5", 300, 104)):
         sets["random_" + cfg] = random_set(cfg, n, seed)
     sets["adversarial"] = adversarial_set()
+    sets["adversarial"].update(ref_encode_set(adversarial_encode_strings()))
     sets["framing"] = framing_set()
     sets["literals"] = literals_set()
     sets.update(blocks_sets())

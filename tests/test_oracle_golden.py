@@ -141,3 +141,29 @@ def test_oracle_literals_match_golden(oracle_codec):
     # every verdict the API defines is exercised by the fixture
     codes = set(((g["h_status"][g["h_status"] >= 0x80] >> 2) & 7).tolist())
     assert {1, 2, 3, 4, 5} <= codes
+
+
+def test_adversarial_encode_fixture_covers_the_rules():
+    """the reference's encode verdicts in adversarial.npz: every 'X'-only string stays raw ('X' is an 8-bit code,
+    never shorter: t/40http3/test.pl:194), and both sides of hpack.c:799-800's edge occur (a string whose code
+    bits are 8 len - 8 compresses to len - 1 bytes, one at 8 len - 7 .. 8 len does not)"""
+    g = load_golden("adversarial")
+    strings = synth.unpack(g["enc_in"], g["enc_in_off"])
+    el = g["enc_len"]
+    xs = [i for i, s in enumerate(strings) if s and set(s) == {ord("X")}]
+    assert len(xs) > 10 and all(el[i] == 0xFFFFFFFF for i in xs)
+    from h2o_amd import tables as T
+
+    nb = np.asarray(T.ENC_NBITS)
+    edge_ok = edge_fail = 0
+    for s, L in zip(strings, el):
+        if not s:
+            continue
+        bits = int(nb[np.frombuffer(s, np.uint8)].sum())
+        if bits == 8 * len(s) - 8:
+            assert L == len(s) - 1
+            edge_ok += 1
+        elif 8 * len(s) - 7 <= bits <= 8 * len(s):
+            assert L == 0xFFFFFFFF
+            edge_fail += 1
+    assert edge_ok > 0 and edge_fail > 0
