@@ -433,6 +433,9 @@ __device__ __forceinline__ void lds_zero(uint8_t* base, uint32_t a, uint32_t b, 
 // the lane's next symbols or lie past its decoded length inside its slot (5 symbols' room), so the stores need
 // no redirection of untaken bytes to a trash byte (c4 decode -7 % against that; one unaligned ds_write_b16 for
 // both bytes was measured too: 0.66 -> 0.98 ms).
+#ifndef HHUFF_DEC_READ_FIRST  // 1 (default): a bulk step's second LUT read goes to the LDS ahead of the first entry's
+#define HHUFF_DEC_READ_FIRST 1   // byte stores: c4 decode -0.6 %, c3 -0.9 % (profiles/r06m_decode_read_first_ab.jsonl)
+#endif
 __device__ __forceinline__ void bulk_put2(uint32_t o, uint32_t e, uint32_t trash) {
     (void)trash;
     lds_st8(o, e);
@@ -476,10 +479,23 @@ __device__ __forceinline__ DecResult decode_staged_lane_v7(const uint32_t* stage
             const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
             const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
             const uint32_t sl = (uint32_t)((int32_t)e >> 31);  // LONG: nothing taken from the window
+            uint32_t cons = lut_l12(e);  // LONG entries carry L12 = 0
+#if HHUFF_DEC_READ_FIRST
+            {  // the second lookup goes to the LDS ahead of the first entry's byte stores (in-order LDS queue)
+                const uint32_t wb = w << cons;
+                const uint32_t eb = T.lut[wb >> (32 - HHUFF_LUT_BITS)];
+                bulk_put2(o, e, trash);
+                o += (e >> 28) & 3u;
+                accb |= e;
+                bulk_put2(o, eb, trash);
+                o += (eb >> 28) & 3u;
+                accb |= eb;
+                cons += lut_l12(eb);
+            }
+#else
             bulk_put2(o, e, trash);
             o += (e >> 28) & 3u;
             accb |= e;
-            uint32_t cons = lut_l12(e);  // LONG entries carry L12 = 0
             {
                 const uint32_t wb = w << cons;
                 const uint32_t eb = T.lut[wb >> (32 - HHUFF_LUT_BITS)];
@@ -488,6 +504,7 @@ __device__ __forceinline__ DecResult decode_staged_lane_v7(const uint32_t* stage
                 accb |= eb;
                 cons += lut_l12(eb);
             }
+#endif
             if (longchk && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
                 if (sl) {
                     const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);

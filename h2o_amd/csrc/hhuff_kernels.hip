@@ -1422,10 +1422,23 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                 const uint32_t w = __builtin_amdgcn_alignbit(x0, x1, ~(uint32_t)pm);
                 const uint32_t e = T.lut[w >> (32 - HHUFF_LUT_BITS)];
                 const uint32_t sl = (uint32_t)((int32_t)e >> 31);
+                uint32_t cons = lut_l12(e);  // LONG entries carry L12 = 0
+#if HHUFF_DEC_READ_FIRST
+                {  // the second lookup ahead of the first entry's byte stores (decode_staged_lane_v7)
+                    const uint32_t wb2 = w << cons;
+                    const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
+                    bulk_put2(o, e, trash);
+                    o += (e >> 28) & 3u;
+                    accb |= e;
+                    bulk_put2(o, eb, trash);
+                    o += (eb >> 28) & 3u;
+                    accb |= eb;
+                    cons += lut_l12(eb);
+                }
+#else
                 bulk_put2(o, e, trash);
                 o += (e >> 28) & 3u;
                 accb |= e;
-                uint32_t cons = lut_l12(e);  // LONG entries carry L12 = 0
                 {
                     const uint32_t wb2 = w << cons;
                     const uint32_t eb = T.lut[wb2 >> (32 - HHUFF_LUT_BITS)];
@@ -1434,6 +1447,7 @@ __global__ __launch_bounds__(WAVES * 64) void decode_stream_kernel(DecArgs A, un
                     accb |= eb;
                     cons += lut_l12(eb);
                 }
+#endif
                 if (longchk && __builtin_amdgcn_ballot_w64(sl != 0u) != 0) {
                     if (sl) {
                         const uint32_t k = min((uint32_t)__builtin_clz(~w | 1u), 30u);
