@@ -164,3 +164,46 @@ def test_multi_device_mode_is_stream_ordered(torch_cuda):
     ref = codec.encode_batch(d, o, n)[1]
     torch.cuda.synchronize()
     assert torch.equal(snap[:n], ref[:n])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["device", "device_copy", "host"])
+def test_multi_sub_batch_and_small_batches(torch_cuda, mode):
+    """offsets that do not start at 0 (a sub-range of a larger buffer), batches smaller than a shard's 64-string
+    unit (everything lands on the last device), and an encode without status: the one-device call's results"""
+    from h2o_amd import codec
+
+    torch = torch_cuda
+    data, off, names, n = _batch("c2", 5000, 41)
+    dev = lambda a: torch.from_numpy(a.view(np.int32) if a.dtype == np.uint32 else a).cuda()  # noqa: E731
+    if mode == "device_copy":
+        os.environ["HHUFF_MULTI_COPY"] = "1"
+    try:
+        for lo, m in ((37, 4000), (1000, 50), (0, 1), (4999, 1)):
+            sub = np.ascontiguousarray(off[lo:lo + m + 1])
+            e1, el1, _ = codec.encode_batch(dev(data), dev(sub), m, in_size=data.size)
+            torch.cuda.synchronize()
+            el1 = el1.cpu().numpy().view(np.uint32)[:m]
+            e1 = e1.cpu().numpy()
+            if mode == "host":
+                out = np.zeros(data.size + 16, np.uint8)
+                ln = np.zeros(m, np.uint32)
+                rc = codec.lib().hhuff_encode_batch_multi(3, codec._devs([0, 0, 0])[1], codec.HOST_MEMORY,
+                                                          data.ctypes.data, data.size, sub.ctypes.data, m,
+                                                          out.ctypes.data, out.size, ln.ctypes.data, None, None)
+                assert rc == 0, codec.lib().hhuff_last_error_string()
+                e2, el2 = out, ln
+            else:
+                d_out = torch.empty(data.size + 16, dtype=torch.uint8, device="cuda")
+                d_ln = torch.empty(m, dtype=torch.int32, device="cuda")
+                dd, ds = dev(data), dev(sub)
+                rc = codec.lib().hhuff_encode_batch_multi(3, codec._devs([0, 0, 0])[1], 0, dd.data_ptr(), data.size,
+                                                          ds.data_ptr(), m, d_out.data_ptr(), d_out.numel(),
+                                                          d_ln.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+                assert rc == 0, codec.lib().hhuff_last_error_string()
+                torch.cuda.synchronize()
+                e2, el2 = d_out.cpu().numpy(), d_ln.cpu().numpy().view(np.uint32)
+            np.testing.assert_array_equal(el2, el1)
+            assert _kept(e2, sub, el2, False) == _kept(e1, sub, el1, False)
+    finally:
+        os.environ.pop("HHUFF_MULTI_COPY", None)
