@@ -841,7 +841,14 @@ struct EncV2 {
 
 // Encode stage bytes [start, start + len) to stage bit `startbit` of the MSB-first output stage at LDS
 // byte address `obase`.  `limit`, `pad`: as encode_chunk.  Returns the code bits or kFailLen.
-template <class O>
+#ifndef HHUFF_ENC_SORTED_U  // whole dwords a bulk-loop trip (encode_chunk_v2's U) in the sorted encoder
+#define HHUFF_ENC_SORTED_U 1
+#endif
+#ifndef HHUFF_ENC_OTHER_U   // ... and in the staged / proportional-lane encoders and the framing kernel
+#define HHUFF_ENC_OTHER_U 1
+#endif
+// U: whole dwords a trip of the bulk loop (1 or 2; the loop's ballots keep the compiler from unrolling it)
+template <int U = 1, class O>
 __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint32_t last, uint32_t start, uint32_t len,
                                                     bool active, O obase, uint32_t startbit,
                                                     const uint2* __restrict__ enc, uint32_t limit, bool pad) {
@@ -870,7 +877,18 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
         const uint32_t jlv = E.live ? jl : 0u;  // a lane that failed in its head places nothing more
         const uint32_t jend = wave_max_u32(jlv);  // uniform trip count: no vote per step
         uint32_t wn = sw[min(0u, jlast)];
-        for (uint32_t j = 0; j < jend; ++j) {  // bulk
+        // U == 2: the extra dword past jend has onm == 0 (jlv <= jend) and a clamped read
+        if constexpr (U == 2) for (uint32_t j = 0; j < jend; j += 2) {
+            const uint32_t w0 = wn, w1 = sw[min(j + 1u, jlast)];
+            wn = sw[min(j + 2u, jlast)];
+            const uint32_t m0 = ~(uint32_t)((int32_t)((j - jf) | (jlv - 1u - j)) >> 31);
+            const uint32_t m1 = ~(uint32_t)((int32_t)((j + 1u - jf) | (jlv - 2u - j)) >> 31);
+            const uint2 a0 = enc[w0 & 0xFFu], a1 = enc[(w0 >> 8) & 0xFFu], a2 = enc[(w0 >> 16) & 0xFFu], a3 = enc[w0 >> 24];
+            const uint2 b0 = enc[w1 & 0xFFu], b1 = enc[(w1 >> 8) & 0xFFu], b2 = enc[(w1 >> 16) & 0xFFu], b3 = enc[w1 >> 24];
+            E.put4m(a0, a1, a2, a3, m0);
+            E.put4m(b0, b1, b2, b3, m1);
+        }
+        else for (uint32_t j = 0; j < jend; ++j) {  // bulk
             const uint32_t w = wn;
             wn = sw[min(j + 1u, jlast)];
             const uint32_t onm = ~(uint32_t)((int32_t)((j - jf) | (jlv - 1u - j)) >> 31);  // jf <= j < jlv

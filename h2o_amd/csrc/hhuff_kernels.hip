@@ -1762,7 +1762,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_staged_kernel(EncArgs A) {
                 const bool act = t.valid && t.len != 0 && t.len <= kMaxStrLen;
                 const uint32_t rel = t.len ? t.s - cur.a0 : 0u;
                 const uint32_t last = cur.span ? cur.span - 4u : 0u;
-                const uint32_t tb = encode_chunk_v2(stage, last, rel, t.len, act, lds_addr(obuf32), 8u * cur.op0, s_enc,
+                const uint32_t tb = encode_chunk_v2<HHUFF_ENC_OTHER_U>(stage, last, rel, t.len, act, lds_addr(obuf32), 8u * cur.op0, s_enc,
                                                     act ? 8 * t.len - 7 : 0xFFFFFFFFu, true);
                 const uint32_t r = tb == kFailLen ? kFailLen : (tb + 7) >> 3;
                 if (act) ol = r;
@@ -2055,7 +2055,7 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
             const uint2 sj = s_str[j];
             const bool vj = cb + j < A.n;
             const bool act = vj && sj.y != 0 && sj.y <= kMaxStrLen;
-            const uint32_t tb = encode_chunk_v2(s_in, span - 4u, sj.x, sj.y, act, lds_addr(s_out), 8u * sj.x, s_enc,
+            const uint32_t tb = encode_chunk_v2<HHUFF_ENC_SORTED_U>(s_in, span - 4u, sj.x, sj.y, act, lds_addr(s_out), 8u * sj.x, s_enc,
                                                 act ? 8 * sj.y - 7 : 0xFFFFFFFFu, true);
             // the encoded length goes back to the string's own record (read by its own thread only), so the
             // lengths and statuses are stored in string order, coalesced
@@ -2340,7 +2340,7 @@ __global__ __launch_bounds__(WAVES * 64) void encode_pl_kernel(EncArgs A, uint32
             }
             // pass 2: the shares' codes OR-ed into the MSB-first output stage (encode_chunk_v2); the share
             // holding the string's end pads it
-            const uint32_t r = encode_chunk_v2(stage, last, cs, clen, big && !sfail && clen != 0, lds_addr(obuf32),
+            const uint32_t r = encode_chunk_v2<HHUFF_ENC_OTHER_U>(stage, last, cs, clen, big && !sfail && clen != 0, lds_addr(obuf32),
                                                8u * (sj - cur.a0) + off, s_enc, multi ? 0xFFFFFFFFu : 8u * lj - 7u,
                                                c1 == lj);
             uint32_t res = kFailLen;  // verdict of this lane's string, as seen by the string's first lane
@@ -2681,7 +2681,7 @@ __global__ __launch_bounds__(WAVES * 64) void flatten_pl_kernel(FlatArgs A, uint
             if (ok && sub == 0)
                 for (uint32_t k = 0; k < hn; ++k) obuf[(orel + k) ^ 3u] = (uint8_t)(hb >> (8 * k));
             // pass 2: Huffman shares place their code bits; raw shares copy their bytes
-            encode_chunk_v2(stage, last, cs, clen, huff && clen != 0, lds_addr(obuf32), 8u * (orel + hn) + (x - xs), s_enc,
+            encode_chunk_v2<HHUFF_ENC_OTHER_U>(stage, last, cs, clen, huff && clen != 0, lds_addr(obuf32), 8u * (orel + hn) + (x - xs), s_enc,
                             0xFFFFFFFFu, c1 == lj);
             PROF_MARK(3);
             if (ok && !huff && clen) {
