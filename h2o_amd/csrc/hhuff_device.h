@@ -774,6 +774,10 @@ __device__ __forceinline__ void place_bits(O obase, uint32_t tb, uint64_t c, uin
     if (sh + n > 64u) or_word(obase, a + 2u, (uint32_t)t << (32u - sh));  // sh > 0 here
 }
 
+#ifndef HHUFF_ENC_OR3  // encode_chunk_v2's bulk step: the third output word ORed on every step (see put4m)
+#define HHUFF_ENC_OR3 0
+#endif
+
 template <class O>
 struct EncV2 {
     const uint2* enc;
@@ -832,9 +836,13 @@ struct EncV2 {
         or_word(obase, a, (uint32_t)(u >> 32));
         or_word(obase, a + 1u, (uint32_t)u);
 #endif
+#if HHUFF_ENC_OR3  // the third word's OR on every step (0 where nothing spills into it): no vote, no branch
+        or_word(obase, a + 2u, sh + nf > 64u ? (uint32_t)t << ((32u - sh) & 31u) : 0u);
+#else
         if (__builtin_amdgcn_ballot_w64(sh + nf > 64u) != 0) {
             if (sh + nf > 64u) or_word(obase, a + 2u, (uint32_t)t << (32u - sh));
         }
+#endif
         tb += nm;
     }
 };
