@@ -536,6 +536,9 @@ __device__ __forceinline__ void decode_direct(const DecArgs& A, uint32_t s, uint
 // never overwrite a source another lane still needs.  The next tile's input then goes into the other
 // half, beside the packed run, before the run's 16-B stores are issued (the pipeline order of the slot
 // layout, whose commit also precedes the stores).
+#ifndef HHUFF_DEC_TI_TOP  // decode_staged_kernel: the tile-after-next's offsets issued at the loop top, consumed in
+#define HHUFF_DEC_TI_TOP 1   // the same trip (c4 decode -2.2 %, c2 -1.5 %; profiles/r06v_decode_ti_top_ab.jsonl)
+#endif
 template <int WAVES, int IN_STAGE, int OUT_STAGE, bool PACKED>
 __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
     constexpr uint32_t Z = IN_STAGE + OUT_STAGE + 256u;  // + 16 slack: the run's last 16-B chunk may read past Z
@@ -634,11 +637,19 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         nxt = plan(base + stride, ti, PACKED ? 1u : 0u);
         nxt_name = ti.name_word;
         if (nxt.fits) pf.issue(A.in, A.in_size, nxt.a0(), nxt.span(), lane);
+#if !HHUFF_DEC_TI_TOP
         ti = issue_tile(base + 2 * stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
+#endif
     }
     PROF_DECL
     for (;;) {
         const uint64_t nbase = base + stride;
+#if HHUFF_DEC_TI_TOP
+        // the offsets of the tile after next, issued at the top and consumed at this tile's plan step below: no
+        // loaded register lives across the loop's back edge, where a PHI copy would wait for it behind this
+        // tile's stores (the ISA had s_waitcnt vmcnt(3) / (2) there, in front of two such copies)
+        ti = issue_tile(nbase + stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
+#endif
         // ---- the current tile: steps and verdicts ----
         const Plan& t = cur;
         const uint32_t ti_i = (uint32_t)base + (uint32_t)lane;
@@ -751,7 +762,9 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
         nn = plan(nbase + stride, ti, PACKED ? par : 0u);
         nn_name = ti.name_word;
         if (have_nn && nn.fits) pf.issue(A.in, A.in_size, nn.a0(), nn.span(), lane);
+#if !HHUFF_DEC_TI_TOP
         ti = issue_tile(nbase + 2 * stride, lane, A.n, A.in_off, A.in_len, A.is_name_bits, A.out_off);
+#endif
         PROF_MARK(3);  // commit + plan
         // ---- the current tile: stores ----
 #if defined(HHUFF_X_NOSTORE) || defined(HHUFF_X_NOSTORE_OUT)  // ablations (output wrong by design): no output stores
