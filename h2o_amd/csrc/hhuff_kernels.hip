@@ -339,12 +339,12 @@ __device__ __forceinline__ void edge_bytes(uint8_t* __restrict__ out, uint64_t g
     if ((lane < 16 || kl != 0) && part && G >= keep_lo && G < keep_hi) out[G] = lds[k + (SWAP ? b ^ 3u : b)];
 }
 // SWAP: the LDS bytes are MSB-first words (the encode stage), byte-swapped in registers on the way out.
-template <int NCH, bool SWAP = false>
+// G: the LDS reads of G chunks ahead of their stores (one LDS round trip per G chunks; 4 (G - 1) more VGPRs)
+template <int NCH, bool SWAP = false, int G = 1>
 __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t gbase, const uint8_t* lds, uint32_t ospan,
                                             uint64_t keep_lo, uint64_t keep_hi, int lane) {
-    for (uint32_t k = (uint32_t)lane * 16u; k < ospan; k += 64u * 16u) {
+    auto put = [&](uint32_t k, uint4 v) {
         const uint64_t g = gbase + k;
-        uint4 v = *reinterpret_cast<const uint4*>(lds + k);
         if (SWAP) v = make_uint4(bswap32(v.x), bswap32(v.y), bswap32(v.z), bswap32(v.w));
         if (g >= keep_lo && g + 16 <= keep_hi) {
             st16_out(out + g, v);
@@ -352,6 +352,19 @@ __device__ __forceinline__ void region_copy(uint8_t* __restrict__ out, uint64_t 
             const uint32_t lo = keep_lo > g ? (uint32_t)min(keep_lo - g, (uint64_t)16) : 0u;
             const uint32_t hi = keep_hi > g ? (uint32_t)min(keep_hi - g, (uint64_t)16) : 0u;
             if (hi > lo) store_range16r(out + g, v, lo, hi);
+        }
+    };
+    for (uint32_t k = (uint32_t)lane * 16u; k < ospan; k += (uint32_t)G * 64u * 16u) {
+        uint4 v[G];
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const uint32_t kj = k + (uint32_t)j * 64u * 16u;
+            v[j] = kj < ospan ? *reinterpret_cast<const uint4*>(lds + kj) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+            const uint32_t kj = k + (uint32_t)j * 64u * 16u;
+            if (kj < ospan) put(kj, v[j]);
         }
     }
     if (HHUFF_EDGE_BYTES) edge_bytes<SWAP>(out, gbase, lds, ospan, keep_lo, keep_hi, lane);
@@ -536,6 +549,9 @@ __device__ __forceinline__ void decode_direct(const DecArgs& A, uint32_t s, uint
 // never overwrite a source another lane still needs.  The next tile's input then goes into the other
 // half, beside the packed run, before the run's 16-B stores are issued (the pipeline order of the slot
 // layout, whose commit also precedes the stores).
+#ifndef HHUFF_DEC_COPY_G  // decode_staged_kernel's slot-layout copy-out: chunks whose LDS reads go ahead of their stores
+#define HHUFF_DEC_COPY_G 1
+#endif
 #ifndef HHUFF_DEC_TI_TOP  // decode_staged_kernel: the tile-after-next's offsets issued at the loop top, consumed in
 #define HHUFF_DEC_TI_TOP 1   // the same trip (c4 decode -2.2 %, c2 -1.5 %; profiles/r06v_decode_ti_top_ab.jsonl)
 #endif
@@ -785,7 +801,8 @@ __global__ __launch_bounds__(WAVES * 64) void decode_staged_kernel(DecArgs A) {
                     region_copy_deferred(A.out, cur.obase(), obuf, cur.ospan, cur.olo(), cur.ohi(), lane,
                                          A.edges + 2 * (base >> 6));
                 else
-                    region_copy<(OUT_STAGE + 1023) / 1024>(A.out, cur.obase(), obuf, cur.ospan, cur.olo(), cur.ohi(), lane);
+                    region_copy<(OUT_STAGE + 1023) / 1024, false, HHUFF_DEC_COPY_G>(A.out, cur.obase(), obuf, cur.ospan,
+                                                                                           cur.olo(), cur.ohi(), lane);
             } else if (t.valid && ol != kFailLen) {
                 lane_copy(A.out + cur.dst_g, obuf + cur.op0, ol);
             }
@@ -1886,6 +1903,9 @@ __device__ __forceinline__ SortChunk sort_chunk_issue(const EncArgs& A, uint64_t
     return SortChunk{A.in_off[ic], A.in_off[ic + 1], A.in_off[min(cb, (uint64_t)A.n - 1u)],
                      A.in_off[min(cb + ns, (uint64_t)A.n)]};
 }
+#ifndef HHUFF_ENC_COPY_BATCH  // sorted encoder's copy-out: all LDS reads of a thread's chunks ahead of the stores
+#define HHUFF_ENC_COPY_BATCH 1   // (c4 encode -2.0 %, c2 -3.8 %; 122 VGPRs, still 4 waves a SIMD: r06aa_encode_copy_batch_ab.jsonl)
+#endif
 #ifndef HHUFF_ENC_EARLY
 // 1: the next chunk's offsets are loaded a chunk ahead and both they and the next span are waited for after
 // barrier 3, before the chunk's stores (c4 encode 0.680 -> 0.655 ms, profiles/r04aa_encode_early_ab.log);
@@ -2097,10 +2117,27 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
         // the stage's MSB-first words, byte-swapped on the way out (each read chunk is zeroed for the next
         // chunk); the chunk's first and last 16-B chunks are deferred (edge_fix_kernel)
         const uint32_t kl = (span - 1u) & ~15u;
+#if HHUFF_ENC_COPY_BATCH
+        // every chunk's LDS read first (NV of them), then the stores: one LDS round trip a chunk, not one each
+        uint4 cv[NV];
+#pragma unroll
+        for (int jv = 0; jv < NV; ++jv) {
+            const uint32_t k = (uint32_t)jv * (16u * NT) + t * 16u;
+            if (k < span) cv[jv] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s_out) + k);
+        }
+#pragma unroll
+        for (int jv = 0; jv < NV; ++jv) {
+            const uint32_t k = (uint32_t)jv * (16u * NT) + t * 16u;
+            if (k >= span) break;
+            const uint64_t g = (uint64_t)a0 + k;
+            uint4* sp = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_out) + k);
+            uint4 v = cv[jv];
+#else
         for (uint32_t k = t * 16u; k < span; k += 16u * NT) {
             const uint64_t g = (uint64_t)a0 + k;
             uint4* sp = reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s_out) + k);
             uint4 v = *sp;
+#endif
             const bool full = g >= lo && g + 16 <= hi;
             // (a partial edge chunk stored one byte a lane below is zeroed there, after its bytes are read)
             if (full || A.edges || !HHUFF_EDGE_BYTES) *sp = make_uint4(0u, 0u, 0u, 0u);
