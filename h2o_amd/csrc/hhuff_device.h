@@ -774,6 +774,9 @@ __device__ __forceinline__ void place_bits(O obase, uint32_t tb, uint64_t c, uin
     if (sh + n > 64u) or_word(obase, a + 2u, (uint32_t)t << (32u - sh));  // sh > 0 here
 }
 
+#ifndef HHUFF_ENC_HEAD_REUSE  // encode_chunk_v2: the head's stage word seeds the bulk loop (no second read of it)
+#define HHUFF_ENC_HEAD_REUSE 0
+#endif
 #ifndef HHUFF_ENC_OR3  // encode_chunk_v2's bulk step: the third output word ORed on every step (see put4m)
 #define HHUFF_ENC_OR3 0
 #endif
@@ -869,8 +872,7 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
     const uint32_t mlast = (uint32_t)(0xFFFFFFFFull >> ((32u - 8u * (end & 3u)) & 31u));
     // tlim < 2^31 keeps tb + n - tlim a signed quantity (stage bits are < 2^20)
     EncV2<O> E{enc, obase, startbit, limit >= 0x40000000u ? 0x7FFFFFFFu : startbit + limit, active, false};
-    auto masked = [&](uint32_t j, bool on) {  // one dword with byte masks (head / tail)
-        const uint32_t w = stage[min(a0 + 4u * j, last) >> 2];
+    auto masked = [&](uint32_t j, bool on, uint32_t w) {  // one dword with byte masks (head / tail); w: its word
         uint32_t vm = j == 0 ? mfirst : 0xFFFFFFFFu;
         vm &= (j + 1 == ndw) ? mlast : 0xFFFFFFFFu;
         vm = on ? vm : 0u;
@@ -878,13 +880,20 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
         E.put4(enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0400u)], enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0501u)],
                enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0602u)], enc[__builtin_amdgcn_perm(iw, w, 0x0C0C0703u)], on);
     };
-    masked(0, active && jf != 0);  // head
+    // the head's word is the bulk loop's first word too (an active lane has a0 <= last; an inactive lane's words
+    // are never placed): one LDS read, issued before the head's lookups and ORs
+    const uint32_t w0 = stage[min(a0, last) >> 2];
+    masked(0, active && jf != 0, w0);  // head
     const uint32_t* sw = stage + (a0 >> 2);
     const uint32_t jlast = (last >> 2) - (a0 >> 2);  // stage reads are clamped to the span
     {
         const uint32_t jlv = E.live ? jl : 0u;  // a lane that failed in its head places nothing more
         const uint32_t jend = wave_max_u32(jlv);  // uniform trip count: no vote per step
+#if HHUFF_ENC_HEAD_REUSE
+        uint32_t wn = w0;
+#else
         uint32_t wn = sw[min(0u, jlast)];
+#endif
         // U == 2: the extra dword past jend has onm == 0 (jlv <= jend) and a clamped read
         if constexpr (U == 2) for (uint32_t j = 0; j < jend; j += 2) {
             const uint32_t w0 = wn, w1 = sw[min(j + 1u, jlast)];
@@ -921,7 +930,7 @@ __device__ __forceinline__ uint32_t encode_chunk_v2(const uint32_t* stage, uint3
     }
     E.fail = E.fail || (E.live && E.tb >= E.tlim);
     E.live = E.live && !E.fail;
-    masked(jl, active && (end & 3u) != 0 && jl >= jf);  // tail
+    masked(jl, active && (end & 3u) != 0 && jl >= jf, stage[min(a0 + 4u * jl, last) >> 2]);  // tail
     if (E.fail || !active) return kFailLen;
     const uint32_t tbits = E.tb - startbit;
     if (pad) {  // fill the last byte with ones (EOS prefix, hpack.c:795-798); strings start on a byte, so the
