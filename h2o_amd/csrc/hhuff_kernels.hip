@@ -1903,6 +1903,9 @@ __device__ __forceinline__ SortChunk sort_chunk_issue(const EncArgs& A, uint64_t
     return SortChunk{A.in_off[ic], A.in_off[ic + 1], A.in_off[min(cb, (uint64_t)A.n - 1u)],
                      A.in_off[min(cb + ns, (uint64_t)A.n)]};
 }
+#ifndef HHUFF_ENC_SORTREC  // sorted encoder: one record read (place -> offset | length) before a lane's encode
+#define HHUFF_ENC_SORTREC 0
+#endif
 #ifndef HHUFF_ENC_COPY_BATCH  // sorted encoder's copy-out: all LDS reads of a thread's chunks ahead of the stores
 #define HHUFF_ENC_COPY_BATCH 1   // (c4 encode -2.0 %, c2 -3.8 %; 122 VGPRs, still 4 waves a SIMD: r06aa_encode_copy_batch_ab.jsonl)
 #endif
@@ -1930,8 +1933,15 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
     __shared__ __attribute__((aligned(16))) uint2 s_enc[512];  // 256..511: bytes outside a string
     __shared__ __attribute__((aligned(16))) uint32_t s_in[CH / 4 + 8];
     __shared__ __attribute__((aligned(16))) uint32_t s_out[CH / 4 + 8];
+#if HHUFF_ENC_SORTREC
+    // sorted place -> {offset in the span (14 bits) | length << 14}, written by the string's own thread once its
+    // place is known, then overwritten with the encoded length (read back by that thread after barrier 3)
+    static_assert(CH <= 16384, "14-bit span offsets");
+    __shared__ uint32_t s_rec[kSortStr];
+#else
     __shared__ uint2 s_str[kSortStr];  // {offset in the span, length} of chunk string t
     __shared__ uint16_t s_perm[kSortStr];
+#endif
     __shared__ uint32_t s_bin[kSortBins];  // strings per bin, then the bins' first places
 #if HHUFF_ENCO_PAD
     __shared__ uint32_t s_pad[HHUFF_ENCO_PAD / 4];
@@ -1985,6 +1995,9 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
     // nothing reads those areas any more (three barriers a chunk in all).
     uint4 pv[NV];
     uint32_t bin[SPT], rank[SPT];
+#if HHUFF_ENC_SORTREC
+    uint32_t mypos[SPT];
+#endif
     auto prepare = [&](const SortChunk (&q)[SPT], uint64_t qb, uint32_t z0) {
         const uint32_t sp = span_of(q[0]);
         if (sp > (uint32_t)CH) return;  // workgroup-uniform: the per-thread path needs none of it
@@ -1995,7 +2008,9 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
         for (int u = 0; u < SPT; ++u) {
             const uint32_t tt = t + (uint32_t)u * NT;
             const uint32_t ln = qb + tt < A.n ? q[u].e - q[u].s : 0u;
+#if !HHUFF_ENC_SORTREC
             s_str[tt] = make_uint2(q[u].s - (q[0].lo & ~15u), ln);
+#endif
             // counting sort by the bulk loop's trip count (encode_chunk_v2: dwords from the string's first
             // aligned dword to its end), which the wave's longest string sets
             bin[u] = ln ? min((q[u].s + ln - (q[u].s & ~3u)) >> 2, kSortBins - 1u) : 0u;
@@ -2069,7 +2084,14 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
 #pragma unroll
             for (int u = 0; u < SPT; ++u) {
                 const uint32_t eb = (uint32_t)__shfl((int)ex, (int)(bin[u] >> 1)), xb = (uint32_t)__shfl((int)x0, (int)(bin[u] >> 1));
+#if HHUFF_ENC_SORTREC
+                const uint32_t tt = t + (uint32_t)u * NT;
+                const uint32_t ln = cb + tt < A.n ? cur[u].e - cur[u].s : 0u;
+                mypos[u] = eb + ((bin[u] & 1u) ? xb : 0u) + rank[u];
+                s_rec[mypos[u]] = (cur[u].s - (cur[0].lo & ~15u)) | (ln << 14);
+#else
                 s_perm[eb + ((bin[u] & 1u) ? xb : 0u) + rank[u]] = (uint16_t)(t + (uint32_t)u * NT);
+#endif
             }
         }
         __syncthreads();
@@ -2084,21 +2106,36 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
         // sorted position NS - 1 - t, so the pair's lengths add up to about twice the mean)
 #pragma unroll
         for (int u = 0; u < SPT; ++u) {
+#if HHUFF_ENC_SORTREC
+            const uint32_t pj = u == 0 ? t : NS - 1u - t;
+            const uint32_t rj = s_rec[pj];
+            const uint2 sj = make_uint2(rj & 0x3FFFu, rj >> 14);
+            const bool vj = true;  // a string past n has length 0
+#else
             const uint32_t j = s_perm[u == 0 ? t : NS - 1u - t];
             const uint2 sj = s_str[j];
             const bool vj = cb + j < A.n;
+#endif
             const bool act = vj && sj.y != 0 && sj.y <= kMaxStrLen;
             const uint32_t tb = encode_chunk_v2<HHUFF_ENC_SORTED_U>(s_in, span - 4u, sj.x, sj.y, act, lds_addr(s_out), 8u * sj.x, s_enc,
                                                 act ? 8 * sj.y - 7 : 0xFFFFFFFFu, true);
             // the encoded length goes back to the string's own record (read by its own thread only), so the
             // lengths and statuses are stored in string order, coalesced
+#if HHUFF_ENC_SORTREC
+            s_rec[pj] = act && tb != kFailLen ? (tb + 7) >> 3 : kFailLen;
+#else
             s_str[j].x = act && tb != kFailLen ? (tb + 7) >> 3 : kFailLen;
+#endif
         }
         PROF_MARK(2);
         __syncthreads();
         uint32_t olen[SPT];
 #pragma unroll
+#if HHUFF_ENC_SORTREC
+        for (int u = 0; u < SPT; ++u) olen[u] = s_rec[mypos[u]];
+#else
         for (int u = 0; u < SPT; ++u) olen[u] = s_str[t + (uint32_t)u * NT].x;
+#endif
 #if HHUFF_ENC_EARLY
         // the next chunk goes in now, before this chunk's stores: its span loads (in flight since the encode
         // began) are then waited for with no store ahead of them in the memory counter
