@@ -1903,6 +1903,9 @@ __device__ __forceinline__ SortChunk sort_chunk_issue(const EncArgs& A, uint64_t
     return SortChunk{A.in_off[ic], A.in_off[ic + 1], A.in_off[min(cb, (uint64_t)A.n - 1u)],
                      A.in_off[min(cb + ns, (uint64_t)A.n)]};
 }
+#ifndef HHUFF_ENC_COPY_EARLY  // sorted encoder: the batched copy-out's reads issued right after barrier 3
+#define HHUFF_ENC_COPY_EARLY 0
+#endif
 #ifndef HHUFF_ENC_SORTREC  // sorted encoder: one record read (place -> offset | length) before a lane's encode
 #define HHUFF_ENC_SORTREC 0
 #endif
@@ -2129,6 +2132,16 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
         }
         PROF_MARK(2);
         __syncthreads();
+#if HHUFF_ENC_COPY_BATCH && HHUFF_ENC_COPY_EARLY
+        // the copy-out's LDS reads right after barrier 3 (the stage is final; prepare() writes only past span),
+        // so their latency runs under the next chunk's prepare and this chunk's length stores
+        uint4 cv[NV];
+#pragma unroll
+        for (int jv = 0; jv < NV; ++jv) {
+            const uint32_t k = (uint32_t)jv * (16u * NT) + t * 16u;
+            if (k < span) cv[jv] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s_out) + k);
+        }
+#endif
         uint32_t olen[SPT];
 #pragma unroll
 #if HHUFF_ENC_SORTREC
@@ -2156,12 +2169,14 @@ __global__ __launch_bounds__(NS / SPT) void encode_sorted_kernel(EncArgs A) {
         const uint32_t kl = (span - 1u) & ~15u;
 #if HHUFF_ENC_COPY_BATCH
         // every chunk's LDS read first (NV of them), then the stores: one LDS round trip a chunk, not one each
+#if !HHUFF_ENC_COPY_EARLY
         uint4 cv[NV];
 #pragma unroll
         for (int jv = 0; jv < NV; ++jv) {
             const uint32_t k = (uint32_t)jv * (16u * NT) + t * 16u;
             if (k < span) cv[jv] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s_out) + k);
         }
+#endif
 #pragma unroll
         for (int jv = 0; jv < NV; ++jv) {
             const uint32_t k = (uint32_t)jv * (16u * NT) + t * 16u;
